@@ -1,0 +1,185 @@
+/*
+ * trivy_secret.h -- C ABI of the MI355X secret-scan engine (libtrivy_secret.so).
+ *
+ * Drop-in boundary for trivy's secret hot path, pkg/fanal/secret:
+ *
+ *   reference (Go)                                    this ABI
+ *   ------------------------------------------------  ---------------------------------
+ *   secret.NewScanner(*Config) Scanner                tsg_ruleset_compile
+ *       scanner.go:293-329 (rule assembly stays in the host language; the final
+ *       Global{Rules, AllowRules, ExcludeBlock} is handed over here)
+ *   regexp compile error via Regexp.UnmarshalYAML     TSG_ERR_CONFIG + err text
+ *       scanner.go:69-81
+ *   Global.AllowPath(path) bool                       tsg_ruleset_allow_path
+ *       scanner.go:55-57 (used by SecretAnalyzer.Required, analyzer/secret/secret.go:145)
+ *   (*Scanner).Scan(ScanArgs) types.Secret            tsg_scan_cpu (one file, exact CPU)
+ *       scanner.go:341-416                            tsg_scan_batch (many files, GPU)
+ *   SecretAnalyzer.Analyze per-file goroutines        tsg_scan_batch: the batching boundary
+ *       analyzer/secret/secret.go:78-110, analyzer.go:419-443
+ *
+ * Error convention: every call returns TSG_OK (0) or a negative TSG_ERR_*; the
+ * message of the last failing call on this thread is tsg_last_error().  No C++
+ * exception crosses the ABI.  All entry points are thread-safe for distinct
+ * tsg_ctx objects; a tsg_ruleset is immutable and may be shared by any number of
+ * threads and contexts.  The library never retains caller pointers past a call,
+ * except that tsg_batch_upload's host buffers must stay valid until the next
+ * tsg_batch_upload / tsg_ctx_destroy on that context (they are read by the host
+ * resolution step of tsg_batch_scan).
+ *
+ * Result format (tsg_result_data), little endian:
+ *   u32 magic 'TSG1' (0x31475354), u32 nfiles, then per file:
+ *     u8  status      0 = no findings  -> types.Secret{}             (scanner.go:401-403)
+ *                     1 = path allowed -> types.Secret{FilePath}      (scanner.go:343-347)
+ *                     2 = findings     -> types.Secret{FilePath, Findings}
+ *     u32 nfindings, then per finding (already in Go sort.Slice order, scanner.go:405-410):
+ *       u32 rule (index into the compiled rule list: RuleID/Category/Severity/Title)
+ *       i32 start_line, i32 end_line, bytes match, u32 nlines, then per line:
+ *         i32 number, u8 flags (1 IsCause, 2 FirstCause, 4 LastCause), bytes content
+ *   bytes = u32 length + raw bytes (Content == Highlighted in the reference).
+ */
+#ifndef TRIVY_SECRET_H
+#define TRIVY_SECRET_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TSG_OK 0
+#define TSG_ERR_CONFIG -1  /* a regex failed to compile (Go regexp syntax) */
+#define TSG_ERR_ARG -2     /* bad argument */
+#define TSG_ERR_GPU -3     /* HIP runtime / device failure */
+#define TSG_ERR_NOMEM -4   /* allocation failure */
+#define TSG_ERR_INTERNAL -5
+
+/* secret.AllowRule (scanner.go:186-191). NULL regex/path = field absent. */
+typedef struct tsg_allow_rule_desc {
+  const char* id;
+  const char* description;
+  const char* regex;
+  const char* path;
+} tsg_allow_rule_desc;
+
+/* secret.Rule (scanner.go:83-94). NULL regex/path = field absent. */
+typedef struct tsg_rule_desc {
+  const char* id;
+  const char* category;
+  const char* title;
+  const char* severity;
+  const char* regex;
+  const char* const* keywords;
+  uint32_t n_keywords;
+  const char* path;
+  const tsg_allow_rule_desc* allow_rules;
+  uint32_t n_allow_rules;
+  const char* const* exclude_regexes; /* ExcludeBlock.Regexes */
+  uint32_t n_exclude_regexes;
+  const char* secret_group_name;
+} tsg_rule_desc;
+
+typedef struct tsg_ruleset tsg_ruleset;
+typedef struct tsg_result tsg_result;
+typedef struct tsg_ctx tsg_ctx;
+
+/* Compile Global{Rules, AllowRules, ExcludeBlock}: regexes, the K1 keyword automaton,
+ * the K2 rule-group DFAs.  On TSG_ERR_CONFIG, err holds Go's error text. */
+int tsg_ruleset_compile(const tsg_rule_desc* rules, uint32_t n_rules,
+                        const tsg_allow_rule_desc* allow_rules, uint32_t n_allow_rules,
+                        const char* const* exclude_regexes, uint32_t n_exclude_regexes,
+                        tsg_ruleset** out, char* err, size_t err_len);
+void tsg_ruleset_destroy(tsg_ruleset* rs);
+
+/* Global.AllowPath: 1 allowed, 0 not, <0 error. */
+int tsg_ruleset_allow_path(const tsg_ruleset* rs, const char* path, size_t path_len);
+
+typedef struct tsg_ruleset_info {
+  uint32_t n_rules;
+  uint32_t n_keywords;      /* K1 keyword ids incl. 2 fallback pseudo keywords */
+  uint32_t n_groups;        /* K2 DFAs */
+  uint32_t n_hostonly;      /* rules without a GPU DFA (state cap) */
+  uint32_t kw_states;       /* K1 automaton states */
+  uint32_t max_group_states;
+  uint64_t table_bytes;     /* all device tables */
+} tsg_ruleset_info;
+int tsg_ruleset_get_info(const tsg_ruleset* rs, tsg_ruleset_info* out);
+
+/* Exact CPU Scan of one file (scanner.go:341-416). */
+int tsg_scan_cpu(const tsg_ruleset* rs, const char* path, size_t path_len,
+                 const uint8_t* content, size_t len, tsg_result** out);
+
+/* Exact CPU Scan of a batch: file i = data[offsets[i] .. offsets[i+1]),
+ * path i = paths[path_offsets[i] .. path_offsets[i+1]). nthreads <= 0: hardware. */
+int tsg_scan_cpu_batch(const tsg_ruleset* rs, const uint8_t* data, const uint64_t* offsets,
+                       uint32_t nfiles, const char* paths, const uint64_t* path_offsets,
+                       int nthreads, tsg_result** out);
+
+const uint8_t* tsg_result_data(const tsg_result* r, size_t* len);
+void tsg_result_free(tsg_result* r);
+
+/* ---- GPU (one context per device; one process per GPU) ---- */
+typedef struct tsg_ctx_options {
+  uint32_t chunk_bytes;      /* bytes per lane (multiple of 16); 0 = default */
+  uint32_t ext_cap;          /* max bytes a lane follows a match past its chunk; 0 = default */
+  uint32_t cand_capacity;    /* candidate records per batch; 0 = default */
+  int32_t host_threads;      /* resolver threads; <= 0 = hardware */
+} tsg_ctx_options;
+
+int tsg_ctx_create(int device, const tsg_ruleset* rs, const tsg_ctx_options* opt,
+                   tsg_ctx** out);
+void tsg_ctx_destroy(tsg_ctx* ctx);
+
+/* Copy a batch into device memory (HBM). Host buffers must stay valid until the next
+ * upload (the exact host resolution reads them). */
+int tsg_batch_upload(tsg_ctx* ctx, const uint8_t* data, const uint64_t* offsets,
+                     uint32_t nfiles, const char* paths, const uint64_t* path_offsets);
+/* K1 + K2 on the device-resident batch, candidates back to the host, exact resolution. */
+int tsg_batch_scan(tsg_ctx* ctx, tsg_result** out);
+/* Only the device part of tsg_batch_scan (kernels + candidate download), no resolution. */
+int tsg_batch_kernels(tsg_ctx* ctx);
+/* upload + scan */
+int tsg_scan_batch(tsg_ctx* ctx, const uint8_t* data, const uint64_t* offsets, uint32_t nfiles,
+                   const char* paths, const uint64_t* path_offsets, tsg_result** out);
+
+typedef struct tsg_stats {
+  double k1_ms;          /* keyword kernel, last batch (HIP events on the ctx stream) */
+  double k2_ms;          /* all rule-group kernel launches, last batch */
+  double aux_ms;         /* memsets + candidate/keyword downloads */
+  double resolve_ms;     /* host exact resolution (wall) */
+  uint64_t bytes;        /* content bytes of the batch */
+  uint64_t k2_bytes;     /* content bytes scanned by K2 (sum over groups of gated bytes) */
+  uint64_t candidates;   /* candidate records produced */
+  uint64_t files_resolved;  /* files that needed exact host work */
+  uint32_t k2_launches;
+  uint32_t overflow;     /* 1 if the candidate buffer overflowed (files resolved whole) */
+} tsg_stats;
+int tsg_ctx_get_stats(const tsg_ctx* ctx, tsg_stats* out);
+
+const char* tsg_last_error(void);
+
+/* ---- test hooks: the Go-regexp engine and the DFA builder in isolation ---- */
+typedef struct tsg_regex tsg_regex;
+int tsg_regex_compile(const char* src, tsg_regex** out, char* err, size_t err_len);
+void tsg_regex_free(tsg_regex* re);
+int tsg_regex_num_slots(const tsg_regex* re);
+/* regexp.MatchString: 1 / 0 */
+int tsg_regex_match(const tsg_regex* re, const uint8_t* text, size_t len);
+/* FindAllIndex (submatch=0, 2 slots/match) or FindAllSubmatchIndex (submatch=1).
+ * Writes up to cap int64 values, returns the number of values needed (>= 0). */
+int64_t tsg_regex_find_all(const tsg_regex* re, const uint8_t* text, size_t len, int submatch,
+                           int64_t* out, size_t cap);
+/* DFA candidate end offsets of one regex over text (all p where a match may end),
+ * computed with the GPU lane algorithm (chunk bytes per lane). Returns count. */
+int64_t tsg_regex_dfa_ends(const tsg_regex* re, const uint8_t* text, size_t len, uint32_t chunk,
+                           int64_t* out, size_t cap);
+
+/* Emulate K1+K2 on the CPU with the GPU algorithm and resolve (tests). */
+int tsg_scan_batch_emulated(const tsg_ruleset* rs, const uint8_t* data, const uint64_t* offsets,
+                            uint32_t nfiles, const char* paths, const uint64_t* path_offsets,
+                            uint32_t chunk, tsg_result** out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* TRIVY_SECRET_H */

@@ -1,0 +1,115 @@
+"""ctypes binding of libtrivy_secret.so (include/trivy_secret.h).
+
+The library is the product: rule compilation, the exact Go-semantics resolver and the
+HIP kernels all live in it.  Importing this module fails loudly when the library has
+not been built (`python -m trivy_amd.build`); there is no Python fallback.
+"""
+import ctypes as C
+import os
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libtrivy_secret.so")
+
+TSG_OK = 0
+TSG_ERR_CONFIG = -1
+TSG_ERR_ARG = -2
+TSG_ERR_GPU = -3
+TSG_ERR_NOMEM = -4
+TSG_ERR_INTERNAL = -5
+
+
+class AllowRuleDesc(C.Structure):
+    _fields_ = [("id", C.c_char_p), ("description", C.c_char_p), ("regex", C.c_char_p),
+                ("path", C.c_char_p)]
+
+
+class RuleDesc(C.Structure):
+    _fields_ = [("id", C.c_char_p), ("category", C.c_char_p), ("title", C.c_char_p),
+                ("severity", C.c_char_p), ("regex", C.c_char_p),
+                ("keywords", C.POINTER(C.c_char_p)), ("n_keywords", C.c_uint32),
+                ("path", C.c_char_p), ("allow_rules", C.POINTER(AllowRuleDesc)),
+                ("n_allow_rules", C.c_uint32), ("exclude_regexes", C.POINTER(C.c_char_p)),
+                ("n_exclude_regexes", C.c_uint32), ("secret_group_name", C.c_char_p)]
+
+
+class RulesetInfo(C.Structure):
+    _fields_ = [("n_rules", C.c_uint32), ("n_keywords", C.c_uint32), ("n_groups", C.c_uint32),
+                ("n_hostonly", C.c_uint32), ("kw_states", C.c_uint32),
+                ("max_group_states", C.c_uint32), ("table_bytes", C.c_uint64)]
+
+
+class CtxOptions(C.Structure):
+    _fields_ = [("chunk_bytes", C.c_uint32), ("ext_cap", C.c_uint32),
+                ("cand_capacity", C.c_uint32), ("host_threads", C.c_int32)]
+
+
+class Stats(C.Structure):
+    _fields_ = [("k1_ms", C.c_double), ("k2_ms", C.c_double), ("aux_ms", C.c_double),
+                ("resolve_ms", C.c_double), ("bytes", C.c_uint64), ("k2_bytes", C.c_uint64),
+                ("candidates", C.c_uint64), ("files_resolved", C.c_uint64),
+                ("k2_launches", C.c_uint32), ("overflow", C.c_uint32)]
+
+
+# (name, restype, argtypes) -- every symbol include/trivy_secret.h declares
+_P = C.c_void_p
+_U8P = C.POINTER(C.c_uint8)
+_U64P = C.POINTER(C.c_uint64)
+_I64P = C.POINTER(C.c_int64)
+SIGNATURES = [
+    ("tsg_ruleset_compile", C.c_int, [C.POINTER(RuleDesc), C.c_uint32, C.POINTER(AllowRuleDesc),
+                                      C.c_uint32, C.POINTER(C.c_char_p), C.c_uint32,
+                                      C.POINTER(_P), C.c_char_p, C.c_size_t]),
+    ("tsg_ruleset_destroy", None, [_P]),
+    ("tsg_ruleset_allow_path", C.c_int, [_P, C.c_char_p, C.c_size_t]),
+    ("tsg_ruleset_get_info", C.c_int, [_P, C.POINTER(RulesetInfo)]),
+    ("tsg_scan_cpu", C.c_int, [_P, C.c_char_p, C.c_size_t, C.c_char_p, C.c_size_t, C.POINTER(_P)]),
+    ("tsg_scan_cpu_batch", C.c_int, [_P, _P, _U64P, C.c_uint32, _P, _U64P, C.c_int,
+                                     C.POINTER(_P)]),
+    ("tsg_result_data", _P, [_P, C.POINTER(C.c_size_t)]),
+    ("tsg_result_free", None, [_P]),
+    ("tsg_ctx_create", C.c_int, [C.c_int, _P, C.POINTER(CtxOptions), C.POINTER(_P)]),
+    ("tsg_ctx_destroy", None, [_P]),
+    ("tsg_batch_upload", C.c_int, [_P, _P, _U64P, C.c_uint32, _P, _U64P]),
+    ("tsg_batch_scan", C.c_int, [_P, C.POINTER(_P)]),
+    ("tsg_batch_kernels", C.c_int, [_P]),
+    ("tsg_scan_batch", C.c_int, [_P, _P, _U64P, C.c_uint32, _P, _U64P, C.POINTER(_P)]),
+    ("tsg_ctx_get_stats", C.c_int, [_P, C.POINTER(Stats)]),
+    ("tsg_last_error", C.c_char_p, []),
+    ("tsg_regex_compile", C.c_int, [C.c_char_p, C.POINTER(_P), C.c_char_p, C.c_size_t]),
+    ("tsg_regex_free", None, [_P]),
+    ("tsg_regex_num_slots", C.c_int, [_P]),
+    ("tsg_regex_match", C.c_int, [_P, C.c_char_p, C.c_size_t]),
+    ("tsg_regex_find_all", C.c_int64, [_P, C.c_char_p, C.c_size_t, C.c_int, _I64P, C.c_size_t]),
+    ("tsg_regex_dfa_ends", C.c_int64, [_P, C.c_char_p, C.c_size_t, C.c_uint32, _I64P,
+                                       C.c_size_t]),
+    ("tsg_scan_batch_emulated", C.c_int, [_P, _P, _U64P, C.c_uint32, _P, _U64P, C.c_uint32,
+                                          C.POINTER(_P)]),
+]
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError("libtrivy_secret.so is not built; run `python -m trivy_amd.build` "
+                              "(expected at %s)" % LIB_PATH)
+        L = C.CDLL(LIB_PATH)
+        for name, res, args in SIGNATURES:
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+class NativeError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__("%s (code %d)" % (msg, code))
+        self.code = code
+
+
+def check(rc):
+    if rc != TSG_OK:
+        raise NativeError(rc, lib().tsg_last_error().decode("utf-8", "replace"))
+    return rc

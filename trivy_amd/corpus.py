@@ -1,0 +1,226 @@
+"""Seeded synthetic corpora for the secret-scan benchmarks and parity tests.
+
+Not part of the scanning path: it produces BASELINE.json-shaped inputs (mixed
+code/config text files, log-normal sizes with median ~6 KiB, planted secrets for
+every builtin rule plus near misses, CRLF lines, long lines, multi-line PEM keys,
+valid non-ASCII UTF-8, invalid bytes and the U+017F / U+212A folding runes) as one
+packed byte stream + offsets + paths (trivy_amd.secret.Batch).
+
+Text is sampled once into a base buffer from a vocabulary that includes the common
+builtin keywords (key, sk, account, -----, lob, live_, pk., sg., ...), then tiled, so
+generating 10 GiB is a memcpy-speed operation.
+"""
+import sre_parse
+import warnings
+
+import numpy as np
+
+from .secret import Batch, builtin_rules
+
+VOCAB = (
+    "the a of to in is for on with as by at from it this that be are was not or and if else "
+    "return def class import func var let const int str bool true false null None self new "
+    "public private static void main print log error warn info debug value values name id "
+    "data result results config settings options path file files dir url host port user "
+    "users password token tokens secret secrets key keys api apikey access account accounts "
+    "task tasks ask disk risk skip desk global blob lobby public_key pk. sg. msg. live_ "
+    "test test_ example vendor buffer index item items list map dict set get put post "
+    "request response client server http https json yaml xml html css js go py rs java "
+    "for while break continue try catch except finally raise throw async await yield "
+    "linear matrix vector hash sha256 md5 base64 encode decode encrypt decrypt cipher "
+    "aws gcp azure heroku slack github gitlab stripe twilio facebook twitter discord "
+    "dropbox mailgun mailchimp linkedin twitch npm pypi ghp_ xoxb- AKIA SK dapi pul- "
+    "----- ===== ##### // /* */ # -- ; { } ( ) [ ] < > => := = == != += -= && || "
+    "0 1 2 3 42 100 1024 0x1f 3.14 2023-01-01 localhost 127.0.0.1 /usr/local/bin "
+    "café naïve résumé über 日本語 中文 Ελληνικά кириллица emoji😀 ✓"
+).split()
+
+
+def _sample(node_list, rng, out):
+    for op, av in node_list:
+        name = str(op)
+        if name == "LITERAL":
+            out.append(chr(av))
+        elif name == "NOT_LITERAL":
+            c = chr(av)
+            out.append("x" if c != "x" else "y")
+        elif name == "ANY":
+            out.append(rng.choice(list("abcxyz012 ")))
+        elif name == "IN":
+            chars = []
+            neg = False
+            for o2, a2 in av:
+                n2 = str(o2)
+                if n2 == "NEGATE":
+                    neg = True
+                elif n2 == "LITERAL":
+                    chars.append(chr(a2))
+                elif n2 == "RANGE":
+                    chars.extend(chr(c) for c in range(a2[0], min(a2[1], 0x7E) + 1))
+                elif n2 == "CATEGORY":
+                    cat = str(a2)
+                    if "DIGIT" in cat:
+                        chars.extend("0123456789")
+                    elif "SPACE" in cat:
+                        chars.extend(" ")
+                    elif "WORD" in cat:
+                        chars.extend("abcXYZ019_")
+            if neg:
+                pool = [c for c in "abcdefghij0123456789 =:" if c not in chars] or ["#"]
+                out.append(rng.choice(pool))
+            else:
+                out.append(rng.choice(chars or ["a"]))
+        elif name == "BRANCH":
+            _sample(av[1][rng.integers(len(av[1]))], rng, out)
+        elif name == "SUBPATTERN":
+            _sample(av[-1], rng, out)
+        elif name in ("MAX_REPEAT", "MIN_REPEAT"):
+            lo, hi, sub = av
+            hi = lo + 3 if hi == sre_parse.MAXREPEAT else hi
+            n = int(rng.integers(lo, hi + 1)) if hi > lo else lo
+            if lo >= 8:
+                n = lo + int(rng.integers(0, max(1, min(hi, lo + 4) - lo + 1)))
+            for _ in range(n):
+                _sample(sub, rng, out)
+        elif name == "AT":
+            pass
+        elif name == "CATEGORY":
+            out.append("0")
+        else:  # pragma: no cover
+            raise ValueError(name)
+
+
+def sample_secret(regex, rng):
+    """A string drawn from (a Python reading of) a rule regex; ASCII only."""
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        tree = sre_parse.parse(regex)
+    out = []
+    _sample(list(tree), rng, out)
+    return "".join(out)
+
+
+def _base_text(nbytes, rng):
+    toks = [t.encode() for t in VOCAB]
+    maxl = max(len(t) for t in toks)
+    table = np.zeros((len(toks), maxl), dtype=np.uint8)
+    lens = np.array([len(t) for t in toks])
+    for i, t in enumerate(toks):
+        table[i, :len(t)] = np.frombuffer(t, dtype=np.uint8)
+    p = 1.0 / np.arange(1, len(toks) + 1) ** 0.6
+    rng.shuffle(p)
+    p /= p.sum()
+    ntok = nbytes // 6 + 16
+    ids = rng.choice(len(toks), size=ntok, p=p)
+    seps = rng.choice(np.frombuffer(b"       ...,:;=()\n\n\n\"'\t", dtype=np.uint8), size=ntok)
+    g = table[ids]
+    mask = np.arange(maxl)[None, :] < lens[ids][:, None]
+    body = np.concatenate([g, seps[:, None]], axis=1)
+    mask = np.concatenate([mask, np.ones((ntok, 1), dtype=bool)], axis=1)
+    text = body[mask]
+    # ~10% of the newlines become CRLF
+    nl = np.flatnonzero(text == 10)
+    crlf = nl[rng.random(len(nl)) < 0.1]
+    if len(crlf):
+        text = np.insert(text, crlf, 13)
+    return text[:nbytes]
+
+
+EXTS = ["go", "py", "js", "ts", "yaml", "json", "sh", "env", "tf", "ini", "txt", "conf", "rb",
+        "java", "md"]
+DIRS = ["src", "pkg", "lib", "app", "cmd", "internal", "config", "deploy", "scripts", "web",
+        "test", "vendor", "examples", "docs", "tools"]
+
+
+def make_corpus(total_bytes, seed=1, plants_per_mib=1.0, median=6 * 1024, sigma=1.2,
+                min_size=10, max_size=2 * 1024 * 1024, base_bytes=None, special=True):
+    """Return (Batch, info).  Deterministic in `seed`."""
+    rng = np.random.default_rng(seed)
+    base_bytes = base_bytes or int(min(total_bytes, 64 << 20))
+    base = _base_text(base_bytes, rng)
+    # file sizes
+    sizes = []
+    acc = 0
+    while acc < total_bytes:
+        n = int(rng.lognormal(np.log(median), sigma, size=4096).clip(min_size, max_size)[0])
+        chunk = rng.lognormal(np.log(median), sigma, size=4096).clip(min_size, max_size).astype(np.int64)
+        cs = np.cumsum(chunk)
+        k = int(np.searchsorted(cs, total_bytes - acc)) + 1
+        sizes.append(chunk[:k])
+        acc += int(cs[min(k, len(cs)) - 1])
+        del n
+    sizes = np.concatenate(sizes)
+    sizes[-1] -= max(0, int(sizes.sum()) - total_bytes)
+    sizes = sizes[sizes > 0]
+    nfiles = len(sizes)
+    offsets = np.zeros(nfiles + 1, dtype=np.uint64)
+    np.cumsum(sizes, out=offsets[1:])
+    total = int(offsets[-1])
+    reps = -(-total // len(base))
+    start = int(rng.integers(0, len(base)))
+    data = np.empty(total + 16, dtype=np.uint8)
+    pos = 0
+    src = np.concatenate([base[start:], base[:start]])
+    for _ in range(reps):
+        n = min(len(src), total - pos)
+        data[pos:pos + n] = src[:n]
+        pos += n
+        if pos >= total:
+            break
+    data[total:] = 0
+    # plants: one valid sample of every builtin rule, round-robin, plus near misses
+    rules, _ = builtin_rules()
+    nplants = max(len(rules), int(plants_per_mib * total / (1 << 20)))
+    pfiles = rng.integers(0, nfiles, size=nplants)
+    planted = 0
+    for i in range(nplants):
+        f = int(pfiles[i])
+        fs, fe = int(offsets[f]), int(offsets[f + 1])
+        r = rules[i % len(rules)]
+        s = sample_secret(r.Regex, rng)
+        if i % 5 == 4:  # near miss: truncate the secret part
+            s = s[: max(1, len(s) - 3)]
+        line = ("\n" + s + "\n").encode()
+        if fe - fs < len(line) + 1:
+            continue
+        at = fs + int(rng.integers(0, fe - fs - len(line)))
+        data[at:at + len(line)] = np.frombuffer(line, dtype=np.uint8)
+        planted += 1
+    if special and nfiles > 100:
+        # invalid bytes (0.1%), folding runes (0.01%), long lines (5%), PEM blocks (0.5%)
+        for f in rng.choice(nfiles, size=max(1, nfiles // 1000), replace=False):
+            fs, fe = int(offsets[f]), int(offsets[f + 1])
+            if fe - fs > 4:
+                data[fs + int(rng.integers(0, fe - fs))] = int(rng.integers(0x80, 0x100))
+        for f in rng.choice(nfiles, size=max(1, nfiles // 10000), replace=False):
+            fs, fe = int(offsets[f]), int(offsets[f + 1])
+            w = "ſecret=\"abcdefgh12\" KEY".encode()
+            if fe - fs > len(w) + 2:
+                at = fs + int(rng.integers(0, fe - fs - len(w)))
+                data[at:at + len(w)] = np.frombuffer(w, dtype=np.uint8)
+        pem = ("-----BEGIN RSA PRIVATE KEY-----\n" + "\n".join(
+            "".join(rng.choice(list("ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789+/"),
+                               size=64)) for _ in range(8)) + "\n-----END RSA PRIVATE KEY-----\n").encode()
+        for f in rng.choice(nfiles, size=max(1, nfiles // 200), replace=False):
+            fs, fe = int(offsets[f]), int(offsets[f + 1])
+            if fe - fs > len(pem) + 2:
+                at = fs + int(rng.integers(0, fe - fs - len(pem)))
+                data[at:at + len(pem)] = np.frombuffer(pem, dtype=np.uint8)
+        for f in rng.choice(nfiles, size=max(1, nfiles // 20), replace=False):
+            fs, fe = int(offsets[f]), int(offsets[f + 1])
+            if fe - fs > 300:
+                at = fs + int(rng.integers(0, fe - fs - 250))
+                seg = data[at:at + 250]
+                seg[seg == 10] = 32
+    # paths
+    d = rng.integers(0, len(DIRS), size=nfiles)
+    d2 = rng.integers(0, len(DIRS), size=nfiles)
+    e = rng.integers(0, len(EXTS), size=nfiles)
+    pb = [("%s/%s/f%d.%s" % (DIRS[a], DIRS[b], i, EXTS[c])).encode()
+          for i, (a, b, c) in enumerate(zip(d, d2, e))]
+    plen = np.array([len(x) for x in pb], dtype=np.uint64)
+    poffs = np.zeros(nfiles + 1, dtype=np.uint64)
+    np.cumsum(plen, out=poffs[1:])
+    paths = np.frombuffer(b"".join(pb), dtype=np.uint8)
+    batch = Batch(data, offsets, paths, poffs)
+    return batch, {"files": nfiles, "bytes": total, "planted": planted, "seed": seed}

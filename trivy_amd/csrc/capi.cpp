@@ -1,0 +1,299 @@
+// C ABI, host part (rule compilation, CPU scans, test hooks).  See include/trivy_secret.h.
+#include <cstring>
+#include <exception>
+#include <thread>
+
+#include "internal.hpp"
+
+namespace tsg {
+
+static thread_local std::string g_last_error;
+
+void set_error(const std::string& msg) { g_last_error = msg; }
+int fail(int code, const std::string& msg) {
+  g_last_error = msg;
+  return code;
+}
+
+static void copy_err(const std::string& m, char* err, size_t len) {
+  if (!err || len == 0) return;
+  size_t n = std::min(len - 1, m.size());
+  std::memcpy(err, m.data(), n);
+  err[n] = 0;
+}
+
+static std::string str(const char* s) { return s ? std::string(s) : std::string(); }
+
+static std::shared_ptr<Regexp> compile_opt(const char* src, std::string* err) {
+  if (!src) return nullptr;
+  std::string e;
+  auto re = Regexp::Compile(src, &e);
+  if (!re) *err = "regexp compile error: " + e;
+  return re;
+}
+
+static int hw_threads(int n) {
+  if (n > 0) return n;
+  unsigned h = std::thread::hardware_concurrency();
+  if (h == 0) h = 4;
+  return (int)std::min<unsigned>(h, 16);
+}
+
+}  // namespace tsg
+
+using namespace tsg;
+
+extern "C" {
+
+const char* tsg_last_error(void) { return g_last_error.c_str(); }
+
+int tsg_ruleset_compile(const tsg_rule_desc* rules, uint32_t n_rules,
+                        const tsg_allow_rule_desc* allow_rules, uint32_t n_allow_rules,
+                        const char* const* exclude_regexes, uint32_t n_exclude_regexes,
+                        tsg_ruleset** out, char* err, size_t err_len) {
+  if (!out || (n_rules && !rules) || (n_allow_rules && !allow_rules) ||
+      (n_exclude_regexes && !exclude_regexes)) {
+    copy_err("bad argument", err, err_len);
+    return fail(TSG_ERR_ARG, "bad argument");
+  }
+  try {
+    auto h = std::make_unique<tsg_ruleset>();
+    std::string e;
+    auto allow_of = [&](const tsg_allow_rule_desc& a, AllowRuleC* o) -> bool {
+      o->id = str(a.id);
+      o->description = str(a.description);
+      o->regex = compile_opt(a.regex, &e);
+      if (a.regex && !o->regex) return false;
+      o->path = compile_opt(a.path, &e);
+      if (a.path && !o->path) return false;
+      return true;
+    };
+    for (uint32_t i = 0; i < n_rules; i++) {
+      const tsg_rule_desc& d = rules[i];
+      RuleC r;
+      r.id = str(d.id);
+      r.category = str(d.category);
+      r.title = str(d.title);
+      r.severity = str(d.severity);
+      r.secret_group_name = str(d.secret_group_name);
+      r.regex = compile_opt(d.regex, &e);
+      if (d.regex && !r.regex) goto bad;
+      r.path = compile_opt(d.path, &e);
+      if (d.path && !r.path) goto bad;
+      for (uint32_t k = 0; k < d.n_keywords; k++) {
+        std::string kw = str(d.keywords[k]), low;
+        r.keywords.push_back(kw);
+        go_to_lower((const uint8_t*)kw.data(), kw.size(), &low);  // strings.ToLower
+        r.kw_lower.push_back(low);
+      }
+      for (uint32_t k = 0; k < d.n_allow_rules; k++) {
+        AllowRuleC a;
+        if (!allow_of(d.allow_rules[k], &a)) goto bad;
+        r.allow.push_back(std::move(a));
+      }
+      for (uint32_t k = 0; k < d.n_exclude_regexes; k++) {
+        auto re = compile_opt(d.exclude_regexes[k], &e);
+        if (!re) goto bad;
+        r.exclude.push_back(re);
+      }
+      if (r.regex && !r.secret_group_name.empty()) {
+        const auto& names = r.regex->SubexpNames();
+        for (size_t g = 0; g < names.size(); g++)
+          if (names[g] == r.secret_group_name) r.group_idx.push_back((int)g);
+      }
+      h->rs.rules.push_back(std::move(r));
+    }
+    for (uint32_t k = 0; k < n_allow_rules; k++) {
+      AllowRuleC a;
+      if (!allow_of(allow_rules[k], &a)) goto bad;
+      h->rs.allow.push_back(std::move(a));
+    }
+    for (uint32_t k = 0; k < n_exclude_regexes; k++) {
+      auto re = compile_opt(exclude_regexes[k], &e);
+      if (!re) goto bad;
+      h->rs.exclude.push_back(re);
+    }
+    {
+      PlanOptions po;
+      std::string pe;
+      h->plan = build_plan(h->rs, po, &pe);
+      if (!h->plan) {
+        copy_err(pe, err, err_len);
+        return fail(TSG_ERR_INTERNAL, pe);
+      }
+    }
+    *out = h.release();
+    return TSG_OK;
+  bad:
+    copy_err(e, err, err_len);
+    return fail(TSG_ERR_CONFIG, e);
+  } catch (const std::bad_alloc&) {
+    return fail(TSG_ERR_NOMEM, "out of memory");
+  } catch (const std::exception& ex) {
+    copy_err(ex.what(), err, err_len);
+    return fail(TSG_ERR_INTERNAL, ex.what());
+  }
+}
+
+void tsg_ruleset_destroy(tsg_ruleset* rs) { delete rs; }
+
+int tsg_ruleset_allow_path(const tsg_ruleset* rs, const char* path, size_t path_len) {
+  if (!rs || (!path && path_len)) return fail(TSG_ERR_ARG, "bad argument");
+  return rs->rs.AllowPath(std::string(path ? path : "", path_len)) ? 1 : 0;
+}
+
+int tsg_ruleset_get_info(const tsg_ruleset* rs, tsg_ruleset_info* o) {
+  if (!rs || !o) return fail(TSG_ERR_ARG, "bad argument");
+  const Plan& p = *rs->plan;
+  std::memset(o, 0, sizeof(*o));
+  o->n_rules = (uint32_t)rs->rs.rules.size();
+  o->n_keywords = (uint32_t)p.n_kw;
+  o->n_groups = (uint32_t)p.groups.size();
+  for (uint8_t h : p.rule_hostonly) o->n_hostonly += h;
+  o->kw_states = (uint32_t)p.kw_dfa->nstates;
+  uint64_t tb = (uint64_t)p.kw_dfa->nstates * p.kw_dfa->nclasses * 2;
+  for (const auto& g : p.groups) {
+    o->max_group_states = std::max<uint32_t>(o->max_group_states, (uint32_t)g.dfa->nstates);
+    tb += (uint64_t)g.dfa->nstates * g.dfa->nclasses * 2;
+  }
+  o->table_bytes = tb;
+  return TSG_OK;
+}
+
+int tsg_scan_cpu(const tsg_ruleset* rs, const char* path, size_t path_len, const uint8_t* content,
+                 size_t len, tsg_result** out) {
+  if (!rs || !out || (!content && len) || (!path && path_len)) return fail(TSG_ERR_ARG, "bad argument");
+  try {
+    FileResult fr;
+    scan_file(rs->rs, std::string(path ? path : "", path_len), content, len, nullptr, &fr);
+    auto r = std::make_unique<tsg_result>();
+    serialize_results({fr}, &r->buf);
+    *out = r.release();
+    return TSG_OK;
+  } catch (const std::bad_alloc&) {
+    return fail(TSG_ERR_NOMEM, "out of memory");
+  } catch (const std::exception& ex) {
+    return fail(TSG_ERR_INTERNAL, ex.what());
+  }
+}
+
+int tsg_scan_cpu_batch(const tsg_ruleset* rs, const uint8_t* data, const uint64_t* offsets,
+                       uint32_t nfiles, const char* paths, const uint64_t* path_offsets,
+                       int nthreads, tsg_result** out) {
+  if (!rs || !out || !offsets || !path_offsets) return fail(TSG_ERR_ARG, "bad argument");
+  try {
+    BatchView b{data, offsets, nfiles, paths, path_offsets};
+    std::vector<FileResult> res;
+    scan_batch_cpu(rs->rs, b, hw_threads(nthreads), &res);
+    auto r = std::make_unique<tsg_result>();
+    serialize_results(res, &r->buf);
+    *out = r.release();
+    return TSG_OK;
+  } catch (const std::bad_alloc&) {
+    return fail(TSG_ERR_NOMEM, "out of memory");
+  } catch (const std::exception& ex) {
+    return fail(TSG_ERR_INTERNAL, ex.what());
+  }
+}
+
+int tsg_scan_batch_emulated(const tsg_ruleset* rs, const uint8_t* data, const uint64_t* offsets,
+                            uint32_t nfiles, const char* paths, const uint64_t* path_offsets,
+                            uint32_t chunk, tsg_result** out) {
+  if (!rs || !out || !offsets || !path_offsets || chunk == 0) return fail(TSG_ERR_ARG, "bad argument");
+  try {
+    BatchView b{data, offsets, nfiles, paths, path_offsets};
+    KernelOutput ko;
+    emulate_kernels(*rs->plan, b, chunk, 1u << 16, &ko);
+    std::vector<FileResult> res;
+    resolve_batch(rs->rs, *rs->plan, b, ko, hw_threads(0), &res);
+    auto r = std::make_unique<tsg_result>();
+    serialize_results(res, &r->buf);
+    *out = r.release();
+    return TSG_OK;
+  } catch (const std::bad_alloc&) {
+    return fail(TSG_ERR_NOMEM, "out of memory");
+  } catch (const std::exception& ex) {
+    return fail(TSG_ERR_INTERNAL, ex.what());
+  }
+}
+
+const uint8_t* tsg_result_data(const tsg_result* r, size_t* len) {
+  if (!r) {
+    if (len) *len = 0;
+    return nullptr;
+  }
+  if (len) *len = r->buf.size();
+  return (const uint8_t*)r->buf.data();
+}
+
+void tsg_result_free(tsg_result* r) { delete r; }
+
+// ---- test hooks
+struct tsg_regex {
+  std::shared_ptr<Regexp> re;
+};
+
+int tsg_regex_compile(const char* src, tsg_regex** out, char* err, size_t err_len) {
+  if (!src || !out) return fail(TSG_ERR_ARG, "bad argument");
+  std::string e;
+  auto re = Regexp::Compile(src, &e);
+  if (!re) {
+    copy_err(e, err, err_len);
+    return fail(TSG_ERR_CONFIG, e);
+  }
+  *out = new tsg_regex{re};
+  return TSG_OK;
+}
+
+void tsg_regex_free(tsg_regex* re) { delete re; }
+
+int tsg_regex_num_slots(const tsg_regex* re) { return re ? re->re->NumSlots() : TSG_ERR_ARG; }
+
+int tsg_regex_match(const tsg_regex* re, const uint8_t* text, size_t len) {
+  if (!re) return fail(TSG_ERR_ARG, "bad argument");
+  return re->re->Match(text, len) ? 1 : 0;
+}
+
+int64_t tsg_regex_find_all(const tsg_regex* re, const uint8_t* text, size_t len, int submatch,
+                           int64_t* out, size_t cap) {
+  if (!re) return fail(TSG_ERR_ARG, "bad argument");
+  std::vector<int64_t> v;
+  re->re->FindAll(text, len, submatch != 0, &v);
+  if (out) std::memcpy(out, v.data(), sizeof(int64_t) * std::min(cap, v.size()));
+  return (int64_t)v.size();
+}
+
+int64_t tsg_regex_dfa_ends(const tsg_regex* re, const uint8_t* text, size_t len, uint32_t chunk,
+                           int64_t* out, size_t cap) {
+  if (!re || chunk == 0) return fail(TSG_ERR_ARG, "bad argument");
+  DFAOptions o;
+  o.max_states = 1 << 16;
+  std::string e;
+  auto d = build_dfa({&re->re->prog()}, o, &e);
+  if (!d) return fail(TSG_ERR_INTERNAL, e);
+  // one "group" with one rule, chunked exactly like the kernels
+  Plan p;
+  p.n_kw = 0;
+  p.kw_words = 1;
+  p.fb_kw0 = 0;
+  p.kw_dfa = build_keyword_dfa({}, o, &e);
+  GroupPlan g;
+  g.dfa = std::move(d);
+  g.rules = {0};
+  g.always = true;
+  g.kwmask = {0};
+  p.groups.push_back(std::move(g));
+  uint64_t offs[2] = {0, len};
+  uint64_t poffs[2] = {0, 0};
+  BatchView b{text, offs, 1, "", poffs};
+  KernelOutput ko;
+  emulate_kernels(p, b, chunk, 1u << 30, &ko);
+  std::vector<int64_t> ends;
+  for (const auto& c : ko.cand) ends.push_back(c.end);
+  std::sort(ends.begin(), ends.end());
+  ends.erase(std::unique(ends.begin(), ends.end()), ends.end());
+  if (out) std::memcpy(out, ends.data(), sizeof(int64_t) * std::min(cap, ends.size()));
+  return (int64_t)ends.size();
+}
+
+}  // extern "C"

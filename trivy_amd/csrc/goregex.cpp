@@ -1,0 +1,1259 @@
+// Go 1.19 regexp dialect: parser, compiler and Pike VM.  See goregex.hpp.
+#include "goregex.hpp"
+
+#include <algorithm>
+#include <cstring>
+
+namespace tsg {
+
+#include "unicode_tables.inc"
+
+// ------------------------------------------------------------------ unicode helpers
+int32_t decode_rune(const uint8_t* b, size_t n, size_t pos, int* width) {
+  if (pos >= n) {
+    *width = 0;
+    return kEOT;
+  }
+  uint8_t c0 = b[pos];
+  if (c0 < 0x80) {
+    *width = 1;
+    return c0;
+  }
+  auto cont = [&](size_t k, uint8_t lo, uint8_t hi) {
+    return pos + k < n && b[pos + k] >= lo && b[pos + k] <= hi;
+  };
+  if (c0 >= 0xC2 && c0 <= 0xDF) {
+    if (cont(1, 0x80, 0xBF)) {
+      *width = 2;
+      return ((c0 & 0x1F) << 6) | (b[pos + 1] & 0x3F);
+    }
+  } else if (c0 >= 0xE0 && c0 <= 0xEF) {
+    uint8_t lo = c0 == 0xE0 ? 0xA0 : 0x80, hi = c0 == 0xED ? 0x9F : 0xBF;
+    if (cont(1, lo, hi) && cont(2, 0x80, 0xBF)) {
+      *width = 3;
+      return ((c0 & 0x0F) << 12) | ((b[pos + 1] & 0x3F) << 6) | (b[pos + 2] & 0x3F);
+    }
+  } else if (c0 >= 0xF0 && c0 <= 0xF4) {
+    uint8_t lo = c0 == 0xF0 ? 0x90 : 0x80, hi = c0 == 0xF4 ? 0x8F : 0xBF;
+    if (cont(1, lo, hi) && cont(2, 0x80, 0xBF) && cont(3, 0x80, 0xBF)) {
+      *width = 4;
+      return ((c0 & 0x07) << 18) | ((b[pos + 1] & 0x3F) << 12) | ((b[pos + 2] & 0x3F) << 6) |
+             (b[pos + 3] & 0x3F);
+    }
+  }
+  *width = 1;
+  return kRuneError;
+}
+
+static const RunePair* find_pair(const RunePair* t, size_t n, int32_t r) {
+  size_t lo = 0, hi = n;
+  while (lo < hi) {
+    size_t m = (lo + hi) / 2;
+    if (t[m].a < r) lo = m + 1;
+    else hi = m;
+  }
+  return (lo < n && t[lo].a == r) ? &t[lo] : nullptr;
+}
+
+void fold_orbit(int32_t r, std::vector<int32_t>* out) {
+  out->clear();
+  out->push_back(r);
+  const size_t n = sizeof(kFoldNext) / sizeof(kFoldNext[0]);
+  const RunePair* p = find_pair(kFoldNext, n, r);
+  if (!p) return;
+  int32_t x = p->b;
+  while (x != r) {
+    out->push_back(x);
+    x = find_pair(kFoldNext, n, x)->b;
+  }
+  std::sort(out->begin(), out->end());
+}
+
+int32_t simple_lower(int32_t r) {
+  if (r < 0x80) return (r >= 'A' && r <= 'Z') ? r + 32 : r;
+  const RunePair* p = find_pair(kLower, sizeof(kLower) / sizeof(kLower[0]), r);
+  return p ? p->b : r;
+}
+
+static void append_utf8(int32_t r, std::string* out) {
+  if (r < 0 || r > kMaxRune || (r >= 0xD800 && r <= 0xDFFF)) r = kRuneError;
+  if (r < 0x80) {
+    out->push_back((char)r);
+  } else if (r < 0x800) {
+    out->push_back((char)(0xC0 | (r >> 6)));
+    out->push_back((char)(0x80 | (r & 0x3F)));
+  } else if (r < 0x10000) {
+    out->push_back((char)(0xE0 | (r >> 12)));
+    out->push_back((char)(0x80 | ((r >> 6) & 0x3F)));
+    out->push_back((char)(0x80 | (r & 0x3F)));
+  } else {
+    out->push_back((char)(0xF0 | (r >> 18)));
+    out->push_back((char)(0x80 | ((r >> 12) & 0x3F)));
+    out->push_back((char)(0x80 | ((r >> 6) & 0x3F)));
+    out->push_back((char)(0x80 | (r & 0x3F)));
+  }
+}
+
+void go_to_lower(const uint8_t* b, size_t n, std::string* out) {
+  out->clear();
+  bool ascii = true;
+  for (size_t i = 0; i < n; i++)
+    if (b[i] >= 0x80) {
+      ascii = false;
+      break;
+    }
+  if (ascii) {
+    out->resize(n);
+    for (size_t i = 0; i < n; i++) {
+      uint8_t c = b[i];
+      (*out)[i] = (char)((c >= 'A' && c <= 'Z') ? c + 32 : c);
+    }
+    return;
+  }
+  out->reserve(n);
+  size_t i = 0;
+  while (i < n) {
+    int w;
+    int32_t r = decode_rune(b, n, i, &w);
+    append_utf8(simple_lower(r), out);
+    i += w;
+  }
+}
+
+bool empty_ok(uint32_t op, int32_t r1, int32_t r2) {
+  if (op == 0) return true;
+  if (op & kBeginLine) {
+    if (r1 != '\n' && r1 >= 0) return false;
+    op &= ~kBeginLine;
+  }
+  if (op & kBeginText) {
+    if (r1 >= 0) return false;
+    op &= ~kBeginText;
+  }
+  if (op == 0) return true;
+  if (op & kEndLine) {
+    if (r2 != '\n' && r2 >= 0) return false;
+    op &= ~kEndLine;
+  }
+  if (op & kEndText) {
+    if (r2 >= 0) return false;
+    op &= ~kEndText;
+  }
+  if (op == 0) return true;
+  if (is_word_byte(r1) != is_word_byte(r2)) op &= ~kWordBoundary;
+  else op &= ~kNoWordBoundary;
+  return op == 0;
+}
+
+// ------------------------------------------------------------------ ranges
+static Ranges clean(Ranges r) {
+  std::sort(r.begin(), r.end());
+  Ranges out;
+  for (auto& p : r) {
+    if (!out.empty() && (int64_t)p.first <= (int64_t)out.back().second + 1) {
+      if (p.second > out.back().second) out.back().second = p.second;
+    } else {
+      out.push_back(p);
+    }
+  }
+  return out;
+}
+
+static Ranges negate(const Ranges& in) {
+  Ranges r = clean(in), out;
+  int32_t next = 0;
+  for (auto& p : r) {
+    if (p.first > next) out.push_back({next, p.first - 1});
+    next = p.second + 1;
+  }
+  if (next <= kMaxRune) out.push_back({next, kMaxRune});
+  return out;
+}
+
+// appendFoldedRange: every rune plus its SimpleFold orbit
+static Ranges fold(const Ranges& in) {
+  Ranges out = in;
+  const size_t n = sizeof(kFoldNext) / sizeof(kFoldNext[0]);
+  std::vector<int32_t> orb;
+  for (auto& p : in) {
+    // walk only the runes that have orbits
+    size_t lo = 0, hi = n;
+    while (lo < hi) {
+      size_t m = (lo + hi) / 2;
+      if (kFoldNext[m].a < p.first) lo = m + 1;
+      else hi = m;
+    }
+    for (size_t k = lo; k < n && kFoldNext[k].a <= p.second; k++) {
+      fold_orbit(kFoldNext[k].a, &orb);
+      for (int32_t x : orb) out.push_back({x, x});
+    }
+  }
+  return clean(out);
+}
+
+static const Ranges kPerlD = {{'0', '9'}};
+static const Ranges kPerlS = {{'\t', '\n'}, {'\f', '\r'}, {' ', ' '}};
+static const Ranges kPerlW = {{'0', '9'}, {'A', 'Z'}, {'_', '_'}, {'a', 'z'}};
+
+struct PosixEnt {
+  const char* name;
+  Ranges r;
+};
+static const std::vector<PosixEnt>& posix_classes() {
+  static const std::vector<PosixEnt> t = {
+      {"alnum", {{'0', '9'}, {'A', 'Z'}, {'a', 'z'}}},
+      {"alpha", {{'A', 'Z'}, {'a', 'z'}}},
+      {"ascii", {{0, 0x7F}}},
+      {"blank", {{'\t', '\t'}, {' ', ' '}}},
+      {"cntrl", {{0, 0x1F}, {0x7F, 0x7F}}},
+      {"digit", {{'0', '9'}}},
+      {"graph", {{'!', '~'}}},
+      {"lower", {{'a', 'z'}}},
+      {"print", {{' ', '~'}}},
+      {"punct", {{'!', '/'}, {':', '@'}, {'[', '`'}, {'{', '~'}}},
+      {"space", {{'\t', '\r'}, {' ', ' '}}},
+      {"upper", {{'A', 'Z'}}},
+      {"word", {{'0', '9'}, {'A', 'Z'}, {'_', '_'}, {'a', 'z'}}},
+      {"xdigit", {{'0', '9'}, {'A', 'F'}, {'a', 'f'}}},
+  };
+  return t;
+}
+
+// ------------------------------------------------------------------ AST
+enum class NK : uint8_t {
+  Empty, NoMatch, Rune, BOT, EOT, BOL, EOL, WB, NWB, Cap, Cat, Alt, Star, Plus, Quest, Repeat
+};
+
+struct Node {
+  NK k = NK::Empty;
+  bool greedy = true;
+  int cap = 0, min = 0, max = 0;
+  Ranges r;
+  std::vector<int> sub;
+};
+
+enum : int { FOLD = 1, DOTNL = 2, ONELINE = 4, NONGREEDY = 8 };
+
+struct ParseError {
+  std::string msg;
+};
+
+class Parser {
+ public:
+  explicit Parser(const std::string& s) : s_(s) {}
+
+  int parse() {
+    int n = parse_alt();
+    if (i_ != s_.size()) fail("unexpected )");
+    return n;
+  }
+
+  std::vector<Node> nodes;
+  std::vector<std::string> names{""};
+  int ncap = 0;
+
+ private:
+  const std::string& s_;
+  size_t i_ = 0;
+  int flags_ = ONELINE;  // Perl: ClassNL|OneLine|PerlX|UnicodeGroups
+
+  [[noreturn]] void fail(const std::string& m) {
+    throw ParseError{"error parsing regexp: " + m + ": `" + s_ + "`"};
+  }
+  int peek(size_t k = 0) const { return i_ + k < s_.size() ? (uint8_t)s_[i_ + k] : -1; }
+
+  // next source rune (patterns are UTF-8)
+  int32_t next_rune() {
+    int w;
+    int32_t r = decode_rune((const uint8_t*)s_.data(), s_.size(), i_, &w);
+    if (r == kRuneError && w == 1) fail("invalid UTF-8");
+    i_ += w;
+    return r;
+  }
+
+  int add(Node n) {
+    nodes.push_back(std::move(n));
+    return (int)nodes.size() - 1;
+  }
+  int leaf(NK k) {
+    Node n;
+    n.k = k;
+    return add(std::move(n));
+  }
+  int rune_node(Ranges r) {
+    Node n;
+    n.k = NK::Rune;
+    n.r = std::move(r);
+    return add(std::move(n));
+  }
+  int literal(int32_t r) {
+    if (flags_ & FOLD) {
+      std::vector<int32_t> orb;
+      fold_orbit(r, &orb);
+      Ranges rs;
+      for (int32_t x : orb) rs.push_back({x, x});
+      return rune_node(clean(rs));
+    }
+    return rune_node({{r, r}});
+  }
+
+  int parse_alt() {
+    std::vector<int> alts{parse_concat()};
+    while (peek() == '|') {
+      i_++;
+      alts.push_back(parse_concat());
+    }
+    if (alts.size() == 1) return alts[0];
+    Node n;
+    n.k = NK::Alt;
+    n.sub = alts;
+    return add(std::move(n));
+  }
+
+  int parse_concat() {
+    std::vector<int> items;
+    while (true) {
+      int c = peek();
+      if (c < 0 || c == '|' || c == ')') break;
+      int a = parse_atom();
+      if (a < 0) continue;
+      items.push_back(parse_repeat(a));
+    }
+    if (items.empty()) return leaf(NK::Empty);
+    if (items.size() == 1) return items[0];
+    Node n;
+    n.k = NK::Cat;
+    n.sub = items;
+    return add(std::move(n));
+  }
+
+  bool try_braces(int* lo, int* hi) {
+    size_t j = i_ + 1;
+    auto digits = [&](size_t k) {
+      while (k < s_.size() && s_[k] >= '0' && s_[k] <= '9') k++;
+      return k;
+    };
+    size_t k = digits(j);
+    if (k == j) return false;
+    long long a = std::stoll(s_.substr(j, std::min<size_t>(k - j, 9)));
+    if (k - j > 9) a = 100000;
+    long long b = a;
+    j = k;
+    if (j < s_.size() && s_[j] == ',') {
+      j++;
+      if (j < s_.size() && s_[j] == '}') {
+        b = -1;
+      } else {
+        k = digits(j);
+        if (k == j) return false;
+        b = std::stoll(s_.substr(j, std::min<size_t>(k - j, 9)));
+        if (k - j > 9) b = 100000;
+        j = k;
+      }
+    }
+    if (j >= s_.size() || s_[j] != '}') return false;
+    i_ = j + 1;
+    if (a > 1000 || b > 1000 || (b >= 0 && b < a)) fail("invalid repeat count");
+    *lo = (int)a;
+    *hi = (int)b;
+    return true;
+  }
+
+  int parse_repeat(int atom) {
+    bool last_rep = false;
+    size_t rep_start = 0;
+    while (true) {
+      int c = peek();
+      size_t start = i_;
+      int lo, hi;
+      NK k;
+      if (c == '*') {
+        i_++;
+        k = NK::Star;
+        lo = 0;
+        hi = -1;
+      } else if (c == '+') {
+        i_++;
+        k = NK::Plus;
+        lo = 1;
+        hi = -1;
+      } else if (c == '?') {
+        i_++;
+        k = NK::Quest;
+        lo = 0;
+        hi = 1;
+      } else if (c == '{') {
+        if (!try_braces(&lo, &hi)) return atom;
+        k = NK::Repeat;
+      } else {
+        return atom;
+      }
+      if (last_rep)
+        fail("invalid nested repetition operator: `" + s_.substr(rep_start, i_ - rep_start) + "`");
+      bool greedy = true;
+      if (peek() == '?') {
+        i_++;
+        greedy = false;
+      }
+      if (flags_ & NONGREEDY) greedy = !greedy;
+      Node n;
+      n.k = k;
+      n.min = lo;
+      n.max = hi;
+      n.greedy = greedy;
+      n.sub = {atom};
+      atom = add(std::move(n));
+      last_rep = true;
+      rep_start = start;
+    }
+  }
+
+  int parse_atom() {
+    int c = peek();
+    if (c == '(') return parse_group();
+    if (c == '[') return rune_node(parse_class());
+    if (c == '*' || c == '+' || c == '?')
+      fail(std::string("missing argument to repetition operator: `") + (char)c + "`");
+    if (c == '{') {
+      size_t save = i_;
+      int lo, hi;
+      if (try_braces(&lo, &hi)) fail("missing argument to repetition operator: `" + s_.substr(save, i_ - save) + "`");
+    }
+    if (c == '.') {
+      i_++;
+      if (flags_ & DOTNL) return rune_node({{0, kMaxRune}});
+      return rune_node({{0, '\n' - 1}, {'\n' + 1, kMaxRune}});
+    }
+    if (c == '^') {
+      i_++;
+      return leaf((flags_ & ONELINE) ? NK::BOT : NK::BOL);
+    }
+    if (c == '$') {
+      i_++;
+      return leaf((flags_ & ONELINE) ? NK::EOT : NK::EOL);
+    }
+    if (c == '\\') return parse_backslash();
+    return literal(next_rune());
+  }
+
+  void close() {
+    if (peek() != ')') fail("missing closing )");
+    i_++;
+  }
+
+  int parse_group() {
+    i_++;
+    int saved = flags_;
+    if (s_.compare(i_, 3, "?P=") == 0) fail("invalid named capture");
+    if (s_.compare(i_, 3, "?P<") == 0) {
+      size_t end = s_.find('>', i_);
+      if (end == std::string::npos) fail("invalid named capture");
+      std::string name = s_.substr(i_ + 3, end - i_ - 3);
+      bool ok = !name.empty();
+      for (char ch : name)
+        if (!(isalnum((unsigned char)ch) || ch == '_')) ok = false;
+      if (!ok) fail("invalid named capture: `" + s_.substr(i_ - 1, end - i_ + 2) + "`");
+      i_ = end + 1;
+      int idx = ++ncap;
+      names.push_back(name);
+      int sub = parse_alt();
+      close();
+      flags_ = saved;
+      Node n;
+      n.k = NK::Cap;
+      n.cap = idx;
+      n.sub = {sub};
+      return add(std::move(n));
+    }
+    if (peek() == '?') {
+      size_t j = i_ + 1;
+      bool neg = false, sawflag = false;
+      int fl = flags_;
+      char ch = 0;
+      while (true) {
+        if (j >= s_.size()) fail("missing closing )");
+        ch = s_[j];
+        if (ch == 'i') {
+          fl = neg ? (fl & ~FOLD) : (fl | FOLD);
+          sawflag = true;
+        } else if (ch == 'm') {
+          fl = neg ? (fl | ONELINE) : (fl & ~ONELINE);
+          sawflag = true;
+        } else if (ch == 's') {
+          fl = neg ? (fl & ~DOTNL) : (fl | DOTNL);
+          sawflag = true;
+        } else if (ch == 'U') {
+          fl = neg ? (fl & ~NONGREEDY) : (fl | NONGREEDY);
+          sawflag = true;
+        } else if (ch == '-') {
+          if (neg) fail("invalid or unsupported Perl syntax");
+          neg = true;
+          sawflag = false;
+        } else if (ch == ')' || ch == ':') {
+          bool empty_flags = (j == i_ + 1);
+          if ((neg && !sawflag) || (empty_flags && ch == ')'))
+            fail("invalid or unsupported Perl syntax");
+          break;
+        } else {
+          fail("invalid or unsupported Perl syntax");
+        }
+        j++;
+      }
+      i_ = j + 1;
+      flags_ = fl;
+      if (ch == ')') return -1;  // flags persist to the end of the enclosing group
+      int sub = parse_alt();
+      close();
+      flags_ = saved;
+      return sub;
+    }
+    int idx = ++ncap;
+    names.push_back("");
+    int sub = parse_alt();
+    close();
+    flags_ = saved;
+    Node n;
+    n.k = NK::Cap;
+    n.cap = idx;
+    n.sub = {sub};
+    return add(std::move(n));
+  }
+
+  Ranges perl_group(char ch) {
+    char lc = (char)tolower(ch);
+    Ranges base = lc == 'd' ? kPerlD : lc == 's' ? kPerlS : kPerlW;
+    if (flags_ & FOLD) base = fold(base);
+    return isupper((unsigned char)ch) ? negate(base) : clean(base);
+  }
+
+  Ranges unicode_class() {
+    bool neg = s_[i_ + 1] == 'P';
+    size_t j = i_ + 2;
+    if (j >= s_.size()) fail("invalid character class range");
+    std::string name;
+    if (s_[j] == '{') {
+      size_t end = s_.find('}', j);
+      if (end == std::string::npos) fail("invalid character class range");
+      name = s_.substr(j + 1, end - j - 1);
+      i_ = end + 1;
+    } else {
+      i_ = j;
+      int32_t r = next_rune();
+      std::string t;
+      append_utf8(r, &t);
+      name = t;
+    }
+    if (!name.empty() && name[0] == '^') {
+      neg = !neg;
+      name = name.substr(1);
+    }
+    Ranges rs;
+    if (name == "Any") {
+      rs = {{0, kMaxRune}};
+    } else {
+      bool found = false;
+      for (const auto& c : kCats) {
+        if (name == c.name) {
+          for (int k = 0; k < c.n; k++) rs.push_back({c.r[k].a, c.r[k].b});
+          found = true;
+        }
+      }
+      if (!found) fail("invalid character class range: `\\p{" + name + "}`");
+    }
+    if (flags_ & FOLD) rs = fold(rs);
+    return neg ? negate(rs) : clean(rs);
+  }
+
+  int parse_backslash() {
+    int nx = peek(1);
+    if (nx < 0) fail("trailing backslash at end of expression");
+    switch (nx) {
+      case 'A': i_ += 2; return leaf(NK::BOT);
+      case 'z': i_ += 2; return leaf(NK::EOT);
+      case 'b': i_ += 2; return leaf(NK::WB);
+      case 'B': i_ += 2; return leaf(NK::NWB);
+      case 'Q': {
+        size_t end = s_.find("\\E", i_ + 2);
+        std::string lit = end == std::string::npos ? s_.substr(i_ + 2) : s_.substr(i_ + 2, end - i_ - 2);
+        i_ = end == std::string::npos ? s_.size() : end + 2;
+        std::vector<int> items;
+        size_t k = 0;
+        while (k < lit.size()) {
+          int w;
+          int32_t r = decode_rune((const uint8_t*)lit.data(), lit.size(), k, &w);
+          k += w;
+          items.push_back(literal(r));
+        }
+        if (items.empty()) return -1;
+        if (items.size() == 1) return items[0];
+        Node n;
+        n.k = NK::Cat;
+        n.sub = items;
+        return add(std::move(n));
+      }
+      case 'p':
+      case 'P':
+        return rune_node(unicode_class());
+      case 'd': case 'D': case 's': case 'S': case 'w': case 'W':
+        i_ += 2;
+        return rune_node(perl_group((char)nx));
+      default:
+        return literal(parse_escape());
+    }
+  }
+
+  int32_t parse_escape() {
+    i_++;  // backslash
+    if (i_ >= s_.size()) fail("trailing backslash at end of expression");
+    int32_t c = next_rune();
+    if (c >= '1' && c <= '7') {
+      int d = peek();
+      if (!(d >= '0' && d <= '7')) fail("invalid escape sequence: `\\" + std::string(1, (char)c) + "`");
+    }
+    if (c >= '0' && c <= '7') {
+      int32_t r = c - '0';
+      for (int k = 0; k < 2; k++) {
+        int d = peek();
+        if (d >= '0' && d <= '7') {
+          r = r * 8 + (d - '0');
+          i_++;
+        } else {
+          break;
+        }
+      }
+      return r;
+    }
+    if (c == 'x') {
+      auto hexv = [](int ch) {
+        if (ch >= '0' && ch <= '9') return ch - '0';
+        if (ch >= 'a' && ch <= 'f') return ch - 'a' + 10;
+        if (ch >= 'A' && ch <= 'F') return ch - 'A' + 10;
+        return -1;
+      };
+      if (peek() == '{') {
+        size_t j = i_ + 1;
+        int64_t r = 0;
+        int nd = 0;
+        while (j < s_.size() && hexv((uint8_t)s_[j]) >= 0) {
+          r = r * 16 + hexv((uint8_t)s_[j]);
+          if (r > kMaxRune) fail("invalid escape sequence");
+          j++;
+          nd++;
+        }
+        if (nd == 0 || j >= s_.size() || s_[j] != '}') fail("invalid escape sequence");
+        i_ = j + 1;
+        return (int32_t)r;
+      }
+      int h1 = hexv(peek()), h2 = hexv(peek(1));
+      if (h1 < 0 || h2 < 0) fail("invalid escape sequence");
+      i_ += 2;
+      return h1 * 16 + h2;
+    }
+    switch (c) {
+      case 'a': return 7;
+      case 'f': return 12;
+      case 'n': return 10;
+      case 'r': return 13;
+      case 't': return 9;
+      case 'v': return 11;
+    }
+    if (c < 0x80 && !isalnum(c)) return c;
+    std::string t;
+    append_utf8(c, &t);
+    fail("invalid escape sequence: `\\" + t + "`");
+  }
+
+  Ranges parse_class() {
+    i_++;
+    bool neg = false;
+    if (peek() == '^') {
+      neg = true;
+      i_++;
+    }
+    Ranges rs;
+    bool first = true;
+    while (peek() != ']' || first) {
+      if (peek() < 0) fail("missing closing ]");
+      first = false;
+      if (peek() == '[' && peek(1) == ':') {
+        size_t end = s_.find(":]", i_ + 2);
+        if (end != std::string::npos) {
+          std::string name = s_.substr(i_ + 2, end - i_ - 2);
+          bool pneg = !name.empty() && name[0] == '^';
+          if (pneg) name = name.substr(1);
+          const Ranges* base = nullptr;
+          for (const auto& e : posix_classes())
+            if (name == e.name) base = &e.r;
+          if (!base) fail("invalid character class range: `[:" + name + ":]`");
+          Ranges r2 = *base;
+          if (flags_ & FOLD) r2 = fold(r2);
+          if (pneg) r2 = negate(r2);
+          rs.insert(rs.end(), r2.begin(), r2.end());
+          i_ = end + 2;
+          continue;
+        }
+      }
+      if (peek() == '\\' && (peek(1) == 'p' || peek(1) == 'P')) {
+        Ranges r2 = unicode_class();
+        rs.insert(rs.end(), r2.begin(), r2.end());
+        continue;
+      }
+      if (peek() == '\\' && peek(1) >= 0 && strchr("dDsSwW", peek(1))) {
+        Ranges r2 = perl_group((char)peek(1));
+        rs.insert(rs.end(), r2.begin(), r2.end());
+        i_ += 2;
+        continue;
+      }
+      int32_t lo = class_char(), hi = lo;
+      if (peek() == '-' && peek(1) >= 0 && peek(1) != ']') {
+        i_++;
+        hi = class_char();
+        if (hi < lo) fail("invalid character class range");
+      }
+      if (flags_ & FOLD) {
+        Ranges r2 = fold({{lo, hi}});
+        rs.insert(rs.end(), r2.begin(), r2.end());
+      } else {
+        rs.push_back({lo, hi});
+      }
+    }
+    i_++;
+    rs = clean(rs);
+    return neg ? negate(rs) : rs;
+  }
+
+  int32_t class_char() {
+    if (peek() < 0) fail("missing closing ]");
+    if (peek() == '\\') return parse_escape();
+    return next_rune();
+  }
+};
+
+// ------------------------------------------------------------------ compiler
+namespace {
+
+struct Frag {
+  uint32_t i = 0;
+  std::vector<uint32_t> out;  // patch list: inst << 1 | (1 = arg)
+  bool nullable = false;
+};
+
+class Compiler {
+ public:
+  // relax >= 0: GPU superset program -- every counted repetition x{n,m} whose bounds
+  // exceed `relax` becomes x{min(n,relax),} (see Regexp::RelaxedProg)
+  Compiler(const std::vector<Node>& nodes, Prog* p, int relax = -1)
+      : n_(nodes), p_(p), relax_(relax) {
+    p_->inst.push_back(Inst{Op::Fail, 0, 0});
+  }
+
+  Frag compile(int idx) {
+    const Node& nd = n_[idx];
+    switch (nd.k) {
+      case NK::NoMatch: return Frag{};
+      case NK::Empty: return nop();
+      case NK::Rune: return rune(nd.r);
+      case NK::BOT: return empty(kBeginText);
+      case NK::EOT: return empty(kEndText);
+      case NK::BOL: return empty(kBeginLine);
+      case NK::EOL: return empty(kEndLine);
+      case NK::WB: return empty(kWordBoundary);
+      case NK::NWB: return empty(kNoWordBoundary);
+      case NK::Cap: {
+        Frag bra = cap((uint32_t)nd.cap * 2);
+        Frag sub = compile(nd.sub[0]);
+        Frag ket = cap((uint32_t)nd.cap * 2 + 1);
+        return cat(cat(bra, sub), ket);
+      }
+      case NK::Cat: {
+        Frag f;
+        bool firstf = true;
+        for (int s : nd.sub) {
+          if (firstf) {
+            f = compile(s);
+            firstf = false;
+          } else {
+            f = cat(f, compile(s));
+          }
+        }
+        return firstf ? nop() : f;
+      }
+      case NK::Alt: {
+        Frag f;
+        for (int s : nd.sub) f = alt(f, compile(s));
+        return f;
+      }
+      case NK::Star:
+      case NK::Plus:
+      case NK::Quest:
+      case NK::Repeat:
+        return repeat(nd);
+    }
+    return Frag{};
+  }
+
+  Frag finish(int root) {
+    Frag f = compile(root);
+    uint32_t m = inst(Op::Match);
+    patch(f.out, m);
+    p_->start = f.i;
+    return f;
+  }
+
+ private:
+  const std::vector<Node>& n_;
+  Prog* p_;
+  int relax_;
+
+  uint32_t inst(Op op) {
+    p_->inst.push_back(Inst{op, 0, 0});
+    return (uint32_t)p_->inst.size() - 1;
+  }
+  void patch(const std::vector<uint32_t>& l, uint32_t v) {
+    for (uint32_t x : l) {
+      Inst& in = p_->inst[x >> 1];
+      if (x & 1) in.arg = v;
+      else in.out = v;
+    }
+  }
+  Frag nop() {
+    Frag f;
+    f.i = inst(Op::Nop);
+    f.out = {f.i << 1};
+    f.nullable = true;
+    return f;
+  }
+  Frag empty(uint32_t op) {
+    Frag f;
+    f.i = inst(Op::Empty);
+    p_->inst[f.i].arg = op;
+    f.out = {f.i << 1};
+    f.nullable = true;
+    return f;
+  }
+  Frag cap(uint32_t slot) {
+    Frag f;
+    f.i = inst(Op::Cap);
+    p_->inst[f.i].arg = slot;
+    f.out = {f.i << 1};
+    f.nullable = true;
+    if ((int)slot + 1 > p_->nslots) p_->nslots = (int)slot + 1;
+    return f;
+  }
+  Frag rune(const Ranges& r) {
+    Frag f;
+    f.i = inst(Op::Rune);
+    p_->runes.push_back(r);
+    p_->inst[f.i].arg = (uint32_t)p_->runes.size() - 1;
+    f.out = {f.i << 1};
+    f.nullable = false;
+    return f;
+  }
+  Frag cat(Frag f1, Frag f2) {
+    if (f1.i == 0 || f2.i == 0) return Frag{};
+    patch(f1.out, f2.i);
+    Frag f;
+    f.i = f1.i;
+    f.out = std::move(f2.out);
+    f.nullable = f1.nullable && f2.nullable;
+    return f;
+  }
+  Frag alt(Frag f1, Frag f2) {
+    if (f1.i == 0) return f2;
+    if (f2.i == 0) return f1;
+    Frag f;
+    f.i = inst(Op::Alt);
+    p_->inst[f.i].out = f1.i;
+    p_->inst[f.i].arg = f2.i;
+    f.out = std::move(f1.out);
+    f.out.insert(f.out.end(), f2.out.begin(), f2.out.end());
+    f.nullable = f1.nullable || f2.nullable;
+    return f;
+  }
+  Frag quest(Frag f1, bool nongreedy) {
+    Frag f;
+    f.i = inst(Op::Alt);
+    if (nongreedy) {
+      p_->inst[f.i].arg = f1.i;
+      f.out = {f.i << 1};
+    } else {
+      p_->inst[f.i].out = f1.i;
+      f.out = {(f.i << 1) | 1};
+    }
+    f.out.insert(f.out.end(), f1.out.begin(), f1.out.end());
+    f.nullable = true;
+    return f;
+  }
+  Frag loop(Frag f1, bool nongreedy) {
+    Frag f;
+    f.i = inst(Op::Alt);
+    if (nongreedy) {
+      p_->inst[f.i].arg = f1.i;
+      f.out = {f.i << 1};
+    } else {
+      p_->inst[f.i].out = f1.i;
+      f.out = {(f.i << 1) | 1};
+    }
+    patch(f1.out, f.i);
+    f.nullable = true;
+    return f;
+  }
+  Frag plus(Frag f1, bool nongreedy) {
+    Frag l = loop(f1, nongreedy);
+    Frag f;
+    f.i = f1.i;
+    f.out = std::move(l.out);
+    f.nullable = f1.nullable;
+    return f;
+  }
+  Frag star(Frag f1, bool nongreedy) {
+    if (f1.nullable) return quest(plus(f1, nongreedy), nongreedy);  // golang.org/issue/46123
+    return loop(f1, nongreedy);
+  }
+
+  bool is_empty_match(int idx) const { return n_[idx].k == NK::Empty; }
+
+  // regexp/syntax Simplify of star/plus/quest/repeat, then compile
+  Frag repeat(const Node& nd) {
+    int sub = nd.sub[0];
+    bool ng = !nd.greedy;
+    NK k = nd.k;
+    int lo = nd.min, hi = nd.max;
+    if (k == NK::Repeat && relax_ >= 0 && (hi == -1 || hi > relax_)) {
+      lo = std::min(lo, relax_);
+      hi = -1;
+    }
+    if (k == NK::Repeat) {
+      if (lo == 0 && hi == 0) return nop();
+      if (hi == -1) {
+        if (lo == 0) k = NK::Star;
+        else if (lo == 1) k = NK::Plus;
+      } else if (lo == 1 && hi == 1) {
+        return compile(sub);
+      }
+    }
+    // simplify1: op of an empty match is the empty match; x** -> x*
+    if (k != NK::Repeat) {
+      if (is_empty_match(sub)) return nop();
+      const Node& s = n_[sub];
+      if (s.k == k && s.greedy == nd.greedy) return compile(sub);
+      if (k == NK::Star) return star(compile(sub), ng);
+      if (k == NK::Plus) return plus(compile(sub), ng);
+      return quest(compile(sub), ng);
+    }
+    if (is_empty_match(sub)) return nop();
+    if (hi == -1) {  // x{n,} = x^(n-1) x+
+      Frag f;
+      bool firstf = true;
+      for (int i = 0; i < lo - 1; i++) {
+        Frag c = compile(sub);
+        f = firstf ? c : cat(f, c);
+        firstf = false;
+      }
+      Frag p = simplified_plus(sub, ng, nd.greedy);
+      return firstf ? p : cat(f, p);
+    }
+    // x{n,m} = x^n (x(x(x)?)?)?  -- suffix built inside-out
+    Frag f;
+    bool firstf = true;
+    for (int i = 0; i < lo; i++) {
+      Frag c = compile(sub);
+      f = firstf ? c : cat(f, c);
+      firstf = false;
+    }
+    if (hi > lo) {
+      Frag suffix = suffix_chain(sub, hi - lo, ng, nd.greedy);
+      f = firstf ? suffix : cat(f, suffix);
+      firstf = false;
+    }
+    return f;
+  }
+
+  Frag simplified_plus(int sub, bool ng, bool greedy) {
+    const Node& s = n_[sub];
+    if (s.k == NK::Plus && s.greedy == greedy) return compile(sub);
+    return plus(compile(sub), ng);
+  }
+
+  // depth copies nested: (x(x(x)?)?)?  (depth = m - n)
+  Frag suffix_chain(int sub, int depth, bool ng, bool greedy) {
+    if (depth == 1) {
+      const Node& s = n_[sub];
+      if (s.k == NK::Quest && s.greedy == greedy) return compile(sub);
+      return quest(compile(sub), ng);
+    }
+    Frag x = compile(sub);
+    Frag rest = suffix_chain(sub, depth - 1, ng, greedy);
+    return quest(cat(x, rest), ng);
+  }
+};
+
+}  // namespace
+
+struct Regexp::Ast {
+  std::vector<Node> nodes;
+  int root = 0;
+  int ncap = 0;
+};
+
+Regexp::Regexp() = default;
+Regexp::~Regexp() = default;
+
+std::shared_ptr<Regexp> Regexp::Compile(const std::string& src, std::string* err) {
+  auto re = std::make_shared<Regexp>();
+  try {
+    Parser p(src);
+    int root = p.parse();
+    re->src_ = src;
+    re->names_ = p.names;
+    re->prog_.nslots = 2 * (p.ncap + 1);
+    Compiler c(p.nodes, &re->prog_);
+    c.finish(root);
+    re->prog_.nslots = 2 * (p.ncap + 1);
+    re->ast_ = std::make_shared<Ast>();
+    re->ast_->nodes = std::move(p.nodes);
+    re->ast_->root = root;
+    re->ast_->ncap = p.ncap;
+  } catch (const ParseError& e) {
+    if (err) *err = e.msg;
+    return nullptr;
+  }
+  return re;
+}
+
+Prog Regexp::RelaxedProg(int k) const {
+  Prog p;
+  p.nslots = 2 * (ast_->ncap + 1);
+  Compiler c(ast_->nodes, &p, k);
+  c.finish(ast_->root);
+  p.nslots = 2 * (ast_->ncap + 1);
+  return p;
+}
+
+// ------------------------------------------------------------------ Pike VM
+namespace {
+
+inline bool rune_in(const Ranges& r, int32_t c) {
+  if (c < 0) return false;
+  if (r.size() <= 8) {
+    for (auto& p : r) {
+      if (c < p.first) return false;
+      if (c <= p.second) return true;
+    }
+    return false;
+  }
+  size_t lo = 0, hi = r.size();
+  while (lo < hi) {
+    size_t m = (lo + hi) / 2;
+    if (r[m].second < c) lo = m + 1;
+    else hi = m;
+  }
+  return lo < r.size() && r[lo].first <= c;
+}
+
+struct Queue {
+  std::vector<uint32_t> sparse;
+  std::vector<std::pair<uint32_t, int>> dense;  // pc, thread (-1 = none)
+  explicit Queue(size_t n) : sparse(n, 0) { dense.reserve(n); }
+  bool contains(uint32_t pc) const {
+    uint32_t j = sparse[pc];
+    return j < dense.size() && dense[j].first == pc;
+  }
+};
+
+class Machine {
+ public:
+  Machine(const Prog& p, int nslots) : p_(p), ns_(nslots), q0_(p.inst.size()), q1_(p.inst.size()) {
+    matchcap_.assign(ns_ > 0 ? ns_ : 1, -1);
+  }
+
+  bool run(const uint8_t* b, size_t n, int64_t pos, int64_t start_hi) {
+    matched_ = false;
+    std::fill(matchcap_.begin(), matchcap_.end(), -1);
+    Queue* runq = &q0_;
+    Queue* nextq = &q1_;
+    int w, w1 = 0;
+    int32_t r = decode_rune(b, n, (size_t)pos, &w), r1 = kEOT;
+    if (r != kEOT) r1 = decode_rune(b, n, (size_t)pos + w, &w1);
+    int32_t fr1, fr2;  // flag (before, after)
+    if (pos == 0) {
+      fr1 = kEOT;
+      fr2 = r;
+    } else {
+      fr1 = b[pos - 1];  // only word/newline-ness matters: any byte >= 0x80 is a non-word rune
+      fr2 = r;
+    }
+    while (true) {
+      if (runq->dense.empty()) {
+        if (matched_) break;
+        if (pos > start_hi) break;
+      }
+      if (!matched_ && pos <= start_hi) {
+        if (ns_ > 0) matchcap_[0] = pos;
+        add2(*runq, p_.start, pos, -2, fr1, fr2, -1);
+      }
+      fr1 = r;
+      fr2 = r1;
+      step(*runq, *nextq, pos, pos + w, r, fr1, fr2);
+      if (w == 0) break;
+      if (ns_ == 0 && matched_) break;
+      pos += w;
+      r = r1;
+      w = w1;
+      if (r != kEOT) r1 = decode_rune(b, n, (size_t)pos + w, &w1);
+      std::swap(runq, nextq);
+    }
+    clear(*nextq);
+    clear(*runq);
+    return matched_;
+  }
+
+  const std::vector<int64_t>& matchcap() const { return matchcap_; }
+
+ private:
+  const Prog& p_;
+  int ns_;
+  Queue q0_, q1_;
+  std::vector<int64_t> matchcap_;
+  std::vector<int64_t> pool_caps_;
+  std::vector<int> free_;
+  bool matched_ = false;
+
+  int alloc() {
+    if (!free_.empty()) {
+      int t = free_.back();
+      free_.pop_back();
+      return t;
+    }
+    int t = (int)(pool_caps_.size() / (ns_ > 0 ? ns_ : 1));
+    pool_caps_.resize(pool_caps_.size() + (ns_ > 0 ? ns_ : 1), -1);
+    return t;
+  }
+  int64_t* caps(int t) { return pool_caps_.data() + (size_t)t * (ns_ > 0 ? ns_ : 1); }
+  void release(int t) { free_.push_back(t); }
+  void clear(Queue& q) {
+    for (auto& d : q.dense)
+      if (d.second >= 0) release(d.second);
+    q.dense.clear();
+  }
+
+  int64_t* capp(int owner) { return owner == -2 ? matchcap_.data() : caps(owner); }
+
+  // machine.add (regexp/exec.go). The capture array is named by its owner (a thread
+  // id, or -2 for matchcap_) because alloc() can grow pool_caps_ and move it.
+  int add2(Queue& q, uint32_t pc, int64_t pos, int owner, int32_t f1, int32_t f2, int t) {
+  again:
+    if (pc == 0) return t;
+    if (q.contains(pc)) return t;
+    size_t j = q.dense.size();
+    q.dense.push_back({pc, -1});
+    q.sparse[pc] = (uint32_t)j;
+    const Inst& i = p_.inst[pc];
+    switch (i.op) {
+      case Op::Fail:
+        break;
+      case Op::Alt:
+        t = add2(q, i.out, pos, owner, f1, f2, t);
+        pc = i.arg;
+        goto again;
+      case Op::Empty:
+        if (empty_ok(i.arg, f1, f2)) {
+          pc = i.out;
+          goto again;
+        }
+        break;
+      case Op::Nop:
+        pc = i.out;
+        goto again;
+      case Op::Cap:
+        if ((int)i.arg < ns_) {
+          int64_t opos = capp(owner)[i.arg];
+          capp(owner)[i.arg] = pos;
+          add2(q, i.out, pos, owner, f1, f2, -1);
+          capp(owner)[i.arg] = opos;
+        } else {
+          pc = i.out;
+          goto again;
+        }
+        break;
+      case Op::Match:
+      case Op::Rune: {
+        if (t < 0) t = alloc();
+        if (ns_ > 0 && t != owner) {
+          int64_t* src = capp(owner);
+          int64_t* dst = caps(t);
+          if (src != dst) std::memcpy(dst, src, sizeof(int64_t) * ns_);
+        }
+        q.dense[j].second = t;
+        t = -1;
+        break;
+      }
+    }
+    return t;
+  }
+
+  void step(Queue& runq, Queue& nextq, int64_t pos, int64_t next_pos, int32_t c, int32_t f1,
+            int32_t f2) {
+    for (size_t j = 0; j < runq.dense.size(); j++) {
+      int t = runq.dense[j].second;
+      if (t < 0) continue;
+      const Inst& i = p_.inst[runq.dense[j].first];
+      bool addit = false;
+      bool cut = false;
+      if (i.op == Op::Match) {
+        if (ns_ > 0) {
+          caps(t)[1] = pos;
+          std::memcpy(matchcap_.data(), caps(t), sizeof(int64_t) * ns_);
+        }
+        // first-match mode: cut off all lower-priority threads
+        for (size_t k = j + 1; k < runq.dense.size(); k++)
+          if (runq.dense[k].second >= 0) release(runq.dense[k].second);
+        cut = true;
+        matched_ = true;
+      } else {
+        addit = rune_in(p_.runes[i.arg], c);
+      }
+      if (addit) t = add2(nextq, i.out, next_pos, t, f1, f2, t);
+      if (t >= 0) release(t);
+      if (cut) break;
+    }
+    runq.dense.clear();
+  }
+};
+
+}  // namespace
+
+bool Regexp::Match(const uint8_t* b, size_t n) const {
+  Machine m(prog_, 0);
+  return m.run(b, n, 0, (int64_t)n);
+}
+
+void Regexp::FindAll(const uint8_t* b, size_t n, bool submatch, std::vector<int64_t>* out,
+                     size_t lo, size_t start_hi) const {
+  // regexp.allMatches (regexp/regexp.go)
+  Machine m(prog_, prog_.nslots);
+  int64_t end = (int64_t)n;
+  int64_t pos = (int64_t)lo, prev_end = -1;
+  int64_t hi = start_hi == SIZE_MAX ? end : (int64_t)std::min<size_t>(start_hi, n);
+  while (pos <= end) {
+    if (pos > hi) break;
+    if (!m.run(b, n, pos, hi)) break;
+    const auto& mc = m.matchcap();
+    bool accept = true;
+    if (mc[1] == pos) {
+      if (mc[0] == prev_end) accept = false;
+      int w;
+      decode_rune(b, n, (size_t)pos, &w);
+      pos = w > 0 ? pos + w : end + 1;
+    } else {
+      pos = mc[1];
+    }
+    prev_end = mc[1];
+    if (accept) {
+      if (submatch) out->insert(out->end(), mc.begin(), mc.begin() + prog_.nslots);
+      else out->insert(out->end(), mc.begin(), mc.begin() + 2);
+    }
+  }
+}
+
+}  // namespace tsg

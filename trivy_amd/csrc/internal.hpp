@@ -1,0 +1,22 @@
+// Shared internals of the C ABI (capi.cpp, gpu.hip).
+#pragma once
+#include <memory>
+#include <string>
+
+#include "../../include/trivy_secret.h"
+#include "plan.hpp"
+#include "scanner.hpp"
+
+struct tsg_ruleset {
+  tsg::Ruleset rs;
+  std::unique_ptr<tsg::Plan> plan;
+};
+
+struct tsg_result {
+  std::string buf;
+};
+
+namespace tsg {
+void set_error(const std::string& msg);
+int fail(int code, const std::string& msg);
+}  // namespace tsg

@@ -1,0 +1,91 @@
+// Compiled plan for the GPU pipeline of one rule set, and the host resolver.
+//
+//   K1  keyword automaton  : every distinct lowercased ASCII keyword of every rule
+//                            (Rule.MatchKeywords, scanner.go:164-176) + two pseudo
+//                            keywords for the only non-ASCII runes whose simple
+//                            lowercase is ASCII (U+0130 -> 'i', U+212A -> 'k'); a file
+//                            containing them gets its keyword gate checked exactly.
+//   K2  rule-group DFAs    : the rules' regexes packed into groups (one DFA each,
+//                            accept bit per rule); a group is scanned only over the
+//                            files whose keyword bits gate at least one of its rules.
+//   resolver (host)        : candidate end offsets -> exact windows -> scan_file.
+#pragma once
+#include <cstdint>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "dfa.hpp"
+#include "scanner.hpp"
+
+namespace tsg {
+
+enum KwMode : uint8_t { kKwAlways = 0, kKwBits = 1, kKwUnknown = 2 };
+
+struct GroupPlan {
+  std::unique_ptr<DFA> dfa;
+  std::vector<uint32_t> rules;   // group-local accept id -> global rule index
+  std::vector<uint32_t> kwmask;  // keyword ids gating this group [kw_words]
+  bool always = false;           // some member rule is not keyword-gated on the GPU
+};
+
+struct Plan {
+  std::unique_ptr<DFA> kw_dfa;
+  int n_kw = 0;        // keyword ids incl. the 2 fallback pseudo keywords at the end
+  int kw_words = 1;    // 32-bit words per file
+  int fb_kw0 = 0;      // first fallback pseudo keyword id
+  std::vector<uint8_t> rule_kw_mode;            // per rule
+  std::vector<std::vector<uint32_t>> rule_kws;  // per rule: keyword ids
+  std::vector<GroupPlan> groups;
+  std::vector<int> rule_group;       // per rule: group index, -1 = no GPU DFA
+  std::vector<uint8_t> rule_hostonly;  // regex without a GPU DFA (host scans gated files)
+  std::vector<int64_t> rule_maxlen;  // longest EXACT match in bytes, -1 unbounded
+  std::vector<int> rule_relax;       // relaxation used for the GPU program (-1 exact)
+  std::vector<Prog> rule_prog;       // the program the rule's GPU DFA was built from
+  std::unique_ptr<DFA> allow_path_dfa;  // Global.AllowPath on ASCII paths
+};
+
+struct PlanOptions {
+  int max_group_states = 1024;
+  int max_group_table_bytes = 48 * 1024;
+  int max_rules_per_group = 64;
+};
+
+std::unique_ptr<Plan> build_plan(const Ruleset& rs, const PlanOptions& opt, std::string* err);
+
+// One GPU candidate: rule `rule` has a match ending at byte `end` of file `file`.
+struct Candidate {
+  uint32_t file;
+  uint32_t rule;
+  uint32_t end;
+};
+
+// Everything the kernels hand back for one batch.
+struct KernelOutput {
+  std::vector<uint32_t> kw;        // [nfiles * kw_words]
+  std::vector<Candidate> cand;
+  std::vector<uint8_t> overflow;   // [nfiles] 1 = resolve the whole file exactly
+};
+
+struct BatchView {
+  const uint8_t* data;
+  const uint64_t* offsets;  // [nfiles + 1]
+  uint32_t nfiles;
+  const char* paths;
+  const uint64_t* path_offsets;  // [nfiles + 1]
+};
+
+// Host resolution: exact findings for every file of the batch.
+void resolve_batch(const Ruleset& rs, const Plan& plan, const BatchView& b,
+                   const KernelOutput& ko, int nthreads, std::vector<FileResult>* out);
+
+// Exact CPU path for a whole batch (no GPU).
+void scan_batch_cpu(const Ruleset& rs, const BatchView& b, int nthreads,
+                    std::vector<FileResult>* out);
+
+// CPU emulation of the two kernels' algorithm (same chunking, same tables);
+// used by the CPU tests and as the reference for the HIP kernels.
+void emulate_kernels(const Plan& plan, const BatchView& b, uint32_t chunk, uint32_t ext_cap,
+                     KernelOutput* ko);
+
+}  // namespace tsg

@@ -1,0 +1,454 @@
+// Exact per-file Scan (host).  See scanner.hpp for the reference mapping.
+#include "scanner.hpp"
+
+#include <algorithm>
+#include <cstring>
+
+namespace tsg {
+
+// ------------------------------------------------------------------ allow rules
+static bool allow_path(const std::vector<AllowRuleC>& rules, const std::string& path) {
+  for (const auto& r : rules)  // scanner.go:195-202
+    if (r.path && r.path->Match((const uint8_t*)path.data(), path.size())) return true;
+  return false;
+}
+
+static bool allow_match(const std::vector<AllowRuleC>& rules, const uint8_t* m, size_t n) {
+  for (const auto& r : rules)  // scanner.go:204-211
+    if (r.regex && r.regex->Match(m, n)) return true;
+  return false;
+}
+
+bool Ruleset::AllowPath(const std::string& path) const { return allow_path(allow, path); }
+bool Ruleset::Allow(const uint8_t* m, size_t n) const { return allow_match(allow, m, n); }
+
+bool match_keywords(const RuleC& r, const std::string& lowered) {
+  if (r.kw_lower.empty()) return true;  // scanner.go:165-167
+  for (const auto& kw : r.kw_lower)
+    if (lowered.find(kw) != std::string::npos) return true;
+  return false;
+}
+
+// ------------------------------------------------------------------ Go sort.Slice
+// pdqsort_func from Go 1.19 sort/zsortfunc.go, restated over a vector with `less`.
+namespace gosort {
+
+template <class T, class L>
+struct Data {
+  std::vector<T>& x;
+  L less;
+  bool Less(int i, int j) const { return less(x[i], x[j]); }
+  void Swap(int i, int j) { std::swap(x[i], x[j]); }
+};
+
+template <class D>
+void insertion_sort(D& d, int a, int b) {
+  for (int i = a + 1; i < b; i++)
+    for (int j = i; j > a && d.Less(j, j - 1); j--) d.Swap(j, j - 1);
+}
+
+template <class D>
+void sift_down(D& d, int lo, int hi, int first) {
+  int root = lo;
+  for (;;) {
+    int child = 2 * root + 1;
+    if (child >= hi) return;
+    if (child + 1 < hi && d.Less(first + child, first + child + 1)) child++;
+    if (!d.Less(first + root, first + child)) return;
+    d.Swap(first + root, first + child);
+    root = child;
+  }
+}
+
+template <class D>
+void heap_sort(D& d, int a, int b) {
+  int first = a, lo = 0, hi = b - a;
+  for (int i = (hi - 1) / 2; i >= 0; i--) sift_down(d, i, hi, first);
+  for (int i = hi - 1; i >= 0; i--) {
+    d.Swap(first, first + i);
+    sift_down(d, lo, i, first);
+  }
+}
+
+enum Hint { kUnknown, kIncreasing, kDecreasing };
+
+inline int bits_len(uint64_t x) {
+  int n = 0;
+  while (x) {
+    n++;
+    x >>= 1;
+  }
+  return n;
+}
+
+template <class D>
+void break_patterns(D& d, int a, int b) {
+  int length = b - a;
+  if (length >= 8) {
+    uint64_t r = (uint64_t)length;
+    uint64_t modulus = 1ull << bits_len((uint64_t)length);
+    int idx = a + (length / 4) * 2 - 1;
+    for (int i = 0; i < 3; i++) {
+      r ^= r << 13;
+      r ^= r >> 17;
+      r ^= r << 5;
+      int other = (int)(r & (modulus - 1));
+      if (other >= length) other -= length;
+      d.Swap(idx - 1 + i, a + other);
+    }
+  }
+}
+
+template <class D>
+void order2(D& d, int& a, int& b, int* swaps) {
+  if (d.Less(b, a)) {
+    (*swaps)++;
+    std::swap(a, b);
+  }
+}
+
+template <class D>
+int median(D& d, int a, int b, int c, int* swaps) {
+  order2(d, a, b, swaps);
+  order2(d, b, c, swaps);
+  order2(d, a, b, swaps);
+  return b;
+}
+
+template <class D>
+int choose_pivot(D& d, int a, int b, Hint* hint) {
+  const int shortest_ninther = 50, max_swaps = 4 * 3;
+  int l = b - a;
+  int swaps = 0;
+  int i = a + l / 4 * 1, j = a + l / 4 * 2, k = a + l / 4 * 3;
+  if (l >= 8) {
+    if (l >= shortest_ninther) {
+      i = median(d, i - 1, i, i + 1, &swaps);
+      j = median(d, j - 1, j, j + 1, &swaps);
+      k = median(d, k - 1, k, k + 1, &swaps);
+    }
+    j = median(d, i, j, k, &swaps);
+  }
+  *hint = swaps == 0 ? kIncreasing : swaps == max_swaps ? kDecreasing : kUnknown;
+  return j;
+}
+
+template <class D>
+void reverse_range(D& d, int a, int b) {
+  for (int i = a, j = b - 1; i < j; i++, j--) d.Swap(i, j);
+}
+
+template <class D>
+bool partial_insertion_sort(D& d, int a, int b) {
+  const int max_steps = 5, shortest_shifting = 50;
+  int i = a + 1;
+  for (int j = 0; j < max_steps; j++) {
+    while (i < b && !d.Less(i, i - 1)) i++;
+    if (i == b) return true;
+    if (b - a < shortest_shifting) return false;
+    d.Swap(i, i - 1);
+    if (i - a >= 2) {
+      for (int k = i - 1; k >= 1; k--) {
+        if (!d.Less(k, k - 1)) break;
+        d.Swap(k, k - 1);
+      }
+    }
+    if (b - i >= 2) {
+      for (int k = i + 1; k < b; k++) {
+        if (!d.Less(k, k - 1)) break;
+        d.Swap(k, k - 1);
+      }
+    }
+  }
+  return false;
+}
+
+template <class D>
+int partition_equal(D& d, int a, int b, int pivot) {
+  d.Swap(a, pivot);
+  int i = a + 1, j = b - 1;
+  for (;;) {
+    while (i <= j && !d.Less(a, i)) i++;
+    while (i <= j && d.Less(a, j)) j--;
+    if (i > j) break;
+    d.Swap(i, j);
+    i++;
+    j--;
+  }
+  return i;
+}
+
+template <class D>
+int partition(D& d, int a, int b, int pivot, bool* already) {
+  d.Swap(a, pivot);
+  int i = a + 1, j = b - 1;
+  while (i <= j && d.Less(i, a)) i++;
+  while (i <= j && !d.Less(j, a)) j--;
+  if (i > j) {
+    d.Swap(j, a);
+    *already = true;
+    return j;
+  }
+  d.Swap(i, j);
+  i++;
+  j--;
+  for (;;) {
+    while (i <= j && d.Less(i, a)) i++;
+    while (i <= j && !d.Less(j, a)) j--;
+    if (i > j) break;
+    d.Swap(i, j);
+    i++;
+    j--;
+  }
+  d.Swap(j, a);
+  *already = false;
+  return j;
+}
+
+template <class D>
+void pdqsort(D& d, int a, int b, int limit) {
+  const int max_insertion = 12;
+  bool was_balanced = true, was_partitioned = true;
+  for (;;) {
+    int length = b - a;
+    if (length <= max_insertion) {
+      insertion_sort(d, a, b);
+      return;
+    }
+    if (limit == 0) {
+      heap_sort(d, a, b);
+      return;
+    }
+    if (!was_balanced) {
+      break_patterns(d, a, b);
+      limit--;
+    }
+    Hint hint;
+    int pivot = choose_pivot(d, a, b, &hint);
+    if (hint == kDecreasing) {
+      reverse_range(d, a, b);
+      pivot = (b - 1) - (pivot - a);
+      hint = kIncreasing;
+    }
+    if (was_balanced && was_partitioned && hint == kIncreasing) {
+      if (partial_insertion_sort(d, a, b)) return;
+    }
+    if (a > 0 && !d.Less(a - 1, pivot)) {
+      a = partition_equal(d, a, b, pivot);
+      continue;
+    }
+    bool already;
+    int mid = partition(d, a, b, pivot, &already);
+    was_partitioned = already;
+    int left_len = mid - a, right_len = b - mid;
+    int balance_threshold = length / 8;
+    if (left_len < right_len) {
+      was_balanced = left_len >= balance_threshold;
+      pdqsort(d, a, mid, limit);
+      a = mid + 1;
+    } else {
+      was_balanced = right_len >= balance_threshold;
+      pdqsort(d, mid + 1, b, limit);
+      b = mid;
+    }
+  }
+}
+
+template <class T, class L>
+void sort_slice(std::vector<T>& x, L less) {
+  Data<T, L> d{x, less};
+  pdqsort(d, 0, (int)x.size(), bits_len(x.size()));
+}
+
+}  // namespace gosort
+
+// ------------------------------------------------------------------ materialise
+namespace {
+
+struct Loc {
+  int64_t start, end;
+};
+
+// Blocks (scanner.go:227-265): exclude-block spans, searched lazily once per file
+struct Blocks {
+  const uint8_t* content;
+  size_t n;
+  const std::vector<std::shared_ptr<Regexp>>* regexes;
+  bool done = false;
+  std::vector<Loc> locs;
+
+  bool Match(const Loc& b) {
+    if (!done) {
+      done = true;
+      std::vector<int64_t> idx;
+      for (const auto& re : *regexes) {
+        idx.clear();
+        re->FindAll(content, n, false, &idx);
+        for (size_t k = 0; k + 1 < idx.size(); k += 2) locs.push_back({idx[k], idx[k + 1]});
+      }
+    }
+    for (const auto& l : locs)
+      if (l.start <= b.start && b.end <= l.end) return true;
+    return false;
+  }
+};
+
+// findLocation (scanner.go:445-502) over the censored buffer with a newline index
+void find_location(int64_t start, int64_t end, const std::string& content,
+                   const std::vector<int64_t>& nl, Finding* f) {
+  const int64_t n = (int64_t)content.size();
+  int64_t start_line = std::lower_bound(nl.begin(), nl.end(), start) - nl.begin();
+  int64_t line_start = start_line > 0 ? nl[start_line - 1] + 1 : 0;
+  int64_t line_end = start_line < (int64_t)nl.size() ? nl[start_line] : n;
+  int64_t nl_in_match = (std::lower_bound(nl.begin(), nl.end(), end) - nl.begin()) - start_line;
+  int64_t end_line = start_line + nl_in_match;
+  if (line_end - line_start > 100) {
+    int64_t ts = start - 30 < 0 ? 0 : start - 30;
+    int64_t te = end + 20 > n ? n : end + 20;
+    f->match.assign(content, ts, te - ts);
+  } else {
+    f->match.assign(content, line_start, line_end - line_start);
+  }
+  const int64_t nlines = (int64_t)nl.size() + 1;
+  int64_t code_start = start_line - 2 < 0 ? 0 : start_line - 2;
+  int64_t code_end = end_line + 2 > nlines ? nlines : end_line + 2;
+  bool found_first = false;
+  f->lines.clear();
+  for (int64_t i = code_start; i < code_end; i++) {
+    int64_t ls = i > 0 ? nl[i - 1] + 1 : 0;
+    int64_t le = i < (int64_t)nl.size() ? nl[i] : n;
+    bool cause = i >= start_line && i <= end_line;
+    Line ln;
+    ln.number = (int32_t)(i + 1);
+    ln.flags = (uint8_t)((cause ? 1 : 0) | ((!found_first && cause) ? 2 : 0));
+    ln.content.assign(content, ls, le - ls);
+    found_first = found_first || cause;
+    f->lines.push_back(std::move(ln));
+  }
+  for (auto it = f->lines.rbegin(); it != f->lines.rend(); ++it)
+    if (it->flags & 1) {
+      it->flags |= 4;
+      break;
+    }
+  f->start_line = (int32_t)(start_line + 1);
+  f->end_line = (int32_t)(end_line + 1);
+}
+
+}  // namespace
+
+void scan_file(const Ruleset& rs, const std::string& path, const uint8_t* content, size_t n,
+               const FileGate* gate, FileResult* out) {
+  out->findings.clear();
+  out->status = kNoFindings;
+  if (rs.AllowPath(path)) {  // scanner.go:343-347
+    out->status = kPathAllowed;
+    return;
+  }
+  std::string lowered;
+  bool have_lowered = false;
+  Blocks global{content, n, &rs.exclude};
+  std::vector<std::pair<uint32_t, Loc>> matched;
+  std::string censored;
+  bool have_censored = false;
+  std::vector<int64_t> idx;
+
+  for (size_t ri = 0; ri < rs.rules.size(); ri++) {  // scanner.go:355
+    const RuleC& r = rs.rules[ri];
+    const RuleWindows* win = nullptr;
+    if (gate) {
+      // GPU: no candidate end offset for this rule -> its regex has no match here
+      win = gate->windows[ri];
+      if (!win) continue;
+      if (gate->kw_state[ri] == 0) continue;
+    }
+    if (r.path && !r.path->Match((const uint8_t*)path.data(), path.size())) continue;
+    if (allow_path(r.allow, path)) continue;
+    if (!gate || gate->kw_state[ri] == 2) {
+      if (!have_lowered) {
+        go_to_lower(content, n, &lowered);
+        have_lowered = true;
+      }
+      if (!match_keywords(r, lowered)) continue;
+    }
+    if (!r.regex) continue;
+    // FindLocations / FindSubmatchLocations (scanner.go:96-141)
+    const bool sub = !r.secret_group_name.empty();
+    const int ns = sub ? r.regex->NumSlots() : 2;
+    idx.clear();
+    if (!win || win->whole) {
+      r.regex->FindAll(content, n, sub, &idx);
+    } else {
+      for (const auto& iv : win->iv) r.regex->FindAll(content, n, sub, &idx, iv.first, iv.second);
+    }
+    std::vector<Loc> locs;
+    for (size_t k = 0; k + ns - 1 < idx.size(); k += ns) {
+      int64_t s = idx[k], e = idx[k + 1];
+      if (rs.Allow(content + s, e - s) || allow_match(r.allow, content + s, e - s)) continue;
+      if (!sub) {
+        locs.push_back({s, e});
+      } else {
+        for (int g : r.group_idx) locs.push_back({idx[k + 2 * g], idx[k + 2 * g + 1]});
+      }
+    }
+    if (locs.empty()) continue;
+    Blocks local{content, n, &r.exclude};
+    for (const auto& loc : locs) {
+      if (global.Match(loc) || local.Match(loc)) continue;
+      if (loc.start < 0) continue;  // reference panics (slice bounds); never produced by valid rules
+      matched.push_back({(uint32_t)ri, loc});
+      if (!have_censored) {
+        censored.assign((const char*)content, n);
+        have_censored = true;
+      }
+      std::memset(&censored[loc.start], '*', loc.end - loc.start);  // censorLocation
+    }
+  }
+  if (matched.empty()) return;  // Secret{}
+  std::vector<int64_t> nl;
+  for (size_t i = 0; i < censored.size(); i++)
+    if (censored[i] == '\n') nl.push_back((int64_t)i);
+  out->findings.resize(matched.size());
+  for (size_t k = 0; k < matched.size(); k++) {
+    out->findings[k].rule = matched[k].first;
+    find_location(matched[k].second.start, matched[k].second.end, censored, nl, &out->findings[k]);
+  }
+  const auto& rules = rs.rules;
+  gosort::sort_slice(out->findings, [&rules](const Finding& a, const Finding& b) {
+    const std::string& ia = rules[a.rule].id;
+    const std::string& ib = rules[b.rule].id;
+    if (ia != ib) return ia < ib;
+    return a.match < b.match;
+  });
+  out->status = kHasFindings;
+}
+
+// ------------------------------------------------------------------ serialization
+static void put_u32(std::string* o, uint32_t v) { o->append((const char*)&v, 4); }
+static void put_bytes(std::string* o, const std::string& s) {
+  put_u32(o, (uint32_t)s.size());
+  o->append(s);
+}
+
+void serialize_results(const std::vector<FileResult>& res, std::string* out) {
+  out->clear();
+  put_u32(out, 0x31475354u);  // "TSG1"
+  put_u32(out, (uint32_t)res.size());
+  for (const auto& r : res) {
+    out->push_back((char)r.status);
+    put_u32(out, (uint32_t)r.findings.size());
+    for (const auto& f : r.findings) {
+      put_u32(out, f.rule);
+      put_u32(out, (uint32_t)f.start_line);
+      put_u32(out, (uint32_t)f.end_line);
+      put_bytes(out, f.match);
+      put_u32(out, (uint32_t)f.lines.size());
+      for (const auto& ln : f.lines) {
+        put_u32(out, (uint32_t)ln.number);
+        out->push_back((char)ln.flags);
+        put_bytes(out, ln.content);
+      }
+    }
+  }
+}
+
+}  // namespace tsg

@@ -1,0 +1,95 @@
+// Host side of the secret engine: the rule set and the exact per-file Scan.
+//
+// Mirrors trivy pkg/fanal/secret/scanner.go:
+//   Rule / AllowRule / ExcludeBlock / Global      scanner.go:23-94, 186-225
+//   Scanner.Scan                                  scanner.go:341-416
+//   FindLocations / FindSubmatchLocations         scanner.go:96-141
+//   AllowLocation, getMatchSubgroupsLocations     scanner.go:143-158
+//   Blocks (lazy exclude-block search)            scanner.go:227-265
+//   censorLocation / toFinding / findLocation     scanner.go:418-502
+//   sort.Slice(findings, RuleID, Match)           scanner.go:405-410 (Go 1.19 pdqsort_func)
+// The GPU kernels only decide WHERE this exact code has to look (per-file keyword
+// bits and per-rule candidate end offsets); everything that reaches the output is
+// computed here with Go semantics.
+#pragma once
+#include <cstdint>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "goregex.hpp"
+
+namespace tsg {
+
+struct AllowRuleC {
+  std::string id, description;
+  std::shared_ptr<Regexp> regex, path;
+};
+
+struct RuleC {
+  std::string id, category, title, severity;
+  std::shared_ptr<Regexp> regex;  // may be null
+  std::vector<std::string> keywords;
+  std::shared_ptr<Regexp> path;
+  std::vector<AllowRuleC> allow;
+  std::vector<std::shared_ptr<Regexp>> exclude;
+  std::string secret_group_name;
+  // derived
+  std::vector<std::string> kw_lower;  // strings.ToLower(kw)
+  std::vector<int> group_idx;         // i where SubexpNames()[i] == secret_group_name
+};
+
+struct Ruleset {
+  std::vector<RuleC> rules;
+  std::vector<AllowRuleC> allow;
+  std::vector<std::shared_ptr<Regexp>> exclude;
+
+  bool AllowPath(const std::string& path) const;       // Global.AllowPath
+  bool Allow(const uint8_t* m, size_t n) const;        // Global.Allow
+};
+
+struct Line {
+  int32_t number;
+  uint8_t flags;  // 1 IsCause, 2 FirstCause, 4 LastCause
+  std::string content;
+};
+
+struct Finding {
+  uint32_t rule;
+  int32_t start_line, end_line;
+  std::string match;
+  std::vector<Line> lines;
+};
+
+enum FileStatus : uint8_t { kNoFindings = 0, kPathAllowed = 1, kHasFindings = 2 };
+
+struct FileResult {
+  uint8_t status = kNoFindings;
+  std::vector<Finding> findings;
+};
+
+// Where the exact matcher must look for one rule in one file.
+struct RuleWindows {
+  bool whole = false;                               // run FindAll over the whole file
+  std::vector<std::pair<int64_t, int64_t>> iv;      // [lo, start_hi] intervals, sorted, disjoint
+};
+
+// Per-file gating decided by the GPU (null = CPU path: decide everything exactly).
+struct FileGate {
+  // kw_state[r]: 0 keyword gate known false, 1 known true, 2 unknown (check exactly)
+  const uint8_t* kw_state = nullptr;
+  // windows[r] == nullptr -> the rule has no candidate in this file (regex cannot match)
+  const RuleWindows* const* windows = nullptr;
+};
+
+// Exact Scan of one file (scanner.go:341-416).
+void scan_file(const Ruleset& rs, const std::string& path, const uint8_t* content, size_t n,
+               const FileGate* gate, FileResult* out);
+
+// Rule.MatchKeywords (scanner.go:164-176) with the lowercased content computed once.
+bool match_keywords(const RuleC& r, const std::string& lowered);
+
+// Serialization of results (format documented in include/trivy_secret.h).
+void serialize_results(const std::vector<FileResult>& res, std::string* out);
+
+}  // namespace tsg

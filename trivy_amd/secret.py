@@ -1,0 +1,415 @@
+"""Host-side mirror of trivy's `pkg/fanal/secret` API over the native engine.
+
+Same names, argument meaning and error behaviour as the reference:
+  Config / Rule / AllowRule / ExcludeBlock / Global      scanner.go:23-94, 186-225
+  ParseConfig(path) -> Config | None                      scanner.go:267-291
+  NewScanner(config) -> Scanner                           scanner.go:293-329
+  Scanner.Scan(ScanArgs) -> Secret                        scanner.go:341-416 (exact, CPU)
+  Scanner.AllowPath(path)                                 scanner.go:55-57
+and the batching boundary the GPU needs:
+  Scanner.ScanBatch([ScanArgs], device=...) -> [Secret]   (K1 + K2 on the MI355X, exact
+                                                          host resolution of candidates)
+
+`Secret` values are dicts shaped like Go's types.Secret:
+  {"FilePath": str, "Findings": None | [SecretFinding]}
+with SecretFinding = {"RuleID", "Category", "Severity", "Title", "StartLine", "EndLine",
+"Code": {"Lines": [Line]}, "Match"}; Match and line Content/Highlighted are `bytes`
+(Go strings are byte strings; content need not be valid UTF-8).
+"""
+import ctypes as C
+import json
+import os
+import struct
+from dataclasses import dataclass, field
+from typing import List, Optional
+
+import numpy as np
+import yaml
+
+from . import _native as N
+
+_RULES_JSON = os.path.join(os.path.dirname(os.path.abspath(__file__)), "rules",
+                           "builtin_rules.json")
+
+
+class ConfigError(ValueError):
+    """secrets config decode / regexp compile error (scanner.go:74-77, 286-288)."""
+
+
+def _check_regex(src):
+    """regexp.Compile on the native engine; raises ConfigError like UnmarshalYAML."""
+    h = C.c_void_p()
+    err = C.create_string_buffer(512)
+    rc = N.lib().tsg_regex_compile(src.encode("utf-8", "surrogateescape"), C.byref(h), err, 512)
+    if rc != N.TSG_OK:
+        raise ConfigError("regexp compile error: %s" % err.value.decode("utf-8", "replace"))
+    N.lib().tsg_regex_free(h)
+    return src
+
+
+@dataclass
+class AllowRule:
+    ID: str = ""
+    Description: str = ""
+    Regex: Optional[str] = None
+    Path: Optional[str] = None
+
+
+@dataclass
+class ExcludeBlock:
+    Description: str = ""
+    Regexes: List[str] = field(default_factory=list)
+
+
+@dataclass
+class Rule:
+    ID: str = ""
+    Category: str = ""
+    Title: str = ""
+    Severity: str = ""
+    Regex: Optional[str] = None
+    Keywords: List[str] = field(default_factory=list)
+    Path: Optional[str] = None
+    AllowRules: List[AllowRule] = field(default_factory=list)
+    ExcludeBlock: ExcludeBlock = field(default_factory=ExcludeBlock)
+    SecretGroupName: str = ""
+
+
+@dataclass
+class Config:
+    EnableBuiltinRuleIDs: List[str] = field(default_factory=list)
+    DisableRuleIDs: List[str] = field(default_factory=list)
+    DisableAllowRuleIDs: List[str] = field(default_factory=list)
+    CustomRules: List[Rule] = field(default_factory=list)
+    CustomAllowRules: List[AllowRule] = field(default_factory=list)
+    ExcludeBlock: ExcludeBlock = field(default_factory=ExcludeBlock)
+
+
+@dataclass
+class ScanArgs:
+    FilePath: str
+    Content: bytes
+
+
+def _s(v):
+    return "" if v is None else str(v)
+
+
+def _rx(v):
+    return None if v is None else _check_regex(str(v))
+
+
+def _allow(lst):
+    return [AllowRule(_s(a.get("id")), _s(a.get("description")), _rx(a.get("regex")),
+                      _rx(a.get("path"))) for a in (lst or [])]
+
+
+def _exclude(d):
+    d = d or {}
+    return ExcludeBlock(_s(d.get("description")), [_rx(x) for x in (d.get("regexes") or [])])
+
+
+def config_from_dict(doc):
+    if not isinstance(doc, dict):
+        raise ConfigError("secrets config decode error")
+    c = Config()
+    c.EnableBuiltinRuleIDs = [str(x) for x in (doc.get("enable-builtin-rules") or [])]
+    c.DisableRuleIDs = [str(x) for x in (doc.get("disable-rules") or [])]
+    c.DisableAllowRuleIDs = [str(x) for x in (doc.get("disable-allow-rules") or [])]
+    for r in doc.get("rules") or []:
+        c.CustomRules.append(Rule(
+            ID=_s(r.get("id")), Category=_s(r.get("category")), Title=_s(r.get("title")),
+            Severity=_s(r.get("severity")), Regex=_rx(r.get("regex")),
+            Keywords=[str(k) for k in (r.get("keywords") or [])], Path=_rx(r.get("path")),
+            AllowRules=_allow(r.get("allow-rules")), ExcludeBlock=_exclude(r.get("exclude-block")),
+            SecretGroupName=_s(r.get("secret-group-name"))))
+    c.CustomAllowRules = _allow(doc.get("allow-rules"))
+    c.ExcludeBlock = _exclude(doc.get("exclude-block"))
+    return c
+
+
+def ParseConfig(config_path):
+    """scanner.go:267-291: "" or a missing file -> None (builtins only)."""
+    if not config_path:
+        return None
+    if not os.path.exists(config_path):
+        return None
+    with open(config_path, "rb") as f:
+        doc = yaml.safe_load(f)
+    if doc is None:
+        raise ConfigError("secrets config decode error: EOF")
+    return config_from_dict(doc)
+
+
+_BUILTINS = None
+
+
+def builtin_rules():
+    """The 83 builtin rules and 12 builtin allow rules (builtin-rules.go, builtin-allow-rules.go)."""
+    global _BUILTINS
+    if _BUILTINS is None:
+        d = json.load(open(_RULES_JSON))
+        rules = [Rule(ID=r["id"], Category=r["category"], Title=r["title"],
+                      Severity=r["severity"], Regex=r["regex"], Keywords=list(r["keywords"]),
+                      SecretGroupName=r["secret_group_name"]) for r in d["rules"]]
+        allow = [AllowRule(a["id"], a["description"], a["regex"], a["path"])
+                 for a in d["allow_rules"]]
+        _BUILTINS = (rules, allow)
+    return _BUILTINS
+
+
+def NewScanner(config=None):
+    """scanner.go:293-329"""
+    b_rules, b_allow = builtin_rules()
+    if config is None:
+        return Scanner(list(b_rules), list(b_allow), ExcludeBlock())
+    enabled = list(b_rules)
+    if config.EnableBuiltinRuleIDs:
+        enabled = [r for r in b_rules if r.ID in config.EnableBuiltinRuleIDs]
+    enabled = enabled + list(config.CustomRules)
+    rules = [r for r in enabled if r.ID not in config.DisableRuleIDs]
+    allow = [a for a in list(b_allow) + list(config.CustomAllowRules)
+             if a.ID not in config.DisableAllowRuleIDs]
+    return Scanner(rules, allow, config.ExcludeBlock)
+
+
+def _b(s):
+    return None if s is None else s.encode("utf-8", "surrogateescape")
+
+
+class _Keep:
+    """Keeps ctypes buffers alive for the duration of a native call."""
+
+    def __init__(self):
+        self.refs = []
+
+    def cstr(self, s):
+        b = _b(s)
+        self.refs.append(b)
+        return b
+
+    def arr(self, ctype, items):
+        a = (ctype * max(1, len(items)))(*items)
+        self.refs.append(a)
+        return a
+
+
+class Batch:
+    """Files packed for the engine: one contiguous byte stream + u64 offsets (+ paths)."""
+
+    def __init__(self, data, offsets, paths, path_offsets):
+        self.data = np.ascontiguousarray(data, dtype=np.uint8)
+        self.offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+        self.paths = np.ascontiguousarray(paths, dtype=np.uint8)
+        self.path_offsets = np.ascontiguousarray(path_offsets, dtype=np.uint64)
+        self.nfiles = len(self.offsets) - 1
+
+    @classmethod
+    def from_args(cls, args):
+        lens = np.array([len(a.Content) for a in args], dtype=np.uint64)
+        offs = np.zeros(len(args) + 1, dtype=np.uint64)
+        np.cumsum(lens, out=offs[1:])
+        data = np.frombuffer(b"".join(a.Content for a in args) or b"\0", dtype=np.uint8)
+        pb = [a.FilePath.encode("utf-8", "surrogateescape") for a in args]
+        plens = np.array([len(p) for p in pb], dtype=np.uint64)
+        poffs = np.zeros(len(args) + 1, dtype=np.uint64)
+        np.cumsum(plens, out=poffs[1:])
+        paths = np.frombuffer(b"".join(pb) or b"\0", dtype=np.uint8)
+        return cls(data, offs, paths, poffs)
+
+    def ptrs(self):
+        u64p = C.POINTER(C.c_uint64)
+        return (C.c_void_p(self.data.ctypes.data), self.offsets.ctypes.data_as(u64p),
+                C.c_uint32(self.nfiles), C.c_void_p(self.paths.ctypes.data),
+                self.path_offsets.ctypes.data_as(u64p))
+
+    def path(self, i):
+        return bytes(self.paths[int(self.path_offsets[i]):int(self.path_offsets[i + 1])]).decode(
+            "utf-8", "surrogateescape")
+
+
+class Scanner:
+    """secret.Scanner{Global}: compiled once, shared read-only (thread-safe natively)."""
+
+    def __init__(self, rules, allow_rules, exclude_block):
+        self.Rules = list(rules)
+        self.AllowRules = list(allow_rules)
+        self.ExcludeBlock = exclude_block
+        self._h = None
+        self._compile()
+
+    def _compile(self):
+        L = N.lib()
+        keep = _Keep()
+        descs = []
+        for r in self.Rules:
+            kws = keep.arr(C.c_char_p, [keep.cstr(k) for k in r.Keywords])
+            ars = keep.arr(N.AllowRuleDesc, [N.AllowRuleDesc(keep.cstr(a.ID),
+                                                              keep.cstr(a.Description),
+                                                              keep.cstr(a.Regex), keep.cstr(a.Path))
+                                              for a in r.AllowRules])
+            exc = keep.arr(C.c_char_p, [keep.cstr(x) for x in r.ExcludeBlock.Regexes])
+            descs.append(N.RuleDesc(keep.cstr(r.ID), keep.cstr(r.Category), keep.cstr(r.Title),
+                                    keep.cstr(r.Severity), keep.cstr(r.Regex), kws,
+                                    len(r.Keywords), keep.cstr(r.Path), ars, len(r.AllowRules),
+                                    exc, len(r.ExcludeBlock.Regexes),
+                                    keep.cstr(r.SecretGroupName)))
+        rd = keep.arr(N.RuleDesc, descs)
+        ad = keep.arr(N.AllowRuleDesc, [N.AllowRuleDesc(keep.cstr(a.ID), keep.cstr(a.Description),
+                                                        keep.cstr(a.Regex), keep.cstr(a.Path))
+                                        for a in self.AllowRules])
+        ex = keep.arr(C.c_char_p, [keep.cstr(x) for x in self.ExcludeBlock.Regexes])
+        h = C.c_void_p()
+        err = C.create_string_buffer(1024)
+        rc = L.tsg_ruleset_compile(rd, len(descs), ad, len(self.AllowRules), ex,
+                                   len(self.ExcludeBlock.Regexes), C.byref(h), err, 1024)
+        if rc == N.TSG_ERR_CONFIG:
+            raise ConfigError(err.value.decode("utf-8", "replace"))
+        N.check(rc)
+        self._h = h
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            N.lib().tsg_ruleset_destroy(self._h)
+            self._h = None
+
+    @property
+    def handle(self):
+        return self._h
+
+    def info(self):
+        i = N.RulesetInfo()
+        N.check(N.lib().tsg_ruleset_get_info(self._h, C.byref(i)))
+        return {k: getattr(i, k) for k, _ in N.RulesetInfo._fields_}
+
+    def AllowPath(self, path):
+        b = _b(path)
+        rc = N.lib().tsg_ruleset_allow_path(self._h, b, len(b))
+        if rc < 0:
+            N.check(rc)
+        return rc == 1
+
+    def Scan(self, args):
+        """scanner.go:341-416 on the exact CPU path."""
+        p = _b(args.FilePath)
+        out = C.c_void_p()
+        N.check(N.lib().tsg_scan_cpu(self._h, p, len(p), bytes(args.Content), len(args.Content),
+                                     C.byref(out)))
+        return self.decode(out, [args.FilePath])[0]
+
+    def ScanBatch(self, args, device=None, ctx=None, emulate_chunk=0, nthreads=0):
+        """Scan many files.  device=int -> MI355X kernels; emulate_chunk>0 -> the kernels'
+        algorithm emulated on the CPU (tests); otherwise the exact CPU batch path."""
+        batch = args if isinstance(args, Batch) else Batch.from_args(args)
+        paths = [batch.path(i) for i in range(batch.nfiles)]
+        out = C.c_void_p()
+        L = N.lib()
+        if device is not None or ctx is not None:
+            own = ctx is None
+            if own:
+                ctx = GpuContext(self, device)
+            try:
+                N.check(L.tsg_scan_batch(ctx.handle, *batch.ptrs(), C.byref(out)))
+            finally:
+                if own:
+                    ctx.close()
+        elif emulate_chunk:
+            N.check(L.tsg_scan_batch_emulated(self._h, *batch.ptrs(), emulate_chunk, C.byref(out)))
+        else:
+            N.check(L.tsg_scan_cpu_batch(self._h, *batch.ptrs(), nthreads, C.byref(out)))
+        return self.decode(out, paths)
+
+    def decode(self, out, paths):
+        L = N.lib()
+        n = C.c_size_t()
+        ptr = L.tsg_result_data(out, C.byref(n))
+        buf = C.string_at(ptr, n.value)
+        L.tsg_result_free(out)
+        return decode_results(buf, paths, self.Rules)
+
+
+def decode_results(buf, paths, rules):
+    magic, nfiles = struct.unpack_from("<II", buf, 0)
+    assert magic == 0x31475354 and nfiles == len(paths)
+    pos = 8
+    out = []
+    for i in range(nfiles):
+        status = buf[pos]
+        (nf,) = struct.unpack_from("<I", buf, pos + 1)
+        pos += 5
+        findings = []
+        for _ in range(nf):
+            ri, sl, el, ml = struct.unpack_from("<IiiI", buf, pos)
+            pos += 16
+            match = buf[pos:pos + ml]
+            pos += ml
+            (nl,) = struct.unpack_from("<I", buf, pos)
+            pos += 4
+            lines = []
+            for _ in range(nl):
+                num, fl, cl = struct.unpack_from("<iBI", buf, pos)
+                pos += 9
+                content = buf[pos:pos + cl]
+                pos += cl
+                lines.append({"Number": num, "Content": content, "IsCause": bool(fl & 1),
+                              "Annotation": "", "Truncated": False, "Highlighted": content,
+                              "FirstCause": bool(fl & 2), "LastCause": bool(fl & 4)})
+            r = rules[ri]
+            findings.append({"RuleID": r.ID, "Category": r.Category,
+                             "Severity": r.Severity if r.Severity != "" else "UNKNOWN",
+                             "Title": r.Title, "StartLine": sl, "EndLine": el,
+                             "Code": {"Lines": lines or None}, "Match": match})
+        if status == 0:
+            out.append({"FilePath": "", "Findings": None})
+        elif status == 1:
+            out.append({"FilePath": paths[i], "Findings": None})
+        else:
+            out.append({"FilePath": paths[i], "Findings": findings})
+    return out
+
+
+class GpuContext:
+    """One device context (tsg_ctx): replicated rule tables + batch buffers in HBM."""
+
+    def __init__(self, scanner, device=0, chunk_bytes=0, ext_cap=0, cand_capacity=0,
+                 host_threads=0):
+        self.scanner = scanner
+        opt = N.CtxOptions(chunk_bytes, ext_cap, cand_capacity, host_threads)
+        h = C.c_void_p()
+        N.check(N.lib().tsg_ctx_create(int(device), scanner.handle, C.byref(opt), C.byref(h)))
+        self._h = h
+        self._batch = None
+
+    @property
+    def handle(self):
+        return self._h
+
+    def upload(self, batch):
+        N.check(N.lib().tsg_batch_upload(self._h, *batch.ptrs()))
+        self._batch = batch  # host buffers must outlive the scans
+
+    def kernels(self):
+        N.check(N.lib().tsg_batch_kernels(self._h))
+
+    def scan_raw(self):
+        out = C.c_void_p()
+        N.check(N.lib().tsg_batch_scan(self._h, C.byref(out)))
+        return out
+
+    def scan(self):
+        out = self.scan_raw()
+        b = self._batch
+        return self.scanner.decode(out, [b.path(i) for i in range(b.nfiles)])
+
+    def stats(self):
+        s = N.Stats()
+        N.check(N.lib().tsg_ctx_get_stats(self._h, C.byref(s)))
+        return {k: getattr(s, k) for k, _ in N.Stats._fields_}
+
+    def close(self):
+        if self._h:
+            N.lib().tsg_ctx_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        self.close()
