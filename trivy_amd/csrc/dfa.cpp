@@ -369,7 +369,7 @@ class Builder {
     d_->eot_acc[s] = intern_mask(mm);
     d_->noinject[s] = key.noinject ? 1 : 0;
     d_->dead[s] = (key.noinject && key.k.empty()) ? 1 : 0;
-    d_->to_noinject[s] = key.noinject ? s : get_state(key.k, (Ctx)key.ctx, true);
+    d_->to_noinject[s] = (key.noinject || !opt_.with_noinject) ? s : get_state(key.k, (Ctx)key.ctx, true);
   }
 };
 

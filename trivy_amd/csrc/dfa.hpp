@@ -56,6 +56,8 @@ struct DFA {
 
 struct DFAOptions {
   int max_states = 8192;
+  // build the noinject twin states (K2); K1 keywords are bounded and use an overlap instead
+  bool with_noinject = true;
 };
 
 // Build a DFA over `progs` (accept id = index).  Returns nullptr if the state

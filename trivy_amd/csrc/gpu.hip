@@ -43,6 +43,7 @@ struct DevDFA {
   const uint32_t* rules;   // K2: group-local id -> global rule
   const uint32_t* kwmask;  // K2: [kw_words]
   uint32_t nc, ns, mw, always;
+  uint32_t ext;  // K1 overlap: longest keyword - 1
   uint32_t start[4];
 };
 
@@ -174,25 +175,27 @@ __global__ void __launch_bounds__(256) dfa_scan_kernel(
     if (__builtin_expect(e_ & 0x8000u, 0)) sink.accept(d, d.acc[ix_], (uint32_t)((POS) - fs)); \
     s = e_ & 0x7FFFu;                                                    \
   }
-        while (p < se && (p & 15)) {
+        // K1: keywords are bounded -> overlap of ext bytes in inject mode instead of noinject
+        const uint64_t le = KW ? min(fe, se + d.ext) : se;
+        while (p < le && (p & 15)) {
           TSG_STEP(data[p], p);
           p++;
         }
-        while (p + 16 <= se) {
+        while (p + 16 <= le) {
           const uint4 v = *(const uint4*)(data + p);
           const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
           for (int k = 0; k < 16; k++) TSG_STEP((wv[k >> 2] >> ((k & 3) * 8)) & 0xFF, p + k);
           p += 16;
         }
-        while (p < se) {
+        while (p < le) {
           TSG_STEP(data[p], p);
           p++;
         }
-        if (se >= fe) {
+        if (le >= fe) {
           const uint32_t m = d.eot[s];
           if (m) sink.accept(d, m, (uint32_t)(fe - fs));
-        } else {
+        } else if (!KW) {
           // follow the threads that started in [a, se) past the chunk end
           s = d.to_ni[s];
           uint64_t q = se;
@@ -272,6 +275,7 @@ static int make_device_dfa(const DFA& d, const std::vector<uint32_t>& rules,
   v.ns = (uint32_t)d.nstates;
   v.mw = (uint32_t)d.mask_words;
   v.always = always ? 1 : 0;
+  v.ext = d.max_len > 1 ? (uint32_t)(d.max_len - 1) : 0;
   for (int k = 0; k < 4; k++) v.start[k] = d.start[k];
   out->lds_table_bytes = (uint32_t)(((tab.size() * 2 + 15) & ~(size_t)15) + 256);
   return TSG_OK;
@@ -441,6 +445,9 @@ int tsg_batch_kernels(tsg_ctx* c) {
   int grid = (int)std::min<uint64_t>(need_blocks ? need_blocks : 1, (uint64_t)c->grid);
   if (nchunks) {
     size_t lds = c->kw.lds_table_bytes + (size_t)W * block * 4;
+    if (lds > 160 * 1024) return fail(TSG_ERR_INTERNAL, "keyword automaton exceeds LDS");
+    HIP_TRY(hipFuncSetAttribute((const void*)dfa_scan_kernel<true>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     hipLaunchKernelGGL(dfa_scan_kernel<true>, dim3(grid), dim3(block), lds, st, c->kw.dev, c->d_data,
                        c->d_off, c->d_chunk_file, c->total, nchunks, chunk, c->opt.ext_cap, c->d_kw, W,
                        c->d_cand, c->d_count, c->opt.cand_capacity, c->d_ovf);
@@ -450,6 +457,9 @@ int tsg_batch_kernels(tsg_ctx* c) {
   if (nchunks) {
     for (auto& g : c->groups) {
       size_t lds = g.lds_table_bytes + 16;
+      if (lds > 64 * 1024)
+        HIP_TRY(hipFuncSetAttribute((const void*)dfa_scan_kernel<false>,
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
       hipLaunchKernelGGL(dfa_scan_kernel<false>, dim3(grid), dim3(block), lds, st, g.dev, c->d_data,
                          c->d_off, c->d_chunk_file, c->total, nchunks, chunk, c->opt.ext_cap, c->d_kw,
                          W, c->d_cand, c->d_count, c->opt.cand_capacity, c->d_ovf);

@@ -56,7 +56,8 @@ std::unique_ptr<Plan> build_plan(const Ruleset& rs, const PlanOptions& opt, std:
   p->kw_words = (p->n_kw + 31) / 32;
   {
     DFAOptions o;
-    o.max_states = 65535;
+    o.max_states = 32767;
+    o.with_noinject = false;
     std::string e;
     p->kw_dfa = build_keyword_dfa(kws, o, &e);
     if (!p->kw_dfa) {
@@ -344,6 +345,24 @@ bool run_segment(const DFA& d, const uint8_t* data, uint64_t fs, uint64_t fe, ui
   return false;
 }
 
+// K1: keywords are bounded, so the lane simply keeps going in inject mode for
+// max_len - 1 bytes past its piece (every keyword occurrence that starts in the piece
+// is seen; occurrences found in the overlap are real occurrences too).
+template <class OnAcc>
+void run_kw_segment(const DFA& d, const uint8_t* data, uint64_t fs, uint64_t fe, uint64_t a,
+                    uint64_t b, OnAcc on_acc) {
+  const int nc = d.nclasses;
+  uint64_t ext = d.max_len > 1 ? (uint64_t)d.max_len - 1 : 0;
+  uint64_t stop = std::min(fe, b + ext);
+  uint32_t s = (a == fs) ? d.start[kCtxBOT] : d.start[DFA::ctx_of(data[a - 1], d)];
+  for (uint64_t p = a; p < stop; p++) {
+    size_t e = (size_t)s * nc + d.cls[data[p]];
+    if (d.acc[e]) on_acc(d.acc[e], p - fs);
+    s = d.next[e];
+  }
+  if (stop == fe && d.eot_acc[s]) on_acc(d.eot_acc[s], fe - fs);
+}
+
 }  // namespace
 
 void emulate_kernels(const Plan& plan, const BatchView& bv, uint32_t chunk, uint32_t ext_cap,
@@ -367,7 +386,7 @@ void emulate_kernels(const Plan& plan, const BatchView& bv, uint32_t chunk, uint
         uint64_t se = std::min(b, fe);
         if (pass == 0) {
           const DFA& d = *plan.kw_dfa;
-          run_segment(d, bv.data, fs, fe, a, se, ext_cap, [&](uint32_t mi, uint64_t) {
+          run_kw_segment(d, bv.data, fs, fe, a, se, [&](uint32_t mi, uint64_t) {
             const auto& m = d.masks[mi];
             for (int k = 0; k < plan.n_kw; k++)
               if ((m[k / 64] >> (k % 64)) & 1) ko->kw[(size_t)f * plan.kw_words + k / 32] |= 1u << (k % 32);
