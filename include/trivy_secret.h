@@ -96,7 +96,7 @@ int tsg_ruleset_allow_path(const tsg_ruleset* rs, const char* path, size_t path_
 
 typedef struct tsg_ruleset_info {
   uint32_t n_rules;
-  uint32_t n_keywords;      /* K1 keyword ids incl. 2 fallback pseudo keywords */
+  uint32_t n_keywords;      /* K1 keyword ids incl. 3 fallback pseudo keywords */
   uint32_t n_groups;        /* K2 DFAs */
   uint32_t n_hostonly;      /* rules without a GPU DFA (state cap) */
   uint32_t kw_states;       /* K1 automaton states */
@@ -173,6 +173,16 @@ int64_t tsg_regex_find_all(const tsg_regex* re, const uint8_t* text, size_t len,
  * computed with the GPU lane algorithm (chunk bytes per lane). Returns count. */
 int64_t tsg_regex_dfa_ends(const tsg_regex* re, const uint8_t* text, size_t len, uint32_t chunk,
                            int64_t* out, size_t cap);
+
+/* Emulate K1+K2 on the CPU (no resolution) and report, per rule, the number of
+ * candidate end offsets and of files whose keyword gate passed (plan tuning). */
+int tsg_emulate_candidate_stats(const tsg_ruleset* rs, const uint8_t* data,
+                                const uint64_t* offsets, uint32_t nfiles, uint32_t chunk,
+                                uint64_t* cand_per_rule, uint64_t* gated_bytes_per_group);
+
+/* Plan introspection: per rule group id (-1 host-only), relaxation (-1 exact), max len. */
+int tsg_ruleset_rule_plan(const tsg_ruleset* rs, uint32_t rule, int32_t* group, int32_t* relax,
+                          int64_t* max_len);
 
 /* Emulate K1+K2 on the CPU with the GPU algorithm and resolve (tests). */
 int tsg_scan_batch_emulated(const tsg_ruleset* rs, const uint8_t* data, const uint64_t* offsets,

@@ -83,6 +83,10 @@ SIGNATURES = [
                                        C.c_size_t]),
     ("tsg_scan_batch_emulated", C.c_int, [_P, _P, _U64P, C.c_uint32, _P, _U64P, C.c_uint32,
                                           C.POINTER(_P)]),
+    ("tsg_emulate_candidate_stats", C.c_int, [_P, _P, _U64P, C.c_uint32, C.c_uint32, _U64P,
+                                              _U64P]),
+    ("tsg_ruleset_rule_plan", C.c_int, [_P, C.c_uint32, C.POINTER(C.c_int32),
+                                        C.POINTER(C.c_int32), C.POINTER(C.c_int64)]),
 ]
 
 _lib = None

@@ -28,8 +28,8 @@ VOCAB = (
     "request response client server http https json yaml xml html css js go py rs java "
     "for while break continue try catch except finally raise throw async await yield "
     "linear matrix vector hash sha256 md5 base64 encode decode encrypt decrypt cipher "
-    "aws gcp azure heroku slack github gitlab stripe twilio facebook twitter discord "
-    "dropbox mailgun mailchimp linkedin twitch npm pypi ghp_ xoxb- AKIA SK dapi pul- "
+    "aws gcp azure cloud storage bucket region queue cache redis postgres mysql docker "
+    "kubernetes deploy build release version commit branch merge SK "
     "----- ===== ##### // /* */ # -- ; { } ( ) [ ] < > => := = == != += -= && || "
     "0 1 2 3 42 100 1024 0x1f 3.14 2023-01-01 localhost 127.0.0.1 /usr/local/bin "
     "café naïve résumé über 日本語 中文 Ελληνικά кириллица emoji😀 ✓"

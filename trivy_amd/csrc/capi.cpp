@@ -217,6 +217,44 @@ int tsg_scan_batch_emulated(const tsg_ruleset* rs, const uint8_t* data, const ui
   }
 }
 
+int tsg_emulate_candidate_stats(const tsg_ruleset* rs, const uint8_t* data,
+                                const uint64_t* offsets, uint32_t nfiles, uint32_t chunk,
+                                uint64_t* cand_per_rule, uint64_t* gated_bytes_per_group) {
+  if (!rs || !offsets || chunk == 0) return fail(TSG_ERR_ARG, "bad argument");
+  std::vector<uint64_t> poff(nfiles + 1, 0);
+  BatchView b{data, offsets, nfiles, "", poff.data()};
+  KernelOutput ko;
+  emulate_kernels(*rs->plan, b, chunk, 1u << 16, &ko);
+  const Plan& p = *rs->plan;
+  if (cand_per_rule) {
+    std::fill(cand_per_rule, cand_per_rule + rs->rs.rules.size(), 0);
+    for (const auto& c : ko.cand) cand_per_rule[c.rule]++;
+  }
+  if (gated_bytes_per_group) {
+    for (size_t g = 0; g < p.groups.size(); g++) {
+      uint64_t bytes = 0;
+      for (uint32_t f = 0; f < nfiles; f++) {
+        const uint32_t* kw = ko.kw.data() + (size_t)f * p.kw_words;
+        bool gate = p.groups[g].always;
+        for (int w = 0; w < p.kw_words && !gate; w++) gate = (kw[w] & p.groups[g].kwmask[w]) != 0;
+        if (gate) bytes += offsets[f + 1] - offsets[f];
+      }
+      gated_bytes_per_group[g] = bytes;
+    }
+  }
+  return TSG_OK;
+}
+
+int tsg_ruleset_rule_plan(const tsg_ruleset* rs, uint32_t rule, int32_t* group, int32_t* relax,
+                          int64_t* max_len) {
+  if (!rs || rule >= rs->rs.rules.size()) return fail(TSG_ERR_ARG, "bad argument");
+  const Plan& p = *rs->plan;
+  if (group) *group = p.rule_hostonly[rule] ? -1 : p.rule_group[rule];
+  if (relax) *relax = p.rule_relax[rule];
+  if (max_len) *max_len = p.rule_maxlen[rule];
+  return TSG_OK;
+}
+
 const uint8_t* tsg_result_data(const tsg_result* r, size_t* len) {
   if (!r) {
     if (len) *len = 0;

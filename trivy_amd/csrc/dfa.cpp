@@ -101,6 +101,10 @@ bool ranges_contain(const Ranges& r, int32_t c) {
 }
 
 void add_rune_edges(NFA& nfa, uint32_t from, uint32_t to, const Ranges& r) {
+  if (r.size() == 1 && r[0].first == kHighByteRune) {  // relaxed program: any byte >= 0x80
+    nfa.n[from].bytes.push_back({0x80, 0xFF, to});
+    return;
+  }
   std::vector<Seq> seqs;
   for (auto& p : r) split_range(p.first, p.second, &seqs);
   for (auto& s : seqs) {

@@ -800,6 +800,21 @@ class Compiler {
     return f;
   }
 
+  // a prefix of the flattened top-level concatenation (GPU filter programs)
+  Frag finish_atoms(const std::vector<int>& atoms) {
+    Frag f;
+    if (atoms.empty()) {
+      f = nop();
+    } else {
+      f = compile(atoms[0]);
+      for (size_t i = 1; i < atoms.size(); i++) f = cat(f, compile(atoms[i]));
+    }
+    uint32_t m = inst(Op::Match);
+    patch(f.out, m);
+    p_->start = f.i;
+    return f;
+  }
+
  private:
   const std::vector<Node>& n_;
   Prog* p_;
@@ -840,7 +855,7 @@ class Compiler {
     if ((int)slot + 1 > p_->nslots) p_->nslots = (int)slot + 1;
     return f;
   }
-  Frag rune(const Ranges& r) {
+  Frag rune1(const Ranges& r) {
     Frag f;
     f.i = inst(Op::Rune);
     p_->runes.push_back(r);
@@ -848,6 +863,30 @@ class Compiler {
     f.out = {f.i << 1};
     f.nullable = false;
     return f;
+  }
+  Frag rune(const Ranges& r) {
+    if (relax_ < 0 || r.empty() || r.back().second < 0x80) return rune1(r);
+    // relaxed (GPU) program: the ASCII part stays exact, every non-ASCII member of the
+    // set becomes "one or more bytes >= 0x80" -- a superset of any rune's encoding and of
+    // an invalid byte -- so the byte DFA needs no UTF-8 sub-states
+    Ranges ascii;
+    bool other_high = false;
+    for (auto& p : r) {
+      if (p.first < 0x80) ascii.push_back({p.first, std::min<int32_t>(p.second, 0x7F)});
+      for (int32_t lo = std::max<int32_t>(p.first, 0x80); lo <= p.second; lo++) {
+        // U+017F / U+212A only enter a set through (?i) folding of s / k; files that
+        // contain them are resolved whole on the host (K1 fallback keywords), so the
+        // GPU program may ignore them
+        if (lo != 0x17F && lo != 0x212A) {
+          other_high = true;
+          break;
+        }
+      }
+    }
+    if (!other_high) return rune1(ascii);
+    Frag high = plus(rune1({{kHighByteRune, kHighByteRune}}), false);
+    if (ascii.empty()) return high;
+    return alt(rune1(ascii), high);
   }
   Frag cat(Frag f1, Frag f2) {
     if (f1.i == 0 || f2.i == 0) return Frag{};
@@ -1021,11 +1060,36 @@ std::shared_ptr<Regexp> Regexp::Compile(const std::string& src, std::string* err
   return re;
 }
 
-Prog Regexp::RelaxedProg(int k) const {
+// top-level concatenation with captures and nested concatenations flattened
+static void flatten_atoms(const std::vector<Node>& nodes, int idx, std::vector<int>* out) {
+  const Node& n = nodes[idx];
+  if (n.k == NK::Cat) {
+    for (int s : n.sub) flatten_atoms(nodes, s, out);
+  } else if (n.k == NK::Cap) {
+    flatten_atoms(nodes, n.sub[0], out);
+  } else {
+    out->push_back(idx);
+  }
+}
+
+int Regexp::NumAtoms() const {
+  std::vector<int> atoms;
+  flatten_atoms(ast_->nodes, ast_->root, &atoms);
+  return (int)atoms.size();
+}
+
+Prog Regexp::RelaxedProg(int k, int natoms) const {
   Prog p;
   p.nslots = 2 * (ast_->ncap + 1);
   Compiler c(ast_->nodes, &p, k);
-  c.finish(ast_->root);
+  if (natoms < 0) {
+    c.finish(ast_->root);
+  } else {
+    std::vector<int> atoms;
+    flatten_atoms(ast_->nodes, ast_->root, &atoms);
+    atoms.resize(std::min<size_t>(atoms.size(), (size_t)natoms));
+    c.finish_atoms(atoms);
+  }
   p.nslots = 2 * (ast_->ncap + 1);
   return p;
 }
@@ -1252,6 +1316,43 @@ void Regexp::FindAll(const uint8_t* b, size_t n, bool submatch, std::vector<int6
     if (accept) {
       if (submatch) out->insert(out->end(), mc.begin(), mc.begin() + prog_.nslots);
       else out->insert(out->end(), mc.begin(), mc.begin() + 2);
+    }
+  }
+}
+
+void Regexp::FindAllWindows(const uint8_t* b, size_t n, bool submatch,
+                            const std::vector<std::pair<int64_t, int64_t>>& iv,
+                            std::vector<int64_t>* out) const {
+  // Go's allMatches iteration, skipping the stretches in which no match can start:
+  // `pos` and the previous match end carry from one window to the next, so a match
+  // that runs past its window is handled exactly as the global iteration would.
+  Machine m(prog_, prog_.nslots);
+  const int64_t end = (int64_t)n;
+  int64_t pos = 0, prev_end = -1;
+  for (const auto& w : iv) {
+    if (pos > end) break;
+    if (w.first > pos) pos = w.first;
+    const int64_t hi = std::min<int64_t>(w.second, end);
+    while (pos <= end && pos <= hi) {
+      if (!m.run(b, n, pos, hi)) {
+        pos = hi + 1;  // no match starts in [pos, hi]
+        break;
+      }
+      const auto& mc = m.matchcap();
+      bool accept = true;
+      if (mc[1] == pos) {
+        if (mc[0] == prev_end) accept = false;
+        int wd;
+        decode_rune(b, n, (size_t)pos, &wd);
+        pos = wd > 0 ? pos + wd : end + 1;
+      } else {
+        pos = mc[1];
+      }
+      prev_end = mc[1];
+      if (accept) {
+        if (submatch) out->insert(out->end(), mc.begin(), mc.begin() + prog_.nslots);
+        else out->insert(out->end(), mc.begin(), mc.begin() + 2);
+      }
     }
   }
 }

@@ -26,6 +26,8 @@ namespace tsg {
 constexpr int32_t kMaxRune = 0x10FFFF;
 constexpr int32_t kRuneError = 0xFFFD;
 constexpr int32_t kEOT = -1;
+// Pseudo rune used only in relaxed (GPU) programs: "any single byte >= 0x80".
+constexpr int32_t kHighByteRune = 0x110000;
 
 using Ranges = std::vector<std::pair<int32_t, int32_t>>;  // sorted, non-overlapping
 
@@ -77,7 +79,11 @@ class Regexp {
   // match of this one with the same start and end, so its DFA reports a superset of
   // the exact end offsets while avoiding the state blow-up of re-entrant counters
   // such as (?i)lob[a-z0-9_ .\-,]{0,25}.
-  Prog RelaxedProg(int k) const;
+  // natoms >= 0 keeps only that many leading elements of the (flattened) top-level
+  // concatenation: each match of the regex then has a prefix match with the same start.
+  // Non-ASCII members of rune sets become "one or more bytes >= 0x80" (kHighByteRune).
+  Prog RelaxedProg(int k, int natoms = -1) const;
+  int NumAtoms() const;
 
   const std::string& source() const { return src_; }
   const std::vector<std::string>& SubexpNames() const { return names_; }
@@ -96,6 +102,14 @@ class Regexp {
   // start_hi = n this is exactly Go's FindAll.
   void FindAll(const uint8_t* b, size_t n, bool submatch, std::vector<int64_t>* out,
                size_t lo = 0, size_t start_hi = SIZE_MAX) const;
+
+  // Go's FindAll iteration restricted to match STARTS inside the given windows
+  // [lo, hi] (sorted, disjoint, lo on a rune boundary).  The iteration position and the
+  // previous match end carry across windows, so the result equals FindAll whenever
+  // every match start lies in some window -- matches may end beyond their window.
+  void FindAllWindows(const uint8_t* b, size_t n, bool submatch,
+                      const std::vector<std::pair<int64_t, int64_t>>& iv,
+                      std::vector<int64_t>* out) const;
 
  private:
   struct Ast;

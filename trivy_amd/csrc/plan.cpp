@@ -51,7 +51,8 @@ std::unique_ptr<Plan> build_plan(const Ruleset& rs, const PlanOptions& opt, std:
   }
   p->fb_kw0 = (int)kws.size();
   kws.push_back("\xc4\xb0");      // U+0130, bytes.ToLower -> "i"
-  kws.push_back("\xe2\x84\xaa");  // U+212A, bytes.ToLower -> "k"
+  kws.push_back("\xe2\x84\xaa");  // U+212A, bytes.ToLower -> "k"; (?i)k folds to it
+  kws.push_back("\xc5\xbf");      // U+017F, (?i)s folds to it
   p->n_kw = (int)kws.size();
   p->kw_words = (p->n_kw + 31) / 32;
   {
@@ -98,12 +99,16 @@ std::unique_ptr<Plan> build_plan(const Ruleset& rs, const PlanOptions& opt, std:
     cur.clear();
   };
   p->rule_relax.assign(R, -1);
+  p->rule_atoms.assign(R, -1);
+  p->rule_winback.assign(R, -1);
   p->rule_prog.assign(R, Prog{});
   for (size_t r = 0; r < R; r++) {
     const RuleC& rule = rs.rules[r];
     if (!rule.regex) continue;
     p->rule_maxlen[r] = max_match_len(rule.regex->prog());
-    // exact program first, then ever stronger relaxations of counted repetitions
+    p->rule_winback[r] = p->rule_maxlen[r];
+    // exact program first, then ever stronger relaxations of counted repetitions, then
+    // ever shorter prefixes of the top-level concatenation
     std::unique_ptr<DFA> single;
     for (int k : {-1, 32, 16, 8, 4, 2, 1, 0}) {
       Prog pr = k < 0 ? rule.regex->prog() : rule.regex->RelaxedProg(k);
@@ -114,6 +119,21 @@ std::unique_ptr<Plan> build_plan(const Ruleset& rs, const PlanOptions& opt, std:
         p->rule_relax[r] = k;
         p->rule_prog[r] = std::move(pr);
         break;
+      }
+    }
+    for (int t = rule.regex->NumAtoms() - 1; !single && t >= 1; t--) {
+      for (int k : {8, 2, 0}) {
+        Prog pr = rule.regex->RelaxedProg(k, t);
+        std::string e;
+        auto d = build_dfa({&pr}, one, &e);
+        if (d && fits(*d, 1)) {
+          single = std::move(d);
+          p->rule_relax[r] = k;
+          p->rule_atoms[r] = t;
+          p->rule_prog[r] = std::move(pr);
+          p->rule_winback[r] = max_match_len(rule.regex->RelaxedProg(-1, t));
+          break;
+        }
       }
     }
     if (!single) {
@@ -258,7 +278,9 @@ void resolve_batch(const Ruleset& rs, const Plan& plan, const BatchView& b,
           return 0;
       }
     };
-    const bool ovf = !ko.overflow.empty() && ko.overflow[f];
+    // kernel overflow, or a folding rune (U+0130/U+212A/U+017F) the GPU programs ignore:
+    // resolve every rule over the whole file
+    const bool ovf = (!ko.overflow.empty() && ko.overflow[f]) || fb;
     bool any_host = false;
     for (uint32_t r : hostonly)
       if (kw_state(r) != 0) any_host = true;
@@ -288,18 +310,15 @@ void resolve_batch(const Ruleset& rs, const Plan& plan, const BatchView& b,
       RuleWindows& w = wins[r];
       wptr[r] = &w;
       if (!w.whole) {
-        const int64_t M = plan.rule_maxlen[r];
-        if (M < 0) {
-          w.whole = true;
-        } else {
-          for (uint32_t j = k; j < e; j++) {
-            int64_t end = cand[j].end;
-            int64_t lo = align_rune(content, n, std::max<int64_t>(0, end - M));
-            if (!w.iv.empty() && lo <= w.iv.back().second + 1) {
-              w.iv.back().second = std::max<int64_t>(w.iv.back().second, end);
-            } else {
-              w.iv.push_back({lo, end});
-            }
+        // every match start lies in [end - winback, end] of some candidate end offset
+        const int64_t back = plan.rule_winback[r];
+        for (uint32_t j = k; j < e; j++) {
+          int64_t end = cand[j].end;
+          int64_t lo = back < 0 ? 0 : align_rune(content, n, std::max<int64_t>(0, end - back));
+          if (!w.iv.empty() && lo <= w.iv.back().second + 1) {
+            w.iv.back().second = std::max<int64_t>(w.iv.back().second, end);
+          } else {
+            w.iv.push_back({lo, end});
           }
         }
       }

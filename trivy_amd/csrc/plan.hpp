@@ -31,7 +31,7 @@ struct GroupPlan {
 
 struct Plan {
   std::unique_ptr<DFA> kw_dfa;
-  int n_kw = 0;        // keyword ids incl. the 2 fallback pseudo keywords at the end
+  int n_kw = 0;        // keyword ids incl. the 3 fallback pseudo keywords at the end
   int kw_words = 1;    // 32-bit words per file
   int fb_kw0 = 0;      // first fallback pseudo keyword id
   std::vector<uint8_t> rule_kw_mode;            // per rule
@@ -41,6 +41,9 @@ struct Plan {
   std::vector<uint8_t> rule_hostonly;  // regex without a GPU DFA (host scans gated files)
   std::vector<int64_t> rule_maxlen;  // longest EXACT match in bytes, -1 unbounded
   std::vector<int> rule_relax;       // relaxation used for the GPU program (-1 exact)
+  std::vector<int> rule_atoms;       // GPU program = prefix of this many atoms (-1 = all)
+  // a GPU end offset e says "a match may START in [e - winback, e]" (-1: anywhere before e)
+  std::vector<int64_t> rule_winback;
   std::vector<Prog> rule_prog;       // the program the rule's GPU DFA was built from
   std::unique_ptr<DFA> allow_path_dfa;  // Global.AllowPath on ASCII paths
 };

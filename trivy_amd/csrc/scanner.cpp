@@ -378,7 +378,7 @@ void scan_file(const Ruleset& rs, const std::string& path, const uint8_t* conten
     if (!win || win->whole) {
       r.regex->FindAll(content, n, sub, &idx);
     } else {
-      for (const auto& iv : win->iv) r.regex->FindAll(content, n, sub, &idx, iv.first, iv.second);
+      r.regex->FindAllWindows(content, n, sub, win->iv, &idx);
     }
     std::vector<Loc> locs;
     for (size_t k = 0; k + ns - 1 < idx.size(); k += ns) {
