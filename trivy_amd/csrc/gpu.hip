@@ -141,6 +141,10 @@ __device__ __forceinline__ uint32_t ctx_of(uint8_t c) {
   return 3;
 }
 
+// dense items are kStreams consecutive chunks; inside one file they are stepped as
+// kStreams interleaved DFA chains (ILP to cover the LDS latency)
+constexpr int kStreams = 4;
+
 struct ScanArgsDev {
   const uint8_t* data;
   const uint64_t* off;
@@ -170,6 +174,8 @@ struct Lane {
   uint32_t file;
   uint64_t fs;
 
+  // rare path (an accept); the unrolled loops below never call it directly: they only OR
+  // the accept bits of 16 transitions and replay the word through step() when one is set
   __device__ __forceinline__ void emit(uint32_t mi, uint64_t pos) {
     const uint64_t* m = (d.state_acc && mi < d.nmasks) ? s_masks + (size_t)mi * d.mw : d.masks + (size_t)mi * d.mw;
     if (KW) {
@@ -202,11 +208,124 @@ struct Lane {
     return e & 0x7FFFu;
   }
 
+  // transition only; accept bit returned in bit 15
+  __device__ __forceinline__ uint32_t fast(uint32_t s, uint32_t byte) const {
+    return s_tab[s * d.nc + s_cls[byte]];
+  }
+
+  // 16 bytes: tight loop, then a (rare) replay with accept handling
   __device__ __forceinline__ uint32_t step16(uint32_t s, const uint4 v, uint64_t p) {
     const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
+    const uint32_t s0 = s;
+    uint32_t any = 0;
 #pragma unroll
-    for (int k = 0; k < 16; k++) s = step(s, (wv[k >> 2] >> ((k & 3) * 8)) & 0xFF, p + k);
+    for (int k = 0; k < 16; k++) {
+      const uint32_t e = fast(s, (wv[k >> 2] >> ((k & 3) * 8)) & 0xFF);
+      any |= e;
+      s = e & 0x7FFFu;
+    }
+    if (__builtin_expect(any & 0x8000u, 0)) replay16(s0, v, p);
     return s;
+  }
+
+  // no dynamically indexed arrays (they would live in scratch): bytes are selected
+  __device__ __forceinline__ void replay16(uint32_t s, const uint4 v, uint64_t p) {
+#pragma unroll 1
+    for (uint32_t k = 0; k < 16; k++) {
+      const uint32_t w = k < 8 ? (k < 4 ? v.x : v.y) : (k < 12 ? v.z : v.w);
+      s = step(s, (w >> ((k & 3) * 8)) & 0xFF, p + k);
+    }
+  }
+
+  // tail of a stream that ends at b (< fe): K1 keyword overlap / K2 noinject follow-up
+  __device__ __forceinline__ void tail(uint32_t s, uint64_t fe, uint64_t b) {
+    const uint8_t* data = A.data;
+    if (KW) {
+      const uint64_t le = min(fe, b + d.ext);
+      uint64_t q = b;
+      for (; q < le; q++) s = step(s, data[q], q);
+      if (q >= fe) {
+        const uint32_t m = d.eot[s];
+        if (m) emit(m, fe);
+      }
+      return;
+    }
+    if (b >= fe) {
+      const uint32_t m = d.eot[s];
+      if (m) emit(m, fe);
+      return;
+    }
+    s = d.to_ni[s];
+    uint64_t q = b;
+    while (q < fe && !d.dead[s]) {
+      if (q - b >= A.ext_cap) {
+        A.ovf[file] = 1;
+        return;
+      }
+      s = step(s, data[q], q);
+      q++;
+    }
+    if (q == fe && !d.dead[s]) {
+      const uint32_t m = d.eot[s];
+      if (m) emit(m, fe);
+    }
+  }
+
+  // NS consecutive chunks [a, a + NS*C) that all lie inside file [fs, fe): NS independent
+  // DFA chains interleaved byte by byte, so NS LDS look-ups are in flight per lane
+  template <int NS>
+  __device__ void streams(uint64_t fe, uint64_t a, uint32_t C) {
+    const uint8_t* data = A.data;
+    if (KW)
+      for (uint32_t w = 0; w < A.kw_words; w++) s_kwacc[w * blockDim.x + threadIdx.x] = 0;
+    uint32_t s[NS];
+#pragma unroll
+    for (int i = 0; i < NS; i++) {
+      const uint64_t b0 = a + (uint64_t)i * C;
+      s[i] = (b0 == fs) ? d.start[0] : d.start[ctx_of(data[b0 - 1])];
+    }
+    uint4 cur[NS];
+#pragma unroll
+    for (int i = 0; i < NS; i++) cur[i] = *(const uint4*)(data + a + (uint64_t)i * C);
+    for (uint32_t j = 0; j < C; j += 16) {
+      uint4 nxt[NS];
+#pragma unroll
+      for (int i = 0; i < NS; i++) nxt[i] = *(const uint4*)(data + a + (uint64_t)i * C + j + 16);
+      uint32_t wv[NS][4];
+#pragma unroll
+      for (int i = 0; i < NS; i++) {
+        wv[i][0] = cur[i].x;
+        wv[i][1] = cur[i].y;
+        wv[i][2] = cur[i].z;
+        wv[i][3] = cur[i].w;
+      }
+      uint32_t s0[NS], any[NS];
+#pragma unroll
+      for (int i = 0; i < NS; i++) {
+        s0[i] = s[i];
+        any[i] = 0;
+      }
+#pragma unroll
+      for (int k = 0; k < 16; k++)
+#pragma unroll
+        for (int i = 0; i < NS; i++) {
+          const uint32_t e = fast(s[i], (wv[i][k >> 2] >> ((k & 3) * 8)) & 0xFF);
+          any[i] |= e;
+          s[i] = e & 0x7FFFu;
+        }
+#pragma unroll
+      for (int i = 0; i < NS; i++)
+        if (__builtin_expect(any[i] & 0x8000u, 0)) replay16(s0[i], cur[i], a + (uint64_t)i * C + j);
+#pragma unroll
+      for (int i = 0; i < NS; i++) cur[i] = nxt[i];
+    }
+#pragma unroll
+    for (int i = 0; i < NS; i++) tail(s[i], fe, a + (uint64_t)(i + 1) * C);
+    if (KW)
+      for (uint32_t w = 0; w < A.kw_words; w++) {
+        uint32_t v = s_kwacc[w * blockDim.x + threadIdx.x];
+        if (v) atomicOr(&A.kw[(size_t)file * A.kw_words + w], v);
+      }
   }
 
   // one file piece [a, se) of file [fs, fe)
@@ -302,15 +421,28 @@ __global__ void __launch_bounds__(256) dfa_scan_kernel(DevDFA d, ScanArgsDev A) 
         L.piece(fe, a, b);
       }
     } else {
-      uint64_t a = it * A.chunk;
-      const uint64_t b = min(a + A.chunk, A.total);
-      uint32_t f = A.chunk_file[it];
+      // item = kStreams consecutive chunks
+      uint64_t a = it * kStreams * A.chunk;
+      const uint64_t b = min(a + (uint64_t)kStreams * A.chunk, A.total);
+      uint32_t f = A.chunk_file[it * kStreams];
+      {
+        const uint64_t fs = A.off[f], fe = A.off[f + 1];
+        if (b == a + (uint64_t)kStreams * A.chunk && b <= fe) {  // common case: one file
+          if (KW || group_gated(A.kw + (size_t)f * A.kw_words, A.gmask, A.kw_words, A.galways)) {
+            L.file = f;
+            L.fs = fs;
+            L.template streams<kStreams>(fe, a, A.chunk);
+          }
+          continue;
+        }
+      }
       while (a < b) {
         const uint64_t fs = A.off[f], fe = A.off[f + 1];
         if (fe == fs) {
           f++;
           continue;
         }
+        // the lane owns every match start in [item start, b): pieces may span chunks
         const uint64_t se = min(b, fe);
         if (KW || group_gated(A.kw + (size_t)f * A.kw_words, A.gmask, A.kw_words, A.galways)) {
           L.file = f;
@@ -635,7 +767,7 @@ int tsg_batch_kernels(tsg_ctx* c) {
   A.ovf = c->d_ovf;
   int rc;
   // ---- K1
-  A.nitems = nchunks;
+  A.nitems = (nchunks + kStreams - 1) / kStreams;
   if ((rc = launch_scan<true, false>(c, c->kw.dev, A))) return rc;
   HIP_TRY(hipEventRecord(c->ev[2], st));
   // ---- gate: per-group gated bytes / files
@@ -687,7 +819,7 @@ int tsg_batch_kernels(tsg_ctx* c) {
   // ---- K2
   for (uint32_t g : dense_groups) {
     ScanArgsDev B = A;
-    B.nitems = nchunks;
+    B.nitems = (nchunks + kStreams - 1) / kStreams;
     B.gmask = c->d_gmask + (size_t)g * W;
     B.galways = p.groups[g].always ? 1 : 0;
     if ((rc = launch_scan<false, false>(c, c->groups[g].dev, B))) return rc;
