@@ -143,18 +143,24 @@ int tsg_scan_batch(tsg_ctx* ctx, const uint8_t* data, const uint64_t* offsets, u
                    const char* paths, const uint64_t* path_offsets, tsg_result** out);
 
 typedef struct tsg_stats {
-  double k1_ms;          /* keyword kernel, last batch (HIP events on the ctx stream) */
-  double k2_ms;          /* all rule-group kernel launches, last batch */
+  double k1_ms;          /* K1 literal automaton + run counters, last batch (HIP events) */
+  double k2_ms;          /* all rule-group (K2) launches, last batch */
   double aux_ms;         /* memsets + candidate/keyword downloads */
   double resolve_ms;     /* host exact resolution (wall) */
   uint64_t bytes;        /* content bytes of the batch */
-  uint64_t k2_bytes;     /* content bytes scanned by K2 (sum over groups of gated bytes) */
+  uint64_t k2_bytes;     /* chunk bytes K2 scans (sum over groups of item bytes) */
   uint64_t candidates;   /* candidate records produced */
   uint64_t files_resolved;  /* files that needed exact host work */
   uint32_t k2_launches;
   uint32_t overflow;     /* 1 if the candidate buffer overflowed (files resolved whole) */
+  double gate_ms;        /* keyword gates + K2 item lists (incl. one host round trip) */
+  uint64_t k2_items;     /* (file, chunk) items of the sparse K2 launch */
 } tsg_stats;
 int tsg_ctx_get_stats(const tsg_ctx* ctx, tsg_stats* out);
+
+/* K1 output of the last tsg_batch_kernels: keyword bits [nfiles * kw_words] and chunk
+ * event bits [ceil(bytes / chunk_bytes)] (test hook; either pointer may be NULL). */
+int tsg_batch_k1_output(tsg_ctx* ctx, uint32_t* kw, size_t kw_len, uint32_t* ev, size_t ev_len);
 
 const char* tsg_last_error(void);
 
@@ -175,14 +181,26 @@ int64_t tsg_regex_dfa_ends(const tsg_regex* re, const uint8_t* text, size_t len,
                            int64_t* out, size_t cap);
 
 /* Emulate K1+K2 on the CPU (no resolution) and report, per rule, the number of
- * candidate end offsets and of files whose keyword gate passed (plan tuning). */
+ * candidate end offsets, and per rule group the bytes K2 scans (plan tuning). */
 int tsg_emulate_candidate_stats(const tsg_ruleset* rs, const uint8_t* data,
                                 const uint64_t* offsets, uint32_t nfiles, uint32_t chunk,
                                 uint64_t* cand_per_rule, uint64_t* gated_bytes_per_group);
 
+/* K1 reference semantics on the CPU (plan.hpp k1_reference): same layout as
+ * tsg_batch_k1_output. */
+int tsg_emulate_k1(const tsg_ruleset* rs, const uint8_t* data, const uint64_t* offsets,
+                   uint32_t nfiles, uint32_t chunk, uint32_t* kw, size_t kw_len, uint32_t* ev,
+                   size_t ev_len);
+
 /* Plan introspection: per rule group id (-1 host-only), relaxation (-1 exact), max len. */
 int tsg_ruleset_rule_plan(const tsg_ruleset* rs, uint32_t rule, int32_t* group, int32_t* relax,
                           int64_t* max_len);
+
+/* Plan introspection: the rule's K1 event bits (1 run U, 2 run D, 4.. literal classes,
+ * 1<<31 none), the largest distance from a GPU-program match start to its event byte,
+ * and a description of the anchor. */
+int tsg_ruleset_rule_anchor(const tsg_ruleset* rs, uint32_t rule, uint32_t* event, int64_t* evdist,
+                            char* desc, size_t desc_len);
 
 /* Emulate K1+K2 on the CPU with the GPU algorithm and resolve (tests). */
 int tsg_scan_batch_emulated(const tsg_ruleset* rs, const uint8_t* data, const uint64_t* offsets,

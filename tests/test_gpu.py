@@ -60,6 +60,44 @@ def test_corpus_vs_emulation(builtin, chunk):
     assert got == want
 
 
+def _small_files_batch(seed):
+    """Many tiny and empty files (shorter than the K1 warm-up) between normal ones."""
+    import numpy as np
+    rng = np.random.default_rng(seed)
+    big, _ = corpus.make_corpus(1 << 20, seed=seed, plants_per_mib=200)
+    args = []
+    for i in range(big.nfiles):
+        c = bytes(big.data[int(big.offsets[i]):int(big.offsets[i + 1])])
+        args.append(S.ScanArgs(big.path(i), c))
+        if i % 3 == 0:
+            n = int(rng.integers(0, 40))
+            args.append(S.ScanArgs("t/%d.txt" % i, (b"key sk account ghp_ " * 3)[:n]))
+        if i % 7 == 0:
+            args.append(S.ScanArgs("e/%d.txt" % i, b""))
+    return S.Batch.from_args(args)
+
+
+@pytest.mark.parametrize("chunk", [16, 48, 256, 1024])
+def test_k1_matches_reference(builtin, chunk):
+    """K1 keyword bits and chunk events are exactly the reference semantics."""
+    import numpy as np
+    batch = _small_files_batch(chunk)
+    ctx = S.GpuContext(builtin, 0, chunk_bytes=chunk)
+    ctx.upload(batch)
+    ctx.kernels()
+    kw, ev = ctx.k1_output(chunk)
+    ctx.close()
+    rkw, rev = builtin.k1_reference(batch, chunk)
+    assert np.array_equal(kw, rkw)
+    assert np.array_equal(ev, rev)
+    assert (ev & 1).any() and (ev >> 2).any()
+
+
+def test_small_files_vs_cpu_exact(builtin):
+    batch = _small_files_batch(5)
+    assert builtin.ScanBatch(batch, device=0) == builtin.ScanBatch(batch, nthreads=16)
+
+
 def test_corpus_vs_oracle(builtin):
     from oracle import secret as O
     batch, _ = corpus.make_corpus(256 << 10, seed=7, plants_per_mib=300)

@@ -28,6 +28,8 @@ def main():
         e2e = time.perf_counter() - t
         st = ctx.stats()
         print(json.dumps({"chunk": ch, "k1_ms": round(best["k1_ms"], 3), "k2_ms": round(best["k2_ms"], 3),
+                          "gate_ms": round(best["gate_ms"], 3), "items": best["k2_items"],
+                          "k2_bytes": best["k2_bytes"],
                           "k1_GBps": round(info["bytes"] / best["k1_ms"] / 1e6, 1),
                           "resolve_ms": round(st["resolve_ms"], 1), "e2e_ms": round(e2e * 1e3, 1),
                           "cands": st["candidates"], "launches": st["k2_launches"]}), flush=True)

@@ -1,6 +1,9 @@
 #!/usr/bin/env python3
-"""Plan tuning report: per-rule GPU plan and candidate counts on a synthetic corpus
-(emulated kernels on the CPU)."""
+"""Plan tuning report: per-rule GPU plan (anchor event, group, relaxation) and candidate
+counts, plus the bytes K2 scans per group, on a synthetic corpus (emulated kernels, CPU).
+
+    python tools/plan_stats.py [MiB] [seed] [chunk]
+"""
 import ctypes as C
 import sys
 import os
@@ -23,17 +26,20 @@ def main(mb=64, seed=2, chunk=256):
     N.check(L.tsg_emulate_candidate_stats(sc.handle, C.c_void_p(b.data.ctypes.data),
                                           b.offsets.ctypes.data_as(u64p), b.nfiles, chunk,
                                           cpr.ctypes.data_as(u64p), gb.ctypes.data_as(u64p)))
-    print("emulated in %.1fs; corpus %s" % (time.time() - t, info))
+    print("emulated in %.1fs; corpus %s; plan %s" % (time.time() - t, info, info_))
     rows = []
     for r in range(R):
         g, rl, ml = C.c_int32(), C.c_int32(), C.c_int64()
         L.tsg_ruleset_rule_plan(sc.handle, r, C.byref(g), C.byref(rl), C.byref(ml))
+        ev, ed = C.c_uint32(), C.c_int64()
+        desc = C.create_string_buffer(128)
+        L.tsg_ruleset_rule_anchor(sc.handle, r, C.byref(ev), C.byref(ed), desc, 128)
         rows.append((int(cpr[r]), sc.Rules[r].ID, g.value, rl.value, ml.value,
-                     int(gb[g.value]) if g.value >= 0 else -1))
+                     int(gb[g.value]) if g.value >= 0 else -1, ev.value, ed.value, desc.value.decode()))
     for row in sorted(rows, reverse=True):
-        print("%8d cand  %-32s group=%3d relax=%3d maxlen=%5d gated=%.1f%%" % (
-            row[0], row[1], row[2], row[3], row[4], 100.0 * row[5] / info["bytes"]))
-    print("total gated bytes over groups: %.2fx corpus" % (gb.sum() / info["bytes"]))
+        print("%7d cand %-30s g=%3d relax=%3d maxlen=%5d k2=%6.2f%% ev=%08x d=%4d %s" % (
+            row[0], row[1], row[2], row[3], row[4], 100.0 * row[5] / info["bytes"], row[6], row[7], row[8]))
+    print("K2 bytes over all groups: %.4fx corpus" % (gb.sum() / info["bytes"]))
 
 
 if __name__ == "__main__":

@@ -46,7 +46,8 @@ class Stats(C.Structure):
     _fields_ = [("k1_ms", C.c_double), ("k2_ms", C.c_double), ("aux_ms", C.c_double),
                 ("resolve_ms", C.c_double), ("bytes", C.c_uint64), ("k2_bytes", C.c_uint64),
                 ("candidates", C.c_uint64), ("files_resolved", C.c_uint64),
-                ("k2_launches", C.c_uint32), ("overflow", C.c_uint32)]
+                ("k2_launches", C.c_uint32), ("overflow", C.c_uint32),
+                ("gate_ms", C.c_double), ("k2_items", C.c_uint64)]
 
 
 # (name, restype, argtypes) -- every symbol include/trivy_secret.h declares
@@ -87,6 +88,12 @@ SIGNATURES = [
                                               _U64P]),
     ("tsg_ruleset_rule_plan", C.c_int, [_P, C.c_uint32, C.POINTER(C.c_int32),
                                         C.POINTER(C.c_int32), C.POINTER(C.c_int64)]),
+    ("tsg_batch_k1_output", C.c_int, [_P, C.POINTER(C.c_uint32), C.c_size_t,
+                                      C.POINTER(C.c_uint32), C.c_size_t]),
+    ("tsg_emulate_k1", C.c_int, [_P, _P, _U64P, C.c_uint32, C.c_uint32, C.POINTER(C.c_uint32),
+                                 C.c_size_t, C.POINTER(C.c_uint32), C.c_size_t]),
+    ("tsg_ruleset_rule_anchor", C.c_int, [_P, C.c_uint32, C.POINTER(C.c_uint32),
+                                          C.POINTER(C.c_int64), C.c_char_p, C.c_size_t]),
 ]
 
 _lib = None

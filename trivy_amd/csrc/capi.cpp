@@ -224,24 +224,26 @@ int tsg_emulate_candidate_stats(const tsg_ruleset* rs, const uint8_t* data,
   std::vector<uint64_t> poff(nfiles + 1, 0);
   BatchView b{data, offsets, nfiles, "", poff.data()};
   KernelOutput ko;
-  emulate_kernels(*rs->plan, b, chunk, 1u << 16, &ko);
-  const Plan& p = *rs->plan;
+  std::vector<uint64_t> gib;
+  emulate_kernels(*rs->plan, b, chunk, 1u << 16, &ko, &gib);
   if (cand_per_rule) {
     std::fill(cand_per_rule, cand_per_rule + rs->rs.rules.size(), 0);
     for (const auto& c : ko.cand) cand_per_rule[c.rule]++;
   }
-  if (gated_bytes_per_group) {
-    for (size_t g = 0; g < p.groups.size(); g++) {
-      uint64_t bytes = 0;
-      for (uint32_t f = 0; f < nfiles; f++) {
-        const uint32_t* kw = ko.kw.data() + (size_t)f * p.kw_words;
-        bool gate = p.groups[g].always;
-        for (int w = 0; w < p.kw_words && !gate; w++) gate = (kw[w] & p.groups[g].kwmask[w]) != 0;
-        if (gate) bytes += offsets[f + 1] - offsets[f];
-      }
-      gated_bytes_per_group[g] = bytes;
-    }
-  }
+  if (gated_bytes_per_group) std::copy(gib.begin(), gib.end(), gated_bytes_per_group);
+  return TSG_OK;
+}
+
+int tsg_emulate_k1(const tsg_ruleset* rs, const uint8_t* data, const uint64_t* offsets,
+                   uint32_t nfiles, uint32_t chunk, uint32_t* kw, size_t kw_len, uint32_t* ev,
+                   size_t ev_len) {
+  if (!rs || !offsets || chunk == 0) return fail(TSG_ERR_ARG, "bad argument");
+  std::vector<uint64_t> poff(nfiles + 1, 0);
+  BatchView b{data, offsets, nfiles, "", poff.data()};
+  std::vector<uint32_t> k, e;
+  k1_reference(*rs->plan, b, chunk, &k, &e);
+  if (kw) std::memcpy(kw, k.data(), sizeof(uint32_t) * std::min(kw_len, k.size()));
+  if (ev) std::memcpy(ev, e.data(), sizeof(uint32_t) * std::min(ev_len, e.size()));
   return TSG_OK;
 }
 
@@ -252,6 +254,16 @@ int tsg_ruleset_rule_plan(const tsg_ruleset* rs, uint32_t rule, int32_t* group, 
   if (group) *group = p.rule_hostonly[rule] ? -1 : p.rule_group[rule];
   if (relax) *relax = p.rule_relax[rule];
   if (max_len) *max_len = p.rule_maxlen[rule];
+  return TSG_OK;
+}
+
+int tsg_ruleset_rule_anchor(const tsg_ruleset* rs, uint32_t rule, uint32_t* event, int64_t* evdist,
+                            char* desc, size_t desc_len) {
+  if (!rs || rule >= rs->rs.rules.size()) return fail(TSG_ERR_ARG, "bad argument");
+  const Plan& p = *rs->plan;
+  if (event) *event = p.rule_event[rule];
+  if (evdist) *evdist = p.rule_evdist[rule];
+  copy_err(p.rule_anchor[rule], desc, desc_len);
   return TSG_OK;
 }
 
@@ -315,6 +327,7 @@ int64_t tsg_regex_dfa_ends(const tsg_regex* re, const uint8_t* text, size_t len,
   p.kw_words = 1;
   p.fb_kw0 = 0;
   p.kw_dfa = build_keyword_dfa({}, o, &e);
+  p.kw_mask_events.assign(p.kw_dfa->masks.size(), 0);
   GroupPlan g;
   g.dfa = std::move(d);
   g.rules = {0};

@@ -1078,20 +1078,123 @@ int Regexp::NumAtoms() const {
   return (int)atoms.size();
 }
 
-Prog Regexp::RelaxedProg(int k, int natoms) const {
+Prog Regexp::RelaxedProg(int k, int natoms, int first_atom) const {
   Prog p;
   p.nslots = 2 * (ast_->ncap + 1);
   Compiler c(ast_->nodes, &p, k);
-  if (natoms < 0) {
+  if (natoms < 0 && first_atom <= 0) {
     c.finish(ast_->root);
   } else {
     std::vector<int> atoms;
     flatten_atoms(ast_->nodes, ast_->root, &atoms);
-    atoms.resize(std::min<size_t>(atoms.size(), (size_t)natoms));
-    c.finish_atoms(atoms);
+    size_t a = std::min<size_t>(atoms.size(), (size_t)std::max(first_atom, 0));
+    size_t b = natoms < 0 ? atoms.size() : std::min<size_t>(atoms.size(), a + (size_t)natoms);
+    c.finish_atoms(std::vector<int>(atoms.begin() + a, atoms.begin() + b));
   }
   p.nslots = 2 * (ast_->ncap + 1);
   return p;
+}
+
+// ------------------------------------------------------------------ atom shapes
+static int utf8_width(int32_t r) { return r < 0x80 ? 1 : r < 0x800 ? 2 : r < 0x10000 ? 3 : 4; }
+
+static AtomInfo node_info(const std::vector<Node>& nodes, int idx) {
+  const Node& n = nodes[idx];
+  AtomInfo a;
+  auto cat = [](AtomInfo x, const AtomInfo& y) {
+    x.min_bytes += y.min_bytes;
+    x.max_bytes = (x.max_bytes < 0 || y.max_bytes < 0) ? -1 : x.max_bytes + y.max_bytes;
+    x.ascii_only = x.ascii_only && y.ascii_only;
+    x.set[0] |= y.set[0];
+    x.set[1] |= y.set[1];
+    x.lit = -1;
+    return x;
+  };
+  switch (n.k) {
+    case NK::Rune: {
+      a.min_bytes = 1;
+      a.max_bytes = 1;
+      for (auto& p : n.r) {
+        for (int32_t c = p.first; c <= std::min<int32_t>(p.second, 0x7F); c++)
+          a.set[c >> 6] |= 1ull << (c & 63);
+        if (p.second >= 0x80) {
+          // the only non-ASCII members (?i) folds into ASCII letters (see AtomInfo)
+          bool only_fold = true;
+          for (int32_t c = std::max<int32_t>(p.first, 0x80); c <= p.second && only_fold; c++)
+            only_fold = c == 0x17F || c == 0x212A;
+          if (!only_fold) {
+            a.ascii_only = false;
+            a.max_bytes = std::max<int64_t>(a.max_bytes, utf8_width(p.second));
+            if (p.first <= 0xFFFD && 0xFFFD <= p.second) a.max_bytes = std::max<int64_t>(a.max_bytes, 3);
+          }
+        }
+      }
+      const int cnt = __builtin_popcountll(a.set[0]) + __builtin_popcountll(a.set[1]);
+      auto has = [&](int c) { return (a.set[c >> 6] >> (c & 63)) & 1; };
+      if (a.ascii_only && cnt == 1) {
+        int c = a.set[0] ? __builtin_ctzll(a.set[0]) : 64 + __builtin_ctzll(a.set[1]);
+        a.lit = (c >= 'A' && c <= 'Z') ? c + 32 : c;
+      } else if (a.ascii_only && cnt == 2) {
+        for (int c = 'a'; c <= 'z'; c++)
+          if (has(c) && has(c - 32)) {
+            a.lit = c;
+            a.lit_fold = true;
+          }
+      }
+      return a;
+    }
+    case NK::Cap:
+      return node_info(nodes, n.sub[0]);
+    case NK::Cat: {
+      for (size_t i = 0; i < n.sub.size(); i++) a = cat(a, node_info(nodes, n.sub[i]));
+      if (n.sub.size() == 1) a = node_info(nodes, n.sub[0]);
+      return a;
+    }
+    case NK::Alt: {
+      bool first = true;
+      for (int s : n.sub) {
+        AtomInfo b = node_info(nodes, s);
+        if (first) {
+          a = b;
+          first = false;
+        } else {
+          a.min_bytes = std::min(a.min_bytes, b.min_bytes);
+          a.max_bytes = (a.max_bytes < 0 || b.max_bytes < 0) ? -1 : std::max(a.max_bytes, b.max_bytes);
+          a.ascii_only = a.ascii_only && b.ascii_only;
+          a.set[0] |= b.set[0];
+          a.set[1] |= b.set[1];
+          a.lit = -1;
+        }
+      }
+      a.lit = -1;
+      return a;
+    }
+    case NK::Star:
+    case NK::Plus:
+    case NK::Quest:
+    case NK::Repeat: {
+      AtomInfo b = node_info(nodes, n.sub[0]);
+      int64_t lo = n.k == NK::Plus ? 1 : n.k == NK::Repeat ? n.min : 0;
+      int64_t hi = n.k == NK::Quest ? 1 : n.k == NK::Repeat ? n.max : -1;
+      a = b;
+      a.lit = -1;
+      a.min_bytes = lo * b.min_bytes;
+      a.max_bytes = (hi < 0 || b.max_bytes < 0) ? (b.max_bytes == 0 ? 0 : -1) : hi * b.max_bytes;
+      return a;
+    }
+    case NK::NoMatch:
+    case NK::Empty:
+    default:
+      return a;  // assertions and empty: zero width
+  }
+}
+
+std::vector<AtomInfo> Regexp::Atoms() const {
+  std::vector<int> atoms;
+  flatten_atoms(ast_->nodes, ast_->root, &atoms);
+  std::vector<AtomInfo> out;
+  for (int i : atoms) out.push_back(node_info(ast_->nodes, i));
+  return out;
 }
 
 // ------------------------------------------------------------------ Pike VM

@@ -31,6 +31,18 @@ constexpr int32_t kHighByteRune = 0x110000;
 
 using Ranges = std::vector<std::pair<int32_t, int32_t>>;  // sorted, non-overlapping
 
+// Shape of one element of a regex's flattened top-level concatenation, for choosing
+// the GPU anchor of a rule (plan.cpp).  Runes U+017F / U+212A (the only non-ASCII
+// members (?i) adds to ASCII letters) are ignored: files containing them are resolved
+// whole on the host.
+struct AtomInfo {
+  int64_t min_bytes = 0, max_bytes = 0;  // bytes one occurrence consumes; max -1 = unbounded
+  bool ascii_only = true;                // consumes only ASCII bytes
+  uint64_t set[2] = {0, 0};              // ASCII bytes it can consume
+  int lit = -1;                          // a single char, ASCII-case-folded: its lowercase
+  bool lit_fold = false;                 // lit matched case-insensitively
+};
+
 // utf8.DecodeRune on b[pos:n]; returns width 0 at end of text.
 int32_t decode_rune(const uint8_t* b, size_t n, size_t pos, int* width);
 
@@ -82,8 +94,11 @@ class Regexp {
   // natoms >= 0 keeps only that many leading elements of the (flattened) top-level
   // concatenation: each match of the regex then has a prefix match with the same start.
   // Non-ASCII members of rune sets become "one or more bytes >= 0x80" (kHighByteRune).
-  Prog RelaxedProg(int k, int natoms = -1) const;
+  // first_atom > 0 drops that many leading elements instead (a suffix program: every
+  // match of the regex ends where a match of the suffix ends).
+  Prog RelaxedProg(int k, int natoms = -1, int first_atom = 0) const;
   int NumAtoms() const;
+  std::vector<AtomInfo> Atoms() const;
 
   const std::string& source() const { return src_; }
   const std::vector<std::string>& SubexpNames() const { return names_; }

@@ -1,30 +1,30 @@
-// MI355X (gfx950) device path of the secret engine: K1 keyword automaton and K2
-// rule-group DFAs over a device-resident batch of file blobs.
+// MI355X (gfx950) device path of the secret engine over a device-resident batch of file
+// blobs packed back to back in one HBM stream (chunk c = bytes [c*C, (c+1)*C)).
 //
-// Work decomposition: files are packed back to back in one HBM stream; a lane owns a
-// chunk of `chunk` bytes (a chunk may hold pieces of several files).  For each file
-// piece [a, b) the lane runs the DFA in inject mode (a thread starts at every byte)
-// and, if the file continues past b, follows the threads that started inside its
-// piece in noinject mode until they have all died (K2), or keeps going for the
-// longest-keyword overlap (K1).  Every match start is owned by exactly one lane, so no
-// lane needs state from a neighbour and the reported end offsets are exact for the
-// DFA's language (dfa.hpp).
-//
-//   K1   dense over every chunk: keyword bits per file (per-lane LDS accumulator,
-//        one atomicOr per word per piece).
-//   gate one thread per file: which K2 groups a file's keyword bits switch on; per
-//        group gated bytes/files (LDS atomics, one global atomic per block).
-//   K2   per rule group: DENSE (every chunk, lanes skip ungated pieces) when the group
-//        is gated on a large share of the batch, otherwise LIST: only the (file, chunk)
-//        items of gated files, appended by the gate_list pass.  Accepts append
-//        {file, rule, end} candidate records with an atomic counter.
-// Tables: transitions (u16: next | 0x8000 accept bit), byte classes, and -- when the
-// DFA's accepts depend on the state only (no look-ahead assertion) -- the per-state
-// accept index and the accept masks all live in LDS, so an accept never waits on L2.
+//   K1   one dense pass over every byte: the Aho-Corasick automaton of the rule set's
+//        literals (keywords of Rule.MatchKeywords + anchor literals) stepped from LDS,
+//        fused with two saturating run counters (class U = token bytes, class D = digits).
+//        Outputs per-file keyword bits and per-chunk event bits (plan.hpp kEv*).  A lane
+//        owns kStreams consecutive chunks of one file and steps them as independent
+//        chains; each chain first replays `warm` bytes of the chunk before it, so every
+//        literal / run that ends inside the chunk is seen without state from other lanes.
+//   gate per file: which K2 groups the keyword bits switch on; per chunk: which of those
+//        groups have an event within `back` chunks after it -> (file, chunk) items,
+//        counted, then appended into per-group regions.
+//   K2   per rule group, its DFA (LDS-resident) over the group's items: one fused launch
+//        for all sparse groups (a block per (group, item range)), a dense launch for a
+//        group whose items cover a large share of the batch.  A lane runs its chunk in
+//        inject mode and then follows the threads that started in it until they die
+//        (noinject), so every match end is found by the lane that owns its start.
+//        Accepts append {file, rule, end} candidate records.
+// Exactness: K1 keyword bits are exact (files with folding runes are flagged), events
+// are a necessary condition of every match of the rule's GPU program (plan.cpp), so the
+// candidate set is a superset of the exact match ends; the host resolves exactly.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
 #include <chrono>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -39,7 +39,13 @@ namespace tsg {
       return fail(TSG_ERR_GPU, std::string(#x) + ": " + hipGetErrorString(e_));       \
   } while (0)
 
-struct DevDFA {
+constexpr int kStreams = 4;   // independent DFA chains per lane (dense passes)
+constexpr int kBlock = 256;
+constexpr int kPad = 256;     // zero bytes before and after the batch in HBM (>= K1 warm-up)
+constexpr int kMaxBack = 16;  // event windows up to this many chunks; larger -> whole file
+
+// ---------------------------------------------------------------- device tables
+struct DevDFA {  // K2 rule group
   const uint16_t* tab;        // [ns * nc] next | 0x8000 if the transition accepts
   const uint16_t* acc;        // [ns * nc] accept-mask index (look-ahead DFAs)
   const uint16_t* acc_state;  // [ns] accept-mask index per state (state_acc DFAs)
@@ -48,18 +54,36 @@ struct DevDFA {
   const uint8_t* dead;        // [ns]
   const uint64_t* masks;      // [nmasks * mw]
   const uint8_t* cls;         // [256]
-  const uint32_t* rules;      // K2: group-local id -> global rule
-  uint32_t nc, ns, mw, nmasks, state_acc, ext;
+  const uint32_t* rules;      // group-local id -> global rule
+  uint32_t nc, ns, mw, nmasks, state_acc;
   uint32_t start[4];
-  // LDS layout (bytes)
-  uint32_t o_cls, o_accs, o_masks, o_kwacc, lds_bytes;
+  uint32_t o_cls, o_accs, o_masks, lds_bytes;
+};
+
+struct DevK1 {
+  const uint16_t* tab;    // [ns * nc] next | 0x8000 if the next state ends a literal
+  const uint32_t* cls;    // [256] class | 0xFF00 if in run class D | 0xFFFF0000 if in U
+  const uint16_t* accs;   // [ns] accept-mask index of the literals a state ends
+  const uint32_t* masks;  // [nmasks * mw] keyword words (kw_words), then the event word
+  uint32_t nc, ns, nmasks, mw, kw_words, start, warm, kU, kD;  // kD = threshold << 8
+  uint32_t o_cls, o_accs, o_masks, lds_bytes;
 };
 
 struct DevCand {
   uint32_t file, rule, end;
 };
 
-// ---------------------------------------------------------------- small kernels
+__device__ __forceinline__ uint32_t ctx_of(uint8_t c) {
+  if (c == '\n') return 1;
+  if ((c >= '0' && c <= '9') || (c >= 'A' && c <= 'Z') || (c >= 'a' && c <= 'z') || c == '_') return 2;
+  return 3;
+}
+
+__device__ __forceinline__ uint32_t byte_of(const uint4 v, uint32_t k) {
+  const uint32_t w = k < 8 ? (k < 4 ? v.x : v.y) : (k < 12 ? v.z : v.w);
+  return (w >> ((k & 3) * 8)) & 0xFF;
+}
+
 __global__ void chunk_file_kernel(const uint64_t* __restrict__ off, uint32_t nfiles, uint32_t chunk,
                                   uint32_t* __restrict__ chunk_file) {
   uint32_t f = blockIdx.x * blockDim.x + threadIdx.x;
@@ -70,6 +94,246 @@ __global__ void chunk_file_kernel(const uint64_t* __restrict__ off, uint32_t nfi
   for (uint64_t c = c0; c < c1; c++) chunk_file[c] = f;
 }
 
+// ---------------------------------------------------------------- K1
+typedef unsigned short us2 __attribute__((ext_vector_type(2)));
+
+// run counters: high half = U run length, low half = D run length << 8 (both saturating);
+// m (the byte's class word) keeps the halves of the classes the byte belongs to
+__device__ __forceinline__ uint32_t run_step(uint32_t cnt, uint32_t m) {
+  const us2 inc = {(unsigned short)0x0100, (unsigned short)0x0001};
+  us2 c = __builtin_elementwise_add_sat(__builtin_bit_cast(us2, cnt), inc);
+  return __builtin_bit_cast(uint32_t, c) & m;
+}
+__device__ __forceinline__ uint32_t run_max(uint32_t a, uint32_t b) {
+  return __builtin_bit_cast(uint32_t,
+                            __builtin_elementwise_max(__builtin_bit_cast(us2, a), __builtin_bit_cast(us2, b)));
+}
+
+struct K1Args {
+  const uint8_t* data;
+  const uint64_t* off;
+  const uint32_t* chunk_file;
+  uint64_t total, nchunks, nitems, item_step;
+  uint32_t chunk, nfiles;
+  uint32_t* kw;    // [nfiles * kw_words]
+  uint32_t* ev;    // [nchunks, padded to whole items]
+  uint32_t* hits;  // [ns] arrivals per accepting state (sampling pass) or null
+};
+
+// one chain = one chunk: automaton state, run counters, the file the chain is in and the
+// keyword bits already sent for it (so each bit costs one atomic per chain and file)
+template <int KWW>
+struct K1Chain {
+  uint32_t s, cnt, mx, evl, f;
+  uint64_t fe;
+  uint32_t sent[KWW];
+};
+
+template <int KWW>
+struct K1Lane {
+  const DevK1& d;
+  const K1Args& A;
+  const uint16_t* s_tab;
+  const uint32_t* s_cls;
+  const uint16_t* s_accs;
+  const uint32_t* s_masks;
+
+  __device__ __forceinline__ void reset(K1Chain<KWW>& c) {
+    c.s = d.start;
+    c.cnt = 0;
+#pragma unroll
+    for (int w = 0; w < KWW; w++) c.sent[w] = 0;
+  }
+  // byte p lies past the chain's file: move to the file containing p
+  __device__ __forceinline__ void next_file(K1Chain<KWW>& c, uint64_t p) {
+    do {
+      c.f++;
+    } while (c.f < A.nfiles && A.off[c.f + 1] <= p);
+    c.fe = c.f < A.nfiles ? A.off[c.f + 1] : ~0ull;
+    reset(c);
+  }
+  // arrival in accepting state s: keyword bits of the chain's file, event bits of its chunk
+  __device__ __forceinline__ void accept(K1Chain<KWW>& c, uint32_t s) {
+    if (A.hits) atomicAdd(&A.hits[s], 1u);
+    const uint32_t* m = s_masks + (size_t)s_accs[s] * d.mw;
+    if (c.f < A.nfiles) {
+      uint32_t* kwf = A.kw + (size_t)c.f * d.kw_words;
+#pragma unroll
+      for (int w = 0; w < KWW; w++) {
+        if ((uint32_t)w >= d.kw_words) break;
+        const uint32_t bits = m[w] & ~c.sent[w];
+        if (bits) {
+          atomicOr(&kwf[w], bits);
+          c.sent[w] |= bits;
+        }
+      }
+      for (uint32_t w = KWW; w < d.kw_words; w++)
+        if (m[w]) atomicOr(&kwf[w], m[w]);
+    }
+    c.evl |= m[d.kw_words];
+  }
+  __device__ __forceinline__ uint32_t run_bits(uint32_t mx) const {
+    return ((mx >> 16) >= d.kU ? kEvRunU : 0u) | ((mx & 0xFFFFu) >= d.kD ? kEvRunD : 0u);
+  }
+  __device__ __forceinline__ void replay16(K1Chain<KWW>& c, uint32_t s, const uint4 v) {
+#pragma unroll 1
+    for (uint32_t k = 0; k < 16; k++) {
+      const uint32_t e = s_tab[s * d.nc + (s_cls[byte_of(v, k)] & 0xFFu)];
+      s = e & 0x7FFFu;
+      if (e & 0x8000u) accept(c, s);
+    }
+  }
+  // one chain, 16 bytes at p: file boundaries inside (or bytes below lo skipped: warm-up)
+  // (positions are signed: the warm-up of the first chunk starts before byte 0)
+  __device__ __forceinline__ void slow16(K1Chain<KWW>& c, const uint4 v, int64_t p, int64_t lo, bool record) {
+#pragma unroll 1
+    for (uint32_t k = 0; k < 16; k++) {
+      const int64_t q = p + k;
+      if (q < lo) continue;
+      if ((uint64_t)q >= c.fe) next_file(c, (uint64_t)q);
+      const uint32_t m = s_cls[byte_of(v, k)];
+      const uint32_t e = s_tab[c.s * d.nc + (m & 0xFFu)];
+      c.s = e & 0x7FFFu;
+      c.cnt = run_step(c.cnt, m);
+      if (record) {
+        c.mx = run_max(c.mx, c.cnt);
+        if (e & 0x8000u) accept(c, c.s);
+      }
+    }
+  }
+  // one chain, 16 bytes inside its file
+  __device__ __forceinline__ void fast16(K1Chain<KWW>& c, const uint4 v) {
+    const uint32_t s0 = c.s;
+    uint32_t any = 0;
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+      const uint32_t m = s_cls[byte_of(v, k)];
+      const uint32_t e = s_tab[c.s * d.nc + (m & 0xFFu)];
+      any |= e;
+      c.s = e & 0x7FFFu;
+      c.cnt = run_step(c.cnt, m);
+      c.mx = run_max(c.mx, c.cnt);
+    }
+    if (__builtin_expect(any & 0x8000u, 0)) replay16(c, s0, v);
+  }
+
+  // item = NS consecutive chunks from a: NS chains interleaved byte by byte
+  template <int NS>
+  __device__ void item(uint64_t a) {
+    const uint8_t* data = A.data;
+    const uint32_t C = A.chunk;
+    const uint64_t c0 = a / C;
+    K1Chain<KWW> c[NS];
+    uint64_t lo[NS];
+#pragma unroll
+    for (int i = 0; i < NS; i++) {
+      const uint64_t Ai = a + (uint64_t)i * C;
+      if (Ai < A.total) {
+        c[i].f = A.chunk_file[c0 + i];
+        lo[i] = A.off[c[i].f];
+        c[i].fe = A.off[c[i].f + 1];
+      } else {
+        c[i].f = A.nfiles;
+        lo[i] = Ai;
+        c[i].fe = ~0ull;
+      }
+      reset(c[i]);
+      c[i].mx = 0;
+      c[i].evl = 0;
+    }
+    // warm-up: the bytes before each chunk that belong to the chunk's first file
+    bool slow = false;
+#pragma unroll
+    for (int i = 0; i < NS; i++) slow |= (int64_t)lo[i] > (int64_t)(a + (uint64_t)i * C) - (int64_t)d.warm;
+    for (uint32_t j = 0; j < d.warm; j += 16) {
+      uint4 v[NS];
+#pragma unroll
+      for (int i = 0; i < NS; i++) v[i] = *(const uint4*)(data + a + (uint64_t)i * C - d.warm + j);
+      if (!slow) {
+#pragma unroll
+        for (int k = 0; k < 16; k++)
+#pragma unroll
+          for (int i = 0; i < NS; i++) {
+            const uint32_t m = s_cls[byte_of(v[i], k)];
+            c[i].s = s_tab[c[i].s * d.nc + (m & 0xFFu)] & 0x7FFFu;
+            c[i].cnt = run_step(c[i].cnt, m);
+          }
+      } else {
+#pragma unroll
+        for (int i = 0; i < NS; i++)
+          slow16(c[i], v[i], (int64_t)(a + (uint64_t)i * C) - (int64_t)d.warm + j, (int64_t)lo[i], false);
+      }
+    }
+    uint4 cur[NS];
+#pragma unroll
+    for (int i = 0; i < NS; i++) cur[i] = *(const uint4*)(data + a + (uint64_t)i * C);
+    for (uint32_t j = 0; j < C; j += 16) {
+      uint4 nxt[NS];
+#pragma unroll
+      for (int i = 0; i < NS; i++) nxt[i] = *(const uint4*)(data + a + (uint64_t)i * C + j + 16);
+      bool sl = false;
+#pragma unroll
+      for (int i = 0; i < NS; i++) sl |= c[i].fe < a + (uint64_t)i * C + j + 16;
+      if (__builtin_expect(!sl, 1)) {
+        uint32_t s0[NS], any[NS];
+#pragma unroll
+        for (int i = 0; i < NS; i++) {
+          s0[i] = c[i].s;
+          any[i] = 0;
+        }
+#pragma unroll
+        for (int k = 0; k < 16; k++)
+#pragma unroll
+          for (int i = 0; i < NS; i++) {
+            const uint32_t m = s_cls[byte_of(cur[i], k)];
+            const uint32_t e = s_tab[c[i].s * d.nc + (m & 0xFFu)];
+            any[i] |= e;
+            c[i].s = e & 0x7FFFu;
+            c[i].cnt = run_step(c[i].cnt, m);
+            c[i].mx = run_max(c[i].mx, c[i].cnt);
+          }
+#pragma unroll
+        for (int i = 0; i < NS; i++)
+          if (__builtin_expect(any[i] & 0x8000u, 0)) replay16(c[i], s0[i], cur[i]);
+      } else {
+#pragma unroll
+        for (int i = 0; i < NS; i++) {
+          const uint64_t p = a + (uint64_t)i * C + j;
+          if (c[i].fe < p + 16) slow16(c[i], cur[i], (int64_t)p, 0, true);
+          else fast16(c[i], cur[i]);
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < NS; i++) cur[i] = nxt[i];
+    }
+#pragma unroll
+    for (int i = 0; i < NS; i++) A.ev[c0 + i] = c[i].evl | run_bits(c[i].mx);
+  }
+};
+
+template <int KWW>
+__global__ void __launch_bounds__(kBlock) k1_kernel(DevK1 d, K1Args A) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  uint16_t* s_tab = (uint16_t*)smem;
+  uint32_t* s_cls = (uint32_t*)(smem + d.o_cls);
+  uint16_t* s_accs = (uint16_t*)(smem + d.o_accs);
+  uint32_t* s_masks = (uint32_t*)(smem + d.o_masks);
+  {
+    const uint32_t* src = (const uint32_t*)d.tab;
+    uint32_t* dst = (uint32_t*)s_tab;
+    for (uint32_t i = threadIdx.x; i < (d.ns * d.nc + 1) / 2; i += blockDim.x) dst[i] = src[i];
+    for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) s_cls[i] = d.cls[i];
+    for (uint32_t i = threadIdx.x; i < d.ns; i += blockDim.x) s_accs[i] = d.accs[i];
+    for (uint32_t i = threadIdx.x; i < d.nmasks * d.mw; i += blockDim.x) s_masks[i] = d.masks[i];
+  }
+  __syncthreads();
+  K1Lane<KWW> L{d, A, s_tab, s_cls, s_accs, s_masks};
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t it = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; it < A.nitems; it += stride)
+    L.template item<kStreams>(it * A.item_step * kStreams * A.chunk);
+}
+
+// ---------------------------------------------------------------- gate + items
 __device__ __forceinline__ bool group_gated(const uint32_t* __restrict__ kwf, const uint32_t* __restrict__ gm,
                                             uint32_t W, uint32_t always) {
   if (always) return true;
@@ -78,91 +342,114 @@ __device__ __forceinline__ bool group_gated(const uint32_t* __restrict__ kwf, co
   return false;
 }
 
-// per group: gated bytes and files (block-local LDS atomics, then one global atomic)
-__global__ void gate_count_kernel(const uint64_t* __restrict__ off, uint32_t nfiles,
-                                  const uint32_t* __restrict__ kw, uint32_t W,
-                                  const uint32_t* __restrict__ gmask, const uint32_t* __restrict__ galways,
-                                  uint32_t G, unsigned long long* __restrict__ gbytes,
-                                  uint32_t* __restrict__ gfiles) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  unsigned long long* sb = (unsigned long long*)smem;
-  uint32_t* sf = (uint32_t*)(sb + G);
-  for (uint32_t g = threadIdx.x; g < G; g += blockDim.x) {
-    sb[g] = 0;
-    sf[g] = 0;
+// per file: bit g of ggate[f * GW + g / 64] = group g gated (Rule.MatchKeywords may pass)
+__global__ void ggate_kernel(const uint32_t* __restrict__ kw, uint32_t F, uint32_t W,
+                             const uint32_t* __restrict__ gmask, const uint32_t* __restrict__ galways,
+                             uint32_t G, uint32_t GW, unsigned long long* __restrict__ ggate) {
+  const uint32_t f = blockIdx.x * blockDim.x + threadIdx.x;
+  if (f >= F) return;
+  const uint32_t* kwf = kw + (size_t)f * W;
+  for (uint32_t w = 0; w < GW; w++) {
+    unsigned long long bits = 0;
+    for (uint32_t g = w * 64; g < min(G, w * 64 + 64); g++)
+      if (group_gated(kwf, gmask + (size_t)g * W, W, galways[g])) bits |= 1ull << (g - w * 64);
+    ggate[(size_t)f * GW + w] = bits;
   }
-  __syncthreads();
-  uint32_t f = blockIdx.x * blockDim.x + threadIdx.x;
-  if (f < nfiles) {
-    uint64_t len = off[f + 1] - off[f];
-    if (len) {
-      const uint32_t* kwf = kw + (size_t)f * W;
-      for (uint32_t g = 0; g < G; g++)
-        if (group_gated(kwf, gmask + (size_t)g * W, W, galways[g])) {
-          atomicAdd(&sb[g], (unsigned long long)len);
-          atomicAdd(&sf[g], 1u);
+}
+
+struct ItemArgs {
+  const uint64_t* off;
+  const uint32_t* chunk_file;
+  const uint32_t* ev;
+  const unsigned long long* ggate;  // [F * GW]
+  const unsigned long long* gofbit;  // [32 * GW] groups listening to event bit b
+  const uint32_t* gevents;          // [G]
+  const uint32_t* gback;            // [G] chunks (kMaxBack + 1 = whole file)
+  uint64_t nchunks;
+  uint32_t F, G, GW, chunk, maxback;
+  uint32_t* count;            // [G]
+  const uint64_t* base;       // [G] item region of each group (emit pass), null: count pass
+  uint32_t* cursor;           // [G]
+  const uint8_t* listed;      // [G] 1 = list group (emit pass)
+  uint2* items;
+};
+
+// one thread per chunk c: for every file overlapping c and every gated group with an
+// event in [c, c + back] (inside the file): item (file, c) of the group
+template <bool EMIT>
+__global__ void __launch_bounds__(kBlock) items_kernel(ItemArgs A) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  uint32_t* s_count = (uint32_t*)smem;
+  if (!EMIT) {
+    for (uint32_t g = threadIdx.x; g < A.G; g += blockDim.x) s_count[g] = 0;
+    __syncthreads();
+  }
+  const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c < A.nchunks) {
+    const uint64_t cs = c * A.chunk, ce = cs + A.chunk;
+    for (uint32_t f = A.chunk_file[c]; f < A.F && A.off[f] < ce; f++) {
+      const uint64_t fs = A.off[f], fe = A.off[f + 1];
+      if (fe == fs) continue;
+      const uint64_t cf1 = (fe - 1) / A.chunk;
+      // OR of the events of chunks [c, c + k] inside the file, k = 0..maxback
+      uint32_t win[kMaxBack + 1];
+      uint32_t acc = 0;
+#pragma unroll
+      for (uint32_t k = 0; k <= kMaxBack; k++) {
+        if (k <= A.maxback && c + k <= cf1) acc |= A.ev[c + k];
+        win[k] = acc;
+      }
+      const uint32_t all = acc | kEvAlways;
+      for (uint32_t w = 0; w < A.GW; w++) {
+        unsigned long long cand = 0;
+        for (uint32_t b = 0; b < 32; b++)
+          if ((all >> b) & 1) cand |= A.gofbit[b * A.GW + w];
+        cand &= A.ggate[(size_t)f * A.GW + w];
+        while (cand) {
+          const uint32_t g = w * 64 + __builtin_ctzll(cand);
+          cand &= cand - 1;
+          const uint32_t back = A.gback[g];
+          uint32_t ew = kEvAlways;
+#pragma unroll
+          for (uint32_t k = 0; k <= kMaxBack; k++)
+            if (k == back) ew |= win[k];
+          if (back > kMaxBack) ew = ~0u;  // window longer than kMaxBack chunks: every chunk
+          if (!(ew & A.gevents[g])) continue;
+          if (!EMIT) {
+            atomicAdd(&s_count[g], 1u);
+          } else if (A.listed[g]) {
+            const uint32_t k = atomicAdd(&A.cursor[g], 1u);
+            A.items[A.base[g] + k] = make_uint2(f, (uint32_t)c);
+          }
         }
+      }
     }
   }
-  __syncthreads();
-  for (uint32_t g = threadIdx.x; g < G; g += blockDim.x) {
-    if (sb[g]) atomicAdd(&gbytes[g], sb[g]);
-    if (sf[g]) atomicAdd(&gfiles[g], sf[g]);
+  if (!EMIT) {
+    __syncthreads();
+    for (uint32_t g = threadIdx.x; g < A.G; g += blockDim.x)
+      if (s_count[g]) atomicAdd(&A.count[g], s_count[g]);
   }
 }
 
-// LIST-mode groups: append one (file, chunk) item per chunk a gated file touches
-__global__ void gate_list_kernel(const uint64_t* __restrict__ off, uint32_t nfiles,
-                                 const uint32_t* __restrict__ kw, uint32_t W,
-                                 const uint32_t* __restrict__ gmask, const uint32_t* __restrict__ galways,
-                                 const uint32_t* __restrict__ list_groups, uint32_t nlist,
-                                 const uint64_t* __restrict__ item_base, uint32_t* __restrict__ item_count,
-                                 uint2* __restrict__ items, uint32_t chunk) {
-  uint32_t f = blockIdx.x * blockDim.x + threadIdx.x;
-  if (f >= nfiles) return;
-  uint64_t fs = off[f], fe = off[f + 1];
-  if (fe == fs) return;
-  const uint32_t* kwf = kw + (size_t)f * W;
-  uint32_t c0 = (uint32_t)(fs / chunk), c1 = (uint32_t)((fe - 1) / chunk);
-  for (uint32_t j = 0; j < nlist; j++) {
-    uint32_t g = list_groups[j];
-    if (!group_gated(kwf, gmask + (size_t)g * W, W, galways[g])) continue;
-    uint32_t n = c1 - c0 + 1;
-    uint32_t base = atomicAdd(&item_count[j], n);
-    uint2* it = items + item_base[j] + base;
-    for (uint32_t k = 0; k < n; k++) it[k] = make_uint2(f, c0 + k);
-  }
-}
-
-// ---------------------------------------------------------------- the scan kernel
-__device__ __forceinline__ uint32_t ctx_of(uint8_t c) {
-  if (c == '\n') return 1;
-  if ((c >= '0' && c <= '9') || (c >= 'A' && c <= 'Z') || (c >= 'a' && c <= 'z') || c == '_') return 2;
-  return 3;
-}
-
-// dense items are kStreams consecutive chunks; inside one file they are stepped as
-// kStreams interleaved DFA chains (ILP to cover the LDS latency)
-constexpr int kStreams = 4;
-
+// ---------------------------------------------------------------- K2
 struct ScanArgsDev {
   const uint8_t* data;
   const uint64_t* off;
   const uint32_t* chunk_file;
   uint64_t total, nitems;
   uint32_t chunk, ext_cap;
-  uint32_t* kw;
+  const uint32_t* kw;
   uint32_t kw_words;
-  const uint32_t* gmask;  // K2 dense: this group's keyword mask [kw_words]
+  const uint32_t* gmask;  // dense: this group's keyword mask [kw_words]
   uint32_t galways;
-  const uint2* items;     // K2 list mode
+  const uint2* items;     // list mode
   DevCand* cand;
   uint32_t* cand_count;
   uint32_t cand_cap;
   uint32_t* ovf;
 };
 
-template <bool KW>
 struct Lane {
   const DevDFA& d;
   const ScanArgsDev& A;
@@ -170,7 +457,6 @@ struct Lane {
   const uint8_t* s_cls;
   const uint16_t* s_accs;
   const uint64_t* s_masks;
-  uint32_t* s_kwacc;
   uint32_t file;
   uint64_t fs;
 
@@ -178,25 +464,17 @@ struct Lane {
   // the accept bits of 16 transitions and replay the word through step() when one is set
   __device__ __forceinline__ void emit(uint32_t mi, uint64_t pos) {
     const uint64_t* m = (d.state_acc && mi < d.nmasks) ? s_masks + (size_t)mi * d.mw : d.masks + (size_t)mi * d.mw;
-    if (KW) {
-      for (uint32_t w = 0; w < d.mw; w++) {
-        uint64_t v = m[w];
-        if (2 * w < A.kw_words) s_kwacc[(2 * w) * blockDim.x + threadIdx.x] |= (uint32_t)v;
-        if (2 * w + 1 < A.kw_words) s_kwacc[(2 * w + 1) * blockDim.x + threadIdx.x] |= (uint32_t)(v >> 32);
-      }
-    } else {
-      uint64_t v = m[0];
-      while (v) {
-        uint32_t k = __builtin_ctzll(v);
-        v &= v - 1;
-        uint32_t idx = atomicAdd(A.cand_count, 1u);
-        if (idx < A.cand_cap) {
-          A.cand[idx].file = file;
-          A.cand[idx].rule = d.rules[k];
-          A.cand[idx].end = (uint32_t)(pos - fs);
-        } else {
-          A.ovf[file] = 1;
-        }
+    uint64_t v = m[0];
+    while (v) {
+      uint32_t k = __builtin_ctzll(v);
+      v &= v - 1;
+      uint32_t idx = atomicAdd(A.cand_count, 1u);
+      if (idx < A.cand_cap) {
+        A.cand[idx].file = file;
+        A.cand[idx].rule = d.rules[k];
+        A.cand[idx].end = (uint32_t)(pos - fs);
+      } else {
+        A.ovf[file] = 1;
       }
     }
   }
@@ -208,19 +486,21 @@ struct Lane {
     return e & 0x7FFFu;
   }
 
-  // transition only; accept bit returned in bit 15
   __device__ __forceinline__ uint32_t fast(uint32_t s, uint32_t byte) const {
     return s_tab[s * d.nc + s_cls[byte]];
   }
 
-  // 16 bytes: tight loop, then a (rare) replay with accept handling
+  __device__ __noinline__ void replay16(uint32_t s, const uint4 v, uint64_t p) {
+#pragma unroll 1
+    for (uint32_t k = 0; k < 16; k++) s = step(s, byte_of(v, k), p + k);
+  }
+
   __device__ __forceinline__ uint32_t step16(uint32_t s, const uint4 v, uint64_t p) {
-    const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
     const uint32_t s0 = s;
     uint32_t any = 0;
 #pragma unroll
     for (int k = 0; k < 16; k++) {
-      const uint32_t e = fast(s, (wv[k >> 2] >> ((k & 3) * 8)) & 0xFF);
+      const uint32_t e = fast(s, byte_of(v, k));
       any |= e;
       s = e & 0x7FFFu;
     }
@@ -228,28 +508,9 @@ struct Lane {
     return s;
   }
 
-  // no dynamically indexed arrays (they would live in scratch): bytes are selected
-  __device__ __forceinline__ void replay16(uint32_t s, const uint4 v, uint64_t p) {
-#pragma unroll 1
-    for (uint32_t k = 0; k < 16; k++) {
-      const uint32_t w = k < 8 ? (k < 4 ? v.x : v.y) : (k < 12 ? v.z : v.w);
-      s = step(s, (w >> ((k & 3) * 8)) & 0xFF, p + k);
-    }
-  }
-
-  // tail of a stream that ends at b (< fe): K1 keyword overlap / K2 noinject follow-up
+  // matches that started before b: follow them past b (noinject) until they all die
   __device__ __forceinline__ void tail(uint32_t s, uint64_t fe, uint64_t b) {
     const uint8_t* data = A.data;
-    if (KW) {
-      const uint64_t le = min(fe, b + d.ext);
-      uint64_t q = b;
-      for (; q < le; q++) s = step(s, data[q], q);
-      if (q >= fe) {
-        const uint32_t m = d.eot[s];
-        if (m) emit(m, fe);
-      }
-      return;
-    }
     if (b >= fe) {
       const uint32_t m = d.eot[s];
       if (m) emit(m, fe);
@@ -271,13 +532,10 @@ struct Lane {
     }
   }
 
-  // NS consecutive chunks [a, a + NS*C) that all lie inside file [fs, fe): NS independent
-  // DFA chains interleaved byte by byte, so NS LDS look-ups are in flight per lane
+  // NS consecutive chunks [a, a + NS*C) inside file [fs, fe): NS interleaved chains
   template <int NS>
   __device__ void streams(uint64_t fe, uint64_t a, uint32_t C) {
     const uint8_t* data = A.data;
-    if (KW)
-      for (uint32_t w = 0; w < A.kw_words; w++) s_kwacc[w * blockDim.x + threadIdx.x] = 0;
     uint32_t s[NS];
 #pragma unroll
     for (int i = 0; i < NS; i++) {
@@ -291,14 +549,6 @@ struct Lane {
       uint4 nxt[NS];
 #pragma unroll
       for (int i = 0; i < NS; i++) nxt[i] = *(const uint4*)(data + a + (uint64_t)i * C + j + 16);
-      uint32_t wv[NS][4];
-#pragma unroll
-      for (int i = 0; i < NS; i++) {
-        wv[i][0] = cur[i].x;
-        wv[i][1] = cur[i].y;
-        wv[i][2] = cur[i].z;
-        wv[i][3] = cur[i].w;
-      }
       uint32_t s0[NS], any[NS];
 #pragma unroll
       for (int i = 0; i < NS; i++) {
@@ -309,7 +559,7 @@ struct Lane {
       for (int k = 0; k < 16; k++)
 #pragma unroll
         for (int i = 0; i < NS; i++) {
-          const uint32_t e = fast(s[i], (wv[i][k >> 2] >> ((k & 3) * 8)) & 0xFF);
+          const uint32_t e = fast(s[i], byte_of(cur[i], k));
           any[i] |= e;
           s[i] = e & 0x7FFFu;
         }
@@ -321,147 +571,116 @@ struct Lane {
     }
 #pragma unroll
     for (int i = 0; i < NS; i++) tail(s[i], fe, a + (uint64_t)(i + 1) * C);
-    if (KW)
-      for (uint32_t w = 0; w < A.kw_words; w++) {
-        uint32_t v = s_kwacc[w * blockDim.x + threadIdx.x];
-        if (v) atomicOr(&A.kw[(size_t)file * A.kw_words + w], v);
-      }
   }
 
   // one file piece [a, se) of file [fs, fe)
   __device__ void piece(uint64_t fe, uint64_t a, uint64_t se) {
     const uint8_t* data = A.data;
-    if (KW)
-      for (uint32_t w = 0; w < A.kw_words; w++) s_kwacc[w * blockDim.x + threadIdx.x] = 0;
     uint32_t s = (a == fs) ? d.start[0] : d.start[ctx_of(data[a - 1])];
     uint64_t p = a;
-    const uint64_t le = KW ? min(fe, se + d.ext) : se;
-    while (p < le && (p & 15)) {
+    while (p < se && (p & 15)) {
       s = step(s, data[p], p);
       p++;
     }
-    if (p + 16 <= le) {
-      // one 16-byte word in flight ahead of the one being stepped (the stream is padded
-      // by 64 bytes, so the look-ahead load never leaves the allocation)
+    if (p + 16 <= se) {
       uint4 cur = *(const uint4*)(data + p);
-      while (p + 16 <= le) {
+      while (p + 16 <= se) {
         const uint4 nxt = *(const uint4*)(data + p + 16);
         s = step16(s, cur, p);
         cur = nxt;
         p += 16;
       }
     }
-    while (p < le) {
+    while (p < se) {
       s = step(s, data[p], p);
       p++;
     }
-    if (le >= fe) {
-      const uint32_t m = d.eot[s];
-      if (m) emit(m, fe);
-    } else if (!KW) {
-      // follow the threads that started in [a, se) past the chunk end
-      s = d.to_ni[s];
-      uint64_t q = se;
-      bool over = false;
-      while (q < fe && !d.dead[s]) {
-        if (q - se >= A.ext_cap) {
-          over = true;
-          break;
-        }
-        s = step(s, data[q], q);
-        q++;
-      }
-      if (over) {
-        A.ovf[file] = 1;
-      } else if (q == fe && !d.dead[s]) {
-        const uint32_t m = d.eot[s];
-        if (m) emit(m, fe);
-      }
-    }
-    if (KW)
-      for (uint32_t w = 0; w < A.kw_words; w++) {
-        uint32_t v = s_kwacc[w * blockDim.x + threadIdx.x];
-        if (v) atomicOr(&A.kw[(size_t)file * A.kw_words + w], v);
-      }
+    tail(s, fe, se);
   }
 };
 
-template <bool KW, bool LIST>
-__global__ void __launch_bounds__(256) dfa_scan_kernel(DevDFA d, ScanArgsDev A) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+__device__ __forceinline__ void stage_dfa(const DevDFA& d, uint8_t* smem) {
   uint16_t* s_tab = (uint16_t*)smem;
+  const uint32_t* src = (const uint32_t*)d.tab;
+  uint32_t* dst = (uint32_t*)s_tab;
+  for (uint32_t i = threadIdx.x; i < (d.ns * d.nc + 1) / 2; i += blockDim.x) dst[i] = src[i];
   uint8_t* s_cls = smem + d.o_cls;
-  uint16_t* s_accs = (uint16_t*)(smem + d.o_accs);
-  uint64_t* s_masks = (uint64_t*)(smem + d.o_masks);
-  const uint32_t tab_entries = d.ns * d.nc;
-  {
-    const uint32_t* src = (const uint32_t*)d.tab;
-    uint32_t* dst = (uint32_t*)s_tab;
-    for (uint32_t i = threadIdx.x; i < (tab_entries + 1) / 2; i += blockDim.x) dst[i] = src[i];
-  }
   for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) s_cls[i] = d.cls[i];
   if (d.state_acc) {
+    uint16_t* s_accs = (uint16_t*)(smem + d.o_accs);
+    uint64_t* s_masks = (uint64_t*)(smem + d.o_masks);
     for (uint32_t i = threadIdx.x; i < d.ns; i += blockDim.x) s_accs[i] = d.acc_state[i];
     for (uint32_t i = threadIdx.x; i < d.nmasks * d.mw; i += blockDim.x) s_masks[i] = d.masks[i];
   }
   __syncthreads();
+}
 
-  Lane<KW> L{d, A, s_tab, s_cls, s_accs, s_masks, (uint32_t*)(smem + d.o_kwacc), 0, 0};
+// dense: every chunk of the batch, lanes skip the pieces of files the group is not gated on
+__global__ void __launch_bounds__(kBlock) k2_dense_kernel(DevDFA d, ScanArgsDev A) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  stage_dfa(d, smem);
+  Lane L{d, A, (const uint16_t*)smem, smem + d.o_cls, (const uint16_t*)(smem + d.o_accs),
+         (const uint64_t*)(smem + d.o_masks), 0, 0};
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   for (uint64_t it = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; it < A.nitems; it += stride) {
-    if (LIST) {
-      const uint2 item = A.items[it];
-      const uint32_t f = item.x;
+    uint64_t a = it * kStreams * A.chunk;
+    const uint64_t b = min(a + (uint64_t)kStreams * A.chunk, A.total);
+    uint32_t f = A.chunk_file[it * kStreams];
+    {
       const uint64_t fs = A.off[f], fe = A.off[f + 1];
-      const uint64_t a = max(fs, (uint64_t)item.y * A.chunk);
-      const uint64_t b = min(fe, (uint64_t)(item.y + 1) * A.chunk);
-      if (a < b) {
-        L.file = f;
-        L.fs = fs;
-        L.piece(fe, a, b);
-      }
-    } else {
-      // item = kStreams consecutive chunks
-      uint64_t a = it * kStreams * A.chunk;
-      const uint64_t b = min(a + (uint64_t)kStreams * A.chunk, A.total);
-      uint32_t f = A.chunk_file[it * kStreams];
-      {
-        const uint64_t fs = A.off[f], fe = A.off[f + 1];
-        if (b == a + (uint64_t)kStreams * A.chunk && b <= fe) {  // common case: one file
-          if (KW || group_gated(A.kw + (size_t)f * A.kw_words, A.gmask, A.kw_words, A.galways)) {
-            L.file = f;
-            L.fs = fs;
-            L.template streams<kStreams>(fe, a, A.chunk);
-          }
-          continue;
-        }
-      }
-      while (a < b) {
-        const uint64_t fs = A.off[f], fe = A.off[f + 1];
-        if (fe == fs) {
-          f++;
-          continue;
-        }
-        // the lane owns every match start in [item start, b): pieces may span chunks
-        const uint64_t se = min(b, fe);
-        if (KW || group_gated(A.kw + (size_t)f * A.kw_words, A.gmask, A.kw_words, A.galways)) {
+      if (b == a + (uint64_t)kStreams * A.chunk && b <= fe) {  // common case: one file
+        if (group_gated(A.kw + (size_t)f * A.kw_words, A.gmask, A.kw_words, A.galways)) {
           L.file = f;
           L.fs = fs;
-          L.piece(fe, a, se);
+          L.template streams<kStreams>(fe, a, A.chunk);
         }
-        a = se;
-        f++;
+        continue;
       }
+    }
+    while (a < b) {
+      const uint64_t fs = A.off[f], fe = A.off[f + 1];
+      if (fe == fs) {
+        f++;
+        continue;
+      }
+      // the lane owns every match start in [item start, b): pieces may span chunks
+      const uint64_t se = min(b, fe);
+      if (group_gated(A.kw + (size_t)f * A.kw_words, A.gmask, A.kw_words, A.galways)) {
+        L.file = f;
+        L.fs = fs;
+        L.piece(fe, a, se);
+      }
+      a = se;
+      f++;
+    }
+  }
+}
+
+// list: block b scans items [first, first + n) of group g; blkmap[b] = (g, first, n)
+__global__ void __launch_bounds__(kBlock) k2_list_kernel(const DevDFA* __restrict__ dfas,
+                                                         const uint4* __restrict__ blkmap,
+                                                         ScanArgsDev A) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const uint4 bm = blkmap[blockIdx.x];
+  const DevDFA d = dfas[__builtin_amdgcn_readfirstlane(bm.x)];
+  stage_dfa(d, smem);
+  Lane L{d, A, (const uint16_t*)smem, smem + d.o_cls, (const uint16_t*)(smem + d.o_accs),
+         (const uint64_t*)(smem + d.o_masks), 0, 0};
+  for (uint32_t i = threadIdx.x; i < bm.z; i += blockDim.x) {
+    const uint2 item = A.items[bm.y + i];
+    const uint32_t f = item.x;
+    const uint64_t fs = A.off[f], fe = A.off[f + 1];
+    const uint64_t a = max(fs, (uint64_t)item.y * A.chunk);
+    const uint64_t b = min(fe, (uint64_t)(item.y + 1) * A.chunk);
+    if (a < b) {
+      L.file = f;
+      L.fs = fs;
+      L.piece(fe, a, b);
     }
   }
 }
 
 // ---------------------------------------------------------------- host side
-struct DeviceDFA {
-  DevDFA dev{};
-  std::vector<void*> allocs;
-};
-
 template <class T>
 static int upload_vec(const std::vector<T>& v, const T** dst, std::vector<void*>* allocs) {
   void* p = nullptr;
@@ -475,8 +694,8 @@ static int upload_vec(const std::vector<T>& v, const T** dst, std::vector<void*>
 
 static uint32_t align16(uint32_t x) { return (x + 15) & ~15u; }
 
-static int make_device_dfa(const DFA& d, const std::vector<uint32_t>& rules, uint32_t kw_words,
-                           bool kw_mode, DeviceDFA* out) {
+static int make_device_dfa(const DFA& d, const std::vector<uint32_t>& rules, DevDFA* out,
+                           std::vector<void*>* allocs) {
   if (d.nstates >= 0x8000) return fail(TSG_ERR_INTERNAL, "DFA too large for u16 tables");
   const size_t nc = d.nclasses;
   std::vector<uint16_t> tab((size_t)d.nstates * nc), acc(tab.size()), accs(d.nstates, 0);
@@ -501,22 +720,21 @@ static int make_device_dfa(const DFA& d, const std::vector<uint32_t>& rules, uin
   std::vector<uint64_t> masks;
   for (const auto& m : d.masks) masks.insert(masks.end(), m.begin(), m.end());
   std::vector<uint8_t> cls(d.cls, d.cls + 256);
-  DevDFA& v = out->dev;
+  DevDFA& v = *out;
   int rc;
-  if ((rc = upload_vec(tab, &v.tab, &out->allocs))) return rc;
-  if ((rc = upload_vec(acc, &v.acc, &out->allocs))) return rc;
-  if ((rc = upload_vec(accs, &v.acc_state, &out->allocs))) return rc;
-  if ((rc = upload_vec(eot, &v.eot, &out->allocs))) return rc;
-  if ((rc = upload_vec(ni, &v.to_ni, &out->allocs))) return rc;
-  if ((rc = upload_vec(dead, &v.dead, &out->allocs))) return rc;
-  if ((rc = upload_vec(masks, &v.masks, &out->allocs))) return rc;
-  if ((rc = upload_vec(cls, &v.cls, &out->allocs))) return rc;
-  if ((rc = upload_vec(rules, &v.rules, &out->allocs))) return rc;
+  if ((rc = upload_vec(tab, &v.tab, allocs))) return rc;
+  if ((rc = upload_vec(acc, &v.acc, allocs))) return rc;
+  if ((rc = upload_vec(accs, &v.acc_state, allocs))) return rc;
+  if ((rc = upload_vec(eot, &v.eot, allocs))) return rc;
+  if ((rc = upload_vec(ni, &v.to_ni, allocs))) return rc;
+  if ((rc = upload_vec(dead, &v.dead, allocs))) return rc;
+  if ((rc = upload_vec(masks, &v.masks, allocs))) return rc;
+  if ((rc = upload_vec(cls, &v.cls, allocs))) return rc;
+  if ((rc = upload_vec(rules, &v.rules, allocs))) return rc;
   v.nc = (uint32_t)nc;
   v.ns = (uint32_t)d.nstates;
   v.mw = (uint32_t)d.mask_words;
   v.nmasks = (uint32_t)d.masks.size();
-  v.ext = d.max_len > 1 ? (uint32_t)(d.max_len - 1) : 0;
   for (int k = 0; k < 4; k++) v.start[k] = d.start[k];
   // LDS layout
   uint32_t o = align16((uint32_t)(tab.size() * 2));
@@ -531,9 +749,66 @@ static int make_device_dfa(const DFA& d, const std::vector<uint32_t>& rules, uin
     v.o_masks = o + align16(d.nstates * 2);
     o += acc_bytes;
   }
-  v.o_kwacc = o;
-  if (kw_mode) o += kw_words * 256 * 4;
   v.lds_bytes = o + 16;
+  if (v.lds_bytes > 160 * 1024) return fail(TSG_ERR_INTERNAL, "DFA tables exceed LDS");
+  return TSG_OK;
+}
+
+// perf experiments only (results are not exact): bit 0 strips the K1 accept flags
+static int k1_debug() {
+  const char* e = getenv("TSG_K1_DEBUG");
+  return e ? atoi(e) : 0;
+}
+
+static int make_device_k1(const Plan& p, DevK1* out, std::vector<void*>* allocs) {
+  const DFA& d = *p.kw_dfa;
+  if (d.nstates >= 0x8000) return fail(TSG_ERR_INTERNAL, "keyword automaton too large");
+  const size_t nc = d.nclasses;
+  if (nc > 256) return fail(TSG_ERR_INTERNAL, "keyword automaton has too many classes");
+  std::vector<uint16_t> tab((size_t)d.nstates * nc), accs(d.nstates);
+  for (int s = 0; s < d.nstates; s++) {
+    accs[s] = (uint16_t)d.eot_acc[s];  // no assertions: the state's match set
+    for (size_t c = 0; c < nc; c++) {
+      const size_t i = (size_t)s * nc + c;
+      if (d.acc[i] != d.eot_acc[s]) return fail(TSG_ERR_INTERNAL, "keyword automaton accepts are not state-based");
+      const uint32_t nx = d.next[i];
+      tab[i] = (uint16_t)(nx | ((d.eot_acc[nx] && !(k1_debug() & 1)) ? 0x8000u : 0u));
+    }
+  }
+  std::vector<uint32_t> cls(256);
+  for (int b = 0; b < 256; b++)
+    cls[b] = d.cls[b] | ((p.run_cls[b] & 2) ? 0xFF00u : 0u) | ((p.run_cls[b] & 1) ? 0xFFFF0000u : 0u);
+  const uint32_t W = (uint32_t)p.kw_words, mw = W + 1;
+  std::vector<uint32_t> masks((size_t)d.masks.size() * mw, 0);
+  for (size_t m = 0; m < d.masks.size(); m++) {
+    for (int k = 0; k < p.n_kw; k++)
+      if ((d.masks[m][k / 64] >> (k % 64)) & 1) masks[m * mw + k / 32] |= 1u << (k % 32);
+    masks[m * mw + W] = p.kw_mask_events[m];
+  }
+  DevK1& v = *out;
+  int rc;
+  if ((rc = upload_vec(tab, &v.tab, allocs))) return rc;
+  if ((rc = upload_vec(cls, &v.cls, allocs))) return rc;
+  if ((rc = upload_vec(accs, &v.accs, allocs))) return rc;
+  if ((rc = upload_vec(masks, &v.masks, allocs))) return rc;
+  v.nc = (uint32_t)nc;
+  v.ns = (uint32_t)d.nstates;
+  v.nmasks = (uint32_t)d.masks.size();
+  v.mw = mw;
+  v.kw_words = W;
+  v.start = d.start[kCtxBOT];
+  v.warm = (uint32_t)p.warm;
+  v.kU = (uint32_t)p.run_k[0];
+  v.kD = (uint32_t)p.run_k[1] << 8;
+  uint32_t o = align16((uint32_t)(tab.size() * 2));
+  v.o_cls = o;
+  o += 1024;
+  v.o_accs = o;
+  o += align16(d.nstates * 2);
+  v.o_masks = o;
+  o += align16((uint32_t)masks.size() * 4);
+  v.lds_bytes = o;
+  if (v.lds_bytes > 160 * 1024) return fail(TSG_ERR_INTERNAL, "keyword automaton exceeds LDS");
   return TSG_OK;
 }
 
@@ -547,10 +822,17 @@ struct tsg_ctx {
   tsg_ctx_options opt{};
   hipStream_t stream = nullptr;
   hipEvent_t ev[8];
-  DeviceDFA kw;
-  std::vector<DeviceDFA> groups;
-  uint32_t* d_gmask = nullptr;    // [G * W]
-  uint32_t* d_galways = nullptr;  // [G]
+  std::vector<void*> tables;        // every rule-table allocation
+  DevK1 k1{};
+  std::vector<DevDFA> groups;
+  DevDFA* d_groups = nullptr;       // [G] (list kernel)
+  uint32_t* d_gmask = nullptr;      // [G * W]
+  uint32_t* d_galways = nullptr;    // [G]
+  uint32_t* d_gevents = nullptr;    // [G]
+  uint32_t* d_gback = nullptr;      // [G]
+  unsigned long long* d_gofbit = nullptr;  // [32 * GW]
+  std::vector<uint32_t> gback;
+  uint32_t GW = 1, maxback = 0;
   // batch
   const uint8_t* h_data = nullptr;
   const uint64_t* h_off = nullptr;
@@ -558,57 +840,59 @@ struct tsg_ctx {
   const uint64_t* h_poff = nullptr;
   uint32_t nfiles = 0;
   uint64_t total = 0;
+  uint8_t* d_data_alloc = nullptr;  // kPad | batch | kPad
   uint8_t* d_data = nullptr;
   size_t d_data_cap = 0;
   uint64_t* d_off = nullptr;
   size_t d_off_cap = 0;
   uint32_t* d_chunk_file = nullptr;
   size_t d_chunk_cap = 0;
+  uint32_t* d_ev = nullptr;
+  size_t d_ev_cap = 0;
   uint32_t* d_kw = nullptr;
   size_t d_kw_cap = 0;
+  unsigned long long* d_ggate = nullptr;
+  size_t d_ggate_cap = 0;
   uint32_t* d_ovf = nullptr;
   size_t d_ovf_cap = 0;
   DevCand* d_cand = nullptr;
   uint32_t* d_count = nullptr;      // [0] candidates
-  unsigned long long* d_gbytes = nullptr;  // [G]
-  uint32_t* d_gfiles = nullptr;     // [G]
-  uint32_t* d_list_groups = nullptr;
-  uint64_t* d_item_base = nullptr;
-  uint32_t* d_item_count = nullptr;
+  uint32_t* d_gcount = nullptr;     // [G] items per group
+  uint32_t* d_cursor = nullptr;     // [G]
+  uint64_t* d_base = nullptr;       // [G]
+  uint8_t* d_listed = nullptr;      // [G]
+  uint4* d_blkmap = nullptr;
+  size_t d_blkmap_cap = 0;
   uint2* d_items = nullptr;
   size_t d_items_cap = 0;
   // host mirrors
   KernelOutput ko;
   uint32_t* h_count = nullptr;
-  std::vector<unsigned long long> h_gbytes;
-  std::vector<uint32_t> h_gfiles;
   tsg_stats stats{};
   int grid = 0;
   bool uploaded = false;
 
   ~tsg_ctx() {
-    hipSetDevice(device);
-    for (auto* p : kw.allocs) hipFree(p);
-    for (auto& g : groups)
-      for (auto* p : g.allocs) hipFree(p);
-    hipFree(d_gmask);
-    hipFree(d_galways);
-    hipFree(d_data);
-    hipFree(d_off);
-    hipFree(d_chunk_file);
-    hipFree(d_kw);
-    hipFree(d_ovf);
-    hipFree(d_cand);
-    hipFree(d_count);
-    hipFree(d_gbytes);
-    hipFree(d_gfiles);
-    hipFree(d_list_groups);
-    hipFree(d_item_base);
-    hipFree(d_item_count);
-    hipFree(d_items);
+    (void)hipSetDevice(device);
+    for (auto* p : tables) (void)hipFree(p);
+    (void)hipFree(d_data_alloc);
+    (void)hipFree(d_off);
+    (void)hipFree(d_chunk_file);
+    (void)hipFree(d_ev);
+    (void)hipFree(d_kw);
+    (void)hipFree(d_ggate);
+    (void)hipFree(d_ovf);
+    (void)hipFree(d_cand);
+    (void)hipFree(d_count);
+    (void)hipFree(d_gcount);
+    (void)hipFree(d_cursor);
+    (void)hipFree(d_base);
+    (void)hipFree(d_listed);
+    (void)hipFree(d_blkmap);
+    (void)hipFree(d_items);
     if (h_count) hipHostFree(h_count);
     for (auto& e : ev)
-      if (e) hipEventDestroy(e);
+      if (e) (void)hipEventDestroy(e);
     if (stream) hipStreamDestroy(stream);
   }
 };
@@ -624,18 +908,20 @@ static int ensure(T** p, size_t* cap, size_t n) {
   return TSG_OK;
 }
 
-template <bool KW, bool LIST>
-static int launch_scan(tsg_ctx* c, const DevDFA& d, ScanArgsDev A) {
-  if (A.nitems == 0) return TSG_OK;
-  if (d.lds_bytes > 160 * 1024) return fail(TSG_ERR_INTERNAL, "DFA tables exceed LDS");
-  auto fn = dfa_scan_kernel<KW, LIST>;
-  if (d.lds_bytes > 64 * 1024)
-    HIP_TRY(hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)d.lds_bytes));
-  const int block = 256;
-  uint64_t need = (A.nitems + block - 1) / block;
-  int grid = (int)std::min<uint64_t>(need, (uint64_t)c->grid);
-  hipLaunchKernelGGL(fn, dim3(grid), dim3(block), d.lds_bytes, c->stream, d, A);
+static const void* k1_fn(uint32_t kw_words) {
+  if (kw_words <= 1) return (const void*)k1_kernel<1>;
+  if (kw_words <= 2) return (const void*)k1_kernel<2>;
+  if (kw_words <= 4) return (const void*)k1_kernel<4>;
+  return (const void*)k1_kernel<8>;
+}
+
+static int launch_k1(tsg_ctx* c, const K1Args& A) {
+  const uint32_t W = c->k1.kw_words;
+  const int grid = (int)std::min<uint64_t>((A.nitems + kBlock - 1) / kBlock, (uint64_t)c->grid);
+  if (W <= 1) hipLaunchKernelGGL(k1_kernel<1>, dim3(grid), dim3(kBlock), c->k1.lds_bytes, c->stream, c->k1, A);
+  else if (W <= 2) hipLaunchKernelGGL(k1_kernel<2>, dim3(grid), dim3(kBlock), c->k1.lds_bytes, c->stream, c->k1, A);
+  else if (W <= 4) hipLaunchKernelGGL(k1_kernel<4>, dim3(grid), dim3(kBlock), c->k1.lds_bytes, c->stream, c->k1, A);
+  else hipLaunchKernelGGL(k1_kernel<8>, dim3(grid), dim3(kBlock), c->k1.lds_bytes, c->stream, c->k1, A);
   HIP_TRY(hipGetLastError());
   return TSG_OK;
 }
@@ -661,30 +947,60 @@ int tsg_ctx_create(int device, const tsg_ruleset* rs, const tsg_ctx_options* opt
   for (auto& e : c->ev) HIP_TRY(hipEventCreate(&e));
   const Plan& p = *rs->plan;
   const uint32_t W = (uint32_t)p.kw_words;
+  const uint32_t chunk = c->opt.chunk_bytes;
+  if (p.warm > kPad) return fail(TSG_ERR_CONFIG, "a keyword is longer than the K1 warm-up window");
   int rc;
-  if ((rc = make_device_dfa(*p.kw_dfa, {}, W, true, &c->kw))) return rc;
-  std::vector<uint32_t> gmask, galways;
-  for (const auto& g : p.groups) {
-    DeviceDFA dd;
-    if ((rc = make_device_dfa(*g.dfa, g.rules, W, false, &dd))) return rc;
-    c->groups.push_back(std::move(dd));
-    gmask.insert(gmask.end(), g.kwmask.begin(), g.kwmask.end());
-    galways.push_back(g.always ? 1 : 0);
+  if ((rc = make_device_k1(p, &c->k1, &c->tables))) return rc;
+  if (c->k1.lds_bytes > 64 * 1024)
+    HIP_TRY(hipFuncSetAttribute(k1_fn(W), hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->k1.lds_bytes));
+  const uint32_t G = (uint32_t)p.groups.size();
+  c->GW = std::max<uint32_t>(1, (G + 63) / 64);
+  std::vector<uint32_t> gmask, galways, gevents;
+  std::vector<unsigned long long> gofbit(32 * c->GW, 0);
+  uint32_t max_lds = 0;
+  for (uint32_t g = 0; g < G; g++) {
+    const auto& gp = p.groups[g];
+    DevDFA dd{};
+    if ((rc = make_device_dfa(*gp.dfa, gp.rules, &dd, &c->tables))) return rc;
+    max_lds = std::max(max_lds, dd.lds_bytes);
+    c->groups.push_back(dd);
+    gmask.insert(gmask.end(), gp.kwmask.begin(), gp.kwmask.end());
+    galways.push_back(gp.always ? 1 : 0);
+    gevents.push_back(gp.events);
+    uint32_t back = group_back(gp, chunk);
+    if (back > (uint32_t)kMaxBack) back = kMaxBack + 1;
+    c->gback.push_back(back);
+    if (back <= (uint32_t)kMaxBack) c->maxback = std::max(c->maxback, back);
+    for (int b = 0; b < 32; b++)
+      if (((gp.events >> b) & 1) || back > (uint32_t)kMaxBack) gofbit[b * c->GW + g / 64] |= 1ull << (g % 64);
   }
-  const size_t G = p.groups.size();
-  std::vector<void*> tmp;
+  if (max_lds > 64 * 1024) {
+    HIP_TRY(hipFuncSetAttribute((const void*)k2_list_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)max_lds));
+    HIP_TRY(hipFuncSetAttribute((const void*)k2_dense_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)max_lds));
+  }
   const uint32_t* cg = nullptr;
-  if ((rc = upload_vec(gmask, &cg, &tmp))) return rc;
+  if ((rc = upload_vec(gmask, &cg, &c->tables))) return rc;
   c->d_gmask = (uint32_t*)cg;
-  if ((rc = upload_vec(galways, &cg, &tmp))) return rc;
+  if ((rc = upload_vec(galways, &cg, &c->tables))) return rc;
   c->d_galways = (uint32_t*)cg;
+  if ((rc = upload_vec(gevents, &cg, &c->tables))) return rc;
+  c->d_gevents = (uint32_t*)cg;
+  if ((rc = upload_vec(c->gback, &cg, &c->tables))) return rc;
+  c->d_gback = (uint32_t*)cg;
+  const unsigned long long* cb = nullptr;
+  if ((rc = upload_vec(gofbit, &cb, &c->tables))) return rc;
+  c->d_gofbit = (unsigned long long*)cb;
+  const DevDFA* cd = nullptr;
+  if ((rc = upload_vec(c->groups, &cd, &c->tables))) return rc;
+  c->d_groups = (DevDFA*)cd;
   HIP_TRY(hipMalloc((void**)&c->d_cand, sizeof(DevCand) * c->opt.cand_capacity));
   HIP_TRY(hipMalloc((void**)&c->d_count, sizeof(uint32_t) * 4));
-  HIP_TRY(hipMalloc((void**)&c->d_gbytes, sizeof(unsigned long long) * (G + 1)));
-  HIP_TRY(hipMalloc((void**)&c->d_gfiles, sizeof(uint32_t) * (G + 1)));
-  HIP_TRY(hipMalloc((void**)&c->d_list_groups, sizeof(uint32_t) * (G + 1)));
-  HIP_TRY(hipMalloc((void**)&c->d_item_base, sizeof(uint64_t) * (G + 1)));
-  HIP_TRY(hipMalloc((void**)&c->d_item_count, sizeof(uint32_t) * (G + 1)));
+  HIP_TRY(hipMalloc((void**)&c->d_gcount, sizeof(uint32_t) * (G + 1)));
+  HIP_TRY(hipMalloc((void**)&c->d_cursor, sizeof(uint32_t) * (G + 1)));
+  HIP_TRY(hipMalloc((void**)&c->d_base, sizeof(uint64_t) * (G + 1)));
+  HIP_TRY(hipMalloc((void**)&c->d_listed, G + 1));
   HIP_TRY(hipHostMalloc((void**)&c->h_count, sizeof(uint32_t) * 4, hipHostMallocDefault));
   hipDeviceProp_t prop;
   HIP_TRY(hipGetDeviceProperties(&prop, device));
@@ -703,19 +1019,34 @@ int tsg_batch_upload(tsg_ctx* c, const uint8_t* data, const uint64_t* offsets, u
   if (offsets[0] != 0) return fail(TSG_ERR_ARG, "offsets[0] must be 0");
   for (uint32_t i = 0; i < nfiles; i++)
     if (offsets[i + 1] < offsets[i]) return fail(TSG_ERR_ARG, "offsets must be non-decreasing");
+  if (total && !data) return fail(TSG_ERR_ARG, "bad argument");
   const uint32_t chunk = c->opt.chunk_bytes;
   if (total / chunk >= (1ull << 32) - 2) return fail(TSG_ERR_ARG, "batch too large for u32 chunk ids");
   int rc;
-  if ((rc = ensure(&c->d_data, &c->d_data_cap, (size_t)total + 64))) return rc;
+  // front pad: K1 warm-up reads before the first chunk; tail: whole K1 items + look-ahead
+  const size_t tail = (size_t)kStreams * chunk + kPad;
+  if (c->d_data_cap < (size_t)total + kPad + tail || !c->d_data_alloc) {
+    if (c->d_data_alloc) HIP_TRY(hipFree(c->d_data_alloc));
+    c->d_data_alloc = nullptr;
+    HIP_TRY(hipMalloc((void**)&c->d_data_alloc, (size_t)total + kPad + tail));
+    c->d_data_cap = (size_t)total + kPad + tail;
+  }
+  c->d_data = c->d_data_alloc + kPad;
   if ((rc = ensure(&c->d_off, &c->d_off_cap, (size_t)nfiles + 1))) return rc;
   const uint64_t nchunks = (total + chunk - 1) / chunk;
-  if ((rc = ensure(&c->d_chunk_file, &c->d_chunk_cap, (size_t)nchunks + 1))) return rc;
+  // K1 items are kStreams chunks: chunk-indexed arrays are padded to whole items
+  const uint64_t nchunks_pad = (nchunks + kStreams - 1) / kStreams * kStreams + 1;
+  if ((rc = ensure(&c->d_chunk_file, &c->d_chunk_cap, (size_t)nchunks_pad))) return rc;
+  if ((rc = ensure(&c->d_ev, &c->d_ev_cap, (size_t)nchunks_pad))) return rc;
   const int W = c->rs->plan->kw_words;
   if ((rc = ensure(&c->d_kw, &c->d_kw_cap, (size_t)nfiles * W + 1))) return rc;
+  if ((rc = ensure(&c->d_ggate, &c->d_ggate_cap, (size_t)nfiles * c->GW + 1))) return rc;
   if ((rc = ensure(&c->d_ovf, &c->d_ovf_cap, (size_t)nfiles + 1))) return rc;
+  HIP_TRY(hipMemsetAsync(c->d_data_alloc, 0, kPad, c->stream));
   if (total) HIP_TRY(hipMemcpyAsync(c->d_data, data, total, hipMemcpyHostToDevice, c->stream));
-  HIP_TRY(hipMemsetAsync(c->d_data + total, 0, 64, c->stream));
+  HIP_TRY(hipMemsetAsync(c->d_data + total, 0, tail, c->stream));
   HIP_TRY(hipMemcpyAsync(c->d_off, offsets, sizeof(uint64_t) * (nfiles + 1), hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(hipMemsetAsync(c->d_chunk_file, 0, sizeof(uint32_t) * nchunks_pad, c->stream));
   if (nfiles) {
     chunk_file_kernel<<<(nfiles + 255) / 256, 256, 0, c->stream>>>(c->d_off, nfiles, chunk, c->d_chunk_file);
     HIP_TRY(hipGetLastError());
@@ -747,11 +1078,84 @@ int tsg_batch_kernels(tsg_ctx* c) {
     HIP_TRY(hipMemsetAsync(c->d_ovf, 0, sizeof(uint32_t) * F, st));
   }
   HIP_TRY(hipMemsetAsync(c->d_count, 0, sizeof(uint32_t) * 4, st));
-  HIP_TRY(hipMemsetAsync(c->d_gbytes, 0, sizeof(unsigned long long) * (G + 1), st));
-  HIP_TRY(hipMemsetAsync(c->d_gfiles, 0, sizeof(uint32_t) * (G + 1), st));
-  HIP_TRY(hipMemsetAsync(c->d_item_count, 0, sizeof(uint32_t) * (G + 1), st));
+  HIP_TRY(hipMemsetAsync(c->d_gcount, 0, sizeof(uint32_t) * (G + 1), st));
+  HIP_TRY(hipMemsetAsync(c->d_cursor, 0, sizeof(uint32_t) * (G + 1), st));
   HIP_TRY(hipEventRecord(c->ev[1], st));
 
+  // ---- K1
+  const uint64_t k1_items = (nchunks + kStreams - 1) / kStreams;
+  int rc;
+  if (k1_items) {
+    K1Args A{c->d_data, c->d_off, c->d_chunk_file, c->total, nchunks, k1_items, 1, chunk, F, c->d_kw, c->d_ev,
+             nullptr};
+    if ((rc = launch_k1(c, A))) return rc;
+  }
+  HIP_TRY(hipEventRecord(c->ev[2], st));
+
+  // ---- gate + item counts
+  std::vector<uint32_t> gcount(G, 0);
+  ItemArgs IA{};
+  IA.off = c->d_off;
+  IA.chunk_file = c->d_chunk_file;
+  IA.ev = c->d_ev;
+  IA.ggate = c->d_ggate;
+  IA.gofbit = c->d_gofbit;
+  IA.gevents = c->d_gevents;
+  IA.gback = c->d_gback;
+  IA.nchunks = nchunks;
+  IA.F = F;
+  IA.G = G;
+  IA.GW = c->GW;
+  IA.chunk = chunk;
+  IA.maxback = c->maxback;
+  IA.count = c->d_gcount;
+  IA.cursor = c->d_cursor;
+  IA.listed = c->d_listed;
+  const int igrid = (int)((nchunks + kBlock - 1) / kBlock);
+  if (F && G && nchunks) {
+    ggate_kernel<<<(F + 255) / 256, 256, 0, st>>>(c->d_kw, F, W, c->d_gmask, c->d_galways, G, c->GW, c->d_ggate);
+    HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL(items_kernel<false>, dim3(igrid), dim3(kBlock), G * sizeof(uint32_t) + 16, st, IA);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpyAsync(gcount.data(), c->d_gcount, sizeof(uint32_t) * G, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+  }
+  // DENSE when a group's items cover a large share of the batch, LIST otherwise
+  std::vector<uint32_t> dense;
+  std::vector<uint64_t> base(G, 0);
+  std::vector<uint8_t> listed(G, 0);
+  std::vector<uint4> blkmap;
+  uint64_t nitems = 0, k2_bytes = 0;
+  uint32_t list_lds = 0;
+  const uint32_t per_block = kBlock * 2;
+  for (uint32_t g = 0; g < G; g++) {
+    if (gcount[g] == 0) continue;
+    k2_bytes += (uint64_t)gcount[g] * chunk;
+    if ((uint64_t)gcount[g] * 2 > nchunks) {
+      dense.push_back(g);
+      continue;
+    }
+    listed[g] = 1;
+    base[g] = nitems;
+    for (uint32_t first = 0; first < gcount[g]; first += per_block)
+      blkmap.push_back(make_uint4(g, (uint32_t)nitems + first, std::min(per_block, gcount[g] - first), 0));
+    nitems += gcount[g];
+    list_lds = std::max(list_lds, c->groups[g].lds_bytes);
+  }
+  if (nitems) {
+    if ((rc = ensure(&c->d_items, &c->d_items_cap, (size_t)nitems))) return rc;
+    if ((rc = ensure(&c->d_blkmap, &c->d_blkmap_cap, blkmap.size()))) return rc;
+    HIP_TRY(hipMemcpyAsync(c->d_base, base.data(), sizeof(uint64_t) * G, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(c->d_listed, listed.data(), G, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(c->d_blkmap, blkmap.data(), sizeof(uint4) * blkmap.size(), hipMemcpyHostToDevice, st));
+    IA.base = c->d_base;
+    IA.items = c->d_items;
+    hipLaunchKernelGGL(items_kernel<true>, dim3(igrid), dim3(kBlock), 16, st, IA);
+    HIP_TRY(hipGetLastError());
+  }
+  HIP_TRY(hipEventRecord(c->ev[3], st));
+
+  // ---- K2
   ScanArgsDev A{};
   A.data = c->d_data;
   A.off = c->d_off;
@@ -765,70 +1169,22 @@ int tsg_batch_kernels(tsg_ctx* c) {
   A.cand_count = c->d_count;
   A.cand_cap = c->opt.cand_capacity;
   A.ovf = c->d_ovf;
-  int rc;
-  // ---- K1
-  A.nitems = (nchunks + kStreams - 1) / kStreams;
-  if ((rc = launch_scan<true, false>(c, c->kw.dev, A))) return rc;
-  HIP_TRY(hipEventRecord(c->ev[2], st));
-  // ---- gate: per-group gated bytes / files
-  if (F && G) {
-    size_t lds = G * (sizeof(unsigned long long) + sizeof(uint32_t)) + 16;
-    gate_count_kernel<<<(F + 255) / 256, 256, lds, st>>>(c->d_off, F, c->d_kw, W, c->d_gmask, c->d_galways,
-                                                           G, c->d_gbytes, c->d_gfiles);
+  if (nitems) {
+    ScanArgsDev B = A;
+    B.items = c->d_items;
+    B.nitems = nitems;
+    hipLaunchKernelGGL(k2_list_kernel, dim3((uint32_t)blkmap.size()), dim3(kBlock), list_lds, st,
+                       (const DevDFA*)c->d_groups, (const uint4*)c->d_blkmap, B);
     HIP_TRY(hipGetLastError());
   }
-  c->h_gbytes.assign(G, 0);
-  c->h_gfiles.assign(G, 0);
-  if (G) {
-    HIP_TRY(hipMemcpyAsync(c->h_gbytes.data(), c->d_gbytes, sizeof(unsigned long long) * G, hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipMemcpyAsync(c->h_gfiles.data(), c->d_gfiles, sizeof(uint32_t) * G, hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipStreamSynchronize(st));
-  }
-  // DENSE when a group is gated on a large share of the batch, LIST otherwise
-  std::vector<uint32_t> list_groups, dense_groups;
-  std::vector<uint64_t> base;
-  uint64_t nitems_total = 0, k2_bytes = 0;
-  for (uint32_t g = 0; g < G; g++) {
-    k2_bytes += c->h_gbytes[g];
-    if (c->h_gbytes[g] == 0) continue;
-    if (c->h_gbytes[g] * 4 > c->total) {
-      dense_groups.push_back(g);
-    } else {
-      list_groups.push_back(g);
-      base.push_back(nitems_total);
-      nitems_total += c->h_gbytes[g] / chunk + 2ull * c->h_gfiles[g];
-    }
-  }
-  if (!list_groups.empty()) {
-    if ((rc = ensure(&c->d_items, &c->d_items_cap, (size_t)nitems_total))) return rc;
-    HIP_TRY(hipMemcpyAsync(c->d_list_groups, list_groups.data(), sizeof(uint32_t) * list_groups.size(),
-                           hipMemcpyHostToDevice, st));
-    HIP_TRY(hipMemcpyAsync(c->d_item_base, base.data(), sizeof(uint64_t) * base.size(), hipMemcpyHostToDevice, st));
-    gate_list_kernel<<<(F + 255) / 256, 256, 0, st>>>(c->d_off, F, c->d_kw, W, c->d_gmask, c->d_galways,
-                                                       c->d_list_groups, (uint32_t)list_groups.size(),
-                                                       c->d_item_base, c->d_item_count, c->d_items, chunk);
-    HIP_TRY(hipGetLastError());
-  }
-  std::vector<uint32_t> item_count(list_groups.size(), 0);
-  if (!list_groups.empty()) {
-    HIP_TRY(hipMemcpyAsync(item_count.data(), c->d_item_count, sizeof(uint32_t) * list_groups.size(),
-                           hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipStreamSynchronize(st));
-  }
-  HIP_TRY(hipEventRecord(c->ev[3], st));
-  // ---- K2
-  for (uint32_t g : dense_groups) {
+  for (uint32_t g : dense) {
     ScanArgsDev B = A;
     B.nitems = (nchunks + kStreams - 1) / kStreams;
     B.gmask = c->d_gmask + (size_t)g * W;
     B.galways = p.groups[g].always ? 1 : 0;
-    if ((rc = launch_scan<false, false>(c, c->groups[g].dev, B))) return rc;
-  }
-  for (size_t j = 0; j < list_groups.size(); j++) {
-    ScanArgsDev B = A;
-    B.nitems = item_count[j];
-    B.items = c->d_items + base[j];
-    if ((rc = launch_scan<false, true>(c, c->groups[list_groups[j]].dev, B))) return rc;
+    const int grid = (int)std::min<uint64_t>((B.nitems + kBlock - 1) / kBlock, (uint64_t)c->grid);
+    hipLaunchKernelGGL(k2_dense_kernel, dim3(grid), dim3(kBlock), c->groups[g].lds_bytes, st, c->groups[g], B);
+    HIP_TRY(hipGetLastError());
   }
   HIP_TRY(hipEventRecord(c->ev[4], st));
   HIP_TRY(hipMemcpyAsync(c->h_count, c->d_count, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
@@ -849,13 +1205,15 @@ int tsg_batch_kernels(tsg_ctx* c) {
   float t[5] = {0, 0, 0, 0, 0};
   for (int k = 0; k < 5; k++) HIP_TRY(hipEventElapsedTime(&t[k], c->ev[k], c->ev[k + 1]));
   c->stats.k1_ms = t[1];
+  c->stats.gate_ms = t[2];
   c->stats.k2_ms = t[3];
-  c->stats.aux_ms = t[0] + t[2] + t[4];
+  c->stats.aux_ms = t[0] + t[4];
   c->stats.bytes = c->total;
   c->stats.k2_bytes = k2_bytes;
+  c->stats.k2_items = nitems;
   c->stats.candidates = *c->h_count;
   c->stats.overflow = *c->h_count > c->opt.cand_capacity ? 1 : 0;
-  c->stats.k2_launches = (uint32_t)(dense_groups.size() + list_groups.size());
+  c->stats.k2_launches = (uint32_t)(dense.size() + (nitems ? 1 : 0));
   return TSG_OK;
 }
 
@@ -890,6 +1248,16 @@ int tsg_scan_batch(tsg_ctx* c, const uint8_t* data, const uint64_t* offsets, uin
   int rc = tsg_batch_upload(c, data, offsets, nfiles, paths, path_offsets);
   if (rc) return rc;
   return tsg_batch_scan(c, out);
+}
+
+int tsg_batch_k1_output(tsg_ctx* c, uint32_t* kw, size_t kw_len, uint32_t* ev, size_t ev_len) {
+  if (!c || !c->uploaded) return fail(TSG_ERR_ARG, "no batch uploaded");
+  HIP_TRY(hipSetDevice(c->device));
+  const uint64_t nchunks = (c->total + c->opt.chunk_bytes - 1) / c->opt.chunk_bytes;
+  if (kw) std::memcpy(kw, c->ko.kw.data(), sizeof(uint32_t) * std::min(kw_len, c->ko.kw.size()));
+  if (ev && nchunks)
+    HIP_TRY(hipMemcpy(ev, c->d_ev, sizeof(uint32_t) * std::min<uint64_t>(ev_len, nchunks), hipMemcpyDeviceToHost));
+  return TSG_OK;
 }
 
 int tsg_ctx_get_stats(const tsg_ctx* c, tsg_stats* out) {

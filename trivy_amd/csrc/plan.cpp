@@ -14,6 +14,89 @@ static bool is_ascii(const std::string& s) {
   return true;
 }
 
+namespace {
+
+bool in_set(const uint64_t* set, const uint8_t* cls, int bit) {
+  for (int c = 0; c < 128; c++)
+    if (((set[c >> 6] >> (c & 63)) & 1) && !((cls[c] >> bit) & 1)) return false;
+  return true;
+}
+
+struct Anchor {
+  uint32_t kind = kEvAlways;  // kEvRunU, kEvRunD, kEvLit0 (literal), kEvAlways
+  std::string lit;
+  int first_atom = 0;
+  int64_t evdist = 0;
+  std::string desc = "none";
+};
+
+// The event every match of a rule must contain, preferring long class runs (the secret
+// part of nearly every rule) over literals: the keyword gate already handles rare
+// literals, and common ones ("key", "sk", "-----") would put events everywhere.
+Anchor choose_anchor(const Regexp& re, const Plan& p) {
+  const std::vector<AtomInfo> at = re.Atoms();
+  const int n = (int)at.size();
+  std::vector<int64_t> B(n + 1, 0);
+  for (int i = 0; i < n; i++)
+    B[i + 1] = (B[i] < 0 || at[i].max_bytes < 0) ? -1 : B[i] + at[i].max_bytes;
+  Anchor best;
+  auto take = [&](uint32_t kind, int t, int64_t len, const std::string& lit, const char* what) {
+    Anchor a;
+    a.kind = kind;
+    a.lit = lit;
+    if (B[t] >= 0) {
+      a.first_atom = 0;
+      a.evdist = B[t] + len - 1;
+    } else {
+      a.first_atom = t;  // unbounded prefix: the GPU program is the suffix from the anchor
+      a.evdist = len - 1;
+    }
+    a.desc = std::string(what) + (lit.empty() ? "" : " '" + lit + "'") + " at atom " +
+             std::to_string(t) + (a.first_atom ? " (suffix)" : "");
+    return a;
+  };
+  for (int bit = 0; bit < 2; bit++) {
+    const int k = p.run_k[bit];
+    for (int i = 0; i < n;) {
+      if (!(at[i].ascii_only && in_set(at[i].set, p.run_cls, bit))) {
+        i++;
+        continue;
+      }
+      int j = i;
+      int64_t run = 0;
+      while (j < n && at[j].ascii_only && in_set(at[j].set, p.run_cls, bit)) run += at[j++].min_bytes;
+      if (run >= k) return take(bit == 0 ? kEvRunU : kEvRunD, i, k, "", bit == 0 ? "run U" : "run D");
+      i = j;
+    }
+  }
+  double best_score = 0;
+  for (int i = 0; i < n;) {
+    if (at[i].lit < 0) {
+      i++;
+      continue;
+    }
+    int j = i;
+    std::string s;
+    double score = 0;
+    while (j < n && at[j].lit >= 0) {
+      int c = at[j].lit;
+      if (s.size() < 24) {
+        s.push_back((char)c);
+        score += (c >= 'a' && c <= 'z') ? 1.0 : (c >= '0' && c <= '9') ? 1.3 : 1.6;
+      }
+      j++;
+    }
+    if (score >= 3.0 && score > best_score) {
+      best_score = score;
+      best = take(1u << kEvLit0, i, (int64_t)s.size(), s, "literal");
+    }
+    i = j;
+  }
+  return best;
+}
+
+}  // namespace
+
 std::unique_ptr<Plan> build_plan(const Ruleset& rs, const PlanOptions& opt, std::string* err) {
   auto p = std::make_unique<Plan>();
   const size_t R = rs.rules.size();
@@ -22,8 +105,19 @@ std::unique_ptr<Plan> build_plan(const Ruleset& rs, const PlanOptions& opt, std:
   p->rule_group.assign(R, -1);
   p->rule_hostonly.assign(R, 0);
   p->rule_maxlen.assign(R, -1);
+  p->rule_event.assign(R, kEvAlways);
+  p->rule_evdist.assign(R, 0);
+  p->rule_first_atom.assign(R, 0);
+  p->rule_anchor.assign(R, "none");
+  // run classes: U = [A-Za-z0-9+/=_.-] (secrets, tokens, base64), D = [0-9-]
+  for (int c = 0; c < 256; c++) {
+    bool u = (c >= 'A' && c <= 'Z') || (c >= 'a' && c <= 'z') || (c >= '0' && c <= '9') ||
+             c == '+' || c == '/' || c == '=' || c == '_' || c == '.' || c == '-';
+    bool d = (c >= '0' && c <= '9') || c == '-';
+    p->run_cls[c] = (uint8_t)((u ? 1 : 0) | (d ? 2 : 0));
+  }
 
-  // ---- K1 keyword automaton
+  // ---- keywords (Rule.MatchKeywords, scanner.go:164-176)
   std::map<std::string, uint32_t> kwid;
   std::vector<std::string> kws;
   for (size_t r = 0; r < R; r++) {
@@ -55,22 +149,74 @@ std::unique_ptr<Plan> build_plan(const Ruleset& rs, const PlanOptions& opt, std:
   kws.push_back("\xc5\xbf");      // U+017F, (?i)s folds to it
   p->n_kw = (int)kws.size();
   p->kw_words = (p->n_kw + 31) / 32;
-  {
-    DFAOptions o;
-    o.max_states = 32767;
-    o.with_noinject = false;
-    std::string e;
-    p->kw_dfa = build_keyword_dfa(kws, o, &e);
-    if (!p->kw_dfa) {
-      if (err) *err = "keyword automaton: " + e;
-      return nullptr;
-    }
-  }
 
-  // ---- K2 rule groups (greedy packing under the state / table caps)
+  // ---- per rule: anchor event and GPU program
   DFAOptions one;
   one.max_states = opt.max_group_states;
-  std::vector<uint32_t> cur;
+  auto fits = [&](const DFA& d, size_t nrules) {
+    return d.nstates <= opt.max_group_states &&
+           (size_t)d.nstates * d.nclasses * 2 <= (size_t)opt.max_group_table_bytes &&
+           (int)nrules <= opt.max_rules_per_group;
+  };
+  p->rule_relax.assign(R, -1);
+  p->rule_atoms.assign(R, -1);
+  p->rule_winback.assign(R, -1);
+  p->rule_prog.assign(R, Prog{});
+  std::vector<std::unique_ptr<DFA>> single(R);
+  std::vector<Anchor> anchor(R);
+  for (size_t r = 0; r < R; r++) {
+    const RuleC& rule = rs.rules[r];
+    if (!rule.regex) continue;
+    p->rule_maxlen[r] = max_match_len(rule.regex->prog());
+    if (opt.anchors) anchor[r] = choose_anchor(*rule.regex, *p);
+    const int fa = anchor[r].first_atom;
+    // exact program first, then ever stronger relaxations of counted repetitions, then
+    // ever shorter prefixes of the top-level concatenation
+    for (int k : {-1, 32, 16, 8, 4, 2, 1, 0}) {
+      Prog pr = (k < 0 && fa == 0) ? rule.regex->prog() : rule.regex->RelaxedProg(k, -1, fa);
+      std::string e;
+      auto d = build_dfa({&pr}, one, &e);
+      if (d && fits(*d, 1)) {
+        single[r] = std::move(d);
+        p->rule_relax[r] = k;
+        p->rule_prog[r] = std::move(pr);
+        break;
+      }
+    }
+    for (int t = rule.regex->NumAtoms() - fa - 1; !single[r] && t >= 1; t--) {
+      for (int k : {8, 2, 0}) {
+        Prog pr = rule.regex->RelaxedProg(k, t, fa);
+        std::string e;
+        auto d = build_dfa({&pr}, one, &e);
+        if (d && fits(*d, 1)) {
+          single[r] = std::move(d);
+          p->rule_relax[r] = k;
+          p->rule_atoms[r] = t;
+          p->rule_prog[r] = std::move(pr);
+          break;
+        }
+      }
+    }
+    if (!single[r]) {
+      p->rule_hostonly[r] = 1;
+      continue;
+    }
+    // where a GPU end offset e lets the exact match start
+    if (fa > 0) {
+      p->rule_winback[r] = -1;
+    } else if (p->rule_atoms[r] >= 0) {
+      p->rule_winback[r] = max_match_len(rule.regex->RelaxedProg(-1, p->rule_atoms[r]));
+    } else {
+      p->rule_winback[r] = p->rule_maxlen[r];
+    }
+    p->rule_event[r] = anchor[r].kind;
+    p->rule_evdist[r] = anchor[r].evdist;
+    p->rule_first_atom[r] = fa;
+    p->rule_anchor[r] = anchor[r].desc;
+  }
+
+  // ---- K2 rule groups: greedy packing under the state / table caps, among rules with
+  // the same kind of event (their windows coincide)
   auto group_kwmask = [&](GroupPlan& g) {
     g.kwmask.assign(p->kw_words, 0);
     for (uint32_t r : g.rules) {
@@ -82,84 +228,106 @@ std::unique_ptr<Plan> build_plan(const Ruleset& rs, const PlanOptions& opt, std:
     }
     for (int k = p->fb_kw0; k < p->n_kw; k++) g.kwmask[k / 32] |= 1u << (k % 32);
   };
-  auto fits = [&](const DFA& d, size_t nrules) {
-    return d.nstates <= opt.max_group_states &&
-           (size_t)d.nstates * d.nclasses * 2 <= (size_t)opt.max_group_table_bytes &&
-           (int)nrules <= opt.max_rules_per_group;
-  };
-  std::unique_ptr<DFA> cur_dfa;
-  auto flush = [&]() {
-    if (cur.empty()) return;
-    GroupPlan g;
-    g.dfa = std::move(cur_dfa);
-    g.rules = cur;
-    group_kwmask(g);
-    for (uint32_t r : cur) p->rule_group[r] = (int)p->groups.size();
-    p->groups.push_back(std::move(g));
-    cur.clear();
-  };
-  p->rule_relax.assign(R, -1);
-  p->rule_atoms.assign(R, -1);
-  p->rule_winback.assign(R, -1);
-  p->rule_prog.assign(R, Prog{});
-  for (size_t r = 0; r < R; r++) {
-    const RuleC& rule = rs.rules[r];
-    if (!rule.regex) continue;
-    p->rule_maxlen[r] = max_match_len(rule.regex->prog());
-    p->rule_winback[r] = p->rule_maxlen[r];
-    // exact program first, then ever stronger relaxations of counted repetitions, then
-    // ever shorter prefixes of the top-level concatenation
-    std::unique_ptr<DFA> single;
-    for (int k : {-1, 32, 16, 8, 4, 2, 1, 0}) {
-      Prog pr = k < 0 ? rule.regex->prog() : rule.regex->RelaxedProg(k);
+  for (uint32_t kind : {kEvRunU, kEvRunD, 1u << kEvLit0, kEvAlways}) {
+    std::vector<uint32_t> cur;
+    std::unique_ptr<DFA> cur_dfa;
+    auto flush = [&]() {
+      if (cur.empty()) return;
+      GroupPlan g;
+      g.dfa = std::move(cur_dfa);
+      g.rules = cur;
+      group_kwmask(g);
+      g.events = kind;
+      g.evdist = 0;
+      for (uint32_t r : cur) {
+        p->rule_group[r] = (int)p->groups.size();
+        g.evdist = std::max(g.evdist, p->rule_evdist[r]);
+      }
+      p->groups.push_back(std::move(g));
+      cur.clear();
+    };
+    for (size_t r = 0; r < R; r++) {
+      if (!single[r] || p->rule_event[r] != kind) continue;
+      if (cur.empty()) {
+        cur.push_back((uint32_t)r);
+        cur_dfa = std::move(single[r]);
+        continue;
+      }
+      std::vector<const Prog*> progs;
+      for (uint32_t q : cur) progs.push_back(&p->rule_prog[q]);
+      progs.push_back(&p->rule_prog[r]);
       std::string e;
-      auto d = build_dfa({&pr}, one, &e);
-      if (d && fits(*d, 1)) {
-        single = std::move(d);
-        p->rule_relax[r] = k;
-        p->rule_prog[r] = std::move(pr);
-        break;
+      auto merged = build_dfa(progs, one, &e);
+      if (merged && fits(*merged, cur.size() + 1)) {
+        cur.push_back((uint32_t)r);
+        cur_dfa = std::move(merged);
+      } else {
+        flush();
+        cur.push_back((uint32_t)r);
+        cur_dfa = std::move(single[r]);
       }
     }
-    for (int t = rule.regex->NumAtoms() - 1; !single && t >= 1; t--) {
-      for (int k : {8, 2, 0}) {
-        Prog pr = rule.regex->RelaxedProg(k, t);
-        std::string e;
-        auto d = build_dfa({&pr}, one, &e);
-        if (d && fits(*d, 1)) {
-          single = std::move(d);
-          p->rule_relax[r] = k;
-          p->rule_atoms[r] = t;
-          p->rule_prog[r] = std::move(pr);
-          p->rule_winback[r] = max_match_len(rule.regex->RelaxedProg(-1, t));
-          break;
-        }
-      }
-    }
-    if (!single) {
-      p->rule_hostonly[r] = 1;
-      continue;
-    }
-    if (cur.empty()) {
-      cur.push_back((uint32_t)r);
-      cur_dfa = std::move(single);
-      continue;
-    }
-    std::vector<const Prog*> progs;
-    for (uint32_t q : cur) progs.push_back(&p->rule_prog[q]);
-    progs.push_back(&p->rule_prog[r]);
-    std::string e;
-    auto merged = build_dfa(progs, one, &e);
-    if (merged && fits(*merged, cur.size() + 1)) {
-      cur.push_back((uint32_t)r);
-      cur_dfa = std::move(merged);
-    } else {
-      flush();
-      cur.push_back((uint32_t)r);
-      cur_dfa = std::move(single);
-    }
+    flush();
   }
-  flush();
+
+  // ---- K1 automaton: keywords + anchor literals; literal groups share event bits
+  std::vector<char> litg(p->groups.size(), 0);
+  for (size_t g = 0; g < p->groups.size(); g++) litg[g] = p->groups[g].events == (1u << kEvLit0);
+  auto build_k1 = [&](bool with_anchors) -> bool {
+    std::vector<std::string> lits = kws;
+    std::vector<uint32_t> lit_event(lits.size(), 0);
+    std::map<std::string, uint32_t> lid;
+    for (size_t i = 0; i < lits.size(); i++) lid.emplace(lits[i], (uint32_t)i);
+    int nlitgroups = 0;
+    for (size_t gi = 0; gi < p->groups.size(); gi++) {
+      GroupPlan& g = p->groups[gi];
+      if (!litg[gi]) continue;
+      if (!with_anchors) {
+        g.events = kEvAlways;
+        for (uint32_t r : g.rules) p->rule_event[r] = kEvAlways;
+        continue;
+      }
+      const uint32_t bit = 1u << (kEvLit0 + (nlitgroups++ % kEvLitBits));
+      g.events = bit;
+      for (uint32_t r : g.rules) {
+        p->rule_event[r] = bit;
+        const std::string& s = anchor[r].lit;
+        auto it = lid.find(s);
+        uint32_t id;
+        if (it == lid.end()) {
+          id = (uint32_t)lits.size();
+          lid.emplace(s, id);
+          lits.push_back(s);
+          lit_event.push_back(0);
+        } else {
+          id = it->second;
+        }
+        lit_event[id] |= bit;
+      }
+    }
+    DFAOptions o;
+    o.max_states = 32767;
+    o.with_noinject = false;
+    std::string e;
+    auto d = build_keyword_dfa(lits, o, &e);
+    if (!d) return false;
+    if ((size_t)d->nstates * d->nclasses * 2 > (size_t)opt.max_kw_table_bytes) return false;
+    p->n_lit = (int)lits.size();
+    p->kw_mask_events.assign(d->masks.size(), 0);
+    for (size_t m = 0; m < d->masks.size(); m++)
+      for (int id = 0; id < p->n_lit; id++)
+        if ((d->masks[m][id / 64] >> (id % 64)) & 1) p->kw_mask_events[m] |= lit_event[id];
+    size_t longest = 0;
+    for (const auto& s : lits) longest = std::max(longest, s.size());
+    int w = (int)std::max<size_t>(longest, (size_t)std::max(p->run_k[0], p->run_k[1]));
+    p->warm = (w - 1 + 15) / 16 * 16;
+    p->kw_dfa = std::move(d);
+    return true;
+  };
+  if (!build_k1(opt.anchors) && !build_k1(false)) {
+    if (err) *err = "keyword automaton exceeds the K1 table budget";
+    return nullptr;
+  }
 
   // ---- Global.AllowPath automaton (exact on ASCII paths)
   std::vector<const Prog*> paths;
@@ -364,69 +532,74 @@ bool run_segment(const DFA& d, const uint8_t* data, uint64_t fs, uint64_t fe, ui
   return false;
 }
 
-// K1: keywords are bounded, so the lane simply keeps going in inject mode for
-// max_len - 1 bytes past its piece (every keyword occurrence that starts in the piece
-// is seen; occurrences found in the overlap are real occurrences too).
-template <class OnAcc>
-void run_kw_segment(const DFA& d, const uint8_t* data, uint64_t fs, uint64_t fe, uint64_t a,
-                    uint64_t b, OnAcc on_acc) {
-  const int nc = d.nclasses;
-  uint64_t ext = d.max_len > 1 ? (uint64_t)d.max_len - 1 : 0;
-  uint64_t stop = std::min(fe, b + ext);
-  uint32_t s = (a == fs) ? d.start[kCtxBOT] : d.start[DFA::ctx_of(data[a - 1], d)];
-  for (uint64_t p = a; p < stop; p++) {
-    size_t e = (size_t)s * nc + d.cls[data[p]];
-    if (d.acc[e]) on_acc(d.acc[e], p - fs);
-    s = d.next[e];
-  }
-  if (stop == fe && d.eot_acc[s]) on_acc(d.eot_acc[s], fe - fs);
-}
-
 }  // namespace
 
-void emulate_kernels(const Plan& plan, const BatchView& bv, uint32_t chunk, uint32_t ext_cap,
-                     KernelOutput* ko) {
+void k1_reference(const Plan& plan, const BatchView& bv, uint32_t chunk, std::vector<uint32_t>* kw,
+                  std::vector<uint32_t>* ev) {
   const uint32_t F = bv.nfiles;
   const uint64_t total = bv.offsets[F];
-  ko->kw.assign((size_t)F * plan.kw_words, 0);
+  const DFA& d = *plan.kw_dfa;
+  const int nc = d.nclasses;
+  const int W = plan.kw_words;
+  kw->assign((size_t)F * W, 0);
+  ev->assign((total + chunk - 1) / chunk, 0);
+  for (uint32_t f = 0; f < F; f++) {
+    const uint64_t fs = bv.offsets[f], fe = bv.offsets[f + 1];
+    uint32_t s = d.start[kCtxBOT];
+    uint32_t cu = 0, cd = 0;
+    for (uint64_t p = fs; p < fe; p++) {
+      const uint8_t c = bv.data[p];
+      s = d.next[(size_t)s * nc + d.cls[c]];
+      uint32_t e = 0;
+      // arrival in state s: the literals its match set holds end with byte p
+      const uint32_t mi = d.eot_acc[s];
+      if (mi) {
+        const auto& m = d.masks[mi];
+        for (int k = 0; k < plan.n_kw; k++)
+          if ((m[k / 64] >> (k % 64)) & 1) (*kw)[(size_t)f * W + k / 32] |= 1u << (k % 32);
+        e |= plan.kw_mask_events[mi];
+      }
+      cu = (plan.run_cls[c] & 1) ? cu + 1 : 0;
+      cd = (plan.run_cls[c] & 2) ? cd + 1 : 0;
+      if ((int)cu >= plan.run_k[0]) e |= kEvRunU;
+      if ((int)cd >= plan.run_k[1]) e |= kEvRunD;
+      (*ev)[p / chunk] |= e;
+    }
+  }
+}
+
+void emulate_kernels(const Plan& plan, const BatchView& bv, uint32_t chunk, uint32_t ext_cap,
+                     KernelOutput* ko, std::vector<uint64_t>* group_item_bytes) {
+  const uint32_t F = bv.nfiles;
+  std::vector<uint32_t> ev;
+  k1_reference(plan, bv, chunk, &ko->kw, &ev);
   ko->cand.clear();
   ko->overflow.assign(F, 0);
-  const uint64_t nchunks = (total + chunk - 1) / chunk;
-  for (int pass = 0; pass < 2; pass++) {
-    for (uint64_t c = 0; c < nchunks; c++) {
-      uint64_t a = c * chunk, b = std::min<uint64_t>(a + chunk, total);
-      uint32_t f = (uint32_t)(std::upper_bound(bv.offsets, bv.offsets + F + 1, a) - bv.offsets) - 1;
-      while (a < b && f < F) {
-        uint64_t fs = bv.offsets[f], fe = bv.offsets[f + 1];
-        if (fe == fs) {
-          f++;
-          continue;
-        }
-        uint64_t se = std::min(b, fe);
-        if (pass == 0) {
-          const DFA& d = *plan.kw_dfa;
-          run_kw_segment(d, bv.data, fs, fe, a, se, [&](uint32_t mi, uint64_t) {
-            const auto& m = d.masks[mi];
-            for (int k = 0; k < plan.n_kw; k++)
-              if ((m[k / 64] >> (k % 64)) & 1) ko->kw[(size_t)f * plan.kw_words + k / 32] |= 1u << (k % 32);
-          });
-        } else {
-          const uint32_t* kw = ko->kw.data() + (size_t)f * plan.kw_words;
-          for (const auto& g : plan.groups) {
-            bool gate = g.always;
-            for (int w = 0; w < plan.kw_words && !gate; w++) gate = (kw[w] & g.kwmask[w]) != 0;
-            if (!gate) continue;
-            const DFA& d = *g.dfa;
-            bool o = run_segment(d, bv.data, fs, fe, a, se, ext_cap, [&](uint32_t mi, uint64_t pos) {
-              const auto& m = d.masks[mi];
-              for (size_t k = 0; k < g.rules.size(); k++)
-                if ((m[k / 64] >> (k % 64)) & 1) ko->cand.push_back({f, g.rules[k], (uint32_t)pos});
-            });
-            if (o) ko->overflow[f] = 1;
-          }
-        }
-        a = se;
-        f++;
+  if (group_item_bytes) group_item_bytes->assign(plan.groups.size(), 0);
+  for (size_t gi = 0; gi < plan.groups.size(); gi++) {
+    const GroupPlan& g = plan.groups[gi];
+    const uint32_t back = group_back(g, chunk);
+    const DFA& d = *g.dfa;
+    for (uint32_t f = 0; f < F; f++) {
+      const uint64_t fs = bv.offsets[f], fe = bv.offsets[f + 1];
+      if (fe == fs) continue;
+      const uint32_t* kw = ko->kw.data() + (size_t)f * plan.kw_words;
+      bool gate = g.always;
+      for (int w = 0; w < plan.kw_words && !gate; w++) gate = (kw[w] & g.kwmask[w]) != 0;
+      if (!gate) continue;
+      const uint64_t c0 = fs / chunk, c1 = (fe - 1) / chunk;
+      for (uint64_t c = c0; c <= c1; c++) {
+        bool need = (g.events & kEvAlways) != 0;
+        for (uint64_t q = c; q <= std::min<uint64_t>(c + back, c1) && !need; q++) need = (ev[q] & g.events) != 0;
+        if (!need) continue;
+        const uint64_t a = std::max<uint64_t>(fs, c * chunk), b = std::min<uint64_t>(fe, (c + 1) * chunk);
+        if (group_item_bytes) (*group_item_bytes)[gi] += b - a;
+        bool o = run_segment(d, bv.data, fs, fe, a, b, ext_cap, [&](uint32_t mi, uint64_t pos) {
+          const auto& m = d.masks[mi];
+          for (size_t k = 0; k < g.rules.size(); k++)
+            if ((m[k / 64] >> (k % 64)) & 1) ko->cand.push_back({f, g.rules[k], (uint32_t)pos});
+        });
+        if (o) ko->overflow[f] = 1;
       }
     }
   }

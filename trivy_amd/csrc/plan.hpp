@@ -22,18 +22,45 @@ namespace tsg {
 
 enum KwMode : uint8_t { kKwAlways = 0, kKwBits = 1, kKwUnknown = 2 };
 
+// Chunk events (K1 output, one u32 per chunk of the batch).  A rule group is scanned by
+// K2 only over the chunks of its gated files that lie within `back` chunks before a
+// chunk carrying one of its event bits (see Plan::rule_event).
+constexpr uint32_t kEvRunU = 1u;        // run of >= run_k[0] bytes of class U
+constexpr uint32_t kEvRunD = 2u;        // run of >= run_k[1] bytes of class D
+constexpr int kEvLit0 = 2;              // bits 2..30: anchor literal classes
+constexpr int kEvLitBits = 29;
+constexpr uint32_t kEvAlways = 1u << 31;  // implicit in every chunk
+
 struct GroupPlan {
   std::unique_ptr<DFA> dfa;
   std::vector<uint32_t> rules;   // group-local accept id -> global rule index
   std::vector<uint32_t> kwmask;  // keyword ids gating this group [kw_words]
   bool always = false;           // some member rule is not keyword-gated on the GPU
+  uint32_t events = kEvAlways;   // OR of the member rules' event bits
+  int64_t evdist = 0;            // max over members of Plan::rule_evdist
 };
 
 struct Plan {
+  // K1: Aho-Corasick automaton over literal ids [0, n_kw) keywords (incl. the 3 fallback
+  // pseudo keywords at fb_kw0..), [n_kw, n_lit) anchor literals that are not keywords.
+  // Its accepts are state-based; kw_mask_events[m] = event bits of accept mask m.
   std::unique_ptr<DFA> kw_dfa;
   int n_kw = 0;        // keyword ids incl. the 3 fallback pseudo keywords at the end
+  int n_lit = 0;
   int kw_words = 1;    // 32-bit words per file
   int fb_kw0 = 0;      // first fallback pseudo keyword id
+  std::vector<uint32_t> kw_mask_events;
+  // run classes for kEvRunU / kEvRunD: byte -> membership bit 0 (U) / 1 (D)
+  uint8_t run_cls[256] = {0};
+  int run_k[2] = {32, 12};
+  int warm = 32;       // K1 warm-up bytes before a chunk (>= longest literal - 1, >= run_k - 1)
+  // per rule: event bits (kEvAlways = none) and the largest distance in bytes from the
+  // start of a match of the rule's GPU program to the event byte inside it; the
+  // program keeps atoms [rule_first_atom, ...) of the regex
+  std::vector<uint32_t> rule_event;
+  std::vector<int64_t> rule_evdist;
+  std::vector<int> rule_first_atom;
+  std::vector<std::string> rule_anchor;  // description, for plan reports
   std::vector<uint8_t> rule_kw_mode;            // per rule
   std::vector<std::vector<uint32_t>> rule_kws;  // per rule: keyword ids
   std::vector<GroupPlan> groups;
@@ -52,6 +79,8 @@ struct PlanOptions {
   int max_group_states = 1024;
   int max_group_table_bytes = 48 * 1024;
   int max_rules_per_group = 64;
+  int max_kw_table_bytes = 96 * 1024;  // K1 transition table must stay LDS-resident
+  bool anchors = true;                 // event windows (false: scan whole gated files)
 };
 
 std::unique_ptr<Plan> build_plan(const Ruleset& rs, const PlanOptions& opt, std::string* err);
@@ -88,7 +117,20 @@ void scan_batch_cpu(const Ruleset& rs, const BatchView& b, int nthreads,
 
 // CPU emulation of the two kernels' algorithm (same chunking, same tables);
 // used by the CPU tests and as the reference for the HIP kernels.
+// group_item_bytes (optional, [groups]): bytes of the K2 items of each group.
 void emulate_kernels(const Plan& plan, const BatchView& b, uint32_t chunk, uint32_t ext_cap,
-                     KernelOutput* ko);
+                     KernelOutput* ko, std::vector<uint64_t>* group_item_bytes = nullptr);
+
+// K1 semantics shared by the HIP kernel and the emulation: keyword bits of every file
+// [nfiles * kw_words] and event bits of every chunk c = bytes [c*chunk, (c+1)*chunk).
+void k1_reference(const Plan& plan, const BatchView& b, uint32_t chunk,
+                  std::vector<uint32_t>* kw, std::vector<uint32_t>* ev);
+
+// Chunks of file f that K2 scans for group g (given the K1 output): chunk c of the file
+// is an item iff the group is gated for f and a chunk in [c, c + back] (inside f)
+// carries one of the group's event bits.  back = ceil(evdist / chunk).
+inline uint32_t group_back(const GroupPlan& g, uint32_t chunk) {
+  return (uint32_t)((g.evdist + chunk - 1) / chunk);
+}
 
 }  // namespace tsg

@@ -282,6 +282,19 @@ class Scanner:
         N.check(N.lib().tsg_ruleset_get_info(self._h, C.byref(i)))
         return {k: getattr(i, k) for k, _ in N.RulesetInfo._fields_}
 
+    def k1_reference(self, batch, chunk):
+        """K1 semantics on the CPU (same layout as GpuContext.k1_output)."""
+        import numpy as np
+        W = (self.info()["n_keywords"] + 31) // 32
+        kw = np.zeros(batch.nfiles * W, dtype=np.uint32)
+        ev = np.zeros((int(batch.offsets[-1]) + chunk - 1) // chunk, dtype=np.uint32)
+        u32p = C.POINTER(C.c_uint32)
+        N.check(N.lib().tsg_emulate_k1(self.handle, C.c_void_p(batch.data.ctypes.data),
+                                       batch.offsets.ctypes.data_as(C.POINTER(C.c_uint64)),
+                                       batch.nfiles, chunk, kw.ctypes.data_as(u32p), kw.size,
+                                       ev.ctypes.data_as(u32p), ev.size))
+        return kw.reshape(batch.nfiles, W), ev
+
     def AllowPath(self, path):
         b = _b(path)
         rc = N.lib().tsg_ruleset_allow_path(self._h, b, len(b))
@@ -373,6 +386,7 @@ class GpuContext:
 
     def __init__(self, scanner, device=0, chunk_bytes=0, ext_cap=0, cand_capacity=0,
                  host_threads=0):
+        self._h = None
         self.scanner = scanner
         opt = N.CtxOptions(chunk_bytes, ext_cap, cand_capacity, host_threads)
         h = C.c_void_p()
@@ -390,6 +404,18 @@ class GpuContext:
 
     def kernels(self):
         N.check(N.lib().tsg_batch_kernels(self._h))
+
+    def k1_output(self, chunk):
+        """(keyword bits [nfiles, kw_words], chunk event bits) of the last kernels() call."""
+        import numpy as np
+        b = self._batch
+        W = (self.scanner.info()["n_keywords"] + 31) // 32
+        kw = np.zeros(b.nfiles * W, dtype=np.uint32)
+        ev = np.zeros((int(b.offsets[-1]) + chunk - 1) // chunk, dtype=np.uint32)
+        u32p = C.POINTER(C.c_uint32)
+        N.check(N.lib().tsg_batch_k1_output(self._h, kw.ctypes.data_as(u32p), kw.size,
+                                            ev.ctypes.data_as(u32p), ev.size))
+        return kw.reshape(b.nfiles, W), ev
 
     def scan_raw(self):
         out = C.c_void_p()
