@@ -124,6 +124,10 @@ typedef struct tsg_ctx_options {
   uint32_t ext_cap;          /* max bytes a lane follows a match past its chunk; 0 = default */
   uint32_t cand_capacity;    /* candidate records per batch; 0 = default */
   int32_t host_threads;      /* resolver threads; <= 0 = hardware */
+  uint32_t adapt_mib;        /* first batch of at least this many MiB samples K1's literal
+                                frequencies and stops reporting the frequent ones (their
+                                keyword gates are then checked on the host); 0 = 64,
+                                0xFFFFFFFF = never */
 } tsg_ctx_options;
 
 int tsg_ctx_create(int device, const tsg_ruleset* rs, const tsg_ctx_options* opt,
@@ -155,6 +159,7 @@ typedef struct tsg_stats {
   uint32_t overflow;     /* 1 if the candidate buffer overflowed (files resolved whole) */
   double gate_ms;        /* keyword gates + K2 item lists (incl. one host round trip) */
   uint64_t k2_items;     /* (file, chunk) items of the sparse K2 launch */
+  uint32_t k1_hot_states;  /* K1 automaton states no longer reported (adaptation) */
 } tsg_stats;
 int tsg_ctx_get_stats(const tsg_ctx* ctx, tsg_stats* out);
 

@@ -82,7 +82,7 @@ def test_k1_matches_reference(builtin, chunk):
     """K1 keyword bits and chunk events are exactly the reference semantics."""
     import numpy as np
     batch = _small_files_batch(chunk)
-    ctx = S.GpuContext(builtin, 0, chunk_bytes=chunk)
+    ctx = S.GpuContext(builtin, 0, chunk_bytes=chunk, adapt_mib=0xFFFFFFFF)
     ctx.upload(batch)
     ctx.kernels()
     kw, ev = ctx.k1_output(chunk)
@@ -91,6 +91,20 @@ def test_k1_matches_reference(builtin, chunk):
     assert np.array_equal(kw, rkw)
     assert np.array_equal(ev, rev)
     assert (ev & 1).any() and (ev >> 2).any()
+
+
+def test_k1_adaptation_exact(builtin):
+    """Frequent literals dropped from K1 after sampling: same findings as the exact CPU path."""
+    batch, _ = corpus.make_corpus(8 << 20, seed=31, plants_per_mib=40)
+    ctx = S.GpuContext(builtin, 0, adapt_mib=1)
+    ctx.upload(batch)
+    got = ctx.scan()
+    st = ctx.stats()
+    again = ctx.scan()  # adapted tables on the second batch too
+    ctx.close()
+    assert st["k1_hot_states"] > 0
+    want = builtin.ScanBatch(batch, nthreads=16)
+    assert got == want and again == want
 
 
 def test_small_files_vs_cpu_exact(builtin):

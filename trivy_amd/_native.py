@@ -39,7 +39,8 @@ class RulesetInfo(C.Structure):
 
 class CtxOptions(C.Structure):
     _fields_ = [("chunk_bytes", C.c_uint32), ("ext_cap", C.c_uint32),
-                ("cand_capacity", C.c_uint32), ("host_threads", C.c_int32)]
+                ("cand_capacity", C.c_uint32), ("host_threads", C.c_int32),
+                ("adapt_mib", C.c_uint32)]
 
 
 class Stats(C.Structure):
@@ -47,7 +48,8 @@ class Stats(C.Structure):
                 ("resolve_ms", C.c_double), ("bytes", C.c_uint64), ("k2_bytes", C.c_uint64),
                 ("candidates", C.c_uint64), ("files_resolved", C.c_uint64),
                 ("k2_launches", C.c_uint32), ("overflow", C.c_uint32),
-                ("gate_ms", C.c_double), ("k2_items", C.c_uint64)]
+                ("gate_ms", C.c_double), ("k2_items", C.c_uint64),
+                ("k1_hot_states", C.c_uint32)]
 
 
 # (name, restype, argtypes) -- every symbol include/trivy_secret.h declares

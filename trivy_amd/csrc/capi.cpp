@@ -1,4 +1,7 @@
 // C ABI, host part (rule compilation, CPU scans, test hooks).  See include/trivy_secret.h.
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <exception>
 #include <thread>
@@ -203,11 +206,20 @@ int tsg_scan_batch_emulated(const tsg_ruleset* rs, const uint8_t* data, const ui
   try {
     BatchView b{data, offsets, nfiles, paths, path_offsets};
     KernelOutput ko;
+    auto t0 = std::chrono::steady_clock::now();
     emulate_kernels(*rs->plan, b, chunk, 1u << 16, &ko);
+    auto t1 = std::chrono::steady_clock::now();
     std::vector<FileResult> res;
     resolve_batch(rs->rs, *rs->plan, b, ko, hw_threads(0), &res);
+    auto t2 = std::chrono::steady_clock::now();
     auto r = std::make_unique<tsg_result>();
     serialize_results(res, &r->buf);
+    auto t3 = std::chrono::steady_clock::now();
+    if (getenv("TSG_PROF"))
+      fprintf(stderr, "emulate %.1f ms resolve %.1f ms serialize %.1f ms (%zu candidates)\n",
+              std::chrono::duration<double, std::milli>(t1 - t0).count(),
+              std::chrono::duration<double, std::milli>(t2 - t1).count(),
+              std::chrono::duration<double, std::milli>(t3 - t2).count(), ko.cand.size());
     *out = r.release();
     return TSG_OK;
   } catch (const std::bad_alloc&) {

@@ -212,6 +212,7 @@ class Builder {
     d->masks.push_back(std::vector<uint64_t>(d->mask_words, 0));
     make_classes();
     for (int c = 0; c < 4; c++) d->start[c] = get_state({}, norm((Ctx)c), false);
+    if (opt_.anchored) d->anchored = get_state({nfa_.start}, norm(kCtxOther), true);
     for (size_t s = 0; s < keys_.size(); s++) {
       if ((int)keys_.size() > opt_.max_states) {
         if (err) *err = "DFA state cap exceeded (" + std::to_string(opt_.max_states) + ")";
@@ -411,6 +412,46 @@ std::unique_ptr<DFA> build_dfa(const std::vector<const Prog*>& progs, const DFAO
   for (size_t i = 0; i < progs.size(); i++) add_prog(nfa, *progs[i], (int)i, nfa.start);
   Builder b(nfa, opt);
   return b.run(err);
+}
+
+std::unique_ptr<DFA> build_reverse_dfa(const Prog& prog, const DFAOptions& opt, std::string* err) {
+  NFA fwd;
+  fwd.start = fwd.add();
+  fwd.nregex = 1;
+  add_prog(fwd, prog, 0, fwd.start);
+  NFA rev;
+  rev.n.resize(fwd.n.size());
+  rev.nregex = 1;
+  for (uint32_t u = 0; u < fwd.n.size(); u++) {
+    const NNode& nd = fwd.n[u];
+    for (uint32_t t : nd.eps) rev.n[t].eps.push_back(u);
+    for (auto& a : nd.asserts) rev.n[a.second].eps.push_back(u);
+    for (auto& e : nd.bytes) rev.n[e.to].bytes.push_back({e.lo, e.hi, u});
+  }
+  rev.start = rev.add();
+  for (uint32_t u = 0; u < fwd.n.size(); u++)
+    if (fwd.n[u].match >= 0) rev.n[rev.start].eps.push_back(u);
+  rev.n[fwd.start].match = 0;
+  DFAOptions o = opt;
+  o.with_noinject = false;
+  o.anchored = true;
+  Builder b(rev, o);
+  return b.run(err);
+}
+
+int64_t reverse_match_start(const DFA& d, const uint8_t* b, int64_t e) {
+  const int nc = d.nclasses;
+  uint32_t s = d.anchored;
+  int64_t best = -1;
+  int64_t q = e;
+  for (; q > 0; q--) {
+    const size_t i = (size_t)s * nc + d.cls[b[q - 1]];
+    if (d.acc[i]) best = q;
+    s = d.next[i];
+    if (d.dead[s]) return best;
+  }
+  if (d.eot_acc[s]) best = 0;
+  return best;
 }
 
 int64_t max_match_len(const Prog& prog) {

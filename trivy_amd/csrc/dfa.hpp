@@ -47,6 +47,7 @@ struct DFA {
   std::vector<uint8_t> dead;         // [nstates] noinject and no live thread
   std::vector<uint8_t> noinject;     // [nstates] mode bit
   int64_t max_len = -1;              // longest match in bytes (-1 = unbounded)
+  uint32_t anchored = 0;             // DFAOptions::anchored: noinject state of the start node
 
   // Host helper: accept mask (words) of regexes matching somewhere in b (MatchString).
   void match_any(const uint8_t* b, size_t n, std::vector<uint64_t>* out) const;
@@ -58,12 +59,21 @@ struct DFAOptions {
   int max_states = 8192;
   // build the noinject twin states (K2); K1 keywords are bounded and use an overlap instead
   bool with_noinject = true;
+  // also build DFA::anchored (one thread at the NFA start, no injection)
+  bool anchored = false;
 };
 
 // Build a DFA over `progs` (accept id = index).  Returns nullptr if the state
 // cap is exceeded.
 std::unique_ptr<DFA> build_dfa(const std::vector<const Prog*>& progs, const DFAOptions& opt,
                                std::string* err);
+
+// Reverse DFA of a program for the host resolver: run from a candidate end e backwards
+// (reverse_match_start) it finds the leftmost s such that [s, e) may match.  Empty-width
+// assertions are dropped (a superset), so "no such s" proves no match ends at e.
+std::unique_ptr<DFA> build_reverse_dfa(const Prog& prog, const DFAOptions& opt, std::string* err);
+// -1: no match of the program ends at e; else the leftmost possible start.
+int64_t reverse_match_start(const DFA& rev, const uint8_t* b, int64_t e);
 
 // Longest match of a program in bytes (-1 = unbounded), over the byte-level NFA.
 int64_t max_match_len(const Prog& prog);

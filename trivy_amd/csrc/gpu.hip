@@ -375,16 +375,9 @@ struct ItemArgs {
 };
 
 // one thread per chunk c: for every file overlapping c and every gated group with an
-// event in [c, c + back] (inside the file): item (file, c) of the group
-template <bool EMIT>
-__global__ void __launch_bounds__(kBlock) items_kernel(ItemArgs A) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  uint32_t* s_count = (uint32_t*)smem;
-  if (!EMIT) {
-    for (uint32_t g = threadIdx.x; g < A.G; g += blockDim.x) s_count[g] = 0;
-    __syncthreads();
-  }
-  const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+// event in [c, c + back] (inside the file): item (file, c) of the group.  visit(f, g).
+template <class V>
+__device__ __forceinline__ void chunk_items(const ItemArgs& A, uint64_t c, V visit) {
   if (c < A.nchunks) {
     const uint64_t cs = c * A.chunk, ce = cs + A.chunk;
     for (uint32_t f = A.chunk_file[c]; f < A.F && A.off[f] < ce; f++) {
@@ -415,21 +408,47 @@ __global__ void __launch_bounds__(kBlock) items_kernel(ItemArgs A) {
             if (k == back) ew |= win[k];
           if (back > kMaxBack) ew = ~0u;  // window longer than kMaxBack chunks: every chunk
           if (!(ew & A.gevents[g])) continue;
-          if (!EMIT) {
-            atomicAdd(&s_count[g], 1u);
-          } else if (A.listed[g]) {
-            const uint32_t k = atomicAdd(&A.cursor[g], 1u);
-            A.items[A.base[g] + k] = make_uint2(f, (uint32_t)c);
-          }
+          visit(f, g);
         }
       }
     }
   }
-  if (!EMIT) {
-    __syncthreads();
-    for (uint32_t g = threadIdx.x; g < A.G; g += blockDim.x)
-      if (s_count[g]) atomicAdd(&A.count[g], s_count[g]);
+}
+
+// count pass: items per group (block totals in LDS, one global atomic per group and block)
+__global__ void __launch_bounds__(kBlock) items_count_kernel(ItemArgs A) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  uint32_t* s_count = (uint32_t*)smem;
+  for (uint32_t g = threadIdx.x; g < A.G; g += blockDim.x) s_count[g] = 0;
+  __syncthreads();
+  const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  chunk_items(A, c, [&](uint32_t, uint32_t g) { atomicAdd(&s_count[g], 1u); });
+  __syncthreads();
+  for (uint32_t g = threadIdx.x; g < A.G; g += blockDim.x)
+    if (s_count[g]) atomicAdd(&A.count[g], s_count[g]);
+}
+
+// emit pass: the block counts its items again, reserves one range per group with a single
+// global atomic, then writes its items into it
+__global__ void __launch_bounds__(kBlock) items_emit_kernel(ItemArgs A) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  uint32_t* s_count = (uint32_t*)smem;
+  uint32_t* s_base = s_count + A.G;
+  for (uint32_t g = threadIdx.x; g < A.G; g += blockDim.x) s_count[g] = 0;
+  __syncthreads();
+  const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  chunk_items(A, c, [&](uint32_t, uint32_t g) {
+    if (A.listed[g]) atomicAdd(&s_count[g], 1u);
+  });
+  __syncthreads();
+  for (uint32_t g = threadIdx.x; g < A.G; g += blockDim.x) {
+    s_base[g] = s_count[g] ? (uint32_t)A.base[g] + atomicAdd(&A.cursor[g], s_count[g]) : 0;
+    s_count[g] = 0;
   }
+  __syncthreads();
+  chunk_items(A, c, [&](uint32_t f, uint32_t g) {
+    if (A.listed[g]) A.items[s_base[g] + atomicAdd(&s_count[g], 1u)] = make_uint2(f, (uint32_t)c);
+  });
 }
 
 // ---------------------------------------------------------------- K2
@@ -720,9 +739,11 @@ static int make_device_dfa(const DFA& d, const std::vector<uint32_t>& rules, Dev
   std::vector<uint64_t> masks;
   for (const auto& m : d.masks) masks.insert(masks.end(), m.begin(), m.end());
   std::vector<uint8_t> cls(d.cls, d.cls + 256);
+  std::vector<uint16_t> tabp = tab;
+  if (tabp.size() & 1) tabp.push_back(0);  // the kernels stage whole dwords
   DevDFA& v = *out;
   int rc;
-  if ((rc = upload_vec(tab, &v.tab, allocs))) return rc;
+  if ((rc = upload_vec(tabp, &v.tab, allocs))) return rc;
   if ((rc = upload_vec(acc, &v.acc, allocs))) return rc;
   if ((rc = upload_vec(accs, &v.acc_state, allocs))) return rc;
   if ((rc = upload_vec(eot, &v.eot, allocs))) return rc;
@@ -760,7 +781,12 @@ static int k1_debug() {
   return e ? atoi(e) : 0;
 }
 
-static int make_device_k1(const Plan& p, DevK1* out, std::vector<void*>* allocs) {
+struct K1Host {  // host copies of the K1 tables (adaptation patches the device table)
+  std::vector<uint16_t> tab, accs;
+  std::vector<uint32_t> masks;
+};
+
+static int make_device_k1(const Plan& p, DevK1* out, std::vector<void*>* allocs, K1Host* host) {
   const DFA& d = *p.kw_dfa;
   if (d.nstates >= 0x8000) return fail(TSG_ERR_INTERNAL, "keyword automaton too large");
   const size_t nc = d.nclasses;
@@ -785,6 +811,7 @@ static int make_device_k1(const Plan& p, DevK1* out, std::vector<void*>* allocs)
       if ((d.masks[m][k / 64] >> (k % 64)) & 1) masks[m * mw + k / 32] |= 1u << (k % 32);
     masks[m * mw + W] = p.kw_mask_events[m];
   }
+  if (tab.size() & 1) tab.push_back(0);  // the kernel stages whole dwords
   DevK1& v = *out;
   int rc;
   if ((rc = upload_vec(tab, &v.tab, allocs))) return rc;
@@ -800,6 +827,9 @@ static int make_device_k1(const Plan& p, DevK1* out, std::vector<void*>* allocs)
   v.warm = (uint32_t)p.warm;
   v.kU = (uint32_t)p.run_k[0];
   v.kD = (uint32_t)p.run_k[1] << 8;
+  host->tab = tab;
+  host->accs = accs;
+  host->masks = masks;
   uint32_t o = align16((uint32_t)(tab.size() * 2));
   v.o_cls = o;
   o += 1024;
@@ -824,6 +854,13 @@ struct tsg_ctx {
   hipEvent_t ev[8];
   std::vector<void*> tables;        // every rule-table allocation
   DevK1 k1{};
+  K1Host k1h;
+  uint32_t* d_hits = nullptr;       // [K1 states] (adaptation sample)
+  bool adapted = false;
+  uint32_t hot_states = 0;
+  std::vector<uint8_t> kw_unknown;  // [n_kw] keywords K1 stopped reporting
+  std::vector<uint32_t> h_galways, h_gevents;
+  std::vector<unsigned long long> h_gofbit;
   std::vector<DevDFA> groups;
   DevDFA* d_groups = nullptr;       // [G] (list kernel)
   uint32_t* d_gmask = nullptr;      // [G * W]
@@ -875,6 +912,7 @@ struct tsg_ctx {
   ~tsg_ctx() {
     (void)hipSetDevice(device);
     for (auto* p : tables) (void)hipFree(p);
+    (void)hipFree(d_hits);
     (void)hipFree(d_data_alloc);
     (void)hipFree(d_off);
     (void)hipFree(d_chunk_file);
@@ -926,6 +964,78 @@ static int launch_k1(tsg_ctx* c, const K1Args& A) {
   return TSG_OK;
 }
 
+// K1 adaptation (once per context, on the first large batch): a sampling pass counts the
+// arrivals in every accepting state; the most frequent states stop raising the accept
+// flag until the rest arrive at most once per 4 KiB.  The literals those states end are
+// then unknown per file: their keyword gates open (host checks them exactly), their
+// anchor events fire everywhere.  Results are unchanged; K1 stops paying per-occurrence
+// accepts for words like "key" that occur in most files anyway.
+static int adapt_k1(tsg_ctx* c, uint64_t nchunks, uint64_t k1_items) {
+  const Plan& p = *c->rs->plan;
+  const uint32_t ns = c->k1.ns, W = c->k1.kw_words, mw = c->k1.mw, G = (uint32_t)c->groups.size();
+  const uint64_t step = std::max<uint64_t>(1, k1_items / 16384);
+  const uint64_t nsamp = (k1_items + step - 1) / step;
+  HIP_TRY(hipMemsetAsync(c->d_hits, 0, sizeof(uint32_t) * ns, c->stream));
+  K1Args A{c->d_data, c->d_off, c->d_chunk_file, c->total, nchunks, nsamp, step, c->opt.chunk_bytes,
+           c->nfiles, c->d_kw, c->d_ev, c->d_hits};
+  int rc;
+  if ((rc = launch_k1(c, A))) return rc;
+  std::vector<uint32_t> hits(ns);
+  HIP_TRY(hipMemcpyAsync(hits.data(), c->d_hits, sizeof(uint32_t) * ns, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  c->adapted = true;
+  const uint64_t sample_bytes = nsamp * kStreams * c->opt.chunk_bytes;
+  uint64_t total = 0;
+  std::vector<uint32_t> order;
+  for (uint32_t s = 0; s < ns; s++)
+    if (hits[s]) {
+      total += hits[s];
+      order.push_back(s);
+    }
+  std::sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return hits[a] > hits[b]; });
+  const uint64_t budget = sample_bytes / 4096;
+  std::vector<uint8_t> hot(ns, 0);
+  std::vector<uint8_t> kw_unknown(p.n_kw, 0);
+  uint32_t ev_hot = 0, nhot = 0;
+  for (uint32_t s : order) {
+    if (total <= budget) break;
+    const uint32_t* m = c->k1h.masks.data() + (size_t)c->k1h.accs[s] * mw;
+    bool fallback = false;  // folding-rune literals must stay exact (they force host resolution)
+    for (int k = p.fb_kw0; k < p.n_kw; k++) fallback |= (m[k / 32] >> (k % 32)) & 1;
+    if (fallback) continue;
+    hot[s] = 1;
+    nhot++;
+    total -= hits[s];
+    for (int k = 0; k < p.n_kw; k++)
+      if ((m[k / 32] >> (k % 32)) & 1) kw_unknown[k] = 1;
+    ev_hot |= m[W];
+  }
+  c->hot_states = nhot;
+  if (!nhot) return TSG_OK;
+  std::vector<uint16_t> tab = c->k1h.tab;
+  for (auto& e : tab)
+    if ((e & 0x8000u) && hot[e & 0x7FFFu]) e &= 0x7FFFu;
+  HIP_TRY(hipMemcpy((void*)c->k1.tab, tab.data(), tab.size() * sizeof(uint16_t), hipMemcpyHostToDevice));
+  // gates of groups with an unknown keyword open; events of hot anchor literals fire everywhere
+  std::vector<uint32_t> galways = c->h_galways, gevents = c->h_gevents;
+  std::vector<unsigned long long> gofbit = c->h_gofbit;
+  for (uint32_t g = 0; g < G; g++) {
+    for (uint32_t r : p.groups[g].rules)
+      if (p.rule_kw_mode[r] == kKwBits)
+        for (uint32_t k : p.rule_kws[r])
+          if (kw_unknown[k]) galways[g] = 1;
+    if (gevents[g] & ev_hot) {
+      gevents[g] |= kEvAlways;
+      gofbit[31 * c->GW + g / 64] |= 1ull << (g % 64);
+    }
+  }
+  HIP_TRY(hipMemcpy(c->d_galways, galways.data(), sizeof(uint32_t) * G, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(c->d_gevents, gevents.data(), sizeof(uint32_t) * G, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(c->d_gofbit, gofbit.data(), sizeof(unsigned long long) * gofbit.size(), hipMemcpyHostToDevice));
+  c->kw_unknown = kw_unknown;
+  return TSG_OK;
+}
+
 extern "C" {
 
 int tsg_ctx_create(int device, const tsg_ruleset* rs, const tsg_ctx_options* opt, tsg_ctx** out) {
@@ -950,7 +1060,8 @@ int tsg_ctx_create(int device, const tsg_ruleset* rs, const tsg_ctx_options* opt
   const uint32_t chunk = c->opt.chunk_bytes;
   if (p.warm > kPad) return fail(TSG_ERR_CONFIG, "a keyword is longer than the K1 warm-up window");
   int rc;
-  if ((rc = make_device_k1(p, &c->k1, &c->tables))) return rc;
+  if ((rc = make_device_k1(p, &c->k1, &c->tables, &c->k1h))) return rc;
+  HIP_TRY(hipMalloc((void**)&c->d_hits, sizeof(uint32_t) * c->k1.ns));
   if (c->k1.lds_bytes > 64 * 1024)
     HIP_TRY(hipFuncSetAttribute(k1_fn(W), hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->k1.lds_bytes));
   const uint32_t G = (uint32_t)p.groups.size();
@@ -991,6 +1102,9 @@ int tsg_ctx_create(int device, const tsg_ruleset* rs, const tsg_ctx_options* opt
   c->d_gback = (uint32_t*)cg;
   const unsigned long long* cb = nullptr;
   if ((rc = upload_vec(gofbit, &cb, &c->tables))) return rc;
+  c->h_galways = galways;
+  c->h_gevents = gevents;
+  c->h_gofbit = gofbit;
   c->d_gofbit = (unsigned long long*)cb;
   const DevDFA* cd = nullptr;
   if ((rc = upload_vec(c->groups, &cd, &c->tables))) return rc;
@@ -1085,6 +1199,10 @@ int tsg_batch_kernels(tsg_ctx* c) {
   // ---- K1
   const uint64_t k1_items = (nchunks + kStreams - 1) / kStreams;
   int rc;
+  const uint64_t adapt_bytes = c->opt.adapt_mib == 0xFFFFFFFFu ? ~0ull
+                               : (uint64_t)(c->opt.adapt_mib ? c->opt.adapt_mib : 64) << 20;
+  if (!c->adapted && k1_items >= 64 && c->total >= adapt_bytes)
+    if ((rc = adapt_k1(c, nchunks, k1_items))) return rc;
   if (k1_items) {
     K1Args A{c->d_data, c->d_off, c->d_chunk_file, c->total, nchunks, k1_items, 1, chunk, F, c->d_kw, c->d_ev,
              nullptr};
@@ -1115,7 +1233,7 @@ int tsg_batch_kernels(tsg_ctx* c) {
   if (F && G && nchunks) {
     ggate_kernel<<<(F + 255) / 256, 256, 0, st>>>(c->d_kw, F, W, c->d_gmask, c->d_galways, G, c->GW, c->d_ggate);
     HIP_TRY(hipGetLastError());
-    hipLaunchKernelGGL(items_kernel<false>, dim3(igrid), dim3(kBlock), G * sizeof(uint32_t) + 16, st, IA);
+    hipLaunchKernelGGL(items_count_kernel, dim3(igrid), dim3(kBlock), G * sizeof(uint32_t) + 16, st, IA);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipMemcpyAsync(gcount.data(), c->d_gcount, sizeof(uint32_t) * G, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
@@ -1131,7 +1249,7 @@ int tsg_batch_kernels(tsg_ctx* c) {
   for (uint32_t g = 0; g < G; g++) {
     if (gcount[g] == 0) continue;
     k2_bytes += (uint64_t)gcount[g] * chunk;
-    if ((uint64_t)gcount[g] * 2 > nchunks) {
+    if ((uint64_t)gcount[g] * 2 > nchunks || nitems + gcount[g] >= (1ull << 31)) {
       dense.push_back(g);
       continue;
     }
@@ -1150,7 +1268,7 @@ int tsg_batch_kernels(tsg_ctx* c) {
     HIP_TRY(hipMemcpyAsync(c->d_blkmap, blkmap.data(), sizeof(uint4) * blkmap.size(), hipMemcpyHostToDevice, st));
     IA.base = c->d_base;
     IA.items = c->d_items;
-    hipLaunchKernelGGL(items_kernel<true>, dim3(igrid), dim3(kBlock), 16, st, IA);
+    hipLaunchKernelGGL(items_emit_kernel, dim3(igrid), dim3(kBlock), 2 * G * sizeof(uint32_t) + 16, st, IA);
     HIP_TRY(hipGetLastError());
   }
   HIP_TRY(hipEventRecord(c->ev[3], st));
@@ -1200,6 +1318,7 @@ int tsg_batch_kernels(tsg_ctx* c) {
   }
   HIP_TRY(hipEventRecord(c->ev[5], st));
   HIP_TRY(hipStreamSynchronize(st));
+  c->ko.kw_unknown = c->kw_unknown;
   c->ko.overflow.assign(F, 0);
   for (uint32_t i = 0; i < F; i++) c->ko.overflow[i] = ovf[i] ? 1 : 0;
   float t[5] = {0, 0, 0, 0, 0};
@@ -1214,6 +1333,7 @@ int tsg_batch_kernels(tsg_ctx* c) {
   c->stats.candidates = *c->h_count;
   c->stats.overflow = *c->h_count > c->opt.cand_capacity ? 1 : 0;
   c->stats.k2_launches = (uint32_t)(dense.size() + (nitems ? 1 : 0));
+  c->stats.k1_hot_states = c->hot_states;
   return TSG_OK;
 }
 

@@ -2,6 +2,9 @@
 #include "plan.hpp"
 
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <atomic>
 #include <map>
 #include <thread>
@@ -313,6 +316,7 @@ std::unique_ptr<Plan> build_plan(const Ruleset& rs, const PlanOptions& opt, std:
     if (!d) return false;
     if ((size_t)d->nstates * d->nclasses * 2 > (size_t)opt.max_kw_table_bytes) return false;
     p->n_lit = (int)lits.size();
+    p->lit_event = lit_event;
     p->kw_mask_events.assign(d->masks.size(), 0);
     for (size_t m = 0; m < d->masks.size(); m++)
       for (int id = 0; id < p->n_lit; id++)
@@ -327,6 +331,23 @@ std::unique_ptr<Plan> build_plan(const Ruleset& rs, const PlanOptions& opt, std:
   if (!build_k1(opt.anchors) && !build_k1(false)) {
     if (err) *err = "keyword automaton exceeds the K1 table budget";
     return nullptr;
+  }
+
+  // ---- host resolver: reverse DFAs of the exact programs
+  p->rule_rev.resize(R);
+  // (only where the forward bound is loose: unbounded or long windows; the subset
+  // construction of the counted generic rules would cost more than it saves)
+  for (size_t r = 0; r < R; r++) {
+    if (!rs.rules[r].regex || (p->rule_winback[r] >= 0 && p->rule_winback[r] <= 1024)) continue;
+    DFAOptions o;
+    o.max_states = 2048;
+    std::string e;
+    auto t0 = std::chrono::steady_clock::now();
+    p->rule_rev[r] = build_reverse_dfa(rs.rules[r].regex->prog(), o, &e);
+    if (getenv("TSG_PROF"))
+      fprintf(stderr, "rev %s: %d states %.1f ms\n", rs.rules[r].id.c_str(),
+              p->rule_rev[r] ? p->rule_rev[r]->nstates : -1,
+              std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
   }
 
   // ---- Global.AllowPath automaton (exact on ASCII paths)
@@ -365,15 +386,22 @@ static void parallel_for(size_t n, int nthreads, F f) {
   for (auto& t : th) t.join();
 }
 
-static bool path_allowed(const Ruleset& rs, const Plan* plan, const std::string& path) {
-  if (plan && plan->allow_path_dfa && is_ascii(path)) {
-    std::vector<uint64_t> m;
-    plan->allow_path_dfa->match_any((const uint8_t*)path.data(), path.size(), &m);
-    for (uint64_t w : m)
-      if (w) return true;
-    return false;
+static bool path_allowed(const Ruleset& rs, const Plan* plan, const char* p, size_t n) {
+  if (plan && plan->allow_path_dfa) {
+    bool ascii = true;
+    for (size_t i = 0; i < n && ascii; i++) ascii = (uint8_t)p[i] < 0x80;
+    if (ascii) {  // any accept (a non-empty mask) = some allow path regexp matches
+      const DFA& d = *plan->allow_path_dfa;
+      uint32_t s = d.start[kCtxBOT];
+      for (size_t i = 0; i < n; i++) {
+        const size_t e = (size_t)s * d.nclasses + d.cls[(uint8_t)p[i]];
+        if (d.acc[e]) return true;
+        s = d.next[e];
+      }
+      return d.eot_acc[s] != 0;
+    }
   }
-  return rs.AllowPath(path);
+  return rs.AllowPath(std::string(p, n));
 }
 
 void scan_batch_cpu(const Ruleset& rs, const BatchView& b, int nthreads,
@@ -422,14 +450,29 @@ void resolve_batch(const Ruleset& rs, const Plan& plan, const BatchView& b,
   for (size_t r = 0; r < R; r++)
     if (plan.rule_hostonly[r]) hostonly.push_back((uint32_t)r);
 
+  static const bool prof = getenv("TSG_PROF") != nullptr;
+  std::atomic<int64_t> t_plain{0}, t_cand{0}, n_cand{0}, n_whole{0};
   parallel_for(F, nthreads, [&](size_t fi) {
+    const auto tp0 = prof ? std::chrono::steady_clock::now() : std::chrono::steady_clock::time_point();
+    struct Tm {
+      bool on;
+      std::chrono::steady_clock::time_point t0;
+      std::atomic<int64_t>* acc;
+      ~Tm() {
+        if (on) *acc += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
+      }
+    };
     const uint32_t f = (uint32_t)fi;
-    std::string path(b.paths + b.path_offsets[f], b.path_offsets[f + 1] - b.path_offsets[f]);
+    const bool has_cand = first[f] != first[f + 1];
+    Tm tm{prof, tp0, has_cand ? &t_cand : &t_plain};
+    if (prof && has_cand) n_cand++;
+    const char* pp = b.paths + b.path_offsets[f];
+    const size_t pn = b.path_offsets[f + 1] - b.path_offsets[f];
     const uint8_t* content = b.data + b.offsets[f];
     const int64_t n = (int64_t)(b.offsets[f + 1] - b.offsets[f]);
     FileResult& res = (*out)[f];
     if (n == 0) {  // the kernels skip empty files; only empty matches are possible
-      scan_file(rs, path, content, 0, nullptr, &res);
+      scan_file(rs, std::string(pp, pn), content, 0, nullptr, &res);
       return;
     }
     const uint32_t* kw = ko.kw.data() + (size_t)f * plan.kw_words;
@@ -443,6 +486,9 @@ void resolve_batch(const Ruleset& rs, const Plan& plan, const BatchView& b,
           if (fb) return 2;
           for (uint32_t k : plan.rule_kws[r])
             if ((kw[k / 32] >> (k % 32)) & 1) return 1;
+          if (!ko.kw_unknown.empty())
+            for (uint32_t k : plan.rule_kws[r])
+              if (ko.kw_unknown[k]) return 2;
           return 0;
       }
     };
@@ -453,9 +499,10 @@ void resolve_batch(const Ruleset& rs, const Plan& plan, const BatchView& b,
     for (uint32_t r : hostonly)
       if (kw_state(r) != 0) any_host = true;
     if (first[f] == first[f + 1] && !ovf && !any_host) {
-      res.status = path_allowed(rs, &plan, path) ? kPathAllowed : kNoFindings;
+      res.status = path_allowed(rs, &plan, pp, pn) ? kPathAllowed : kNoFindings;
       return;
     }
+    const std::string path(pp, pn);
     std::vector<RuleWindows> wins(R);
     std::vector<const RuleWindows*> wptr(R, nullptr);
     std::vector<uint8_t> kws(R);
@@ -478,11 +525,20 @@ void resolve_batch(const Ruleset& rs, const Plan& plan, const BatchView& b,
       RuleWindows& w = wins[r];
       wptr[r] = &w;
       if (!w.whole) {
-        // every match start lies in [end - winback, end] of some candidate end offset
+        // every match start lies in [end - winback, end] of some candidate end offset; the
+        // reverse DFA narrows that to [leftmost start, end] or drops the candidate
         const int64_t back = plan.rule_winback[r];
+        const DFA* rev = plan.rule_rev[r].get();
         for (uint32_t j = k; j < e; j++) {
           int64_t end = cand[j].end;
-          int64_t lo = back < 0 ? 0 : align_rune(content, n, std::max<int64_t>(0, end - back));
+          int64_t lo;
+          if (rev) {
+            lo = reverse_match_start(*rev, content, end);
+            if (lo < 0) continue;
+            lo = align_rune(content, n, lo);
+          } else {
+            lo = back < 0 ? 0 : align_rune(content, n, std::max<int64_t>(0, end - back));
+          }
           if (!w.iv.empty() && lo <= w.iv.back().second + 1) {
             w.iv.back().second = std::max<int64_t>(w.iv.back().second, end);
           } else {
@@ -495,8 +551,14 @@ void resolve_batch(const Ruleset& rs, const Plan& plan, const BatchView& b,
     FileGate gate;
     gate.kw_state = kws.data();
     gate.windows = wptr.data();
+    if (prof)
+      for (size_t r = 0; r < R; r++)
+        if (wptr[r] && (wptr[r]->whole || (!wptr[r]->iv.empty() && wptr[r]->iv[0].first == 0))) n_whole++;
     scan_file(rs, path, content, (size_t)n, &gate, &res);
   });
+  if (prof)
+    fprintf(stderr, "resolve: plain files %.1f ms cpu, candidate files %.1f ms cpu (%ld files, %ld whole-prefix rule scans)\n",
+            t_plain / 1e6, t_cand / 1e6, (long)n_cand, (long)n_whole);
 }
 
 // ------------------------------------------------------------------ kernel emulation

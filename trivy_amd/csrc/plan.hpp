@@ -50,6 +50,7 @@ struct Plan {
   int kw_words = 1;    // 32-bit words per file
   int fb_kw0 = 0;      // first fallback pseudo keyword id
   std::vector<uint32_t> kw_mask_events;
+  std::vector<uint32_t> lit_event;     // [n_lit] event bits of each literal
   // run classes for kEvRunU / kEvRunD: byte -> membership bit 0 (U) / 1 (D)
   uint8_t run_cls[256] = {0};
   int run_k[2] = {32, 12};
@@ -72,6 +73,8 @@ struct Plan {
   // a GPU end offset e says "a match may START in [e - winback, e]" (-1: anywhere before e)
   std::vector<int64_t> rule_winback;
   std::vector<Prog> rule_prog;       // the program the rule's GPU DFA was built from
+  // reverse DFA of the exact program (null: state cap): bounds and filters the windows
+  std::vector<std::unique_ptr<DFA>> rule_rev;
   std::unique_ptr<DFA> allow_path_dfa;  // Global.AllowPath on ASCII paths
 };
 
@@ -97,6 +100,8 @@ struct KernelOutput {
   std::vector<uint32_t> kw;        // [nfiles * kw_words]
   std::vector<Candidate> cand;
   std::vector<uint8_t> overflow;   // [nfiles] 1 = resolve the whole file exactly
+  // [n_kw] (or empty): keyword bits K1 no longer reports (a clear bit proves nothing)
+  std::vector<uint8_t> kw_unknown;
 };
 
 struct BatchView {

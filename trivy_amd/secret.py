@@ -385,10 +385,10 @@ class GpuContext:
     """One device context (tsg_ctx): replicated rule tables + batch buffers in HBM."""
 
     def __init__(self, scanner, device=0, chunk_bytes=0, ext_cap=0, cand_capacity=0,
-                 host_threads=0):
+                 host_threads=0, adapt_mib=0):
         self._h = None
         self.scanner = scanner
-        opt = N.CtxOptions(chunk_bytes, ext_cap, cand_capacity, host_threads)
+        opt = N.CtxOptions(chunk_bytes, ext_cap, cand_capacity, host_threads, adapt_mib)
         h = C.c_void_p()
         N.check(N.lib().tsg_ctx_create(int(device), scanner.handle, C.byref(opt), C.byref(h)))
         self._h = h
