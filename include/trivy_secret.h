@@ -142,6 +142,15 @@ int tsg_batch_upload(tsg_ctx* ctx, const uint8_t* data, const uint64_t* offsets,
 int tsg_batch_scan(tsg_ctx* ctx, tsg_result** out);
 /* Only the device part of tsg_batch_scan (kernels + candidate download), no resolution. */
 int tsg_batch_kernels(tsg_ctx* ctx);
+/* Pipelined form of tsg_batch_scan: submit runs the device part synchronously and starts
+ * the host resolution of that batch in the background; collect returns the results of
+ * the oldest submitted batch (waiting for its resolution).  The device work of the next
+ * submit overlaps the host resolution of the previous ones.  The host buffers of a batch
+ * must stay valid until its results are collected. */
+int tsg_batch_submit(tsg_ctx* ctx);
+int tsg_batch_collect(tsg_ctx* ctx, tsg_result** out);
+/* number of submitted, uncollected batches */
+int tsg_batch_pending(const tsg_ctx* ctx);
 /* upload + scan */
 int tsg_scan_batch(tsg_ctx* ctx, const uint8_t* data, const uint64_t* offsets, uint32_t nfiles,
                    const char* paths, const uint64_t* path_offsets, tsg_result** out);

@@ -1,0 +1,90 @@
+"""The GPU algorithm (K1 literal automaton, gates, K2 rule-group DFAs over event windows,
+host resolution of candidate windows) emulated on the CPU, against the product's exact
+CPU path and the oracle, on seeded synthetic corpora.  No GPU needed.
+
+The fold-rune corpus stresses the one place where the kernels' anchors are not exact:
+U+212A (K) and U+017F (s) join ASCII letters under (?i) and U+0130 lowercases to 'i'
+(bytes.ToLower), so the resolver must add windows around them (plan.cpp resolve_batch).
+Whether Go treats these runes this way is not pinned by any reference fixture: the
+expected behaviour follows Go 1.19's unicode.SimpleFold / unicode.ToLower tables
+(Appendix A.6/A.7 of SURVEY.md) as restated by oracle/gounicode.py.
+"""
+import numpy as np
+import pytest
+
+from tests.helpers import canon_secret
+from trivy_amd import corpus
+from trivy_amd import secret as S
+
+FOLD = {ord("k"): "K", ord("K"): "K", ord("s"): "ſ", ord("S"): "ſ",
+        ord("i"): "İ", ord("I"): "İ"}
+
+
+@pytest.fixture(scope="module")
+def builtin():
+    return S.NewScanner(None)
+
+
+def fold_corpus(seed, nbytes=1 << 20, plants=300, frac=0.3):
+    """Seeded corpus; in `frac` of the files some k/s/i letters become folding runes,
+    mostly inside and around planted secrets and keywords."""
+    rng = np.random.default_rng(seed)
+    b, _ = corpus.make_corpus(nbytes, seed=seed, plants_per_mib=plants)
+    args = []
+    for i in range(b.nfiles):
+        c = bytes(b.data[int(b.offsets[i]):int(b.offsets[i + 1])])
+        if rng.random() < frac and len(c) > 0:
+            t = bytearray()
+            p = float(rng.choice([0.002, 0.02, 0.2]))
+            for ch in c:
+                if ch in FOLD and rng.random() < p:
+                    t += FOLD[ch].encode()
+                else:
+                    t.append(ch)
+            c = bytes(t)
+        args.append(S.ScanArgs(b.path(i), c))
+    # hand-made files: a fold rune inside the secret / keyword of common rules
+    hand = [
+        "aws_secret_access_Key = \"12ASD34qwe56CXZ78tyH10Tna543VBokN85RHCas\"\n",
+        "AWS_ſECRET_ACCESS_KEY=12ASD34qwe56CXZ78tyH10Tna543VBokN85RHCas\n",
+        "ghp_0123456789abcdefghijKlmnopqrstuvwxyz\n",
+        "İntercom_api_token = \"" + "a" * 60 + "\"\n",
+        "gitlab_ſecret glpat-0123456789abcdefghij\n",
+        "-----BEGIN RSA PRIVATE KEY-----\nMIIEabc\n-----END RSA PRIVATE KEY-----\n",
+        "twitch_api_Key = '" + "x" * 30 + "'\n",
+        "facebook_token = '" + "a" * 31 + "K'\n",
+    ]
+    for j, h in enumerate(hand):
+        args.append(S.ScanArgs("hand/f%d.txt" % j, h.encode()))
+    return S.Batch.from_args(args)
+
+
+@pytest.mark.parametrize("chunk", [16, 64, 256])
+def test_corpus_emulated_vs_exact(builtin, chunk):
+    batch, _ = corpus.make_corpus(3 << 20, seed=40 + chunk, plants_per_mib=60)
+    assert builtin.ScanBatch(batch, emulate_chunk=chunk) == builtin.ScanBatch(batch, nthreads=8)
+
+
+@pytest.mark.parametrize("chunk", [16, 256])
+@pytest.mark.parametrize("seed", [1, 2])
+def test_fold_runes_emulated_vs_exact(builtin, chunk, seed):
+    batch = fold_corpus(seed)
+    got = builtin.ScanBatch(batch, emulate_chunk=chunk)
+    want = builtin.ScanBatch(batch, nthreads=8)
+    assert got == want
+    assert sum(1 for w in want if w["Findings"]) > 20
+
+
+def test_fold_runes_exact_vs_oracle(builtin):
+    """The exact CPU path against the oracle on the hand-made and a few folded files."""
+    from oracle import secret as O
+    batch = fold_corpus(3, nbytes=96 << 10, plants=400, frac=0.6)
+    got = builtin.ScanBatch(batch, nthreads=8)
+    osc = O.NewScanner(None)
+    nf = 0
+    for i in range(batch.nfiles):
+        c = bytes(batch.data[int(batch.offsets[i]):int(batch.offsets[i + 1])])
+        want = canon_secret(osc.Scan(batch.path(i), c))
+        assert canon_secret(got[i]) == want, batch.path(i)
+        nf += len(want["Findings"] or [])
+    assert nf > 10

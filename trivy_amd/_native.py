@@ -74,6 +74,9 @@ SIGNATURES = [
     ("tsg_batch_upload", C.c_int, [_P, _P, _U64P, C.c_uint32, _P, _U64P]),
     ("tsg_batch_scan", C.c_int, [_P, C.POINTER(_P)]),
     ("tsg_batch_kernels", C.c_int, [_P]),
+    ("tsg_batch_submit", C.c_int, [_P]),
+    ("tsg_batch_collect", C.c_int, [_P, C.POINTER(_P)]),
+    ("tsg_batch_pending", C.c_int, [_P]),
     ("tsg_scan_batch", C.c_int, [_P, _P, _U64P, C.c_uint32, _P, _U64P, C.POINTER(_P)]),
     ("tsg_ctx_get_stats", C.c_int, [_P, C.POINTER(Stats)]),
     ("tsg_last_error", C.c_char_p, []),

@@ -26,6 +26,8 @@
 #include <chrono>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
+#include <future>
 #include <vector>
 
 #include "internal.hpp"
@@ -908,8 +910,16 @@ struct tsg_ctx {
   tsg_stats stats{};
   int grid = 0;
   bool uploaded = false;
+  // host resolutions of submitted batches, oldest first (tsg_batch_submit / collect)
+  struct Pending {
+    std::future<std::unique_ptr<tsg_result>> res;
+    std::shared_ptr<std::pair<double, uint64_t>> done;  // resolve ms, files with findings
+  };
+  std::deque<Pending> pending;
 
   ~tsg_ctx() {
+    for (auto& pj : pending)
+      if (pj.res.valid()) pj.res.wait();
     (void)hipSetDevice(device);
     for (auto* p : tables) (void)hipFree(p);
     (void)hipFree(d_hits);
@@ -1337,23 +1347,52 @@ int tsg_batch_kernels(tsg_ctx* c) {
   return TSG_OK;
 }
 
-int tsg_batch_scan(tsg_ctx* c, tsg_result** out) {
-  if (!c || !out) return fail(TSG_ERR_ARG, "bad argument");
+// Host resolution of one batch's kernel output (exact findings, serialized).
+static std::unique_ptr<tsg_result> resolve_job(const tsg_ruleset* rs, BatchView b, const KernelOutput& ko,
+                                               int nt, std::pair<double, uint64_t>* done) {
+  auto t0 = std::chrono::steady_clock::now();
+  std::vector<FileResult> res;
+  resolve_batch(rs->rs, *rs->plan, b, ko, nt, &res);
+  auto r = std::make_unique<tsg_result>();
+  serialize_results(res, &r->buf);
+  done->first = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  done->second = 0;
+  for (const auto& fr : res) done->second += fr.status == kHasFindings;
+  return r;
+}
+
+int tsg_batch_submit(tsg_ctx* c) {
+  if (!c) return fail(TSG_ERR_ARG, "bad argument");
   int rc = tsg_batch_kernels(c);
   if (rc) return rc;
   try {
-    auto t0 = std::chrono::steady_clock::now();
+    tsg_ctx::Pending pj;
+    pj.done = std::make_shared<std::pair<double, uint64_t>>(0.0, 0);
+    auto ko = std::make_shared<KernelOutput>(std::move(c->ko));
+    c->ko = KernelOutput{};
     BatchView b{c->h_data, c->h_off, c->nfiles, c->h_paths, c->h_poff};
-    std::vector<FileResult> res;
-    int nt = c->opt.host_threads > 0 ? c->opt.host_threads : 16;
-    resolve_batch(c->rs->rs, *c->rs->plan, b, c->ko, nt, &res);
-    auto r = std::make_unique<tsg_result>();
-    serialize_results(res, &r->buf);
-    auto t1 = std::chrono::steady_clock::now();
-    c->stats.resolve_ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
-    uint64_t nres = 0;
-    for (const auto& fr : res) nres += fr.status == kHasFindings;
-    c->stats.files_resolved = nres;
+    const tsg_ruleset* rs = c->rs;
+    const int nt = c->opt.host_threads > 0 ? c->opt.host_threads : 16;
+    auto done = pj.done;
+    pj.res = std::async(std::launch::async, [rs, b, ko, nt, done]() { return resolve_job(rs, b, *ko, nt, done.get()); });
+    c->pending.push_back(std::move(pj));
+    return TSG_OK;
+  } catch (const std::bad_alloc&) {
+    return fail(TSG_ERR_NOMEM, "out of memory");
+  } catch (const std::exception& ex) {
+    return fail(TSG_ERR_INTERNAL, ex.what());
+  }
+}
+
+int tsg_batch_collect(tsg_ctx* c, tsg_result** out) {
+  if (!c || !out) return fail(TSG_ERR_ARG, "bad argument");
+  if (c->pending.empty()) return fail(TSG_ERR_ARG, "no submitted batch");
+  tsg_ctx::Pending pj = std::move(c->pending.front());
+  c->pending.pop_front();
+  try {
+    std::unique_ptr<tsg_result> r = pj.res.get();
+    c->stats.resolve_ms = pj.done->first;
+    c->stats.files_resolved = pj.done->second;
     *out = r.release();
     return TSG_OK;
   } catch (const std::bad_alloc&) {
@@ -1361,6 +1400,16 @@ int tsg_batch_scan(tsg_ctx* c, tsg_result** out) {
   } catch (const std::exception& ex) {
     return fail(TSG_ERR_INTERNAL, ex.what());
   }
+}
+
+int tsg_batch_pending(const tsg_ctx* c) { return c ? (int)c->pending.size() : TSG_ERR_ARG; }
+
+int tsg_batch_scan(tsg_ctx* c, tsg_result** out) {
+  if (!c || !out) return fail(TSG_ERR_ARG, "bad argument");
+  if (!c->pending.empty()) return fail(TSG_ERR_ARG, "collect the submitted batches first");
+  int rc = tsg_batch_submit(c);
+  if (rc) return rc;
+  return tsg_batch_collect(c, out);
 }
 
 int tsg_scan_batch(tsg_ctx* c, const uint8_t* data, const uint64_t* offsets, uint32_t nfiles,

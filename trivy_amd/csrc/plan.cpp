@@ -430,138 +430,6 @@ static int64_t align_rune(const uint8_t* d, int64_t n, int64_t p) {
   return p;
 }
 
-void resolve_batch(const Ruleset& rs, const Plan& plan, const BatchView& b,
-                   const KernelOutput& ko, int nthreads, std::vector<FileResult>* out) {
-  const uint32_t F = b.nfiles;
-  const size_t R = rs.rules.size();
-  out->assign(F, FileResult{});
-  // bucket candidates by file, sorted by (rule, end)
-  std::vector<Candidate> cand = ko.cand;
-  std::sort(cand.begin(), cand.end(), [](const Candidate& x, const Candidate& y) {
-    if (x.file != y.file) return x.file < y.file;
-    if (x.rule != y.rule) return x.rule < y.rule;
-    return x.end < y.end;
-  });
-  std::vector<uint32_t> first(F + 1, 0);
-  for (const auto& c : cand) first[c.file + 1]++;
-  for (uint32_t f = 0; f < F; f++) first[f + 1] += first[f];
-
-  std::vector<uint32_t> hostonly;
-  for (size_t r = 0; r < R; r++)
-    if (plan.rule_hostonly[r]) hostonly.push_back((uint32_t)r);
-
-  static const bool prof = getenv("TSG_PROF") != nullptr;
-  std::atomic<int64_t> t_plain{0}, t_cand{0}, n_cand{0}, n_whole{0};
-  parallel_for(F, nthreads, [&](size_t fi) {
-    const auto tp0 = prof ? std::chrono::steady_clock::now() : std::chrono::steady_clock::time_point();
-    struct Tm {
-      bool on;
-      std::chrono::steady_clock::time_point t0;
-      std::atomic<int64_t>* acc;
-      ~Tm() {
-        if (on) *acc += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
-      }
-    };
-    const uint32_t f = (uint32_t)fi;
-    const bool has_cand = first[f] != first[f + 1];
-    Tm tm{prof, tp0, has_cand ? &t_cand : &t_plain};
-    if (prof && has_cand) n_cand++;
-    const char* pp = b.paths + b.path_offsets[f];
-    const size_t pn = b.path_offsets[f + 1] - b.path_offsets[f];
-    const uint8_t* content = b.data + b.offsets[f];
-    const int64_t n = (int64_t)(b.offsets[f + 1] - b.offsets[f]);
-    FileResult& res = (*out)[f];
-    if (n == 0) {  // the kernels skip empty files; only empty matches are possible
-      scan_file(rs, std::string(pp, pn), content, 0, nullptr, &res);
-      return;
-    }
-    const uint32_t* kw = ko.kw.data() + (size_t)f * plan.kw_words;
-    bool fb = false;
-    for (int k = plan.fb_kw0; k < plan.n_kw; k++) fb |= (kw[k / 32] >> (k % 32)) & 1;
-    auto kw_state = [&](size_t r) -> uint8_t {
-      switch (plan.rule_kw_mode[r]) {
-        case kKwAlways: return 1;
-        case kKwUnknown: return 2;
-        default:
-          if (fb) return 2;
-          for (uint32_t k : plan.rule_kws[r])
-            if ((kw[k / 32] >> (k % 32)) & 1) return 1;
-          if (!ko.kw_unknown.empty())
-            for (uint32_t k : plan.rule_kws[r])
-              if (ko.kw_unknown[k]) return 2;
-          return 0;
-      }
-    };
-    // kernel overflow, or a folding rune (U+0130/U+212A/U+017F) the GPU programs ignore:
-    // resolve every rule over the whole file
-    const bool ovf = (!ko.overflow.empty() && ko.overflow[f]) || fb;
-    bool any_host = false;
-    for (uint32_t r : hostonly)
-      if (kw_state(r) != 0) any_host = true;
-    if (first[f] == first[f + 1] && !ovf && !any_host) {
-      res.status = path_allowed(rs, &plan, pp, pn) ? kPathAllowed : kNoFindings;
-      return;
-    }
-    const std::string path(pp, pn);
-    std::vector<RuleWindows> wins(R);
-    std::vector<const RuleWindows*> wptr(R, nullptr);
-    std::vector<uint8_t> kws(R);
-    for (size_t r = 0; r < R; r++) kws[r] = kw_state(r);
-    if (ovf) {
-      for (size_t r = 0; r < R; r++) {
-        wins[r].whole = true;
-        wptr[r] = &wins[r];
-      }
-    }
-    for (uint32_t r : hostonly)
-      if (kws[r] != 0) {
-        wins[r].whole = true;
-        wptr[r] = &wins[r];
-      }
-    for (uint32_t k = first[f]; k < first[f + 1];) {
-      uint32_t r = cand[k].rule;
-      uint32_t e = k;
-      while (e < first[f + 1] && cand[e].rule == r) e++;
-      RuleWindows& w = wins[r];
-      wptr[r] = &w;
-      if (!w.whole) {
-        // every match start lies in [end - winback, end] of some candidate end offset; the
-        // reverse DFA narrows that to [leftmost start, end] or drops the candidate
-        const int64_t back = plan.rule_winback[r];
-        const DFA* rev = plan.rule_rev[r].get();
-        for (uint32_t j = k; j < e; j++) {
-          int64_t end = cand[j].end;
-          int64_t lo;
-          if (rev) {
-            lo = reverse_match_start(*rev, content, end);
-            if (lo < 0) continue;
-            lo = align_rune(content, n, lo);
-          } else {
-            lo = back < 0 ? 0 : align_rune(content, n, std::max<int64_t>(0, end - back));
-          }
-          if (!w.iv.empty() && lo <= w.iv.back().second + 1) {
-            w.iv.back().second = std::max<int64_t>(w.iv.back().second, end);
-          } else {
-            w.iv.push_back({lo, end});
-          }
-        }
-      }
-      k = e;
-    }
-    FileGate gate;
-    gate.kw_state = kws.data();
-    gate.windows = wptr.data();
-    if (prof)
-      for (size_t r = 0; r < R; r++)
-        if (wptr[r] && (wptr[r]->whole || (!wptr[r]->iv.empty() && wptr[r]->iv[0].first == 0))) n_whole++;
-    scan_file(rs, path, content, (size_t)n, &gate, &res);
-  });
-  if (prof)
-    fprintf(stderr, "resolve: plain files %.1f ms cpu, candidate files %.1f ms cpu (%ld files, %ld whole-prefix rule scans)\n",
-            t_plain / 1e6, t_cand / 1e6, (long)n_cand, (long)n_whole);
-}
-
-// ------------------------------------------------------------------ kernel emulation
 namespace {
 
 // One lane's work on one file segment [a, b) of file [fs, fe): inject mode over the
@@ -595,6 +463,210 @@ bool run_segment(const DFA& d, const uint8_t* data, uint64_t fs, uint64_t fe, ui
 }
 
 }  // namespace
+
+void resolve_batch(const Ruleset& rs, const Plan& plan, const BatchView& b,
+                   const KernelOutput& ko, int nthreads, std::vector<FileResult>* out) {
+  const uint32_t F = b.nfiles;
+  const size_t R = rs.rules.size();
+  out->assign(F, FileResult{});
+  // bucket candidates by file, sorted by (rule, end)
+  std::vector<Candidate> cand = ko.cand;
+  std::sort(cand.begin(), cand.end(), [](const Candidate& x, const Candidate& y) {
+    if (x.file != y.file) return x.file < y.file;
+    if (x.rule != y.rule) return x.rule < y.rule;
+    return x.end < y.end;
+  });
+  std::vector<uint32_t> first(F + 1, 0);
+  for (const auto& c : cand) first[c.file + 1]++;
+  for (uint32_t f = 0; f < F; f++) first[f + 1] += first[f];
+
+  std::vector<uint32_t> hostonly;
+  for (size_t r = 0; r < R; r++)
+    if (plan.rule_hostonly[r]) hostonly.push_back((uint32_t)r);
+  std::vector<uint8_t> kw_has_i(R, 0), kw_has_k(R, 0);
+  for (size_t r = 0; r < R; r++)
+    for (const auto& k : rs.rules[r].kw_lower) {
+      kw_has_i[r] |= k.find('i') != std::string::npos;
+      kw_has_k[r] |= k.find('k') != std::string::npos;
+    }
+
+  static const bool prof = getenv("TSG_PROF") != nullptr;
+  std::atomic<int64_t> t_plain{0}, t_cand{0}, n_cand{0}, n_whole{0}, t_fast{0}, n_fast{0};
+  parallel_for(F, nthreads, [&](size_t fi) {
+    const auto tp0 = prof ? std::chrono::steady_clock::now() : std::chrono::steady_clock::time_point();
+    struct Tm {
+      bool on;
+      std::chrono::steady_clock::time_point t0;
+      std::atomic<int64_t>* acc;
+      ~Tm() {
+        if (on) *acc += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
+      }
+    };
+    const uint32_t f = (uint32_t)fi;
+    const bool has_cand = first[f] != first[f + 1];
+    Tm tm{prof, tp0, has_cand ? &t_cand : &t_plain};
+    if (prof && has_cand) n_cand++;
+    const char* pp = b.paths + b.path_offsets[f];
+    const size_t pn = b.path_offsets[f + 1] - b.path_offsets[f];
+    const uint8_t* content = b.data + b.offsets[f];
+    const int64_t n = (int64_t)(b.offsets[f + 1] - b.offsets[f]);
+    FileResult& res = (*out)[f];
+    if (n == 0) {  // the kernels skip empty files; only empty matches are possible
+      scan_file(rs, std::string(pp, pn), content, 0, nullptr, &res);
+      return;
+    }
+    const uint32_t* kw = ko.kw.data() + (size_t)f * plan.kw_words;
+    // folding runes present: bit 0 U+0130, bit 1 U+212A, bit 2 U+017F
+    uint32_t fbbits = 0;
+    for (int k = plan.fb_kw0; k < plan.n_kw; k++)
+      if ((kw[k / 32] >> (k % 32)) & 1) fbbits |= 1u << (k - plan.fb_kw0);
+    // Keyword gate.  K1 bits are exact for the ASCII bytes of the file; bytes.ToLower
+    // turns a non-ASCII rune into an ASCII letter only for U+0130 -> 'i' and U+212A -> 'k',
+    // so a clear bit is uncertain only for keywords holding that letter.
+    auto kw_state = [&](size_t r) -> uint8_t {
+      switch (plan.rule_kw_mode[r]) {
+        case kKwAlways: return 1;
+        case kKwUnknown: return 2;
+        default:
+          for (uint32_t k : plan.rule_kws[r])
+            if ((kw[k / 32] >> (k % 32)) & 1) return 1;
+          if (!ko.kw_unknown.empty())
+            for (uint32_t k : plan.rule_kws[r])
+              if (ko.kw_unknown[k]) return 2;  // the kernels scanned the rule's group
+          // 3: uncertain and the kernels did not scan the rule (its keyword bits were clear)
+          if (((fbbits & 1) && kw_has_i[r]) || ((fbbits & 2) && kw_has_k[r])) return 3;
+          return 0;
+      }
+    };
+    // kernel overflow: resolve every rule over the whole file
+    const bool ovf = !ko.overflow.empty() && ko.overflow[f];
+    bool any_host = false;
+    for (uint32_t r : hostonly)
+      if (kw_state(r) != 0) any_host = true;
+    if (first[f] == first[f + 1] && !ovf && !any_host && !fbbits) {  // no match possible
+      if (prof) {
+        n_fast++;
+        tm.acc = &t_fast;
+      }
+      res.status = path_allowed(rs, &plan, pp, pn) ? kPathAllowed : kNoFindings;
+      return;
+    }
+    const std::string path(pp, pn);
+    std::vector<RuleWindows> wins(R);
+    std::vector<const RuleWindows*> wptr(R, nullptr);
+    std::vector<uint8_t> kws(R);
+    for (size_t r = 0; r < R; r++) kws[r] = kw_state(r);
+    if (ovf) {
+      for (size_t r = 0; r < R; r++) {
+        wins[r].whole = true;
+        wptr[r] = &wins[r];
+      }
+    }
+    for (uint32_t r : hostonly)
+      if (kws[r] != 0) {
+        wins[r].whole = true;
+        wptr[r] = &wins[r];
+      }
+    // every match start lies in [end - winback, end] of some candidate end offset; the
+    // reverse DFA narrows that to [leftmost start, end] or drops the candidate
+    auto add_end = [&](RuleWindows& w, uint32_t r, int64_t end) {
+      int64_t lo;
+      if (const DFA* rev = plan.rule_rev[r].get()) {
+        lo = reverse_match_start(*rev, content, end);
+        if (lo < 0) return;
+        lo = align_rune(content, n, lo);
+      } else {
+        const int64_t back = plan.rule_winback[r];
+        lo = back < 0 ? 0 : align_rune(content, n, std::max<int64_t>(0, end - back));
+      }
+      w.iv.push_back({lo, end});
+    };
+    auto normalize = [](RuleWindows& w) {  // sort, merge touching windows
+      std::sort(w.iv.begin(), w.iv.end());
+      size_t o = 0;
+      for (size_t i = 0; i < w.iv.size(); i++) {
+        if (o && w.iv[i].first <= w.iv[o - 1].second + 1)
+          w.iv[o - 1].second = std::max(w.iv[o - 1].second, w.iv[i].second);
+        else
+          w.iv[o++] = w.iv[i];
+      }
+      w.iv.resize(o);
+    };
+    for (uint32_t k = first[f]; k < first[f + 1];) {
+      uint32_t r = cand[k].rule;
+      uint32_t e = k;
+      while (e < first[f + 1] && cand[e].rule == r) e++;
+      RuleWindows& w = wins[r];
+      wptr[r] = &w;
+      if (!w.whole) {
+        for (uint32_t j = k; j < e; j++) add_end(w, r, cand[j].end);
+        normalize(w);
+      }
+      k = e;
+    }
+    if (fbbits & 6) {
+      // U+212A / U+017F join ASCII letters under (?i), which the K1 anchors (literal
+      // automaton, token-run counters) do not see: a match the kernels may have missed
+      // contains one of them, so its start lies within rule_maxlen bytes before it.  A
+      // rule without that bound runs its K2 DFA (which does fold them) over the file here.
+      std::vector<int64_t> fold;
+      for (int64_t q = 0; q + 1 < n; q++) {
+        if (content[q] == 0xC5 && content[q + 1] == 0xBF) fold.push_back(q);
+        else if (content[q] == 0xE2 && q + 2 < n && content[q + 1] == 0x84 && content[q + 2] == 0xAA) fold.push_back(q);
+      }
+      for (size_t r = 0; r < R; r++) {
+        if (kws[r] == 0 || kws[r] == 3 || !rs.rules[r].regex || wins[r].whole || fold.empty()) continue;
+        RuleWindows& w = wins[r];
+        wptr[r] = &w;
+        const int64_t ml = plan.rule_maxlen[r];
+        if (ml >= 0) {
+          for (int64_t q : fold) w.iv.push_back({align_rune(content, n, std::max<int64_t>(0, q - ml)), q});
+        } else if (plan.rule_group[r] >= 0) {
+          const GroupPlan& g = plan.groups[plan.rule_group[r]];
+          size_t local = 0;
+          while (g.rules[local] != r) local++;
+          const DFA& d = *g.dfa;
+          w.iv.clear();
+          run_segment(d, content, 0, (uint64_t)n, 0, (uint64_t)n, ~0u, [&](uint32_t mi, uint64_t pos) {
+            if ((d.masks[mi][local / 64] >> (local % 64)) & 1) add_end(w, (uint32_t)r, (int64_t)pos);
+          });
+        } else {
+          w.whole = true;
+          w.iv.clear();
+          continue;
+        }
+        normalize(w);
+      }
+    }
+    // a rule whose keyword gate is uncertain and that the kernels did not scan (its
+    // keyword bits were clear) is resolved over the whole file when the exact gate passes
+    for (size_t r = 0; r < R; r++)
+      if (kws[r] == 3) {
+        kws[r] = 2;
+        wins[r].whole = true;
+        wptr[r] = &wins[r];
+      }
+    FileGate gate;
+    gate.kw_state = kws.data();
+    gate.windows = wptr.data();
+    gate.path_allowed = path_allowed(rs, &plan, pp, pn) ? 1 : 0;
+    if (prof)
+      for (size_t r = 0; r < R; r++)
+        if (wptr[r] && (wptr[r]->whole || (!wptr[r]->iv.empty() && wptr[r]->iv[0].first == 0))) {
+          n_whole++;
+          if (getenv("TSG_PROF2") && n_whole < 40)
+            fprintf(stderr, "whole-prefix: file %u rule %s n=%ld whole=%d iv0=[%ld,%ld] niv=%zu\n", f, rs.rules[r].id.c_str(), (long)n,
+                    (int)wptr[r]->whole, wptr[r]->iv.empty() ? -1L : (long)wptr[r]->iv[0].first,
+                    wptr[r]->iv.empty() ? -1L : (long)wptr[r]->iv[0].second, wptr[r]->iv.size());
+        }
+    scan_file(rs, path, content, (size_t)n, &gate, &res);
+  });
+  if (prof)
+    fprintf(stderr, "resolve: fast files %.1f ms cpu (%ld), other plain files %.1f ms cpu, candidate files %.1f ms cpu (%ld files, %ld whole-prefix rule scans)\n",
+            t_fast / 1e6, (long)n_fast, t_plain / 1e6, t_cand / 1e6, (long)n_cand, (long)n_whole);
+}
+
+// ------------------------------------------------------------------ kernel emulation
 
 void k1_reference(const Plan& plan, const BatchView& bv, uint32_t chunk, std::vector<uint32_t>* kw,
                   std::vector<uint32_t>* ev) {

@@ -2,7 +2,11 @@
 #include "scanner.hpp"
 
 #include <algorithm>
+#include <atomic>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
+#include <x86intrin.h>
 
 namespace tsg {
 
@@ -336,14 +340,39 @@ void find_location(int64_t start, int64_t end, const std::string& content,
 
 }  // namespace
 
+// TSG_PROF: per-phase cycle counters of scan_file (printed at exit)
+static std::atomic<uint64_t> g_ph[8];
+static const bool g_prof = getenv("TSG_PROF") != nullptr;
+struct PhDump {
+  ~PhDump() {
+    if (!g_prof) return;
+    const char* nm[8] = {"allowpath", "rulegates", "lower", "findall", "allowmatch", "locate", "total", "nfiles"};
+    for (int i = 0; i < 8; i++) fprintf(stderr, "scan_file %-10s %.2f Mcyc\n", nm[i], g_ph[i] / 1e6);
+  }
+};
+static PhDump g_phdump;
+struct PhT {
+  uint64_t t = g_prof ? __rdtsc() : 0;
+  void lap(int i) {
+    if (!g_prof) return;
+    uint64_t n = __rdtsc();
+    g_ph[i] += n - t;
+    t = n;
+  }
+};
+
 void scan_file(const Ruleset& rs, const std::string& path, const uint8_t* content, size_t n,
                const FileGate* gate, FileResult* out) {
+  PhT ph, tot;
+  if (g_prof) g_ph[7] += 1000000;
+  struct TotL { PhT& t; ~TotL() { t.lap(6); } } totl{tot};
   out->findings.clear();
   out->status = kNoFindings;
-  if (rs.AllowPath(path)) {  // scanner.go:343-347
+  if ((gate && gate->path_allowed >= 0) ? gate->path_allowed == 1 : rs.AllowPath(path)) {  // scanner.go:343-347
     out->status = kPathAllowed;
     return;
   }
+  ph.lap(0);
   std::string lowered;
   bool have_lowered = false;
   Blocks global{content, n, &rs.exclude};
@@ -361,14 +390,20 @@ void scan_file(const Ruleset& rs, const std::string& path, const uint8_t* conten
       if (!win) continue;
       if (gate->kw_state[ri] == 0) continue;
     }
+    ph.lap(1);
     if (r.path && !r.path->Match((const uint8_t*)path.data(), path.size())) continue;
     if (allow_path(r.allow, path)) continue;
+    ph.lap(1);
     if (!gate || gate->kw_state[ri] == 2) {
       if (!have_lowered) {
         go_to_lower(content, n, &lowered);
         have_lowered = true;
       }
-      if (!match_keywords(r, lowered)) continue;
+      if (!match_keywords(r, lowered)) {
+        ph.lap(2);
+        continue;
+      }
+      ph.lap(2);
     }
     if (!r.regex) continue;
     // FindLocations / FindSubmatchLocations (scanner.go:96-141)
@@ -380,6 +415,7 @@ void scan_file(const Ruleset& rs, const std::string& path, const uint8_t* conten
     } else {
       r.regex->FindAllWindows(content, n, sub, win->iv, &idx);
     }
+    ph.lap(3);
     std::vector<Loc> locs;
     for (size_t k = 0; k + ns - 1 < idx.size(); k += ns) {
       int64_t s = idx[k], e = idx[k + 1];
@@ -390,6 +426,7 @@ void scan_file(const Ruleset& rs, const std::string& path, const uint8_t* conten
         for (int g : r.group_idx) locs.push_back({idx[k + 2 * g], idx[k + 2 * g + 1]});
       }
     }
+    ph.lap(4);
     if (locs.empty()) continue;
     Blocks local{content, n, &r.exclude};
     for (const auto& loc : locs) {
@@ -403,10 +440,12 @@ void scan_file(const Ruleset& rs, const std::string& path, const uint8_t* conten
       std::memset(&censored[loc.start], '*', loc.end - loc.start);  // censorLocation
     }
   }
+  ph.lap(4);
   if (matched.empty()) return;  // Secret{}
   std::vector<int64_t> nl;
-  for (size_t i = 0; i < censored.size(); i++)
-    if (censored[i] == '\n') nl.push_back((int64_t)i);
+  for (const char *p = censored.data(), *e = p + censored.size();
+       (p = (const char*)std::memchr(p, '\n', e - p)) != nullptr; p++)
+    nl.push_back((int64_t)(p - censored.data()));
   out->findings.resize(matched.size());
   for (size_t k = 0; k < matched.size(); k++) {
     out->findings[k].rule = matched[k].first;
@@ -420,6 +459,7 @@ void scan_file(const Ruleset& rs, const std::string& path, const uint8_t* conten
     return a.match < b.match;
   });
   out->status = kHasFindings;
+  ph.lap(5);
 }
 
 // ------------------------------------------------------------------ serialization

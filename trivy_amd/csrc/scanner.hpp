@@ -80,6 +80,8 @@ struct FileGate {
   const uint8_t* kw_state = nullptr;
   // windows[r] == nullptr -> the rule has no candidate in this file (regex cannot match)
   const RuleWindows* const* windows = nullptr;
+  // Global.AllowPath(path) already evaluated by the caller: 0 no, 1 yes, -1 not known
+  int8_t path_allowed = -1;
 };
 
 // Exact Scan of one file (scanner.go:341-416).

@@ -422,6 +422,24 @@ class GpuContext:
         N.check(N.lib().tsg_batch_scan(self._h, C.byref(out)))
         return out
 
+    def submit(self):
+        """Device part of a scan now; its host resolution runs in the background."""
+        N.check(N.lib().tsg_batch_submit(self._h))
+
+    def collect_raw(self):
+        """Results of the oldest submitted scan (raw tsg_result handle)."""
+        out = C.c_void_p()
+        N.check(N.lib().tsg_batch_collect(self._h, C.byref(out)))
+        return out
+
+    def collect(self):
+        out = self.collect_raw()
+        b = self._batch
+        return self.scanner.decode(out, [b.path(i) for i in range(b.nfiles)])
+
+    def pending(self):
+        return N.lib().tsg_batch_pending(self._h)
+
     def scan(self):
         out = self.scan_raw()
         b = self._batch
