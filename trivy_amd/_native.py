@@ -8,6 +8,10 @@ import ctypes as C
 import os
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libtrivy_secret.so")
+# measurement builds of the same sources with other compile-time tunings (tools/)
+if os.environ.get("TSG_LIB_VARIANT"):
+    LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)),
+                            "libtrivy_secret_%s.so" % os.environ["TSG_LIB_VARIANT"])
 
 TSG_OK = 0
 TSG_ERR_CONFIG = -1
@@ -34,7 +38,8 @@ class RuleDesc(C.Structure):
 class RulesetInfo(C.Structure):
     _fields_ = [("n_rules", C.c_uint32), ("n_keywords", C.c_uint32), ("n_groups", C.c_uint32),
                 ("n_hostonly", C.c_uint32), ("kw_states", C.c_uint32),
-                ("max_group_states", C.c_uint32), ("table_bytes", C.c_uint64)]
+                ("max_group_states", C.c_uint32), ("table_bytes", C.c_uint64),
+                ("kw_classes", C.c_uint32)]
 
 
 class CtxOptions(C.Structure):

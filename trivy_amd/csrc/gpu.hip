@@ -41,7 +41,21 @@ namespace tsg {
       return fail(TSG_ERR_GPU, std::string(#x) + ": " + hipGetErrorString(e_));       \
   } while (0)
 
-constexpr int kStreams = 4;   // independent DFA chains per lane (dense passes)
+#ifndef K1_UNROLL
+#define K1_UNROLL 16
+#endif
+#ifdef K1_EXP_COAL  // timing experiment only (wrong results): wave-coalesced loads
+#define K1_ADDR(a, i, off) \
+  (((a) / ((uint64_t)NS * L * 64) * ((uint64_t)NS * L * 64)) + ((uint64_t)((off) / 16) * NS + (i)) * 1024 + (threadIdx.x & 63) * 16)
+#else
+#define K1_ADDR(a, i, off) ((a) + (uint64_t)(i) * L + (off))
+#endif
+constexpr int kStreams = 4;       // K2 dense: chunks per lane
+constexpr int kK1MaxStreams = 8;  // K1: chains per lane, the largest variant
+constexpr int kK1Seg = 8;         // K1: consecutive chunks per chain
+// static LDS size classes of the K1 kernel (KiB): 3, 2 or 1 blocks per CU
+constexpr int kK1Lds[3] = {52, 80, 156};
+constexpr uint32_t kK1Tab = 1024;  // K1 LDS: 256 class words, then the transition table   // independent DFA chains per lane (dense passes)
 constexpr int kBlock = 256;
 constexpr int kPad = 256;     // zero bytes before and after the batch in HBM (>= K1 warm-up)
 constexpr int kMaxBack = 16;  // event windows up to this many chunks; larger -> whole file
@@ -63,12 +77,16 @@ struct DevDFA {  // K2 rule group
 };
 
 struct DevK1 {
-  const uint16_t* tab;    // [ns * nc] next | 0x8000 if the next state ends a literal
-  const uint32_t* cls;    // [256] class | 0xFF00 if in run class D | 0xFFFF0000 if in U
+  // States are renumbered so that the ones whose arrival must be reported (they end a
+  // literal) come last, and a state is named by its row (id * nc): next = tab[row + class]
+  // needs no multiply, and "arrival reports" is next >= acc_row.
+  const uint16_t* tab;    // [ns * nc] row of the next state
+  const uint32_t* cls;    // [256] class * 2 | 0xFF00 if in run class D | 0xFFFF0000 if in U
   const uint16_t* accs;   // [ns] accept-mask index of the literals a state ends
   const uint32_t* masks;  // [nmasks * mw] keyword words (kw_words), then the event word
-  uint32_t nc, ns, nmasks, mw, kw_words, start, warm, kU, kD;  // kD = threshold << 8
-  uint32_t o_cls, o_accs, o_masks, lds_bytes;
+  uint32_t nc, ns, nmasks, mw, kw_words, start, warm, kU, kD;  // start: row; kD = threshold << 8
+  uint32_t acc_row;
+  uint32_t lds_class;  // index into kK1Lds
 };
 
 struct DevCand {
@@ -120,15 +138,16 @@ struct K1Args {
   uint32_t* kw;    // [nfiles * kw_words]
   uint32_t* ev;    // [nchunks, padded to whole items]
   uint32_t* hits;  // [ns] arrivals per accepting state (sampling pass) or null
+  uint32_t streams;  // chains per lane
+  uint32_t seg;      // consecutive chunks per chain
 };
 
-// one chain = one chunk: automaton state, run counters, the file the chain is in and the
+// one chain = one chunk: automaton row, run counters, the file the chain is in and the
 // keyword bits already sent for it (so each bit costs one atomic per chain and file)
 template <int KWW>
 struct K1Chain {
   uint32_t s, cnt, mx, evl, f;
   uint64_t fe;
-  uint32_t sent[KWW];
 };
 
 template <int KWW>
@@ -143,8 +162,6 @@ struct K1Lane {
   __device__ __forceinline__ void reset(K1Chain<KWW>& c) {
     c.s = d.start;
     c.cnt = 0;
-#pragma unroll
-    for (int w = 0; w < KWW; w++) c.sent[w] = 0;
   }
   // byte p lies past the chain's file: move to the file containing p
   __device__ __forceinline__ void next_file(K1Chain<KWW>& c, uint64_t p) {
@@ -154,22 +171,18 @@ struct K1Lane {
     c.fe = c.f < A.nfiles ? A.off[c.f + 1] : ~0ull;
     reset(c);
   }
-  // arrival in accepting state s: keyword bits of the chain's file, event bits of its chunk
-  __device__ __forceinline__ void accept(K1Chain<KWW>& c, uint32_t s) {
-    if (A.hits) atomicAdd(&A.hits[s], 1u);
-    const uint32_t* m = s_masks + (size_t)s_accs[s] * d.mw;
+  // m's low byte is the byte's class * 2: the entry's byte offset is 2 * row + m[7:0]
+  __device__ __forceinline__ uint32_t next(uint32_t s, uint32_t m) const {
+    return *(const uint16_t*)((const uint8_t*)s_tab + (s + s + (m & 0xFFu)));
+  }
+  // arrival in reporting row r: keyword bits of the chain's file, event bits of its chunk
+  __device__ __forceinline__ void accept(K1Chain<KWW>& c, uint32_t r) {
+    const uint32_t id = r / d.nc;
+    if (A.hits) atomicAdd(&A.hits[id], 1u);
+    const uint32_t* m = s_masks + (size_t)s_accs[id] * d.mw;
     if (c.f < A.nfiles) {
       uint32_t* kwf = A.kw + (size_t)c.f * d.kw_words;
-#pragma unroll
-      for (int w = 0; w < KWW; w++) {
-        if ((uint32_t)w >= d.kw_words) break;
-        const uint32_t bits = m[w] & ~c.sent[w];
-        if (bits) {
-          atomicOr(&kwf[w], bits);
-          c.sent[w] |= bits;
-        }
-      }
-      for (uint32_t w = KWW; w < d.kw_words; w++)
+      for (uint32_t w = 0; w < d.kw_words; w++)
         if (m[w]) atomicOr(&kwf[w], m[w]);
     }
     c.evl |= m[d.kw_words];
@@ -180,9 +193,8 @@ struct K1Lane {
   __device__ __forceinline__ void replay16(K1Chain<KWW>& c, uint32_t s, const uint4 v) {
 #pragma unroll 1
     for (uint32_t k = 0; k < 16; k++) {
-      const uint32_t e = s_tab[s * d.nc + (s_cls[byte_of(v, k)] & 0xFFu)];
-      s = e & 0x7FFFu;
-      if (e & 0x8000u) accept(c, s);
+      s = next(s, s_cls[byte_of(v, k)]);
+      if (s >= d.acc_row) accept(c, s);
     }
   }
   // one chain, 16 bytes at p: file boundaries inside (or bytes below lo skipped: warm-up)
@@ -194,44 +206,65 @@ struct K1Lane {
       if (q < lo) continue;
       if ((uint64_t)q >= c.fe) next_file(c, (uint64_t)q);
       const uint32_t m = s_cls[byte_of(v, k)];
-      const uint32_t e = s_tab[c.s * d.nc + (m & 0xFFu)];
-      c.s = e & 0x7FFFu;
+      c.s = next(c.s, m);
       c.cnt = run_step(c.cnt, m);
       if (record) {
         c.mx = run_max(c.mx, c.cnt);
-        if (e & 0x8000u) accept(c, c.s);
+        if (c.s >= d.acc_row) accept(c, c.s);
       }
     }
   }
-  // one chain, 16 bytes inside its file
-  __device__ __forceinline__ void fast16(K1Chain<KWW>& c, const uint4 v) {
-    const uint32_t s0 = c.s;
-    uint32_t any = 0;
+  // NS chains, 16 bytes each, all inside their files: interleaved byte by byte; a word
+  // in which a chain reached a reporting row is replayed on the rare path
+  template <int NS>
+  __device__ __forceinline__ void fast16(K1Chain<KWW> (&c)[NS], const uint4 (&v)[NS]) {
+    uint32_t s0[NS], top[NS];
 #pragma unroll
-    for (int k = 0; k < 16; k++) {
-      const uint32_t m = s_cls[byte_of(v, k)];
-      const uint32_t e = s_tab[c.s * d.nc + (m & 0xFFu)];
-      any |= e;
-      c.s = e & 0x7FFFu;
-      c.cnt = run_step(c.cnt, m);
-      c.mx = run_max(c.mx, c.cnt);
+    for (int i = 0; i < NS; i++) {
+      s0[i] = c[i].s;
+      top[i] = 0;
     }
-    if (__builtin_expect(any & 0x8000u, 0)) replay16(c, s0, v);
+#pragma unroll(NS > 4 ? K1_UNROLL / 4 : K1_UNROLL)
+    for (int k = 0; k < 16; k++)
+#pragma unroll
+      for (int i = 0; i < NS; i++) {
+#ifdef K1_EXP_NO_CLS  // timing experiments only: wrong results
+        const uint32_t m = (byte_of(v[i], k) & 0x3Fu) * 2u;
+#else
+        const uint32_t m = s_cls[byte_of(v[i], k)];
+#endif
+#ifdef K1_EXP_NO_TAB
+        c[i].s = (c[i].s + m) & 0x3FFFu;
+#else
+        c[i].s = next(c[i].s, m);
+#endif
+        top[i] = max(top[i], c[i].s);
+#ifndef K1_EXP_NO_RUNS
+        c[i].cnt = run_step(c[i].cnt, m);
+        c[i].mx = run_max(c[i].mx, c[i].cnt);
+#endif
+      }
+#pragma unroll
+    for (int i = 0; i < NS; i++)
+      if (__builtin_expect(top[i] >= d.acc_row, 0)) replay16(c[i], s0[i], v[i]);
   }
 
-  // item = NS consecutive chunks from a: NS chains interleaved byte by byte
+  // item = NS segments of A.seg consecutive chunks from a; chain i walks segment i (its
+  // state carries from one chunk to the next, so only the segment start needs the warm-up
+  // replay), the NS chains interleaved byte by byte
   template <int NS>
   __device__ void item(uint64_t a) {
     const uint8_t* data = A.data;
     const uint32_t C = A.chunk;
+    const uint64_t L = (uint64_t)C * A.seg;  // segment bytes
     const uint64_t c0 = a / C;
     K1Chain<KWW> c[NS];
     uint64_t lo[NS];
 #pragma unroll
     for (int i = 0; i < NS; i++) {
-      const uint64_t Ai = a + (uint64_t)i * C;
+      const uint64_t Ai = a + (uint64_t)i * L;
       if (Ai < A.total) {
-        c[i].f = A.chunk_file[c0 + i];
+        c[i].f = A.chunk_file[c0 + (uint64_t)i * A.seg];
         lo[i] = A.off[c[i].f];
         c[i].fe = A.off[c[i].f + 1];
       } else {
@@ -243,96 +276,97 @@ struct K1Lane {
       c[i].mx = 0;
       c[i].evl = 0;
     }
-    // warm-up: the bytes before each chunk that belong to the chunk's first file
+    // warm-up: the bytes before each segment that belong to the segment's first file
     bool slow = false;
 #pragma unroll
-    for (int i = 0; i < NS; i++) slow |= (int64_t)lo[i] > (int64_t)(a + (uint64_t)i * C) - (int64_t)d.warm;
+    for (int i = 0; i < NS; i++) slow |= (int64_t)lo[i] > (int64_t)(a + (uint64_t)i * L) - (int64_t)d.warm;
     for (uint32_t j = 0; j < d.warm; j += 16) {
       uint4 v[NS];
 #pragma unroll
-      for (int i = 0; i < NS; i++) v[i] = *(const uint4*)(data + a + (uint64_t)i * C - d.warm + j);
+      for (int i = 0; i < NS; i++) v[i] = *(const uint4*)(data + a + (uint64_t)i * L - d.warm + j);
       if (!slow) {
 #pragma unroll
         for (int k = 0; k < 16; k++)
 #pragma unroll
           for (int i = 0; i < NS; i++) {
             const uint32_t m = s_cls[byte_of(v[i], k)];
-            c[i].s = s_tab[c[i].s * d.nc + (m & 0xFFu)] & 0x7FFFu;
+            c[i].s = next(c[i].s, m);
             c[i].cnt = run_step(c[i].cnt, m);
           }
       } else {
 #pragma unroll
         for (int i = 0; i < NS; i++)
-          slow16(c[i], v[i], (int64_t)(a + (uint64_t)i * C) - (int64_t)d.warm + j, (int64_t)lo[i], false);
+          slow16(c[i], v[i], (int64_t)(a + (uint64_t)i * L) - (int64_t)d.warm + j, (int64_t)lo[i], false);
       }
     }
-    uint4 cur[NS];
-#pragma unroll
-    for (int i = 0; i < NS; i++) cur[i] = *(const uint4*)(data + a + (uint64_t)i * C);
-    for (uint32_t j = 0; j < C; j += 16) {
-      uint4 nxt[NS];
-#pragma unroll
-      for (int i = 0; i < NS; i++) nxt[i] = *(const uint4*)(data + a + (uint64_t)i * C + j + 16);
+    // Four words in flight per chain, each register set consumed in place (the loop body
+    // is unrolled four times): a set is refilled right after its word is stepped, so a
+    // load has three words of work to land, and no register copy waits on a pending load.
+    uint32_t jc = 0;   // offset inside the current chunk
+    uint64_t ci = c0;  // chunk index of chain 0
+    auto word = [&](uint64_t j, const uint4 (&v)[NS]) {
       bool sl = false;
 #pragma unroll
-      for (int i = 0; i < NS; i++) sl |= c[i].fe < a + (uint64_t)i * C + j + 16;
+      for (int i = 0; i < NS; i++) sl |= c[i].fe < a + (uint64_t)i * L + j + 16;
       if (__builtin_expect(!sl, 1)) {
-        uint32_t s0[NS], any[NS];
-#pragma unroll
-        for (int i = 0; i < NS; i++) {
-          s0[i] = c[i].s;
-          any[i] = 0;
-        }
-#pragma unroll
-        for (int k = 0; k < 16; k++)
-#pragma unroll
-          for (int i = 0; i < NS; i++) {
-            const uint32_t m = s_cls[byte_of(cur[i], k)];
-            const uint32_t e = s_tab[c[i].s * d.nc + (m & 0xFFu)];
-            any[i] |= e;
-            c[i].s = e & 0x7FFFu;
-            c[i].cnt = run_step(c[i].cnt, m);
-            c[i].mx = run_max(c[i].mx, c[i].cnt);
-          }
-#pragma unroll
-        for (int i = 0; i < NS; i++)
-          if (__builtin_expect(any[i] & 0x8000u, 0)) replay16(c[i], s0[i], cur[i]);
+        fast16<NS>(c, v);
       } else {
 #pragma unroll
-        for (int i = 0; i < NS; i++) {
-          const uint64_t p = a + (uint64_t)i * C + j;
-          if (c[i].fe < p + 16) slow16(c[i], cur[i], (int64_t)p, 0, true);
-          else fast16(c[i], cur[i]);
-        }
+        for (int i = 0; i < NS; i++) slow16(c[i], v[i], (int64_t)(a + (uint64_t)i * L + j), 0, true);
       }
+      jc += 16;
+      if (jc == C) {  // chunk end (uniform across the lane's chains): its event bits
 #pragma unroll
-      for (int i = 0; i < NS; i++) cur[i] = nxt[i];
+        for (int i = 0; i < NS; i++) {
+          A.ev[ci + (uint64_t)i * A.seg] = c[i].evl | run_bits(c[i].mx);
+          c[i].evl = 0;
+          c[i].mx = 0;
+        }
+        jc = 0;
+        ci++;
+      }
+    };
+    auto load = [&](uint4 (&v)[NS], uint64_t j) {
+#pragma unroll
+      for (int i = 0; i < NS; i++) v[i] = *(const uint4*)(data + K1_ADDR(a, i, j));
+    };
+    uint4 b0[NS], b1[NS], b2[NS], b3[NS];
+    load(b0, 0);
+    load(b1, 16);
+    load(b2, 32);
+    load(b3, 48);
+    for (uint64_t j = 0; j < L; j += 64) {  // L is a multiple of 128
+      word(j, b0);
+      load(b0, j + 64);
+      word(j + 16, b1);
+      load(b1, j + 80);
+      word(j + 32, b2);
+      load(b2, j + 96);
+      word(j + 48, b3);
+      load(b3, j + 112);
     }
-#pragma unroll
-    for (int i = 0; i < NS; i++) A.ev[c0 + i] = c[i].evl | run_bits(c[i].mx);
   }
 };
 
-template <int KWW>
-__global__ void __launch_bounds__(kBlock) k1_kernel(DevK1 d, K1Args A) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  uint16_t* s_tab = (uint16_t*)smem;
-  uint32_t* s_cls = (uint32_t*)(smem + d.o_cls);
-  uint16_t* s_accs = (uint16_t*)(smem + d.o_accs);
-  uint32_t* s_masks = (uint32_t*)(smem + d.o_masks);
+// K1 LDS image (static, so every table address is a constant): the 256 class words at 0
+// (a byte's word is at byte * 4), the transitions from 1 KiB.  Accept masks stay in
+// global memory (rare path).
+template <int KWW, int LDSK, int NS>
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2, 8))) k1_kernel(DevK1 d, K1Args A) {
+  __shared__ __attribute__((aligned(16))) uint8_t smem[LDSK * 1024];
+  uint32_t* s_cls = (uint32_t*)smem;
+  uint16_t* s_tab = (uint16_t*)(smem + 1024);
   {
     const uint32_t* src = (const uint32_t*)d.tab;
     uint32_t* dst = (uint32_t*)s_tab;
     for (uint32_t i = threadIdx.x; i < (d.ns * d.nc + 1) / 2; i += blockDim.x) dst[i] = src[i];
     for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) s_cls[i] = d.cls[i];
-    for (uint32_t i = threadIdx.x; i < d.ns; i += blockDim.x) s_accs[i] = d.accs[i];
-    for (uint32_t i = threadIdx.x; i < d.nmasks * d.mw; i += blockDim.x) s_masks[i] = d.masks[i];
   }
   __syncthreads();
-  K1Lane<KWW> L{d, A, s_tab, s_cls, s_accs, s_masks};
+  K1Lane<KWW> L{d, A, s_tab, s_cls, d.accs, d.masks};
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   for (uint64_t it = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; it < A.nitems; it += stride)
-    L.template item<kStreams>(it * A.item_step * kStreams * A.chunk);
+    L.template item<NS>(it * A.item_step * NS * A.seg * A.chunk);
 }
 
 // ---------------------------------------------------------------- gate + items
@@ -783,29 +817,63 @@ static int k1_debug() {
   return e ? atoi(e) : 0;
 }
 
-struct K1Host {  // host copies of the K1 tables (adaptation patches the device table)
+struct K1Host {  // host copies of the K1 tables (adaptation rebuilds the device table)
   std::vector<uint16_t> tab, accs;
   std::vector<uint32_t> masks;
+  std::vector<uint32_t> order;  // device state id -> automaton state
 };
+
+// Device numbering of the K1 automaton: states whose arrival is reported (they end a
+// literal, and are not `quiet`) last; rows = id * nc.
+static int k1_tables(const Plan& p, const std::vector<uint8_t>& quiet, K1Host* h, uint32_t* start_row,
+                     uint32_t* acc_row) {
+  const DFA& d = *p.kw_dfa;
+  const size_t nc = d.nclasses, ns = d.nstates;
+  if ((ns - 1) * nc > 0xFFFF) return fail(TSG_ERR_INTERNAL, "keyword automaton too large for 16-bit rows");
+  std::vector<uint32_t> newid(ns);
+  h->order.clear();
+  for (int pass = 0; pass < 2; pass++)
+    for (size_t st = 0; st < ns; st++) {
+      const bool rep = d.eot_acc[st] && !quiet[st] && !(k1_debug() & 1);
+      if (rep == (pass == 1)) {
+        newid[st] = (uint32_t)h->order.size();
+        h->order.push_back((uint32_t)st);
+      }
+    }
+  uint32_t first_rep = (uint32_t)ns;
+  for (size_t i = 0; i < ns; i++) {
+    const uint32_t st = h->order[i];
+    if (d.eot_acc[st] && !quiet[st] && !(k1_debug() & 1)) {
+      first_rep = (uint32_t)i;
+      break;
+    }
+  }
+  h->tab.assign(ns * nc + (ns * nc & 1), 0);  // the kernel stages whole dwords
+  h->accs.assign(ns, 0);
+  for (size_t i = 0; i < ns; i++) {
+    const uint32_t st = h->order[i];
+    h->accs[i] = (uint16_t)d.eot_acc[st];
+    for (size_t c = 0; c < nc; c++) h->tab[i * nc + c] = (uint16_t)(newid[d.next[st * nc + c]] * nc);
+  }
+  *start_row = newid[d.start[kCtxBOT]] * (uint32_t)nc;
+  *acc_row = first_rep * (uint32_t)nc;
+  return TSG_OK;
+}
 
 static int make_device_k1(const Plan& p, DevK1* out, std::vector<void*>* allocs, K1Host* host) {
   const DFA& d = *p.kw_dfa;
-  if (d.nstates >= 0x8000) return fail(TSG_ERR_INTERNAL, "keyword automaton too large");
   const size_t nc = d.nclasses;
-  if (nc > 256) return fail(TSG_ERR_INTERNAL, "keyword automaton has too many classes");
-  std::vector<uint16_t> tab((size_t)d.nstates * nc), accs(d.nstates);
-  for (int s = 0; s < d.nstates; s++) {
-    accs[s] = (uint16_t)d.eot_acc[s];  // no assertions: the state's match set
-    for (size_t c = 0; c < nc; c++) {
-      const size_t i = (size_t)s * nc + c;
-      if (d.acc[i] != d.eot_acc[s]) return fail(TSG_ERR_INTERNAL, "keyword automaton accepts are not state-based");
-      const uint32_t nx = d.next[i];
-      tab[i] = (uint16_t)(nx | ((d.eot_acc[nx] && !(k1_debug() & 1)) ? 0x8000u : 0u));
-    }
-  }
+  if (nc > 128) return fail(TSG_ERR_INTERNAL, "keyword automaton has too many classes");
+  for (int st = 0; st < d.nstates; st++)
+    for (size_t c = 0; c < nc; c++)
+      if (d.acc[(size_t)st * nc + c] != d.eot_acc[st])
+        return fail(TSG_ERR_INTERNAL, "keyword automaton accepts are not state-based");
+  DevK1& v = *out;
+  int rc;
+  if ((rc = k1_tables(p, std::vector<uint8_t>(d.nstates, 0), host, &v.start, &v.acc_row))) return rc;
   std::vector<uint32_t> cls(256);
   for (int b = 0; b < 256; b++)
-    cls[b] = d.cls[b] | ((p.run_cls[b] & 2) ? 0xFF00u : 0u) | ((p.run_cls[b] & 1) ? 0xFFFF0000u : 0u);
+    cls[b] = (uint32_t)d.cls[b] * 2 | ((p.run_cls[b] & 2) ? 0xFF00u : 0u) | ((p.run_cls[b] & 1) ? 0xFFFF0000u : 0u);
   const uint32_t W = (uint32_t)p.kw_words, mw = W + 1;
   std::vector<uint32_t> masks((size_t)d.masks.size() * mw, 0);
   for (size_t m = 0; m < d.masks.size(); m++) {
@@ -813,34 +881,27 @@ static int make_device_k1(const Plan& p, DevK1* out, std::vector<void*>* allocs,
       if ((d.masks[m][k / 64] >> (k % 64)) & 1) masks[m * mw + k / 32] |= 1u << (k % 32);
     masks[m * mw + W] = p.kw_mask_events[m];
   }
-  if (tab.size() & 1) tab.push_back(0);  // the kernel stages whole dwords
-  DevK1& v = *out;
-  int rc;
-  if ((rc = upload_vec(tab, &v.tab, allocs))) return rc;
+  if ((rc = upload_vec(host->tab, &v.tab, allocs))) return rc;
   if ((rc = upload_vec(cls, &v.cls, allocs))) return rc;
-  if ((rc = upload_vec(accs, &v.accs, allocs))) return rc;
+  if ((rc = upload_vec(host->accs, &v.accs, allocs))) return rc;
   if ((rc = upload_vec(masks, &v.masks, allocs))) return rc;
   v.nc = (uint32_t)nc;
   v.ns = (uint32_t)d.nstates;
   v.nmasks = (uint32_t)d.masks.size();
   v.mw = mw;
   v.kw_words = W;
-  v.start = d.start[kCtxBOT];
   v.warm = (uint32_t)p.warm;
   v.kU = (uint32_t)p.run_k[0];
   v.kD = (uint32_t)p.run_k[1] << 8;
-  host->tab = tab;
-  host->accs = accs;
   host->masks = masks;
-  uint32_t o = align16((uint32_t)(tab.size() * 2));
-  v.o_cls = o;
-  o += 1024;
-  v.o_accs = o;
-  o += align16(d.nstates * 2);
-  v.o_masks = o;
-  o += align16((uint32_t)masks.size() * 4);
-  v.lds_bytes = o;
-  if (v.lds_bytes > 160 * 1024) return fail(TSG_ERR_INTERNAL, "keyword automaton exceeds LDS");
+  const uint32_t need = (uint32_t)(host->tab.size() * 2) + 1024;
+  v.lds_class = 3;
+  for (uint32_t k = 0; k < 3; k++)
+    if (need <= (uint32_t)kK1Lds[k] * 1024) {
+      v.lds_class = k;
+      break;
+    }
+  if (v.lds_class > 2) return fail(TSG_ERR_INTERNAL, "keyword automaton exceeds LDS");
   return TSG_OK;
 }
 
@@ -956,20 +1017,42 @@ static int ensure(T** p, size_t* cap, size_t n) {
   return TSG_OK;
 }
 
-static const void* k1_fn(uint32_t kw_words) {
-  if (kw_words <= 1) return (const void*)k1_kernel<1>;
-  if (kw_words <= 2) return (const void*)k1_kernel<2>;
-  if (kw_words <= 4) return (const void*)k1_kernel<4>;
-  return (const void*)k1_kernel<8>;
+template <int LDSK, int NS>
+static const void* k1_fn_w(uint32_t kw_words) {
+  if (kw_words <= 1) return (const void*)k1_kernel<1, LDSK, NS>;
+  if (kw_words <= 2) return (const void*)k1_kernel<2, LDSK, NS>;
+  if (kw_words <= 4) return (const void*)k1_kernel<4, LDSK, NS>;
+  return (const void*)k1_kernel<8, LDSK, NS>;
+}
+
+template <int NS>
+static const void* k1_fn_ns(uint32_t kw_words, uint32_t lds_class) {
+  switch (lds_class) {
+    case 0: return k1_fn_w<kK1Lds[0], NS>(kw_words);
+    case 1: return k1_fn_w<kK1Lds[1], NS>(kw_words);
+    default: return k1_fn_w<kK1Lds[2], NS>(kw_words);
+  }
+}
+
+// independent K1 chains per lane: 4, or kK1MaxStreams with TSG_K1_NS=8 (measurements)
+static uint32_t k1_streams() {
+  const char* e = getenv("TSG_K1_NS");
+  return (e && atoi(e) == kK1MaxStreams) ? (uint32_t)kK1MaxStreams : 4u;
+}
+
+static const void* k1_fn(uint32_t kw_words, uint32_t lds_class, uint32_t ns) {
+  return ns == 4 ? k1_fn_ns<4>(kw_words, lds_class) : k1_fn_ns<kK1MaxStreams>(kw_words, lds_class);
 }
 
 static int launch_k1(tsg_ctx* c, const K1Args& A) {
-  const uint32_t W = c->k1.kw_words;
-  const int grid = (int)std::min<uint64_t>((A.nitems + kBlock - 1) / kBlock, (uint64_t)c->grid);
-  if (W <= 1) hipLaunchKernelGGL(k1_kernel<1>, dim3(grid), dim3(kBlock), c->k1.lds_bytes, c->stream, c->k1, A);
-  else if (W <= 2) hipLaunchKernelGGL(k1_kernel<2>, dim3(grid), dim3(kBlock), c->k1.lds_bytes, c->stream, c->k1, A);
-  else if (W <= 4) hipLaunchKernelGGL(k1_kernel<4>, dim3(grid), dim3(kBlock), c->k1.lds_bytes, c->stream, c->k1, A);
-  else hipLaunchKernelGGL(k1_kernel<8>, dim3(grid), dim3(kBlock), c->k1.lds_bytes, c->stream, c->k1, A);
+  static const int gmul = getenv("TSG_K1_GRID") ? atoi(getenv("TSG_K1_GRID")) : 0;
+  const uint64_t cap = (uint64_t)c->grid / 8 * (gmul > 0 ? gmul : 8);
+  const int grid = (int)std::min<uint64_t>((A.nitems + kBlock - 1) / kBlock, cap);
+  DevK1 d = c->k1;
+  K1Args a = A;
+  void* args[] = {&d, &a};
+  HIP_TRY(hipLaunchKernel(k1_fn(c->k1.kw_words, c->k1.lds_class, A.streams), dim3(grid), dim3(kBlock), args, 0,
+                          c->stream));
   HIP_TRY(hipGetLastError());
   return TSG_OK;
 }
@@ -987,14 +1070,14 @@ static int adapt_k1(tsg_ctx* c, uint64_t nchunks, uint64_t k1_items) {
   const uint64_t nsamp = (k1_items + step - 1) / step;
   HIP_TRY(hipMemsetAsync(c->d_hits, 0, sizeof(uint32_t) * ns, c->stream));
   K1Args A{c->d_data, c->d_off, c->d_chunk_file, c->total, nchunks, nsamp, step, c->opt.chunk_bytes,
-           c->nfiles, c->d_kw, c->d_ev, c->d_hits};
+           c->nfiles, c->d_kw, c->d_ev, c->d_hits, k1_streams(), (uint32_t)kK1Seg};
   int rc;
   if ((rc = launch_k1(c, A))) return rc;
   std::vector<uint32_t> hits(ns);
   HIP_TRY(hipMemcpyAsync(hits.data(), c->d_hits, sizeof(uint32_t) * ns, hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));
   c->adapted = true;
-  const uint64_t sample_bytes = nsamp * kStreams * c->opt.chunk_bytes;
+  const uint64_t sample_bytes = nsamp * A.streams * A.seg * c->opt.chunk_bytes;
   uint64_t total = 0;
   std::vector<uint32_t> order;
   for (uint32_t s = 0; s < ns; s++)
@@ -1004,16 +1087,16 @@ static int adapt_k1(tsg_ctx* c, uint64_t nchunks, uint64_t k1_items) {
     }
   std::sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return hits[a] > hits[b]; });
   const uint64_t budget = sample_bytes / 4096;
-  std::vector<uint8_t> hot(ns, 0);
+  std::vector<uint8_t> hot(p.kw_dfa->nstates, 0);  // automaton states that stop reporting
   std::vector<uint8_t> kw_unknown(p.n_kw, 0);
   uint32_t ev_hot = 0, nhot = 0;
-  for (uint32_t s : order) {
+  for (uint32_t s : order) {  // s: device state id
     if (total <= budget) break;
     const uint32_t* m = c->k1h.masks.data() + (size_t)c->k1h.accs[s] * mw;
     bool fallback = false;  // folding-rune literals must stay exact (they force host resolution)
     for (int k = p.fb_kw0; k < p.n_kw; k++) fallback |= (m[k / 32] >> (k % 32)) & 1;
     if (fallback) continue;
-    hot[s] = 1;
+    hot[c->k1h.order[s]] = 1;
     nhot++;
     total -= hits[s];
     for (int k = 0; k < p.n_kw; k++)
@@ -1022,10 +1105,10 @@ static int adapt_k1(tsg_ctx* c, uint64_t nchunks, uint64_t k1_items) {
   }
   c->hot_states = nhot;
   if (!nhot) return TSG_OK;
-  std::vector<uint16_t> tab = c->k1h.tab;
-  for (auto& e : tab)
-    if ((e & 0x8000u) && hot[e & 0x7FFFu]) e &= 0x7FFFu;
-  HIP_TRY(hipMemcpy((void*)c->k1.tab, tab.data(), tab.size() * sizeof(uint16_t), hipMemcpyHostToDevice));
+  int rc2;
+  if ((rc2 = k1_tables(p, hot, &c->k1h, &c->k1.start, &c->k1.acc_row))) return rc2;
+  HIP_TRY(hipMemcpy((void*)c->k1.tab, c->k1h.tab.data(), c->k1h.tab.size() * sizeof(uint16_t), hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy((void*)c->k1.accs, c->k1h.accs.data(), c->k1h.accs.size() * sizeof(uint16_t), hipMemcpyHostToDevice));
   // gates of groups with an unknown keyword open; events of hot anchor literals fire everywhere
   std::vector<uint32_t> galways = c->h_galways, gevents = c->h_gevents;
   std::vector<unsigned long long> gofbit = c->h_gofbit;
@@ -1072,8 +1155,6 @@ int tsg_ctx_create(int device, const tsg_ruleset* rs, const tsg_ctx_options* opt
   int rc;
   if ((rc = make_device_k1(p, &c->k1, &c->tables, &c->k1h))) return rc;
   HIP_TRY(hipMalloc((void**)&c->d_hits, sizeof(uint32_t) * c->k1.ns));
-  if (c->k1.lds_bytes > 64 * 1024)
-    HIP_TRY(hipFuncSetAttribute(k1_fn(W), hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->k1.lds_bytes));
   const uint32_t G = (uint32_t)p.groups.size();
   c->GW = std::max<uint32_t>(1, (G + 63) / 64);
   std::vector<uint32_t> gmask, galways, gevents;
@@ -1148,7 +1229,7 @@ int tsg_batch_upload(tsg_ctx* c, const uint8_t* data, const uint64_t* offsets, u
   if (total / chunk >= (1ull << 32) - 2) return fail(TSG_ERR_ARG, "batch too large for u32 chunk ids");
   int rc;
   // front pad: K1 warm-up reads before the first chunk; tail: whole K1 items + look-ahead
-  const size_t tail = (size_t)kStreams * chunk + kPad;
+  const size_t tail = (size_t)kK1MaxStreams * kK1Seg * chunk + kPad;
   if (c->d_data_cap < (size_t)total + kPad + tail || !c->d_data_alloc) {
     if (c->d_data_alloc) HIP_TRY(hipFree(c->d_data_alloc));
     c->d_data_alloc = nullptr;
@@ -1159,7 +1240,8 @@ int tsg_batch_upload(tsg_ctx* c, const uint8_t* data, const uint64_t* offsets, u
   if ((rc = ensure(&c->d_off, &c->d_off_cap, (size_t)nfiles + 1))) return rc;
   const uint64_t nchunks = (total + chunk - 1) / chunk;
   // K1 items are kStreams chunks: chunk-indexed arrays are padded to whole items
-  const uint64_t nchunks_pad = (nchunks + kStreams - 1) / kStreams * kStreams + 1;
+  const uint64_t k1_item_chunks = (uint64_t)kK1MaxStreams * kK1Seg;
+  const uint64_t nchunks_pad = (nchunks + k1_item_chunks - 1) / k1_item_chunks * k1_item_chunks + 1;
   if ((rc = ensure(&c->d_chunk_file, &c->d_chunk_cap, (size_t)nchunks_pad))) return rc;
   if ((rc = ensure(&c->d_ev, &c->d_ev_cap, (size_t)nchunks_pad))) return rc;
   const int W = c->rs->plan->kw_words;
@@ -1207,7 +1289,8 @@ int tsg_batch_kernels(tsg_ctx* c) {
   HIP_TRY(hipEventRecord(c->ev[1], st));
 
   // ---- K1
-  const uint64_t k1_items = (nchunks + kStreams - 1) / kStreams;
+  const uint32_t k1s = k1_streams();
+  const uint64_t k1_items = (nchunks + (uint64_t)k1s * kK1Seg - 1) / ((uint64_t)k1s * kK1Seg);
   int rc;
   const uint64_t adapt_bytes = c->opt.adapt_mib == 0xFFFFFFFFu ? ~0ull
                                : (uint64_t)(c->opt.adapt_mib ? c->opt.adapt_mib : 64) << 20;
@@ -1215,7 +1298,7 @@ int tsg_batch_kernels(tsg_ctx* c) {
     if ((rc = adapt_k1(c, nchunks, k1_items))) return rc;
   if (k1_items) {
     K1Args A{c->d_data, c->d_off, c->d_chunk_file, c->total, nchunks, k1_items, 1, chunk, F, c->d_kw, c->d_ev,
-             nullptr};
+             nullptr, k1s, (uint32_t)kK1Seg};
     if ((rc = launch_k1(c, A))) return rc;
   }
   HIP_TRY(hipEventRecord(c->ev[2], st));
