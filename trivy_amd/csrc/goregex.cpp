@@ -1049,6 +1049,11 @@ std::shared_ptr<Regexp> Regexp::Compile(const std::string& src, std::string* err
     Compiler c(p.nodes, &re->prog_);
     c.finish(root);
     re->prog_.nslots = 2 * (p.ncap + 1);
+    re->prog_.ascii.assign(re->prog_.runes.size() * 2, 0);
+    for (size_t k = 0; k < re->prog_.runes.size(); k++)
+      for (const auto& rg : re->prog_.runes[k])
+        for (int32_t c = std::max<int32_t>(rg.first, 0); c <= std::min<int32_t>(rg.second, 127); c++)
+          re->prog_.ascii[k * 2 + c / 64] |= 1ull << (c % 64);
     re->ast_ = std::make_shared<Ast>();
     re->ast_->nodes = std::move(p.nodes);
     re->ast_->root = root;
@@ -1377,6 +1382,8 @@ class Machine {
           if (runq.dense[k].second >= 0) release(runq.dense[k].second);
         cut = true;
         matched_ = true;
+      } else if (c >= 0 && c < 128 && !p_.ascii.empty()) {
+        addit = (p_.ascii[i.arg * 2 + (c >> 6)] >> (c & 63)) & 1;
       } else {
         addit = rune_in(p_.runes[i.arg], c);
       }
@@ -1395,10 +1402,28 @@ bool Regexp::Match(const uint8_t* b, size_t n) const {
   return m.run(b, n, 0, (int64_t)n);
 }
 
+// The leftmost-first match found from `pos` with whole-match positions only (2 slots: the
+// cheap pass), then, for submatches, the same match re-run anchored at its start with every
+// slot: the highest-priority thread that starts there ends at the same place, so the two
+// passes give exactly the single full pass's result.
+struct TwoPass {
+  Machine whole, sub;
+  bool submatch;
+  int nslots;
+  TwoPass(const Prog& p, bool submatch_) : whole(p, 2), sub(p, submatch_ ? p.nslots : 2), submatch(submatch_),
+                                           nslots(p.nslots) {}
+  bool run(const uint8_t* b, size_t n, int64_t pos, int64_t start_hi) {
+    if (!whole.run(b, n, pos, start_hi)) return false;
+    if (submatch && nslots > 2) sub.run(b, n, whole.matchcap()[0], whole.matchcap()[0]);
+    return true;
+  }
+  const std::vector<int64_t>& matchcap() const { return (submatch && nslots > 2) ? sub.matchcap() : whole.matchcap(); }
+};
+
 void Regexp::FindAll(const uint8_t* b, size_t n, bool submatch, std::vector<int64_t>* out,
                      size_t lo, size_t start_hi) const {
   // regexp.allMatches (regexp/regexp.go)
-  Machine m(prog_, prog_.nslots);
+  TwoPass m(prog_, submatch);
   int64_t end = (int64_t)n;
   int64_t pos = (int64_t)lo, prev_end = -1;
   int64_t hi = start_hi == SIZE_MAX ? end : (int64_t)std::min<size_t>(start_hi, n);
@@ -1429,7 +1454,7 @@ void Regexp::FindAllWindows(const uint8_t* b, size_t n, bool submatch,
   // Go's allMatches iteration, skipping the stretches in which no match can start:
   // `pos` and the previous match end carry from one window to the next, so a match
   // that runs past its window is handled exactly as the global iteration would.
-  Machine m(prog_, prog_.nslots);
+  TwoPass m(prog_, submatch);
   const int64_t end = (int64_t)n;
   int64_t pos = 0, prev_end = -1;
   for (const auto& w : iv) {

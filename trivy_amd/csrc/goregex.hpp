@@ -77,6 +77,9 @@ struct Prog {
   std::vector<Ranges> runes;
   uint32_t start = 0;
   int nslots = 2;  // 2 * (number of capture groups + 1)
+  // [runes.size() * 2]: ASCII members of each rune set as a 128-bit map (matcher fast
+  // path; filled by Regexp::Compile, empty for derived programs)
+  std::vector<uint64_t> ascii;
 };
 
 class Regexp {
