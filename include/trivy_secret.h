@@ -190,6 +190,10 @@ int tsg_regex_match(const tsg_regex* re, const uint8_t* text, size_t len);
  * Writes up to cap int64 values, returns the number of values needed (>= 0). */
 int64_t tsg_regex_find_all(const tsg_regex* re, const uint8_t* text, size_t len, int submatch,
                            int64_t* out, size_t cap);
+/* FindAll with a chosen matcher: 0 auto, 1 Pike VM only, 2 bit-state backtracker where
+ * its visited table fits (results must not depend on the choice). */
+int64_t tsg_regex_find_all_engine(const tsg_regex* re, const uint8_t* text, size_t len,
+                                  int submatch, int engine, int64_t* out, size_t cap);
 /* DFA candidate end offsets of one regex over text (all p where a match may end),
  * computed with the GPU lane algorithm (chunk bytes per lane). Returns count. */
 int64_t tsg_regex_dfa_ends(const tsg_regex* re, const uint8_t* text, size_t len, uint32_t chunk,

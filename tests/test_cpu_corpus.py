@@ -88,3 +88,15 @@ def test_fold_runes_exact_vs_oracle(builtin):
         assert canon_secret(got[i]) == want, batch.path(i)
         nf += len(want["Findings"] or [])
     assert nf > 10
+
+
+@pytest.mark.parametrize("unknown", ["key,secret,token", "api,pass,access"])
+def test_unknown_keywords_exact_gate(builtin, unknown, monkeypatch):
+    """After K1 adaptation frequent keywords are not reported; their gates are decided on
+    the host with the ASCII case-folded search (no bytes.ToLower of the file) unless the
+    file holds U+0130/U+212A.  Emulated here by clearing those keyword bits."""
+    monkeypatch.setenv("TSG_EMU_KW_UNKNOWN", unknown)
+    batch = fold_corpus(4, nbytes=1 << 20, plants=300, frac=0.2)
+    got = builtin.ScanBatch(batch, emulate_chunk=64)
+    monkeypatch.delenv("TSG_EMU_KW_UNKNOWN")
+    assert got == builtin.ScanBatch(batch, nthreads=8)

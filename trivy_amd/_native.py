@@ -90,6 +90,7 @@ SIGNATURES = [
     ("tsg_regex_num_slots", C.c_int, [_P]),
     ("tsg_regex_match", C.c_int, [_P, C.c_char_p, C.c_size_t]),
     ("tsg_regex_find_all", C.c_int64, [_P, C.c_char_p, C.c_size_t, C.c_int, _I64P, C.c_size_t]),
+    ("tsg_regex_find_all_engine", C.c_int64, [_P, C.c_char_p, C.c_size_t, C.c_int, C.c_int, _I64P, C.c_size_t]),
     ("tsg_regex_dfa_ends", C.c_int64, [_P, C.c_char_p, C.c_size_t, C.c_uint32, _I64P,
                                        C.c_size_t]),
     ("tsg_scan_batch_emulated", C.c_int, [_P, _P, _U64P, C.c_uint32, _P, _U64P, C.c_uint32,

@@ -88,6 +88,7 @@ int tsg_ruleset_compile(const tsg_rule_desc* rules, uint32_t n_rules,
         r.keywords.push_back(kw);
         go_to_lower((const uint8_t*)kw.data(), kw.size(), &low);  // strings.ToLower
         r.kw_lower.push_back(low);
+        for (unsigned char ch : low) r.kw_ascii &= ch < 0x80;
       }
       for (uint32_t k = 0; k < d.n_allow_rules; k++) {
         AllowRuleC a;
@@ -209,12 +210,27 @@ int tsg_scan_batch_emulated(const tsg_ruleset* rs, const uint8_t* data, const ui
     KernelOutput ko;
     auto t0 = std::chrono::steady_clock::now();
     emulate_kernels(*rs->plan, b, chunk, 1u << 16, &ko);
+    if (const char* u = getenv("TSG_EMU_KW_UNKNOWN")) {
+      // test hook: as after K1 adaptation, these keywords' bits are not reported and their
+      // gates are checked exactly on the host
+      const Plan& p = *rs->plan;
+      ko.kw_unknown.assign(p.n_kw, 0);
+      std::string list(u);
+      for (size_t r = 0; r < rs->rs.rules.size(); r++)
+        for (size_t j = 0; j < p.rule_kws[r].size(); j++) {
+          const std::string& kw = rs->rs.rules[r].kw_lower[j];
+          if (("," + list + ",").find("," + kw + ",") == std::string::npos) continue;
+          const uint32_t k = p.rule_kws[r][j];
+          ko.kw_unknown[k] = 1;
+          for (uint32_t f = 0; f < nfiles; f++) ko.kw[(size_t)f * p.kw_words + k / 32] &= ~(1u << (k % 32));
+        }
+    }
     auto t1 = std::chrono::steady_clock::now();
-    std::vector<FileResult> res;
+    BatchResult res;
     resolve_batch(rs->rs, *rs->plan, b, ko, hw_threads(0), &res);
     auto t2 = std::chrono::steady_clock::now();
     auto r = std::make_unique<tsg_result>();
-    serialize_results(res, &r->buf);
+    serialize_batch(res, &r->buf);
     auto t3 = std::chrono::steady_clock::now();
     if (getenv("TSG_PROF"))
       fprintf(stderr, "emulate %.1f ms resolve %.1f ms serialize %.1f ms (%zu candidates)\n",
@@ -322,6 +338,15 @@ int64_t tsg_regex_find_all(const tsg_regex* re, const uint8_t* text, size_t len,
   if (!re) return fail(TSG_ERR_ARG, "bad argument");
   std::vector<int64_t> v;
   re->re->FindAll(text, len, submatch != 0, &v);
+  if (out) std::memcpy(out, v.data(), sizeof(int64_t) * std::min(cap, v.size()));
+  return (int64_t)v.size();
+}
+
+int64_t tsg_regex_find_all_engine(const tsg_regex* re, const uint8_t* text, size_t len, int submatch,
+                                  int engine, int64_t* out, size_t cap) {
+  if (!re || engine < 0 || engine > 2) return fail(TSG_ERR_ARG, "bad argument");
+  std::vector<int64_t> v;
+  re->re->FindAll(text, len, submatch != 0, &v, 0, SIZE_MAX, engine);
   if (out) std::memcpy(out, v.data(), sizeof(int64_t) * std::min(cap, v.size()));
   return (int64_t)v.size();
 }

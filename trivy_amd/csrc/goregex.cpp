@@ -2,6 +2,7 @@
 #include "goregex.hpp"
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 
 namespace tsg {
@@ -1402,28 +1403,192 @@ bool Regexp::Match(const uint8_t* b, size_t n) const {
   return m.run(b, n, 0, (int64_t)n);
 }
 
+// regexp's bit-state backtracker (regexp/backtrack.go): depth-first in priority order, so
+// the first Match reached from a start position is that start's leftmost-first match, and a
+// (pc, pos) pair is expanded at most once per search (a pair that failed fails again from
+// any later start), which keeps the search linear in prog size x text span.  Go picks it
+// for small programs and inputs; the results equal the Pike VM's.
+class Backtracker {
+ public:
+  explicit Backtracker(const Prog& p, int nslots) : p_(p), ns_(nslots), np_(p.inst.size()) {
+    cap_.assign(ns_, -1);
+    matchcap_.assign(ns_, -1);
+  }
+  // budget for the visited bitmap (bits) above which the caller uses the Pike VM
+  static constexpr uint64_t kMaxBits = 64ull << 20;
+  bool fits(size_t n, int64_t pos) const { return (uint64_t)np_ * (uint64_t)(n - pos + 1) <= kMaxBits; }
+
+  // leftmost-first match starting in [pos, start_hi] (rune steps), as Machine::run
+  bool run(const uint8_t* b, size_t n, int64_t pos, int64_t start_hi) {
+    b_ = b;
+    n_ = (int64_t)n;
+    base_ = pos;
+    maxrow_ = -1;
+    const uint64_t bits = (uint64_t)np_ * (uint64_t)(n_ - base_ + 1);
+    if (visited_.size() * 64 < bits) visited_.resize((bits + 63) / 64, 0);
+    bool found = false;
+    std::fill(matchcap_.begin(), matchcap_.end(), -1);
+    for (int64_t s = pos; s <= n_ && s <= start_hi;) {
+      std::fill(cap_.begin(), cap_.end(), -1);
+      if (ns_ > 0) cap_[0] = s;
+      if (try_at(s)) {
+        found = true;
+        break;
+      }
+      if (s == n_) break;
+      int w;
+      decode_rune(b_, n, (size_t)s, &w);
+      s += w;
+    }
+    // clear the rows touched (only the visited span costs)
+    if (maxrow_ >= 0) {
+      const uint64_t hi = ((uint64_t)(maxrow_ + 1) * np_ + 63) / 64;
+      std::fill(visited_.begin(), visited_.begin() + std::min<uint64_t>(hi, visited_.size()), 0);
+    }
+    return found;
+  }
+  const std::vector<int64_t>& matchcap() const { return matchcap_; }
+
+ private:
+  struct Job {
+    uint32_t pc;
+    bool arg;
+    int64_t pos;
+  };
+  const Prog& p_;
+  int ns_;
+  size_t np_;
+  const uint8_t* b_ = nullptr;
+  int64_t n_ = 0, base_ = 0, maxrow_ = -1;
+  // per-thread visited bitmap, kept all-zero between runs (each run clears what it touched)
+  static std::vector<uint64_t>& visited_buf() {
+    thread_local std::vector<uint64_t> v;
+    return v;
+  }
+  std::vector<uint64_t>& visited_ = visited_buf();
+  std::vector<Job> jobs_;
+  std::vector<int64_t> cap_, matchcap_;
+
+  bool visit(uint32_t pc, int64_t pos) {
+    const int64_t row = pos - base_;
+    if (row > maxrow_) maxrow_ = row;
+    const uint64_t k = (uint64_t)row * np_ + pc;
+    uint64_t& w = visited_[k >> 6];
+    const uint64_t bit = 1ull << (k & 63);
+    if (w & bit) return false;
+    w |= bit;
+    return true;
+  }
+  int32_t before(int64_t pos) const { return pos > 0 ? (int32_t)b_[pos - 1] : kEOT; }
+  int32_t at(int64_t pos) const { return pos < n_ ? (int32_t)b_[pos] : kEOT; }
+
+  bool try_at(int64_t start) {
+    jobs_.clear();
+    jobs_.push_back({p_.start, false, start});
+    while (!jobs_.empty()) {
+      Job j = jobs_.back();
+      jobs_.pop_back();
+      uint32_t pc = j.pc;
+      int64_t pos = j.pos;
+      bool arg = j.arg;
+      if (arg) goto skip;
+    check:
+      if (!visit(pc, pos)) continue;
+    skip : {
+      const Inst& in = p_.inst[pc];
+      switch (in.op) {
+        case Op::Fail:
+          continue;
+        case Op::Alt:
+          if (arg) {
+            arg = false;
+            pc = in.arg;
+            goto check;
+          }
+          jobs_.push_back({pc, true, pos});
+          pc = in.out;
+          goto check;
+        case Op::Rune: {
+          if (pos >= n_) continue;
+          int w;
+          const int32_t c = decode_rune(b_, (size_t)n_, (size_t)pos, &w);
+          bool ok;
+          if (c >= 0 && c < 128 && !p_.ascii.empty()) ok = (p_.ascii[in.arg * 2 + (c >> 6)] >> (c & 63)) & 1;
+          else ok = rune_in(p_.runes[in.arg], c);
+          if (!ok) continue;
+          pos += w;
+          pc = in.out;
+          goto check;
+        }
+        case Op::Cap:
+          if (arg) {
+            cap_[in.arg] = pos;  // restore
+            continue;
+          }
+          if ((int)in.arg < ns_) {
+            jobs_.push_back({pc, true, cap_[in.arg]});
+            cap_[in.arg] = pos;
+          }
+          pc = in.out;
+          goto check;
+        case Op::Empty:
+          if (!empty_ok(in.arg, before(pos), at(pos))) continue;
+          pc = in.out;
+          goto check;
+        case Op::Nop:
+          pc = in.out;
+          goto check;
+        case Op::Match:
+          if (ns_ > 1) cap_[1] = pos;
+          std::copy(cap_.begin(), cap_.end(), matchcap_.begin());
+          return true;
+      }
+    }
+    }
+    return false;
+  }
+};
+
 // The leftmost-first match found from `pos` with whole-match positions only (2 slots: the
 // cheap pass), then, for submatches, the same match re-run anchored at its start with every
 // slot: the highest-priority thread that starts there ends at the same place, so the two
 // passes give exactly the single full pass's result.
 struct TwoPass {
   Machine whole, sub;
+  Backtracker bt;
   bool submatch;
   int nslots;
-  TwoPass(const Prog& p, bool submatch_) : whole(p, 2), sub(p, submatch_ ? p.nslots : 2), submatch(submatch_),
-                                           nslots(p.nslots) {}
+  int engine;    // 0 auto, 1 Pike VM only, 2 backtracker where it fits
+  int mode = 0;  // which matcher produced the last match: 0 whole, 1 sub, 2 backtracker
+  TwoPass(const Prog& p, bool submatch_, int engine_ = 0)
+      : whole(p, 2), sub(p, submatch_ ? p.nslots : 2), bt(p, submatch_ ? p.nslots : 2), submatch(submatch_),
+        nslots(p.nslots), engine(engine_) {}
   bool run(const uint8_t* b, size_t n, int64_t pos, int64_t start_hi) {
+    if (engine != 1 && bt.fits(n, pos) && !(engine == 0 && getenv_pike())) {
+      mode = 2;
+      return bt.run(b, n, pos, start_hi);
+    }
+    mode = 0;
     if (!whole.run(b, n, pos, start_hi)) return false;
-    if (submatch && nslots > 2) sub.run(b, n, whole.matchcap()[0], whole.matchcap()[0]);
+    if (submatch && nslots > 2) {
+      sub.run(b, n, whole.matchcap()[0], whole.matchcap()[0]);
+      mode = 1;
+    }
     return true;
   }
-  const std::vector<int64_t>& matchcap() const { return (submatch && nslots > 2) ? sub.matchcap() : whole.matchcap(); }
+  const std::vector<int64_t>& matchcap() const {
+    return mode == 2 ? bt.matchcap() : mode == 1 ? sub.matchcap() : whole.matchcap();
+  }
+  static bool getenv_pike() {
+    static const bool v = getenv("TSG_PIKE_ONLY") != nullptr;  // tests: the Pike VM alone
+    return v;
+  }
 };
 
 void Regexp::FindAll(const uint8_t* b, size_t n, bool submatch, std::vector<int64_t>* out,
-                     size_t lo, size_t start_hi) const {
+                     size_t lo, size_t start_hi, int engine) const {
   // regexp.allMatches (regexp/regexp.go)
-  TwoPass m(prog_, submatch);
+  TwoPass m(prog_, submatch, engine);
   int64_t end = (int64_t)n;
   int64_t pos = (int64_t)lo, prev_end = -1;
   int64_t hi = start_hi == SIZE_MAX ? end : (int64_t)std::min<size_t>(start_hi, n);

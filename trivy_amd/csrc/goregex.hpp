@@ -118,8 +118,9 @@ class Regexp {
   // iteration starts at `lo` (with the whole text as context for assertions) and only
   // matches whose start is <= start_hi are produced.  With lo = 0 and
   // start_hi = n this is exactly Go's FindAll.
+  // engine (tests): 0 auto, 1 Pike VM only, 2 bit-state backtracker where it fits
   void FindAll(const uint8_t* b, size_t n, bool submatch, std::vector<int64_t>* out,
-               size_t lo = 0, size_t start_hi = SIZE_MAX) const;
+               size_t lo = 0, size_t start_hi = SIZE_MAX, int engine = 0) const;
 
   // Go's FindAll iteration restricted to match STARTS inside the given windows
   // [lo, hi] (sorted, disjoint, lo on a rune boundary).  The iteration position and the

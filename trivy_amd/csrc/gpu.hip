@@ -1434,13 +1434,18 @@ int tsg_batch_kernels(tsg_ctx* c) {
 static std::unique_ptr<tsg_result> resolve_job(const tsg_ruleset* rs, BatchView b, const KernelOutput& ko,
                                                int nt, std::pair<double, uint64_t>* done) {
   auto t0 = std::chrono::steady_clock::now();
-  std::vector<FileResult> res;
+  BatchResult res;
   resolve_batch(rs->rs, *rs->plan, b, ko, nt, &res);
+  auto t1 = std::chrono::steady_clock::now();
   auto r = std::make_unique<tsg_result>();
-  serialize_results(res, &r->buf);
+  serialize_batch(res, &r->buf);
+  if (getenv("TSG_PROF"))
+    fprintf(stderr, "resolve_job: resolve_batch %.1f ms, serialize %.1f ms\n",
+            std::chrono::duration<double, std::milli>(t1 - t0).count(),
+            std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t1).count());
   done->first = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   done->second = 0;
-  for (const auto& fr : res) done->second += fr.status == kHasFindings;
+  for (uint8_t st : res.status) done->second += st == kHasFindings;
   return r;
 }
 

@@ -8,6 +8,7 @@
 #include <atomic>
 #include <map>
 #include <thread>
+#include <x86intrin.h>
 
 namespace tsg {
 
@@ -465,20 +466,22 @@ bool run_segment(const DFA& d, const uint8_t* data, uint64_t fs, uint64_t fe, ui
 }  // namespace
 
 void resolve_batch(const Ruleset& rs, const Plan& plan, const BatchView& b,
-                   const KernelOutput& ko, int nthreads, std::vector<FileResult>* out) {
+                   const KernelOutput& ko, int nthreads, BatchResult* out) {
   const uint32_t F = b.nfiles;
   const size_t R = rs.rules.size();
-  out->assign(F, FileResult{});
-  // bucket candidates by file, sorted by (rule, end)
-  std::vector<Candidate> cand = ko.cand;
-  std::sort(cand.begin(), cand.end(), [](const Candidate& x, const Candidate& y) {
-    if (x.file != y.file) return x.file < y.file;
-    if (x.rule != y.rule) return x.rule < y.rule;
-    return x.end < y.end;
-  });
+  const uint64_t t_ser0 = __rdtsc();
+  // bucket candidates by file (counting sort), then sort each file's few by (rule, end)
   std::vector<uint32_t> first(F + 1, 0);
-  for (const auto& c : cand) first[c.file + 1]++;
+  for (const auto& c : ko.cand) first[c.file + 1]++;
   for (uint32_t f = 0; f < F; f++) first[f + 1] += first[f];
+  std::vector<Candidate> cand(ko.cand.size());
+  {
+    std::vector<uint32_t> fill(first.begin(), first.end() - 1);
+    for (const auto& c : ko.cand) cand[fill[c.file]++] = c;
+  }
+  auto by_rule_end = [](const Candidate& x, const Candidate& y) {
+    return x.rule != y.rule ? x.rule < y.rule : x.end < y.end;
+  };
 
   std::vector<uint32_t> hostonly;
   for (size_t r = 0; r < R; r++)
@@ -490,27 +493,62 @@ void resolve_batch(const Ruleset& rs, const Plan& plan, const BatchView& b,
       kw_has_k[r] |= k.find('k') != std::string::npos;
     }
 
+  // Files that need the exact scan: candidates, empty files, kernel overflow, folding
+  // runes, or a gated rule without a GPU program.  The others only need Global.AllowPath.
+  out->status.assign(F, kNoFindings);
+  out->slot.assign(F, UINT32_MAX);
+  uint32_t nslots = 0;
+  for (uint32_t f = 0; f < F; f++) {
+    bool need = first[f] != first[f + 1] || b.offsets[f + 1] == b.offsets[f] ||
+                (!ko.overflow.empty() && ko.overflow[f]) || !hostonly.empty();
+    if (!need) {
+      const uint32_t* kw = ko.kw.data() + (size_t)f * plan.kw_words;
+      for (int k = plan.fb_kw0; k < plan.n_kw && !need; k++) need = (kw[k / 32] >> (k % 32)) & 1;
+    }
+    if (need) out->slot[f] = nslots++;
+  }
+  out->res.assign(nslots, FileResult{});
+
   static const bool prof = getenv("TSG_PROF") != nullptr;
-  std::atomic<int64_t> t_plain{0}, t_cand{0}, n_cand{0}, n_whole{0}, t_fast{0}, n_fast{0};
+  if (prof) fprintf(stderr, "resolve: serial setup %.1f Mcyc\n", (__rdtsc() - t_ser0) / 1e6);
+  // TSG_PROF: per-thread cycle counters (no shared atomics in the loop)
+  struct alignas(64) Slot {
+    uint64_t cyc[4] = {0, 0, 0, 0};  // fast files, candidate files, other files, count cand
+  };
+  static std::atomic<int> next_tid{0};
+  std::vector<Slot> slots(prof ? 256 : 0);
+  std::atomic<int64_t> n_whole{0};
+  const uint64_t t_par0 = prof ? __rdtsc() : 0;
   parallel_for(F, nthreads, [&](size_t fi) {
-    const auto tp0 = prof ? std::chrono::steady_clock::now() : std::chrono::steady_clock::time_point();
+    thread_local int tid = next_tid++ & 255;
+    const uint64_t tp0 = prof ? __rdtsc() : 0;
     struct Tm {
       bool on;
-      std::chrono::steady_clock::time_point t0;
-      std::atomic<int64_t>* acc;
+      uint64_t t0;
+      uint64_t* acc;
       ~Tm() {
-        if (on) *acc += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
+        if (on) *acc += __rdtsc() - t0;
       }
     };
     const uint32_t f = (uint32_t)fi;
     const bool has_cand = first[f] != first[f + 1];
-    Tm tm{prof, tp0, has_cand ? &t_cand : &t_plain};
-    if (prof && has_cand) n_cand++;
+    Tm tm{prof, tp0, prof ? &slots[tid].cyc[has_cand ? 1 : 2] : nullptr};
+    if (prof && has_cand) slots[tid].cyc[3]++;
     const char* pp = b.paths + b.path_offsets[f];
     const size_t pn = b.path_offsets[f + 1] - b.path_offsets[f];
     const uint8_t* content = b.data + b.offsets[f];
     const int64_t n = (int64_t)(b.offsets[f + 1] - b.offsets[f]);
-    FileResult& res = (*out)[f];
+    if (out->slot[f] == UINT32_MAX) {  // no match possible
+      if (prof) tm.acc = &slots[tid].cyc[0];
+      out->status[f] = path_allowed(rs, &plan, pp, pn) ? kPathAllowed : kNoFindings;
+      return;
+    }
+    FileResult& res = out->res[out->slot[f]];
+    struct SetStatus {
+      FileResult& r;
+      uint8_t& s;
+      ~SetStatus() { s = r.status; }
+    } set_status{res, out->status[f]};
     if (n == 0) {  // the kernels skip empty files; only empty matches are possible
       scan_file(rs, std::string(pp, pn), content, 0, nullptr, &res);
       return;
@@ -544,10 +582,6 @@ void resolve_batch(const Ruleset& rs, const Plan& plan, const BatchView& b,
     for (uint32_t r : hostonly)
       if (kw_state(r) != 0) any_host = true;
     if (first[f] == first[f + 1] && !ovf && !any_host && !fbbits) {  // no match possible
-      if (prof) {
-        n_fast++;
-        tm.acc = &t_fast;
-      }
       res.status = path_allowed(rs, &plan, pp, pn) ? kPathAllowed : kNoFindings;
       return;
     }
@@ -592,6 +626,7 @@ void resolve_batch(const Ruleset& rs, const Plan& plan, const BatchView& b,
       }
       w.iv.resize(o);
     };
+    std::sort(cand.begin() + first[f], cand.begin() + first[f + 1], by_rule_end);
     for (uint32_t k = first[f]; k < first[f + 1];) {
       uint32_t r = cand[k].rule;
       uint32_t e = k;
@@ -650,6 +685,7 @@ void resolve_batch(const Ruleset& rs, const Plan& plan, const BatchView& b,
     gate.kw_state = kws.data();
     gate.windows = wptr.data();
     gate.path_allowed = path_allowed(rs, &plan, pp, pn) ? 1 : 0;
+    gate.ascii_fold_exact = (fbbits & 3) == 0;
     if (prof)
       for (size_t r = 0; r < R; r++)
         if (wptr[r] && (wptr[r]->whole || (!wptr[r]->iv.empty() && wptr[r]->iv[0].first == 0))) {
@@ -661,9 +697,14 @@ void resolve_batch(const Ruleset& rs, const Plan& plan, const BatchView& b,
         }
     scan_file(rs, path, content, (size_t)n, &gate, &res);
   });
-  if (prof)
-    fprintf(stderr, "resolve: fast files %.1f ms cpu (%ld), other plain files %.1f ms cpu, candidate files %.1f ms cpu (%ld files, %ld whole-prefix rule scans)\n",
-            t_fast / 1e6, (long)n_fast, t_plain / 1e6, t_cand / 1e6, (long)n_cand, (long)n_whole);
+  if (prof) {
+    uint64_t t[4] = {0, 0, 0, 0};
+    for (const auto& sl : slots)
+      for (int k = 0; k < 4; k++) t[k] += sl.cyc[k];
+    fprintf(stderr, "resolve: parallel part %.1f Mcyc wall; thread Mcyc: no-candidate files %.1f, candidate files %.1f "
+            "(%lu files, %ld whole-prefix rule scans), other %.1f\n",
+            (__rdtsc() - t_par0) / 1e6, t[0] / 1e6, t[1] / 1e6, (unsigned long)t[3], (long)n_whole, t[2] / 1e6);
+  }
 }
 
 // ------------------------------------------------------------------ kernel emulation

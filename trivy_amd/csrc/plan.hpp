@@ -114,7 +114,7 @@ struct BatchView {
 
 // Host resolution: exact findings for every file of the batch.
 void resolve_batch(const Ruleset& rs, const Plan& plan, const BatchView& b,
-                   const KernelOutput& ko, int nthreads, std::vector<FileResult>* out);
+                   const KernelOutput& ko, int nthreads, BatchResult* out);
 
 // Exact CPU path for a whole batch (no GPU).
 void scan_batch_cpu(const Ruleset& rs, const BatchView& b, int nthreads,

@@ -2,11 +2,13 @@
 #include "scanner.hpp"
 
 #include <algorithm>
+#include <map>
 #include <atomic>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <x86intrin.h>
+#include <emmintrin.h>
 
 namespace tsg {
 
@@ -30,6 +32,40 @@ bool match_keywords(const RuleC& r, const std::string& lowered) {
   if (r.kw_lower.empty()) return true;  // scanner.go:165-167
   for (const auto& kw : r.kw_lower)
     if (lowered.find(kw) != std::string::npos) return true;
+  return false;
+}
+
+// bytes.Contains(bytes.ToLower(s), kw) for an ASCII lowercase keyword kw, valid when s holds
+// neither U+0130 nor U+212A: those are the only runes bytes.ToLower turns into ASCII, so
+// the ASCII bytes of the lowered text are exactly the ASCII bytes of s, lowercased.
+bool contains_fold_ascii(const uint8_t* s, size_t n, const std::string& kw) {
+  const size_t m = kw.size();
+  if (m == 0) return true;
+  if (m > n) return false;
+  const uint8_t c0 = (uint8_t)kw[0];
+  const uint8_t u0 = (c0 >= 'a' && c0 <= 'z') ? (uint8_t)(c0 - 32) : c0;
+  const __m128i v0 = _mm_set1_epi8((char)c0), v1 = _mm_set1_epi8((char)u0);
+  auto rest = [&](size_t i) {
+    for (size_t j = 1; j < m; j++) {
+      uint8_t x = s[i + j];
+      if (x >= 'A' && x <= 'Z') x |= 0x20;
+      if (x != (uint8_t)kw[j]) return false;
+    }
+    return true;
+  };
+  const size_t last = n - m;  // last possible start
+  size_t i = 0;
+  for (; i + 16 <= last + 1; i += 16) {
+    const __m128i b = _mm_loadu_si128((const __m128i*)(s + i));
+    uint32_t bits = (uint32_t)_mm_movemask_epi8(_mm_or_si128(_mm_cmpeq_epi8(b, v0), _mm_cmpeq_epi8(b, v1)));
+    while (bits) {
+      const size_t k = i + (size_t)__builtin_ctz(bits);
+      bits &= bits - 1;
+      if (rest(k)) return true;
+    }
+  }
+  for (; i <= last; i++)
+    if ((s[i] == c0 || s[i] == u0) && rest(i)) return true;
   return false;
 }
 
@@ -342,12 +378,21 @@ void find_location(int64_t start, int64_t end, const std::string& content,
 
 // TSG_PROF: per-phase cycle counters of scan_file (printed at exit)
 static std::atomic<uint64_t> g_ph[8];
+static std::atomic<uint64_t> g_rule_cyc[2048], g_rule_calls[2048], g_rule_bytes[2048];
+static std::string g_rule_name[2048];  // rule ids seen by the profiler (names outlive rule sets)
 static const bool g_prof = getenv("TSG_PROF") != nullptr;
 struct PhDump {
   ~PhDump() {
     if (!g_prof) return;
     const char* nm[8] = {"allowpath", "rulegates", "lower", "findall", "allowmatch", "locate", "total", "nfiles"};
     for (int i = 0; i < 8; i++) fprintf(stderr, "scan_file %-10s %.2f Mcyc\n", nm[i], g_ph[i] / 1e6);
+    std::vector<std::pair<uint64_t, size_t>> v;
+    for (size_t r = 0; r < 2048; r++)
+      if (g_rule_calls[r]) v.push_back({g_rule_cyc[r].load(), r});
+    std::sort(v.rbegin(), v.rend());
+    for (size_t i = 0; i < v.size() && i < 12; i++)
+      fprintf(stderr, "  findall %-32s %8.2f Mcyc %7lu calls %10lu window bytes\n", g_rule_name[v[i].second].c_str(),
+              v[i].first / 1e6, (unsigned long)g_rule_calls[v[i].second].load(), (unsigned long)g_rule_bytes[v[i].second].load());
   }
 };
 static PhDump g_phdump;
@@ -375,6 +420,7 @@ void scan_file(const Ruleset& rs, const std::string& path, const uint8_t* conten
   ph.lap(0);
   std::string lowered;
   bool have_lowered = false;
+  std::map<std::string, int8_t> kwcache;  // keyword -> 1 present, -1 absent
   Blocks global{content, n, &rs.exclude};
   std::vector<std::pair<uint32_t, Loc>> matched;
   std::string censored;
@@ -394,7 +440,18 @@ void scan_file(const Ruleset& rs, const std::string& path, const uint8_t* conten
     if (r.path && !r.path->Match((const uint8_t*)path.data(), path.size())) continue;
     if (allow_path(r.allow, path)) continue;
     ph.lap(1);
-    if (!gate || gate->kw_state[ri] == 2) {
+    if (gate && gate->kw_state[ri] == 2 && gate->ascii_fold_exact && r.kw_ascii) {
+      // exact keyword gate without lowering the file (per-keyword results cached)
+      bool hit = r.kw_lower.empty();
+      for (size_t k = 0; k < r.kw_lower.size() && !hit; k++) {
+        const std::string& kw = r.kw_lower[k];
+        int8_t& c = kwcache[kw];
+        if (c == 0) c = contains_fold_ascii(content, n, kw) ? 1 : -1;
+        hit = c > 0;
+      }
+      ph.lap(2);
+      if (!hit) continue;
+    } else if (!gate || gate->kw_state[ri] == 2) {
       if (!have_lowered) {
         go_to_lower(content, n, &lowered);
         have_lowered = true;
@@ -410,10 +467,20 @@ void scan_file(const Ruleset& rs, const std::string& path, const uint8_t* conten
     const bool sub = !r.secret_group_name.empty();
     const int ns = sub ? r.regex->NumSlots() : 2;
     idx.clear();
+    const uint64_t tf0 = g_prof ? __rdtsc() : 0;
     if (!win || win->whole) {
       r.regex->FindAll(content, n, sub, &idx);
     } else {
       r.regex->FindAllWindows(content, n, sub, win->iv, &idx);
+    }
+    if (g_prof && ri < 2048) {
+      if (g_rule_calls[ri] == 0 && g_rule_name[ri].empty()) g_rule_name[ri] = r.id;  // racy, names only
+      g_rule_cyc[ri] += __rdtsc() - tf0;
+      g_rule_calls[ri]++;
+      uint64_t wb = 0;
+      if (!win || win->whole) wb = n;
+      else for (const auto& w : win->iv) wb += (uint64_t)(w.second - w.first + 1);
+      g_rule_bytes[ri] += wb;
     }
     ph.lap(3);
     std::vector<Loc> locs;
@@ -467,6 +534,66 @@ static void put_u32(std::string* o, uint32_t v) { o->append((const char*)&v, 4);
 static void put_bytes(std::string* o, const std::string& s) {
   put_u32(o, (uint32_t)s.size());
   o->append(s);
+}
+
+namespace {
+struct Writer {
+  char* p;
+  void u8(uint8_t v) { *p++ = (char)v; }
+  void u32(uint32_t v) {
+    std::memcpy(p, &v, 4);
+    p += 4;
+  }
+  void bytes(const std::string& s) {
+    u32((uint32_t)s.size());
+    std::memcpy(p, s.data(), s.size());
+    p += s.size();
+  }
+};
+size_t findings_bytes(const FileResult& r) {
+  size_t n = 0;
+  for (const auto& f : r.findings) {
+    n += 16 + f.match.size() + 4;
+    for (const auto& ln : f.lines) n += 9 + ln.content.size();
+  }
+  return n;
+}
+void write_findings(Writer& w, const FileResult& r) {
+  for (const auto& f : r.findings) {
+    w.u32(f.rule);
+    w.u32((uint32_t)f.start_line);
+    w.u32((uint32_t)f.end_line);
+    w.bytes(f.match);
+    w.u32((uint32_t)f.lines.size());
+    for (const auto& ln : f.lines) {
+      w.u32((uint32_t)ln.number);
+      w.u8(ln.flags);
+      w.bytes(ln.content);
+    }
+  }
+}
+}  // namespace
+
+void serialize_batch(const BatchResult& br, std::string* out) {
+  const size_t F = br.status.size();
+  size_t total = 8 + F * 5;
+  for (const auto& r : br.res) total += findings_bytes(r);
+  out->resize(total);
+  Writer w{&(*out)[0]};
+  w.u32(0x31475354u);  // "TSG1"
+  w.u32((uint32_t)F);
+  for (size_t f = 0; f < F; f++) {
+    const uint32_t k = br.slot[f];
+    if (k == UINT32_MAX) {
+      w.u8(br.status[f]);
+      w.u32(0);
+    } else {
+      const FileResult& r = br.res[k];
+      w.u8(r.status);
+      w.u32((uint32_t)r.findings.size());
+      write_findings(w, r);
+    }
+  }
 }
 
 void serialize_results(const std::vector<FileResult>& res, std::string* out) {

@@ -36,6 +36,7 @@ struct RuleC {
   std::string secret_group_name;
   // derived
   std::vector<std::string> kw_lower;  // strings.ToLower(kw)
+  bool kw_ascii = true;               // every kw_lower is ASCII
   std::vector<int> group_idx;         // i where SubexpNames()[i] == secret_group_name
 };
 
@@ -68,6 +69,14 @@ struct FileResult {
   std::vector<Finding> findings;
 };
 
+// Results of a batch resolved from kernel output: most files need no exact scan, so only
+// those that did hold a FileResult.
+struct BatchResult {
+  std::vector<uint8_t> status;   // [nfiles] FileStatus
+  std::vector<uint32_t> slot;    // [nfiles] index into res, or UINT32_MAX
+  std::vector<FileResult> res;
+};
+
 // Where the exact matcher must look for one rule in one file.
 struct RuleWindows {
   bool whole = false;                               // run FindAll over the whole file
@@ -82,7 +91,12 @@ struct FileGate {
   const RuleWindows* const* windows = nullptr;
   // Global.AllowPath(path) already evaluated by the caller: 0 no, 1 yes, -1 not known
   int8_t path_allowed = -1;
+  // the file holds neither U+0130 nor U+212A: an ASCII keyword is in bytes.ToLower(content)
+  // iff it is in content under ASCII case folding (contains_fold_ascii)
+  bool ascii_fold_exact = false;
 };
+
+bool contains_fold_ascii(const uint8_t* s, size_t n, const std::string& kw);
 
 // Exact Scan of one file (scanner.go:341-416).
 void scan_file(const Ruleset& rs, const std::string& path, const uint8_t* content, size_t n,
@@ -92,6 +106,7 @@ void scan_file(const Ruleset& rs, const std::string& path, const uint8_t* conten
 bool match_keywords(const RuleC& r, const std::string& lowered);
 
 // Serialization of results (format documented in include/trivy_secret.h).
+void serialize_batch(const BatchResult& br, std::string* out);
 void serialize_results(const std::vector<FileResult>& res, std::string* out);
 
 }  // namespace tsg
