@@ -1416,7 +1416,12 @@ class Backtracker {
   }
   // budget for the visited bitmap (bits) above which the caller uses the Pike VM
   static constexpr uint64_t kMaxBits = 64ull << 20;
-  bool fits(size_t n, int64_t pos) const { return (uint64_t)np_ * (uint64_t)(n - pos + 1) <= kMaxBits; }
+  // Go uses it only for programs of at most 500 instructions (backtrack.go maxBacktrackProg):
+  // larger ones (long counted repetitions) visit too many (pc, pos) pairs
+  static constexpr size_t kMaxProg = 500;
+  bool fits(size_t n, int64_t pos) const {
+    return np_ <= kMaxProg && (uint64_t)np_ * (uint64_t)(n - pos + 1) <= kMaxBits;
+  }
 
   // leftmost-first match starting in [pos, start_hi] (rune steps), as Machine::run
   bool run(const uint8_t* b, size_t n, int64_t pos, int64_t start_hi) {

@@ -397,8 +397,10 @@ struct ItemArgs {
   const uint64_t* off;
   const uint32_t* chunk_file;
   const uint32_t* ev;
+  const uint32_t* evlist;           // chunks with event bits (ev_compact_kernel)
+  const uint32_t* nev;              // [1] length of evlist
   const unsigned long long* ggate;  // [F * GW]
-  const unsigned long long* gofbit;  // [32 * GW] groups listening to event bit b
+  const unsigned long long* gofbit;  // [32 * GW] groups listening to event bit b; bit 31 = every chunk
   const uint32_t* gevents;          // [G]
   const uint32_t* gback;            // [G] chunks (kMaxBack + 1 = whole file)
   uint64_t nchunks;
@@ -410,42 +412,68 @@ struct ItemArgs {
   uint2* items;
 };
 
-// one thread per chunk c: for every file overlapping c and every gated group with an
-// event in [c, c + back] (inside the file): item (file, c) of the group.  visit(f, g).
+// chunks whose K1 event word is not empty, appended to `list` (one atomic per wave)
+__global__ void __launch_bounds__(kBlock) ev_compact_kernel(const uint32_t* __restrict__ ev, uint64_t nchunks,
+                                                            uint32_t* __restrict__ list, uint32_t* __restrict__ count) {
+  const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool has = c < nchunks && (ev[c] & ~kEvAlways) != 0;
+  const unsigned long long m = __ballot(has);
+  const uint32_t lane = threadIdx.x & 63;
+  uint32_t base = 0;
+  if (lane == 0 && m) base = atomicAdd(count, (uint32_t)__popcll(m));
+  base = __shfl(base, 0);
+  if (has) list[base + __popcll(m & ((1ull << lane) - 1))] = (uint32_t)c;
+}
+
+// Items of the K2 list: (file f, chunk c) for group g iff g is gated for f and a chunk in
+// [c, c + back_g] of f carries one of g's event bits (groups listening to every chunk:
+// all chunks of f).  Work is generated from the sparse event chunks: event chunk e emits
+// c in (previous event chunk of g, e] within back_g chunks before e and inside f, so every
+// item comes from the first event chunk at or after it, exactly once.  Threads
+// [0, nev) take event chunks, [nev, nev + F) take the files of every-chunk groups.
+// visit(f, g, c_lo, c_hi): items c_lo..c_hi.
 template <class V>
-__device__ __forceinline__ void chunk_items(const ItemArgs& A, uint64_t c, V visit) {
-  if (c < A.nchunks) {
-    const uint64_t cs = c * A.chunk, ce = cs + A.chunk;
-    for (uint32_t f = A.chunk_file[c]; f < A.F && A.off[f] < ce; f++) {
+__device__ __forceinline__ void gen_items(const ItemArgs& A, uint64_t t, V visit) {
+  const uint32_t nev = *A.nev;
+  const uint32_t C = A.chunk;
+  if (t < nev) {
+    const uint64_t e = A.evlist[t];
+    const uint32_t evb = A.ev[e] & ~kEvAlways;
+    const uint64_t ce = (e + 1) * C;
+    for (uint32_t f = A.chunk_file[e]; f < A.F && A.off[f] < ce; f++) {
       const uint64_t fs = A.off[f], fe = A.off[f + 1];
       if (fe == fs) continue;
-      const uint64_t cf1 = (fe - 1) / A.chunk;
-      // OR of the events of chunks [c, c + k] inside the file, k = 0..maxback
-      uint32_t win[kMaxBack + 1];
-      uint32_t acc = 0;
-#pragma unroll
-      for (uint32_t k = 0; k <= kMaxBack; k++) {
-        if (k <= A.maxback && c + k <= cf1) acc |= A.ev[c + k];
-        win[k] = acc;
-      }
-      const uint32_t all = acc | kEvAlways;
+      const uint64_t fc0 = fs / C;
       for (uint32_t w = 0; w < A.GW; w++) {
         unsigned long long cand = 0;
-        for (uint32_t b = 0; b < 32; b++)
-          if ((all >> b) & 1) cand |= A.gofbit[b * A.GW + w];
-        cand &= A.ggate[(size_t)f * A.GW + w];
+        for (uint32_t bits = evb; bits; bits &= bits - 1) cand |= A.gofbit[__builtin_ctz(bits) * A.GW + w];
+        cand &= A.ggate[(size_t)f * A.GW + w] & ~A.gofbit[31 * A.GW + w];
         while (cand) {
           const uint32_t g = w * 64 + __builtin_ctzll(cand);
           cand &= cand - 1;
           const uint32_t back = A.gback[g];
-          uint32_t ew = kEvAlways;
-#pragma unroll
-          for (uint32_t k = 0; k <= kMaxBack; k++)
-            if (k == back) ew |= win[k];
-          if (back > kMaxBack) ew = ~0u;  // window longer than kMaxBack chunks: every chunk
-          if (!(ew & A.gevents[g])) continue;
-          visit(f, g);
+          uint64_t lo = e > fc0 + back ? e - back : fc0;
+          for (uint64_t q = e; q > lo;) {
+            q--;
+            if (A.ev[q] & A.gevents[g]) {
+              lo = q + 1;
+              break;
+            }
+          }
+          visit(f, g, lo, e);
         }
+      }
+    }
+  } else if (t < (uint64_t)nev + A.F) {
+    const uint32_t f = (uint32_t)(t - nev);
+    const uint64_t fs = A.off[f], fe = A.off[f + 1];
+    if (fe == fs) return;
+    for (uint32_t w = 0; w < A.GW; w++) {
+      unsigned long long cand = A.ggate[(size_t)f * A.GW + w] & A.gofbit[31 * A.GW + w];
+      while (cand) {
+        const uint32_t g = w * 64 + __builtin_ctzll(cand);
+        cand &= cand - 1;
+        visit(f, g, fs / C, (fe - 1) / C);
       }
     }
   }
@@ -457,8 +485,8 @@ __global__ void __launch_bounds__(kBlock) items_count_kernel(ItemArgs A) {
   uint32_t* s_count = (uint32_t*)smem;
   for (uint32_t g = threadIdx.x; g < A.G; g += blockDim.x) s_count[g] = 0;
   __syncthreads();
-  const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  chunk_items(A, c, [&](uint32_t, uint32_t g) { atomicAdd(&s_count[g], 1u); });
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  gen_items(A, t, [&](uint32_t, uint32_t g, uint64_t lo, uint64_t hi) { atomicAdd(&s_count[g], (uint32_t)(hi - lo + 1)); });
   __syncthreads();
   for (uint32_t g = threadIdx.x; g < A.G; g += blockDim.x)
     if (s_count[g]) atomicAdd(&A.count[g], s_count[g]);
@@ -472,9 +500,9 @@ __global__ void __launch_bounds__(kBlock) items_emit_kernel(ItemArgs A) {
   uint32_t* s_base = s_count + A.G;
   for (uint32_t g = threadIdx.x; g < A.G; g += blockDim.x) s_count[g] = 0;
   __syncthreads();
-  const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  chunk_items(A, c, [&](uint32_t, uint32_t g) {
-    if (A.listed[g]) atomicAdd(&s_count[g], 1u);
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  gen_items(A, t, [&](uint32_t, uint32_t g, uint64_t lo, uint64_t hi) {
+    if (A.listed[g]) atomicAdd(&s_count[g], (uint32_t)(hi - lo + 1));
   });
   __syncthreads();
   for (uint32_t g = threadIdx.x; g < A.G; g += blockDim.x) {
@@ -482,8 +510,11 @@ __global__ void __launch_bounds__(kBlock) items_emit_kernel(ItemArgs A) {
     s_count[g] = 0;
   }
   __syncthreads();
-  chunk_items(A, c, [&](uint32_t f, uint32_t g) {
-    if (A.listed[g]) A.items[s_base[g] + atomicAdd(&s_count[g], 1u)] = make_uint2(f, (uint32_t)c);
+  gen_items(A, t, [&](uint32_t f, uint32_t g, uint64_t lo, uint64_t hi) {
+    if (!A.listed[g]) return;
+    const uint32_t n = (uint32_t)(hi - lo + 1);
+    uint32_t at = s_base[g] + atomicAdd(&s_count[g], n);
+    for (uint64_t c = lo; c <= hi; c++) A.items[at++] = make_uint2(f, (uint32_t)c);
   });
 }
 
@@ -949,6 +980,8 @@ struct tsg_ctx {
   size_t d_chunk_cap = 0;
   uint32_t* d_ev = nullptr;
   size_t d_ev_cap = 0;
+  uint32_t* d_evlist = nullptr;  // chunks with events
+  size_t d_evlist_cap = 0;
   uint32_t* d_kw = nullptr;
   size_t d_kw_cap = 0;
   unsigned long long* d_ggate = nullptr;
@@ -988,6 +1021,7 @@ struct tsg_ctx {
     (void)hipFree(d_off);
     (void)hipFree(d_chunk_file);
     (void)hipFree(d_ev);
+    (void)hipFree(d_evlist);
     (void)hipFree(d_kw);
     (void)hipFree(d_ggate);
     (void)hipFree(d_ovf);
@@ -1244,6 +1278,7 @@ int tsg_batch_upload(tsg_ctx* c, const uint8_t* data, const uint64_t* offsets, u
   const uint64_t nchunks_pad = (nchunks + k1_item_chunks - 1) / k1_item_chunks * k1_item_chunks + 1;
   if ((rc = ensure(&c->d_chunk_file, &c->d_chunk_cap, (size_t)nchunks_pad))) return rc;
   if ((rc = ensure(&c->d_ev, &c->d_ev_cap, (size_t)nchunks_pad))) return rc;
+  if ((rc = ensure(&c->d_evlist, &c->d_evlist_cap, (size_t)nchunks_pad))) return rc;
   const int W = c->rs->plan->kw_words;
   if ((rc = ensure(&c->d_kw, &c->d_kw_cap, (size_t)nfiles * W + 1))) return rc;
   if ((rc = ensure(&c->d_ggate, &c->d_ggate_cap, (size_t)nfiles * c->GW + 1))) return rc;
@@ -1322,10 +1357,18 @@ int tsg_batch_kernels(tsg_ctx* c) {
   IA.count = c->d_gcount;
   IA.cursor = c->d_cursor;
   IA.listed = c->d_listed;
-  const int igrid = (int)((nchunks + kBlock - 1) / kBlock);
+  IA.evlist = c->d_evlist;
+  IA.nev = c->d_count + 1;
+  int igrid = 0;
   if (F && G && nchunks) {
     ggate_kernel<<<(F + 255) / 256, 256, 0, st>>>(c->d_kw, F, W, c->d_gmask, c->d_galways, G, c->GW, c->d_ggate);
     HIP_TRY(hipGetLastError());
+    ev_compact_kernel<<<(uint32_t)((nchunks + kBlock - 1) / kBlock), kBlock, 0, st>>>(c->d_ev, nchunks, c->d_evlist,
+                                                                                      c->d_count + 1);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpyAsync(c->h_count + 1, c->d_count + 1, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    igrid = (int)(((uint64_t)c->h_count[1] + F + kBlock - 1) / kBlock);
     hipLaunchKernelGGL(items_count_kernel, dim3(igrid), dim3(kBlock), G * sizeof(uint32_t) + 16, st, IA);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipMemcpyAsync(gcount.data(), c->d_gcount, sizeof(uint32_t) * G, hipMemcpyDeviceToHost, st));
