@@ -412,17 +412,43 @@ struct ItemArgs {
   uint2* items;
 };
 
-// chunks whose K1 event word is not empty, appended to `list` (one atomic per wave)
+// chunks whose K1 event word is not empty, compacted into `list`: each block takes a
+// contiguous range, counts it, reserves its output with ONE global atomic, then writes its
+// chunks in order (wave ballots + an LDS prefix over the block's waves)
 __global__ void __launch_bounds__(kBlock) ev_compact_kernel(const uint32_t* __restrict__ ev, uint64_t nchunks,
                                                             uint32_t* __restrict__ list, uint32_t* __restrict__ count) {
-  const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const bool has = c < nchunks && (ev[c] & ~kEvAlways) != 0;
-  const unsigned long long m = __ballot(has);
-  const uint32_t lane = threadIdx.x & 63;
-  uint32_t base = 0;
-  if (lane == 0 && m) base = atomicAdd(count, (uint32_t)__popcll(m));
-  base = __shfl(base, 0);
-  if (has) list[base + __popcll(m & ((1ull << lane) - 1))] = (uint32_t)c;
+  __shared__ uint32_t s_wave[kBlock / 64];
+  __shared__ uint32_t s_base;
+  const uint64_t per = (nchunks + gridDim.x - 1) / gridDim.x;
+  const uint64_t c0 = (uint64_t)blockIdx.x * per, c1 = min(nchunks, c0 + per);
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  uint32_t n = 0;
+  for (uint64_t c = c0 + threadIdx.x; c < c1; c += blockDim.x) n += (ev[c] & ~kEvAlways) != 0;
+  for (int o = 32; o > 0; o >>= 1) n += __shfl_xor(n, o);
+  if (lane == 0) s_wave[wave] = n;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t tot = 0;
+    for (uint32_t w = 0; w < kBlock / 64; w++) tot += s_wave[w];
+    s_base = tot ? atomicAdd(count, tot) : 0;
+  }
+  __syncthreads();
+  uint32_t at = s_base;
+  for (uint64_t cb = c0; cb < c1; cb += blockDim.x) {
+    const uint64_t c = cb + threadIdx.x;
+    const bool has = c < c1 && (ev[c] & ~kEvAlways) != 0;
+    const unsigned long long m = __ballot(has);
+    __syncthreads();  // s_wave reuse
+    if (lane == 0) s_wave[wave] = (uint32_t)__popcll(m);
+    __syncthreads();
+    uint32_t before = 0, tot = 0;
+    for (uint32_t w = 0; w < kBlock / 64; w++) {
+      before += w < wave ? s_wave[w] : 0;
+      tot += s_wave[w];
+    }
+    if (has) list[at + before + __popcll(m & ((1ull << lane) - 1))] = (uint32_t)c;
+    at += tot;
+  }
 }
 
 // Items of the K2 list: (file f, chunk c) for group g iff g is gated for f and a chunk in
@@ -1363,8 +1389,8 @@ int tsg_batch_kernels(tsg_ctx* c) {
   if (F && G && nchunks) {
     ggate_kernel<<<(F + 255) / 256, 256, 0, st>>>(c->d_kw, F, W, c->d_gmask, c->d_galways, G, c->GW, c->d_ggate);
     HIP_TRY(hipGetLastError());
-    ev_compact_kernel<<<(uint32_t)((nchunks + kBlock - 1) / kBlock), kBlock, 0, st>>>(c->d_ev, nchunks, c->d_evlist,
-                                                                                      c->d_count + 1);
+    const uint32_t cgrid = (uint32_t)std::min<uint64_t>((nchunks + kBlock - 1) / kBlock, (uint64_t)c->grid);
+    ev_compact_kernel<<<cgrid, kBlock, 0, st>>>(c->d_ev, nchunks, c->d_evlist, c->d_count + 1);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipMemcpyAsync(c->h_count + 1, c->d_count + 1, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
