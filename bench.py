@@ -33,6 +33,8 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+# FETCH_SIZE of the same command (rocprofv3 --pmc FETCH_SIZE), committed under profiles/
+PMC_FETCH_CSV = os.path.join(ROOT, "profiles", "r01", "bench_10gib_pmc_fetch_v5.csv")
 
 
 def _dist():
@@ -94,6 +96,17 @@ def cpu_baseline(batch, budget_s=12.0):
     return {"value": done / dt / 1e9, "unit": "GB/s", "cores": 1, "kind": "port",
             "sample": "first %d files (%.2f MB) of the same corpus, oracle/secret.py "
                       "(Go regexp restated over Python `regex`), %.1f s" % (nfiles, done / 1e6, dt)}
+
+
+def _traffic(dom, gb):
+    """HBM bytes per launch of the dominant kernel from the committed PMC pass (same
+    10 GiB workload; null for other sizes or when the file is absent)."""
+    if abs(gb - 10.0) > 1e-9 or not os.path.exists(PMC_FETCH_CSV):
+        return None
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    from pmc_traffic import traffic
+    t = traffic(PMC_FETCH_CSV, "k1_kernel" if dom.startswith("K1") else "k2_")
+    return None if t is None else int(t)
 
 
 def cpu_native(sc, batch, max_bytes=256 << 20, nthreads=16):
@@ -200,7 +213,9 @@ def main():
                    "rules": 83, "parallelism": "file-sharded x%d, no collective" % world},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None},
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": _traffic(dom, args.gb),
+                     "algorithmic_bytes": info["bytes"],
+                     "traffic_source": os.path.relpath(PMC_FETCH_CSV, ROOT)},
         "breakdown_ms": {"k1": round(k1_ms, 3), "gate": round(acc["gate"] / args.steps, 3),
                          "k2": round(k2_ms, 3),
                          "resolve": round(res / args.steps, 3), "aux": round(st["aux_ms"], 3),
