@@ -100,3 +100,22 @@ def test_unknown_keywords_exact_gate(builtin, unknown, monkeypatch):
     got = builtin.ScanBatch(batch, emulate_chunk=64)
     monkeypatch.delenv("TSG_EMU_KW_UNKNOWN")
     assert got == builtin.ScanBatch(batch, nthreads=8)
+
+
+def test_k1_keyword_bits_exact_across_file_boundaries(builtin):
+    """K1 runs the batch as one byte stream; its keyword bits must still equal each file
+    scanned on its own (Rule.MatchKeywords, scanner.go:164-176, is per file).  Tiny files
+    are cut out of keyword text so keywords straddle every kind of file boundary."""
+    rng = np.random.default_rng(77)
+    text = b"key sk account ghp_ AKIA secret token xoxb- glpat- private key \xc4\xb0\xe2\x84\xaa\xc5\xbf "
+    args = []
+    for i in range(400):
+        a = int(rng.integers(0, len(text)))
+        n = int(rng.integers(0, 24))
+        args.append(S.ScanArgs("f/%d" % i, (text * 2)[a:a + n]))
+    batch = S.Batch.from_args(args)
+    kw, _ = builtin.k1_reference(batch, 64)
+    for i, a in enumerate(args):
+        one, _ = builtin.k1_reference(S.Batch.from_args([a]), 64)
+        assert np.array_equal(kw[i], one[0]), i
+    assert kw.any()

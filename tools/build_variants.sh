@@ -16,5 +16,8 @@ for v in "$@"; do
     nolds) build $v -DK1_EXP_NO_CLS -DK1_EXP_NO_TAB ;;
     coal) build $v -DK1_EXP_COAL ;;
     coalnolds) build $v -DK1_EXP_COAL -DK1_EXP_NO_CLS -DK1_EXP_NO_TAB ;;
+    noruns) build $v -DK1_EXP_NO_RUNS ;;
+    coalnoruns) build $v -DK1_EXP_COAL -DK1_EXP_NO_RUNS ;;
+    nocls) build $v -DK1_EXP_NO_CLS ;;
   esac
 done

@@ -87,6 +87,8 @@ struct DevK1 {
   uint32_t nc, ns, nmasks, mw, kw_words, start, warm, kU, kD;  // start: row; kD = threshold << 8
   uint32_t acc_row;
   uint32_t lds_class;  // index into kK1Lds
+  const uint16_t* kw_len;  // [kw_words * 32] byte length of each keyword (rare path)
+  uint32_t kw_maxlen;      // longest keyword: an occurrence ending this far into a file fits
 };
 
 struct DevCand {
@@ -142,12 +144,13 @@ struct K1Args {
   uint32_t seg;      // consecutive chunks per chain
 };
 
-// one chain = one chunk: automaton row, run counters, the file the chain is in and the
-// keyword bits already sent for it (so each bit costs one atomic per chain and file)
-template <int KWW>
+// one chain = one segment of consecutive chunks: automaton row, run counters, the running
+// maximum of the counters and the event bits of the current chunk.  Chains do not track
+// files: the automaton and the counters run over the batch as one byte stream (a chunk's
+// events are then a superset of its files' own, see k1_reference), and the rare accept
+// path finds the file of each keyword occurrence and keeps it only if it lies inside it.
 struct K1Chain {
-  uint32_t s, cnt, mx, evl, f;
-  uint64_t fe;
+  uint32_t s, cnt, mx, evl;
 };
 
 template <int KWW>
@@ -159,65 +162,50 @@ struct K1Lane {
   const uint16_t* s_accs;
   const uint32_t* s_masks;
 
-  __device__ __forceinline__ void reset(K1Chain<KWW>& c) {
-    c.s = d.start;
-    c.cnt = 0;
-  }
-  // byte p lies past the chain's file: move to the file containing p
-  __device__ __forceinline__ void next_file(K1Chain<KWW>& c, uint64_t p) {
-    do {
-      c.f++;
-    } while (c.f < A.nfiles && A.off[c.f + 1] <= p);
-    c.fe = c.f < A.nfiles ? A.off[c.f + 1] : ~0ull;
-    reset(c);
-  }
   // m's low byte is the byte's class * 2: the entry's byte offset is 2 * row + m[7:0]
   __device__ __forceinline__ uint32_t next(uint32_t s, uint32_t m) const {
     return *(const uint16_t*)((const uint8_t*)s_tab + (s + s + (m & 0xFFu)));
   }
-  // arrival in reporting row r: keyword bits of the chain's file, event bits of its chunk
-  __device__ __forceinline__ void accept(K1Chain<KWW>& c, uint32_t r) {
+  // arrival in reporting row r with batch byte q: keyword bits of q's file (each keyword
+  // only if it starts inside that file), event bits of the chain's chunk
+  __device__ __forceinline__ void accept(K1Chain& c, uint32_t r, uint64_t q) {
     const uint32_t id = r / d.nc;
     if (A.hits) atomicAdd(&A.hits[id], 1u);
     const uint32_t* m = s_masks + (size_t)s_accs[id] * d.mw;
-    if (c.f < A.nfiles) {
-      uint32_t* kwf = A.kw + (size_t)c.f * d.kw_words;
-      for (uint32_t w = 0; w < d.kw_words; w++)
-        if (m[w]) atomicOr(&kwf[w], m[w]);
-    }
     c.evl |= m[d.kw_words];
+    if (q >= A.total) return;
+    uint32_t f = A.chunk_file[q / A.chunk];  // file holding the chunk's first byte
+    while (A.off[f + 1] <= q) f++;
+    const uint64_t avail = q - A.off[f] + 1;  // bytes of f up to and including q
+    uint32_t* kwf = A.kw + (size_t)f * d.kw_words;
+    for (uint32_t w = 0; w < d.kw_words; w++) {
+      uint32_t bits = m[w];
+      if (!bits) continue;
+      if (avail < d.kw_maxlen) {
+        for (uint32_t t = bits; t; t &= t - 1) {
+          const uint32_t k = __builtin_ctz(t);
+          if (d.kw_len[w * 32 + k] > avail) bits &= ~(1u << k);
+        }
+        if (!bits) continue;
+      }
+      atomicOr(&kwf[w], bits);
+    }
   }
   __device__ __forceinline__ uint32_t run_bits(uint32_t mx) const {
     return ((mx >> 16) >= d.kU ? kEvRunU : 0u) | ((mx & 0xFFFFu) >= d.kD ? kEvRunD : 0u);
   }
-  __device__ __forceinline__ void replay16(K1Chain<KWW>& c, uint32_t s, const uint4 v) {
+  // the word at batch byte p again, byte by byte from row s, reporting every arrival
+  __device__ __forceinline__ void replay16(K1Chain& c, uint32_t s, const uint4 v, uint64_t p) {
 #pragma unroll 1
     for (uint32_t k = 0; k < 16; k++) {
       s = next(s, s_cls[byte_of(v, k)]);
-      if (s >= d.acc_row) accept(c, s);
+      if (s >= d.acc_row) accept(c, s, p + k);
     }
   }
-  // one chain, 16 bytes at p: file boundaries inside (or bytes below lo skipped: warm-up)
-  // (positions are signed: the warm-up of the first chunk starts before byte 0)
-  __device__ __forceinline__ void slow16(K1Chain<KWW>& c, const uint4 v, int64_t p, int64_t lo, bool record) {
-#pragma unroll 1
-    for (uint32_t k = 0; k < 16; k++) {
-      const int64_t q = p + k;
-      if (q < lo) continue;
-      if ((uint64_t)q >= c.fe) next_file(c, (uint64_t)q);
-      const uint32_t m = s_cls[byte_of(v, k)];
-      c.s = next(c.s, m);
-      c.cnt = run_step(c.cnt, m);
-      if (record) {
-        c.mx = run_max(c.mx, c.cnt);
-        if (c.s >= d.acc_row) accept(c, c.s);
-      }
-    }
-  }
-  // NS chains, 16 bytes each, all inside their files: interleaved byte by byte; a word
-  // in which a chain reached a reporting row is replayed on the rare path
+  // NS chains, 16 bytes each, interleaved byte by byte; a word in which a chain reached a
+  // reporting row is replayed on the rare path.  pos[i]: batch byte of chain i's word.
   template <int NS>
-  __device__ __forceinline__ void fast16(K1Chain<KWW> (&c)[NS], const uint4 (&v)[NS]) {
+  __device__ __forceinline__ void fast16(K1Chain (&c)[NS], const uint4 (&v)[NS], const uint64_t (&pos)[NS]) {
     uint32_t s0[NS], top[NS];
 #pragma unroll
     for (int i = 0; i < NS; i++) {
@@ -246,7 +234,7 @@ struct K1Lane {
       }
 #pragma unroll
     for (int i = 0; i < NS; i++)
-      if (__builtin_expect(top[i] >= d.acc_row, 0)) replay16(c[i], s0[i], v[i]);
+      if (__builtin_expect(top[i] >= d.acc_row, 0)) replay16(c[i], s0[i], v[i], pos[i]);
   }
 
   // item = NS segments of A.seg consecutive chunks from a; chain i walks segment i (its
@@ -258,46 +246,28 @@ struct K1Lane {
     const uint32_t C = A.chunk;
     const uint64_t L = (uint64_t)C * A.seg;  // segment bytes
     const uint64_t c0 = a / C;
-    K1Chain<KWW> c[NS];
-    uint64_t lo[NS];
+    K1Chain c[NS];
 #pragma unroll
     for (int i = 0; i < NS; i++) {
-      const uint64_t Ai = a + (uint64_t)i * L;
-      if (Ai < A.total) {
-        c[i].f = A.chunk_file[c0 + (uint64_t)i * A.seg];
-        lo[i] = A.off[c[i].f];
-        c[i].fe = A.off[c[i].f + 1];
-      } else {
-        c[i].f = A.nfiles;
-        lo[i] = Ai;
-        c[i].fe = ~0ull;
-      }
-      reset(c[i]);
+      c[i].s = d.start;
+      c[i].cnt = 0;
       c[i].mx = 0;
       c[i].evl = 0;
     }
-    // warm-up: the bytes before each segment that belong to the segment's first file
-    bool slow = false;
-#pragma unroll
-    for (int i = 0; i < NS; i++) slow |= (int64_t)lo[i] > (int64_t)(a + (uint64_t)i * L) - (int64_t)d.warm;
+    // warm-up: the d.warm bytes before each segment (the front pad before byte 0), with
+    // no reporting: afterwards row and counters equal those of the one-stream run
     for (uint32_t j = 0; j < d.warm; j += 16) {
       uint4 v[NS];
 #pragma unroll
       for (int i = 0; i < NS; i++) v[i] = *(const uint4*)(data + a + (uint64_t)i * L - d.warm + j);
-      if (!slow) {
 #pragma unroll
-        for (int k = 0; k < 16; k++)
+      for (int k = 0; k < 16; k++)
 #pragma unroll
-          for (int i = 0; i < NS; i++) {
-            const uint32_t m = s_cls[byte_of(v[i], k)];
-            c[i].s = next(c[i].s, m);
-            c[i].cnt = run_step(c[i].cnt, m);
-          }
-      } else {
-#pragma unroll
-        for (int i = 0; i < NS; i++)
-          slow16(c[i], v[i], (int64_t)(a + (uint64_t)i * L) - (int64_t)d.warm + j, (int64_t)lo[i], false);
-      }
+        for (int i = 0; i < NS; i++) {
+          const uint32_t m = s_cls[byte_of(v[i], k)];
+          c[i].s = next(c[i].s, m);
+          c[i].cnt = run_step(c[i].cnt, m);
+        }
     }
     // Four words in flight per chain, each register set consumed in place (the loop body
     // is unrolled four times): a set is refilled right after its word is stepped, so a
@@ -305,15 +275,10 @@ struct K1Lane {
     uint32_t jc = 0;   // offset inside the current chunk
     uint64_t ci = c0;  // chunk index of chain 0
     auto word = [&](uint64_t j, const uint4 (&v)[NS]) {
-      bool sl = false;
+      uint64_t pos[NS];
 #pragma unroll
-      for (int i = 0; i < NS; i++) sl |= c[i].fe < a + (uint64_t)i * L + j + 16;
-      if (__builtin_expect(!sl, 1)) {
-        fast16<NS>(c, v);
-      } else {
-#pragma unroll
-        for (int i = 0; i < NS; i++) slow16(c[i], v[i], (int64_t)(a + (uint64_t)i * L + j), 0, true);
-      }
+      for (int i = 0; i < NS; i++) pos[i] = a + (uint64_t)i * L + j;
+      fast16<NS>(c, v, pos);
       jc += 16;
       if (jc == C) {  // chunk end (uniform across the lane's chains): its event bits
 #pragma unroll
@@ -602,7 +567,7 @@ struct Lane {
     return s_tab[s * d.nc + s_cls[byte]];
   }
 
-  __device__ __noinline__ void replay16(uint32_t s, const uint4 v, uint64_t p) {
+  __device__ __forceinline__ void replay16(uint32_t s, const uint4 v, uint64_t p) {
 #pragma unroll 1
     for (uint32_t k = 0; k < 16; k++) s = step(s, byte_of(v, k), p + k);
   }
@@ -950,6 +915,13 @@ static int make_device_k1(const Plan& p, DevK1* out, std::vector<void*>* allocs,
   v.warm = (uint32_t)p.warm;
   v.kU = (uint32_t)p.run_k[0];
   v.kD = (uint32_t)p.run_k[1] << 8;
+  std::vector<uint16_t> kwlen((size_t)W * 32, 0);
+  v.kw_maxlen = 1;
+  for (int k = 0; k < p.n_kw; k++) {
+    kwlen[k] = p.kw_len[k];
+    v.kw_maxlen = std::max<uint32_t>(v.kw_maxlen, p.kw_len[k]);
+  }
+  if ((rc = upload_vec(kwlen, &v.kw_len, allocs))) return rc;
   host->masks = masks;
   const uint32_t need = (uint32_t)(host->tab.size() * 2) + 1024;
   v.lds_class = 3;

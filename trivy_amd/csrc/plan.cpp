@@ -153,6 +153,7 @@ std::unique_ptr<Plan> build_plan(const Ruleset& rs, const PlanOptions& opt, std:
   kws.push_back("\xc5\xbf");      // U+017F, (?i)s folds to it
   p->n_kw = (int)kws.size();
   p->kw_words = (p->n_kw + 31) / 32;
+  for (const auto& k : kws) p->kw_len.push_back((uint16_t)std::min<size_t>(k.size(), 0xFFFF));
 
   // ---- per rule: anchor event and GPU program
   DFAOptions one;
@@ -718,28 +719,28 @@ void k1_reference(const Plan& plan, const BatchView& bv, uint32_t chunk, std::ve
   const int W = plan.kw_words;
   kw->assign((size_t)F * W, 0);
   ev->assign((total + chunk - 1) / chunk, 0);
-  for (uint32_t f = 0; f < F; f++) {
-    const uint64_t fs = bv.offsets[f], fe = bv.offsets[f + 1];
-    uint32_t s = d.start[kCtxBOT];
-    uint32_t cu = 0, cd = 0;
-    for (uint64_t p = fs; p < fe; p++) {
-      const uint8_t c = bv.data[p];
-      s = d.next[(size_t)s * nc + d.cls[c]];
-      uint32_t e = 0;
-      // arrival in state s: the literals its match set holds end with byte p
-      const uint32_t mi = d.eot_acc[s];
-      if (mi) {
-        const auto& m = d.masks[mi];
-        for (int k = 0; k < plan.n_kw; k++)
-          if ((m[k / 64] >> (k % 64)) & 1) (*kw)[(size_t)f * W + k / 32] |= 1u << (k % 32);
-        e |= plan.kw_mask_events[mi];
-      }
-      cu = (plan.run_cls[c] & 1) ? cu + 1 : 0;
-      cd = (plan.run_cls[c] & 2) ? cd + 1 : 0;
-      if ((int)cu >= plan.run_k[0]) e |= kEvRunU;
-      if ((int)cd >= plan.run_k[1]) e |= kEvRunD;
-      (*ev)[p / chunk] |= e;
+  uint32_t s = d.start[kCtxBOT];
+  uint32_t cu = 0, cd = 0, f = 0;
+  for (uint64_t p = 0; p < total; p++) {
+    while (bv.offsets[f + 1] <= p) f++;  // the file holding byte p (skips empty files)
+    const uint8_t c = bv.data[p];
+    s = d.next[(size_t)s * nc + d.cls[c]];
+    uint32_t e = 0;
+    // arrival in state s: the literals its match set holds end with byte p
+    const uint32_t mi = d.eot_acc[s];
+    if (mi) {
+      const auto& m = d.masks[mi];
+      const uint64_t avail = p - bv.offsets[f] + 1;
+      for (int k = 0; k < plan.n_kw; k++)
+        if (((m[k / 64] >> (k % 64)) & 1) && plan.kw_len[k] <= avail)
+          (*kw)[(size_t)f * W + k / 32] |= 1u << (k % 32);
+      e |= plan.kw_mask_events[mi];
     }
+    cu = (plan.run_cls[c] & 1) ? cu + 1 : 0;
+    cd = (plan.run_cls[c] & 2) ? cd + 1 : 0;
+    if ((int)cu >= plan.run_k[0]) e |= kEvRunU;
+    if ((int)cd >= plan.run_k[1]) e |= kEvRunD;
+    (*ev)[p / chunk] |= e;
   }
 }
 

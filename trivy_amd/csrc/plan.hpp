@@ -51,6 +51,7 @@ struct Plan {
   int fb_kw0 = 0;      // first fallback pseudo keyword id
   std::vector<uint32_t> kw_mask_events;
   std::vector<uint32_t> lit_event;     // [n_lit] event bits of each literal
+  std::vector<uint16_t> kw_len;        // [n_kw] byte length of each keyword literal
   // run classes for kEvRunU / kEvRunD: byte -> membership bit 0 (U) / 1 (D)
   uint8_t run_cls[256] = {0};
   int run_k[2] = {32, 12};
@@ -128,6 +129,10 @@ void emulate_kernels(const Plan& plan, const BatchView& b, uint32_t chunk, uint3
 
 // K1 semantics shared by the HIP kernel and the emulation: keyword bits of every file
 // [nfiles * kw_words] and event bits of every chunk c = bytes [c*chunk, (c+1)*chunk).
+// The automaton and the run counters run over the batch as ONE byte stream (they are not
+// reset at file boundaries), so a chunk's event bits are a superset of its files' own.
+// Keyword bits stay exact: an occurrence counts for file f only when the whole keyword
+// lies inside f (its length is checked against the bytes of f before its last byte).
 void k1_reference(const Plan& plan, const BatchView& b, uint32_t chunk,
                   std::vector<uint32_t>* kw, std::vector<uint32_t>* ev);
 
