@@ -230,7 +230,7 @@ int tsg_scan_batch_emulated(const tsg_ruleset* rs, const uint8_t* data, const ui
     resolve_batch(rs->rs, *rs->plan, b, ko, hw_threads(0), &res);
     auto t2 = std::chrono::steady_clock::now();
     auto r = std::make_unique<tsg_result>();
-    serialize_batch(res, &r->buf);
+    serialize_batch(res, &r->buf, hw_threads(0));
     auto t3 = std::chrono::steady_clock::now();
     if (getenv("TSG_PROF"))
       fprintf(stderr, "emulate %.1f ms resolve %.1f ms serialize %.1f ms (%zu candidates)\n",

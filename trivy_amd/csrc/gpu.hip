@@ -116,6 +116,41 @@ __global__ void chunk_file_kernel(const uint64_t* __restrict__ off, uint32_t nfi
   for (uint64_t c = c0; c < c1; c++) chunk_file[c] = f;
 }
 
+// ---------------------------------------------------------------- Global.AllowPath
+// One thread per file runs the allow-path DFA of the rule set over its path (the host's
+// path_allowed, plan.cpp): 1 = some global allow-path regexp matches, 0 = none, 2 = the
+// path holds a non-ASCII byte (the DFA is exact on ASCII paths only; the host decides).
+struct DevPathDFA {
+  const uint32_t* next;  // [ns * nc]
+  const uint32_t* acc;   // [ns * nc] accept-mask index of the transition (0 = none)
+  const uint32_t* eot;   // [ns] accept at end of text
+  const uint8_t* cls;    // [256]
+  uint32_t nc, start;
+};
+
+__global__ void path_allow_kernel(DevPathDFA d, const uint8_t* __restrict__ paths,
+                                  const uint64_t* __restrict__ poff, uint32_t nfiles, uint8_t* __restrict__ out) {
+  const uint32_t f = blockIdx.x * blockDim.x + threadIdx.x;
+  if (f >= nfiles) return;
+  const uint64_t a = poff[f], b = poff[f + 1];
+  bool ascii = true;
+  for (uint64_t p = a; p < b; p++) ascii &= paths[p] < 0x80;
+  if (!ascii) {
+    out[f] = 2;
+    return;
+  }
+  uint32_t s = d.start;
+  for (uint64_t p = a; p < b; p++) {
+    const uint32_t e = s * d.nc + d.cls[paths[p]];
+    if (d.acc[e]) {
+      out[f] = 1;
+      return;
+    }
+    s = d.next[e];
+  }
+  out[f] = d.eot[s] ? 1 : 0;
+}
+
 // ---------------------------------------------------------------- K1
 typedef unsigned short us2 __attribute__((ext_vector_type(2)));
 
@@ -149,6 +184,43 @@ struct K1Args {
 // files: the automaton and the counters run over the batch as one byte stream (a chunk's
 // events are then a superset of its files' own, see k1_reference), and the rare accept
 // path finds the file of each keyword occurrence and keeps it only if it lies inside it.
+// Quad transpose (K1 loads): the 4 lanes of a quad load 64 contiguous bytes of ONE
+// stream per instruction (lane q gets its word q), so a wave instruction touches 16
+// 64-byte segments instead of 64 scattered 16-byte words.  After loads for the 4 streams
+// of the quad, lane q holds word q of every stream; two DPP butterfly stages (across
+// lane^1, then lane^2) leave lane q with the 4 words of its own stream.
+__device__ __forceinline__ uint32_t dpp_xor1(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
+}
+__device__ __forceinline__ uint32_t dpp_xor2(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, false);  // quad_perm [2,3,0,1]
+}
+// a[t] = word q of stream t  ->  a[w] = word w of stream q   (q = lane & 3)
+__device__ __forceinline__ void quad_transpose(uint32_t (&a)[4], bool b0, bool b1) {
+#pragma unroll
+  for (int p = 0; p < 4; p += 2) {
+    const uint32_t r = dpp_xor1(b0 ? a[p] : a[p + 1]);
+    if (b0) a[p] = r;
+    else a[p + 1] = r;
+  }
+#pragma unroll
+  for (int p = 0; p < 2; p++) {
+    const uint32_t r = dpp_xor2(b1 ? a[p] : a[p + 2]);
+    if (b1) a[p] = r;
+    else a[p + 2] = r;
+  }
+}
+__device__ __forceinline__ void quad_transpose4(uint4 (&v)[4], bool b0, bool b1) {
+  uint32_t x[4] = {v[0].x, v[1].x, v[2].x, v[3].x}, y[4] = {v[0].y, v[1].y, v[2].y, v[3].y};
+  uint32_t z[4] = {v[0].z, v[1].z, v[2].z, v[3].z}, w[4] = {v[0].w, v[1].w, v[2].w, v[3].w};
+  quad_transpose(x, b0, b1);
+  quad_transpose(y, b0, b1);
+  quad_transpose(z, b0, b1);
+  quad_transpose(w, b0, b1);
+#pragma unroll
+  for (int t = 0; t < 4; t++) v[t] = make_uint4(x[t], y[t], z[t], w[t]);
+}
+
 struct K1Chain {
   uint32_t s, cnt, mx, evl;
 };
@@ -170,7 +242,7 @@ struct K1Lane {
   // only if it starts inside that file), event bits of the chain's chunk
   __device__ __forceinline__ void accept(K1Chain& c, uint32_t r, uint64_t q) {
     const uint32_t id = r / d.nc;
-    if (A.hits) atomicAdd(&A.hits[id], 1u);
+    if (A.hits && q < A.total) atomicAdd(&A.hits[id], 1u);
     const uint32_t* m = s_masks + (size_t)s_accs[id] * d.mw;
     c.evl |= m[d.kw_words];
     if (q >= A.total) return;
@@ -311,6 +383,97 @@ struct K1Lane {
       load(b3, j + 112);
     }
   }
+
+  // The same walk with quad-transposed loads (see quad_transpose): quad lane t walks item
+  // it0 + t of ib bytes (a ghost lane past the last item repeats it0 and stores nothing).
+  template <int NS>
+  __device__ __forceinline__ void item_quad(uint64_t it0, uint64_t ib, uint32_t q) {
+    const uint8_t* data = A.data;
+    const uint32_t C = A.chunk;
+    const uint64_t L = (uint64_t)C * A.seg;  // segment bytes
+    const bool ghost = it0 + q >= A.nitems;
+    const uint64_t a = (ghost ? it0 : it0 + q) * ib;
+    const uint64_t c0 = a / C;
+    const bool b0 = q & 1, b1 = (q >> 1) & 1;
+    K1Chain c[NS];
+#pragma unroll
+    for (int i = 0; i < NS; i++) {
+      c[i].s = d.start;
+      c[i].cnt = 0;
+      c[i].mx = 0;
+      c[i].evl = 0;
+    }
+    for (uint32_t j = 0; j < d.warm; j += 16) {
+      uint4 v[NS];
+#pragma unroll
+      for (int i = 0; i < NS; i++) v[i] = *(const uint4*)(data + a + (uint64_t)i * L - d.warm + j);
+#pragma unroll
+      for (int k = 0; k < 16; k++)
+#pragma unroll
+        for (int i = 0; i < NS; i++) {
+          const uint32_t m = s_cls[byte_of(v[i], k)];
+          c[i].s = next(c[i].s, m);
+          c[i].cnt = run_step(c[i].cnt, m);
+        }
+    }
+    const uint8_t* src[4];  // word q of quad lane t's item
+#pragma unroll
+    for (int t = 0; t < 4; t++) src[t] = data + (it0 + t < A.nitems ? it0 + t : it0) * ib + 16u * q;
+    uint32_t jc = 0;
+    uint64_t ci = c0;
+    auto word = [&](uint64_t jw, const uint4 (&v)[NS]) __attribute__((always_inline)) {
+      uint64_t pos[NS];
+#pragma unroll
+      for (int i = 0; i < NS; i++) pos[i] = ghost ? A.total : a + (uint64_t)i * L + jw;
+      fast16<NS>(c, v, pos);
+      jc += 16;
+      if (jc == C) {
+        if (!ghost)
+#pragma unroll
+          for (int i = 0; i < NS; i++) A.ev[ci + (uint64_t)i * A.seg] = c[i].evl | run_bits(c[i].mx);
+#pragma unroll
+        for (int i = 0; i < NS; i++) {
+          c[i].evl = 0;
+          c[i].mx = 0;
+        }
+        jc = 0;
+        ci++;
+      }
+    };
+    // 64 bytes of every chain at j: transpose, then the 4 words in order (each word's
+    // registers picked with constant indices so the arrays stay in VGPRs)
+    auto block = [&](uint64_t j, uint4 (&r)[NS][4]) __attribute__((always_inline)) {
+#pragma unroll
+      for (int i = 0; i < NS; i++) quad_transpose4(r[i], b0, b1);
+      uint4 v0[NS], v1[NS], v2[NS], v3[NS];
+#pragma unroll
+      for (int i = 0; i < NS; i++) {
+        v0[i] = r[i][0];
+        v1[i] = r[i][1];
+        v2[i] = r[i][2];
+        v3[i] = r[i][3];
+      }
+      word(j, v0);
+      word(j + 16, v1);
+      word(j + 32, v2);
+      word(j + 48, v3);
+    };
+    auto load = [&](uint4 (&r)[NS][4], uint64_t j) __attribute__((always_inline)) {
+#pragma unroll
+      for (int i = 0; i < NS; i++)
+#pragma unroll
+        for (int t = 0; t < 4; t++) r[i][t] = *(const uint4*)(src[t] + ((uint64_t)i * L + j));
+    };
+    uint4 r0[NS][4], r1[NS][4];
+    load(r0, 0);
+    load(r1, 64);
+    for (uint64_t j = 0; j < L; j += 128) {  // L is a multiple of 128
+      block(j, r0);
+      load(r0, j + 128);
+      block(j + 64, r1);
+      load(r1, j + 192);
+    }
+  }
 };
 
 // K1 LDS image (static, so every table address is a constant): the 256 class words at 0
@@ -330,8 +493,16 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2, 
   __syncthreads();
   K1Lane<KWW> L{d, A, s_tab, s_cls, d.accs, d.masks};
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+#ifdef K1_NO_QUAD
   for (uint64_t it = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; it < A.nitems; it += stride)
     L.template item<NS>(it * A.item_step * NS * A.seg * A.chunk);
+#else
+  // quads walk 4 consecutive items together (uniform trip count inside a quad)
+  const uint32_t q = threadIdx.x & 3;
+  const uint64_t ib = (uint64_t)A.item_step * NS * A.seg * A.chunk;
+  for (uint64_t it0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) & ~3ull; it0 < A.nitems; it0 += stride)
+    L.template item_quad<NS>(it0, ib, q);
+#endif
 }
 
 // ---------------------------------------------------------------- gate + items
@@ -955,6 +1126,14 @@ struct tsg_ctx {
   std::vector<unsigned long long> h_gofbit;
   std::vector<DevDFA> groups;
   DevDFA* d_groups = nullptr;       // [G] (list kernel)
+  DevPathDFA pathdfa{};
+  bool has_pathdfa = false;
+  uint8_t* d_paths = nullptr;       // the batch's paths
+  size_t d_paths_cap = 0;
+  uint64_t* d_poff = nullptr;
+  size_t d_poff_cap = 0;
+  uint8_t* d_pathok = nullptr;      // [F] path_allow_kernel output
+  size_t d_pathok_cap = 0;
   uint32_t* d_gmask = nullptr;      // [G * W]
   uint32_t* d_galways = nullptr;    // [G]
   uint32_t* d_gevents = nullptr;    // [G]
@@ -1031,6 +1210,9 @@ struct tsg_ctx {
     (void)hipFree(d_listed);
     (void)hipFree(d_blkmap);
     (void)hipFree(d_items);
+    (void)hipFree(d_paths);
+    (void)hipFree(d_poff);
+    (void)hipFree(d_pathok);
     if (h_count) hipHostFree(h_count);
     for (auto& e : ev)
       if (e) (void)hipEventDestroy(e);
@@ -1066,14 +1248,15 @@ static const void* k1_fn_ns(uint32_t kw_words, uint32_t lds_class) {
   }
 }
 
-// independent K1 chains per lane: 4, or kK1MaxStreams with TSG_K1_NS=8 (measurements)
+// independent K1 chains per lane: 2 (quad-transposed loads keep two 64-byte blocks per
+// chain in registers), or 4 with TSG_K1_NS=4 (measurements)
 static uint32_t k1_streams() {
   const char* e = getenv("TSG_K1_NS");
-  return (e && atoi(e) == kK1MaxStreams) ? (uint32_t)kK1MaxStreams : 4u;
+  return (e && atoi(e) == 4) ? 4u : 2u;
 }
 
 static const void* k1_fn(uint32_t kw_words, uint32_t lds_class, uint32_t ns) {
-  return ns == 4 ? k1_fn_ns<4>(kw_words, lds_class) : k1_fn_ns<kK1MaxStreams>(kw_words, lds_class);
+  return ns == 2 ? k1_fn_ns<2>(kw_words, lds_class) : k1_fn_ns<4>(kw_words, lds_class);
 }
 
 static int launch_k1(tsg_ctx* c, const K1Args& A) {
@@ -1187,6 +1370,21 @@ int tsg_ctx_create(int device, const tsg_ruleset* rs, const tsg_ctx_options* opt
   int rc;
   if ((rc = make_device_k1(p, &c->k1, &c->tables, &c->k1h))) return rc;
   HIP_TRY(hipMalloc((void**)&c->d_hits, sizeof(uint32_t) * c->k1.ns));
+  if (const DFA* pd = p.allow_path_dfa.get()) {
+    const uint32_t* t = nullptr;
+    if ((rc = upload_vec(pd->next, &t, &c->tables))) return rc;
+    c->pathdfa.next = t;
+    if ((rc = upload_vec(pd->acc, &t, &c->tables))) return rc;
+    c->pathdfa.acc = t;
+    if ((rc = upload_vec(pd->eot_acc, &t, &c->tables))) return rc;
+    c->pathdfa.eot = t;
+    const uint8_t* cl = nullptr;
+    if ((rc = upload_vec(std::vector<uint8_t>(pd->cls, pd->cls + 256), &cl, &c->tables))) return rc;
+    c->pathdfa.cls = cl;
+    c->pathdfa.nc = (uint32_t)pd->nclasses;
+    c->pathdfa.start = pd->start[kCtxBOT];
+    c->has_pathdfa = true;
+  }
   const uint32_t G = (uint32_t)p.groups.size();
   c->GW = std::max<uint32_t>(1, (G + 63) / 64);
   std::vector<uint32_t> gmask, galways, gevents;
@@ -1285,6 +1483,15 @@ int tsg_batch_upload(tsg_ctx* c, const uint8_t* data, const uint64_t* offsets, u
   if (total) HIP_TRY(hipMemcpyAsync(c->d_data, data, total, hipMemcpyHostToDevice, c->stream));
   HIP_TRY(hipMemsetAsync(c->d_data + total, 0, tail, c->stream));
   HIP_TRY(hipMemcpyAsync(c->d_off, offsets, sizeof(uint64_t) * (nfiles + 1), hipMemcpyHostToDevice, c->stream));
+  if (c->has_pathdfa && nfiles) {
+    const uint64_t pbytes = path_offsets[nfiles];
+    if ((rc = ensure(&c->d_paths, &c->d_paths_cap, (size_t)pbytes + 1))) return rc;
+    if ((rc = ensure(&c->d_poff, &c->d_poff_cap, (size_t)nfiles + 1))) return rc;
+    if ((rc = ensure(&c->d_pathok, &c->d_pathok_cap, (size_t)nfiles))) return rc;
+    if (pbytes) HIP_TRY(hipMemcpyAsync(c->d_paths, paths, pbytes, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(c->d_poff, path_offsets, sizeof(uint64_t) * (nfiles + 1), hipMemcpyHostToDevice,
+                           c->stream));
+  }
   HIP_TRY(hipMemsetAsync(c->d_chunk_file, 0, sizeof(uint32_t) * nchunks_pad, c->stream));
   if (nfiles) {
     chunk_file_kernel<<<(nfiles + 255) / 256, 256, 0, c->stream>>>(c->d_off, nfiles, chunk, c->d_chunk_file);
@@ -1359,6 +1566,10 @@ int tsg_batch_kernels(tsg_ctx* c) {
   IA.nev = c->d_count + 1;
   int igrid = 0;
   if (F && G && nchunks) {
+    if (c->has_pathdfa) {
+      path_allow_kernel<<<(F + 255) / 256, 256, 0, st>>>(c->pathdfa, c->d_paths, c->d_poff, F, c->d_pathok);
+      HIP_TRY(hipGetLastError());
+    }
     ggate_kernel<<<(F + 255) / 256, 256, 0, st>>>(c->d_kw, F, W, c->d_gmask, c->d_galways, G, c->GW, c->d_ggate);
     HIP_TRY(hipGetLastError());
     const uint32_t cgrid = (uint32_t)std::min<uint64_t>((nchunks + kBlock - 1) / kBlock, (uint64_t)c->grid);
@@ -1450,6 +1661,11 @@ int tsg_batch_kernels(tsg_ctx* c) {
     HIP_TRY(hipMemcpyAsync(c->ko.kw.data(), c->d_kw, sizeof(uint32_t) * (size_t)F * W, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipMemcpyAsync(ovf.data(), c->d_ovf, sizeof(uint32_t) * F, hipMemcpyDeviceToHost, st));
   }
+  c->ko.path_ok.clear();
+  if (F && c->has_pathdfa) {
+    c->ko.path_ok.resize(F);
+    HIP_TRY(hipMemcpyAsync(c->ko.path_ok.data(), c->d_pathok, F, hipMemcpyDeviceToHost, st));
+  }
   HIP_TRY(hipEventRecord(c->ev[5], st));
   HIP_TRY(hipStreamSynchronize(st));
   c->ko.kw_unknown = c->kw_unknown;
@@ -1479,7 +1695,7 @@ static std::unique_ptr<tsg_result> resolve_job(const tsg_ruleset* rs, BatchView 
   resolve_batch(rs->rs, *rs->plan, b, ko, nt, &res);
   auto t1 = std::chrono::steady_clock::now();
   auto r = std::make_unique<tsg_result>();
-  serialize_batch(res, &r->buf);
+  serialize_batch(res, &r->buf, nt);
   if (getenv("TSG_PROF"))
     fprintf(stderr, "resolve_job: resolve_batch %.1f ms, serialize %.1f ms\n",
             std::chrono::duration<double, std::milli>(t1 - t0).count(),

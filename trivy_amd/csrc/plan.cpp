@@ -510,6 +510,11 @@ void resolve_batch(const Ruleset& rs, const Plan& plan, const BatchView& b,
   }
   out->res.assign(nslots, FileResult{});
 
+  // Global.AllowPath (scanner.go:343-347): from the device when it decided the path
+  auto path_ok = [&](uint32_t f) -> bool {
+    if (!ko.path_ok.empty() && ko.path_ok[f] < 2) return ko.path_ok[f] == 1;
+    return path_allowed(rs, &plan, b.paths + b.path_offsets[f], b.path_offsets[f + 1] - b.path_offsets[f]);
+  };
   static const bool prof = getenv("TSG_PROF") != nullptr;
   if (prof) fprintf(stderr, "resolve: serial setup %.1f Mcyc\n", (__rdtsc() - t_ser0) / 1e6);
   // TSG_PROF: per-thread cycle counters (no shared atomics in the loop)
@@ -541,7 +546,7 @@ void resolve_batch(const Ruleset& rs, const Plan& plan, const BatchView& b,
     const int64_t n = (int64_t)(b.offsets[f + 1] - b.offsets[f]);
     if (out->slot[f] == UINT32_MAX) {  // no match possible
       if (prof) tm.acc = &slots[tid].cyc[0];
-      out->status[f] = path_allowed(rs, &plan, pp, pn) ? kPathAllowed : kNoFindings;
+      out->status[f] = path_ok(f) ? kPathAllowed : kNoFindings;
       return;
     }
     FileResult& res = out->res[out->slot[f]];
@@ -583,7 +588,7 @@ void resolve_batch(const Ruleset& rs, const Plan& plan, const BatchView& b,
     for (uint32_t r : hostonly)
       if (kw_state(r) != 0) any_host = true;
     if (first[f] == first[f + 1] && !ovf && !any_host && !fbbits) {  // no match possible
-      res.status = path_allowed(rs, &plan, pp, pn) ? kPathAllowed : kNoFindings;
+      res.status = path_ok(f) ? kPathAllowed : kNoFindings;
       return;
     }
     const std::string path(pp, pn);
@@ -685,7 +690,7 @@ void resolve_batch(const Ruleset& rs, const Plan& plan, const BatchView& b,
     FileGate gate;
     gate.kw_state = kws.data();
     gate.windows = wptr.data();
-    gate.path_allowed = path_allowed(rs, &plan, pp, pn) ? 1 : 0;
+    gate.path_allowed = path_ok(f) ? 1 : 0;
     gate.ascii_fold_exact = (fbbits & 3) == 0;
     if (prof)
       for (size_t r = 0; r < R; r++)

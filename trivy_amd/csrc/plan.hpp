@@ -103,6 +103,9 @@ struct KernelOutput {
   std::vector<uint8_t> overflow;   // [nfiles] 1 = resolve the whole file exactly
   // [n_kw] (or empty): keyword bits K1 no longer reports (a clear bit proves nothing)
   std::vector<uint8_t> kw_unknown;
+  // [nfiles] (or empty): Global.AllowPath of each path computed on the device:
+  // 0 / 1, or 2 = non-ASCII path, decided on the host
+  std::vector<uint8_t> path_ok;
 };
 
 struct BatchView {

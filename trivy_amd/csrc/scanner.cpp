@@ -4,6 +4,7 @@
 #include <algorithm>
 #include <map>
 #include <atomic>
+#include <thread>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -333,15 +334,25 @@ struct Blocks {
   }
 };
 
-// findLocation (scanner.go:445-502) over the censored buffer with a newline index
-void find_location(int64_t start, int64_t end, const std::string& content,
-                   const std::vector<int64_t>& nl, Finding* f) {
+// newlines in [p, p + n): a branch-free byte loop the compiler vectorizes
+int64_t count_nl(const char* p, int64_t n) {
+  int64_t c = 0;
+  for (int64_t i = 0; i < n; i++) c += p[i] == '\n';
+  return c;
+}
+
+// findLocation (scanner.go:445-502) over the censored buffer.  start_line (0-based) =
+// newlines before start; the lines around the match are found by memchr / memrchr from
+// the match instead of a newline index of the whole file.
+void find_location(int64_t start, int64_t end, const std::string& content, int64_t start_line,
+                   Finding* f) {
+  const char* b = content.data();
   const int64_t n = (int64_t)content.size();
-  int64_t start_line = std::lower_bound(nl.begin(), nl.end(), start) - nl.begin();
-  int64_t line_start = start_line > 0 ? nl[start_line - 1] + 1 : 0;
-  int64_t line_end = start_line < (int64_t)nl.size() ? nl[start_line] : n;
-  int64_t nl_in_match = (std::lower_bound(nl.begin(), nl.end(), end) - nl.begin()) - start_line;
-  int64_t end_line = start_line + nl_in_match;
+  const char* q = start > 0 ? (const char*)memrchr(b, '\n', (size_t)start) : nullptr;
+  const int64_t line_start = q ? q - b + 1 : 0;  // after the last newline before start
+  const char* r = (const char*)std::memchr(b + start, '\n', (size_t)(n - start));
+  const int64_t line_end = r ? r - b : n;  // the first newline at or after start
+  const int64_t end_line = start_line + count_nl(b + start, end - start);
   if (line_end - line_start > 100) {
     int64_t ts = start - 30 < 0 ? 0 : start - 30;
     int64_t te = end + 20 > n ? n : end + 20;
@@ -349,14 +360,18 @@ void find_location(int64_t start, int64_t end, const std::string& content,
   } else {
     f->match.assign(content, line_start, line_end - line_start);
   }
-  const int64_t nlines = (int64_t)nl.size() + 1;
-  int64_t code_start = start_line - 2 < 0 ? 0 : start_line - 2;
-  int64_t code_end = end_line + 2 > nlines ? nlines : end_line + 2;
+  // code lines [start_line - 2, end_line + 2), clamped to the lines of the file
+  const int64_t code_start = start_line - 2 < 0 ? 0 : start_line - 2;
+  int64_t ls = line_start;
+  for (int64_t i = start_line; i > code_start; i--) {  // back to the start of line code_start
+    const char* pq = ls - 1 > 0 ? (const char*)memrchr(b, '\n', (size_t)(ls - 1)) : nullptr;
+    ls = pq ? pq - b + 1 : 0;
+  }
   bool found_first = false;
   f->lines.clear();
-  for (int64_t i = code_start; i < code_end; i++) {
-    int64_t ls = i > 0 ? nl[i - 1] + 1 : 0;
-    int64_t le = i < (int64_t)nl.size() ? nl[i] : n;
+  for (int64_t i = code_start; i < end_line + 2; i++) {
+    const char* e = (const char*)std::memchr(b + ls, '\n', (size_t)(n - ls));
+    const int64_t le = e ? e - b : n;
     bool cause = i >= start_line && i <= end_line;
     Line ln;
     ln.number = (int32_t)(i + 1);
@@ -364,6 +379,8 @@ void find_location(int64_t start, int64_t end, const std::string& content,
     ln.content.assign(content, ls, le - ls);
     found_first = found_first || cause;
     f->lines.push_back(std::move(ln));
+    if (!e) break;  // the last line of the file
+    ls = le + 1;
   }
   for (auto it = f->lines.rbegin(); it != f->lines.rend(); ++it)
     if (it->flags & 1) {
@@ -509,14 +526,20 @@ void scan_file(const Ruleset& rs, const std::string& path, const uint8_t* conten
   }
   ph.lap(4);
   if (matched.empty()) return;  // Secret{}
-  std::vector<int64_t> nl;
-  for (const char *p = censored.data(), *e = p + censored.size();
-       (p = (const char*)std::memchr(p, '\n', e - p)) != nullptr; p++)
-    nl.push_back((int64_t)(p - censored.data()));
+  // line numbers: newlines of the censored buffer counted once, in match-start order
+  std::vector<uint32_t> order(matched.size());
+  for (size_t k = 0; k < order.size(); k++) order[k] = (uint32_t)k;
+  std::sort(order.begin(), order.end(), [&](uint32_t x, uint32_t y) {
+    return matched[x].second.start < matched[y].second.start;
+  });
   out->findings.resize(matched.size());
-  for (size_t k = 0; k < matched.size(); k++) {
+  int64_t pos = 0, line = 0;
+  for (uint32_t k : order) {
+    const Loc& l = matched[k].second;
+    line += count_nl(censored.data() + pos, l.start - pos);
+    pos = l.start;
     out->findings[k].rule = matched[k].first;
-    find_location(matched[k].second.start, matched[k].second.end, censored, nl, &out->findings[k]);
+    find_location(l.start, l.end, censored, line, &out->findings[k]);
   }
   const auto& rules = rs.rules;
   gosort::sort_slice(out->findings, [&rules](const Finding& a, const Finding& b) {
@@ -574,26 +597,48 @@ void write_findings(Writer& w, const FileResult& r) {
 }
 }  // namespace
 
-void serialize_batch(const BatchResult& br, std::string* out) {
+void serialize_batch(const BatchResult& br, std::string* out, int nthreads) {
   const size_t F = br.status.size();
-  size_t total = 8 + F * 5;
-  for (const auto& r : br.res) total += findings_bytes(r);
-  out->resize(total);
+  // file ranges per thread: sizes, prefix offsets, then every range written in parallel
+  const size_t T = std::max<size_t>(1, std::min<size_t>((size_t)std::max(nthreads, 1), F / 32768));
+  std::vector<size_t> lo(T + 1), bytes(T + 1, 0);
+  for (size_t t = 0; t <= T; t++) lo[t] = F * t / T;
+  auto range_bytes = [&](size_t t) {
+    size_t n = 0;
+    for (size_t f = lo[t]; f < lo[t + 1]; f++) {
+      n += 5;
+      if (br.slot[f] != UINT32_MAX) n += findings_bytes(br.res[br.slot[f]]);
+    }
+    bytes[t + 1] = n;
+  };
+  auto write_range = [&](size_t t) {
+    Writer w{&(*out)[0] + 8 + bytes[t]};
+    for (size_t f = lo[t]; f < lo[t + 1]; f++) {
+      const uint32_t k = br.slot[f];
+      if (k == UINT32_MAX) {
+        w.u8(br.status[f]);
+        w.u32(0);
+      } else {
+        const FileResult& r = br.res[k];
+        w.u8(r.status);
+        w.u32((uint32_t)r.findings.size());
+        write_findings(w, r);
+      }
+    }
+  };
+  auto run = [&](auto fn) {
+    std::vector<std::thread> th;
+    for (size_t t = 1; t < T; t++) th.emplace_back(fn, t);
+    fn(0);
+    for (auto& x : th) x.join();
+  };
+  run(range_bytes);
+  for (size_t t = 0; t < T; t++) bytes[t + 1] += bytes[t];
+  out->resize(8 + bytes[T]);
   Writer w{&(*out)[0]};
   w.u32(0x31475354u);  // "TSG1"
   w.u32((uint32_t)F);
-  for (size_t f = 0; f < F; f++) {
-    const uint32_t k = br.slot[f];
-    if (k == UINT32_MAX) {
-      w.u8(br.status[f]);
-      w.u32(0);
-    } else {
-      const FileResult& r = br.res[k];
-      w.u8(r.status);
-      w.u32((uint32_t)r.findings.size());
-      write_findings(w, r);
-    }
-  }
+  run(write_range);
 }
 
 void serialize_results(const std::vector<FileResult>& res, std::string* out) {

@@ -106,7 +106,7 @@ void scan_file(const Ruleset& rs, const std::string& path, const uint8_t* conten
 bool match_keywords(const RuleC& r, const std::string& lowered);
 
 // Serialization of results (format documented in include/trivy_secret.h).
-void serialize_batch(const BatchResult& br, std::string* out);
+void serialize_batch(const BatchResult& br, std::string* out, int nthreads = 1);
 void serialize_results(const std::vector<FileResult>& res, std::string* out);
 
 }  // namespace tsg
