@@ -1429,8 +1429,6 @@ class Backtracker {
     n_ = (int64_t)n;
     base_ = pos;
     maxrow_ = -1;
-    const uint64_t bits = (uint64_t)np_ * (uint64_t)(n_ - base_ + 1);
-    if (visited_.size() * 64 < bits) visited_.resize((bits + 63) / 64, 0);
     bool found = false;
     std::fill(matchcap_.begin(), matchcap_.end(), -1);
     for (int64_t s = pos; s <= n_ && s <= start_hi;) {
@@ -1474,9 +1472,18 @@ class Backtracker {
   std::vector<Job> jobs_;
   std::vector<int64_t> cap_, matchcap_;
 
+  // rows are allocated as the search reaches them (zeroed once, kept zero between runs),
+  // so a run costs what it explores, not the rest of the file
+  void grow(int64_t row) {
+    const size_t need = (size_t)(((uint64_t)(row + 1) * np_ + 63) / 64);
+    if (need > visited_.size()) visited_.resize(std::max(need, visited_.size() * 2), 0);
+  }
   bool visit(uint32_t pc, int64_t pos) {
     const int64_t row = pos - base_;
-    if (row > maxrow_) maxrow_ = row;
+    if (row > maxrow_) {
+      maxrow_ = row;
+      grow(row);
+    }
     const uint64_t k = (uint64_t)row * np_ + pc;
     uint64_t& w = visited_[k >> 6];
     const uint64_t bit = 1ull << (k & 63);

@@ -341,45 +341,108 @@ int64_t count_nl(const char* p, int64_t n) {
   return c;
 }
 
+// The censored buffer of scanner.go:389-392 / censorLocation (:418-426) without copying
+// the file: the content plus the censored spans (sorted, merged).  A newline inside a
+// span is a '*' in the censored buffer, so the line helpers skip it.
+struct Censored {
+  const char* b;
+  int64_t n;
+  std::vector<Loc> cz;
+
+  void finish() {  // sort and merge the spans
+    std::sort(cz.begin(), cz.end(), [](const Loc& x, const Loc& y) { return x.start < y.start; });
+    size_t o = 0;
+    for (size_t i = 0; i < cz.size(); i++) {
+      if (cz[i].end <= cz[i].start) continue;
+      if (o && cz[i].start <= cz[o - 1].end) cz[o - 1].end = std::max(cz[o - 1].end, cz[i].end);
+      else cz[o++] = cz[i];
+    }
+    cz.resize(o);
+  }
+  // the span holding p, or nullptr
+  const Loc* span(int64_t p) const {
+    auto it = std::upper_bound(cz.begin(), cz.end(), p, [](int64_t v, const Loc& l) { return v < l.start; });
+    if (it == cz.begin()) return nullptr;
+    --it;
+    return p < it->end ? &*it : nullptr;
+  }
+  // the first span ending after a (spans are disjoint: ends are sorted too)
+  std::vector<Loc>::const_iterator first_after(int64_t a) const {
+    return std::partition_point(cz.begin(), cz.end(), [a](const Loc& l) { return l.end <= a; });
+  }
+  // newlines of the censored buffer in [a, e)
+  int64_t count(int64_t a, int64_t e) const {
+    int64_t c = count_nl(b + a, e - a);
+    for (auto it = first_after(a); it != cz.end() && it->start < e; ++it) {
+      const int64_t s = std::max(a, it->start), t = std::min(e, it->end);
+      if (s < t) c -= count_nl(b + s, t - s);
+    }
+    return c;
+  }
+  // the first newline at or after x (n if none)
+  int64_t next_nl(int64_t x) const {
+    while (x < n) {
+      const char* p = (const char*)std::memchr(b + x, '\n', (size_t)(n - x));
+      if (!p) return n;
+      const int64_t q = p - b;
+      const Loc* l = span(q);
+      if (!l) return q;
+      x = l->end;
+    }
+    return n;
+  }
+  // the last newline before x (-1 if none)
+  int64_t prev_nl(int64_t x) const {
+    while (x > 0) {
+      const char* p = (const char*)memrchr(b, '\n', (size_t)x);
+      if (!p) return -1;
+      const int64_t q = p - b;
+      const Loc* l = span(q);
+      if (!l) return q;
+      x = l->start;
+    }
+    return -1;
+  }
+  void extract(int64_t a, int64_t e, std::string* out) const {
+    out->assign(b + a, (size_t)(e - a));
+    for (auto it = first_after(a); it != cz.end() && it->start < e; ++it) {
+      const int64_t s = std::max(a, it->start), t = std::min(e, it->end);
+      if (s < t) std::memset(&(*out)[s - a], '*', (size_t)(t - s));
+    }
+  }
+};
+
 // findLocation (scanner.go:445-502) over the censored buffer.  start_line (0-based) =
-// newlines before start; the lines around the match are found by memchr / memrchr from
-// the match instead of a newline index of the whole file.
-void find_location(int64_t start, int64_t end, const std::string& content, int64_t start_line,
-                   Finding* f) {
-  const char* b = content.data();
-  const int64_t n = (int64_t)content.size();
-  const char* q = start > 0 ? (const char*)memrchr(b, '\n', (size_t)start) : nullptr;
-  const int64_t line_start = q ? q - b + 1 : 0;  // after the last newline before start
-  const char* r = (const char*)std::memchr(b + start, '\n', (size_t)(n - start));
-  const int64_t line_end = r ? r - b : n;  // the first newline at or after start
-  const int64_t end_line = start_line + count_nl(b + start, end - start);
+// newlines before start; the lines around the match are found from the match instead of
+// a newline index of the whole file.
+void find_location(int64_t start, int64_t end, const Censored& c, int64_t start_line, Finding* f) {
+  const int64_t n = c.n;
+  const int64_t line_start = c.prev_nl(start) + 1;  // after the last newline before start
+  const int64_t line_end = c.next_nl(start);        // the first newline at or after start
+  const int64_t end_line = start_line + c.count(start, end);
   if (line_end - line_start > 100) {
     int64_t ts = start - 30 < 0 ? 0 : start - 30;
     int64_t te = end + 20 > n ? n : end + 20;
-    f->match.assign(content, ts, te - ts);
+    c.extract(ts, te, &f->match);
   } else {
-    f->match.assign(content, line_start, line_end - line_start);
+    c.extract(line_start, line_end, &f->match);
   }
   // code lines [start_line - 2, end_line + 2), clamped to the lines of the file
   const int64_t code_start = start_line - 2 < 0 ? 0 : start_line - 2;
   int64_t ls = line_start;
-  for (int64_t i = start_line; i > code_start; i--) {  // back to the start of line code_start
-    const char* pq = ls - 1 > 0 ? (const char*)memrchr(b, '\n', (size_t)(ls - 1)) : nullptr;
-    ls = pq ? pq - b + 1 : 0;
-  }
+  for (int64_t i = start_line; i > code_start; i--) ls = c.prev_nl(ls - 1) + 1;
   bool found_first = false;
   f->lines.clear();
   for (int64_t i = code_start; i < end_line + 2; i++) {
-    const char* e = (const char*)std::memchr(b + ls, '\n', (size_t)(n - ls));
-    const int64_t le = e ? e - b : n;
+    const int64_t le = c.next_nl(ls);
     bool cause = i >= start_line && i <= end_line;
     Line ln;
     ln.number = (int32_t)(i + 1);
     ln.flags = (uint8_t)((cause ? 1 : 0) | ((!found_first && cause) ? 2 : 0));
-    ln.content.assign(content, ls, le - ls);
+    c.extract(ls, le, &ln.content);
     found_first = found_first || cause;
     f->lines.push_back(std::move(ln));
-    if (!e) break;  // the last line of the file
+    if (le >= n) break;  // the last line of the file
     ls = le + 1;
   }
   for (auto it = f->lines.rbegin(); it != f->lines.rend(); ++it)
@@ -440,8 +503,7 @@ void scan_file(const Ruleset& rs, const std::string& path, const uint8_t* conten
   std::map<std::string, int8_t> kwcache;  // keyword -> 1 present, -1 absent
   Blocks global{content, n, &rs.exclude};
   std::vector<std::pair<uint32_t, Loc>> matched;
-  std::string censored;
-  bool have_censored = false;
+  Censored censored{(const char*)content, (int64_t)n, {}};
   std::vector<int64_t> idx;
 
   for (size_t ri = 0; ri < rs.rules.size(); ri++) {  // scanner.go:355
@@ -517,11 +579,7 @@ void scan_file(const Ruleset& rs, const std::string& path, const uint8_t* conten
       if (global.Match(loc) || local.Match(loc)) continue;
       if (loc.start < 0) continue;  // reference panics (slice bounds); never produced by valid rules
       matched.push_back({(uint32_t)ri, loc});
-      if (!have_censored) {
-        censored.assign((const char*)content, n);
-        have_censored = true;
-      }
-      std::memset(&censored[loc.start], '*', loc.end - loc.start);  // censorLocation
+      censored.cz.push_back(loc);  // censorLocation
     }
   }
   ph.lap(4);
@@ -533,10 +591,11 @@ void scan_file(const Ruleset& rs, const std::string& path, const uint8_t* conten
     return matched[x].second.start < matched[y].second.start;
   });
   out->findings.resize(matched.size());
+  censored.finish();
   int64_t pos = 0, line = 0;
   for (uint32_t k : order) {
     const Loc& l = matched[k].second;
-    line += count_nl(censored.data() + pos, l.start - pos);
+    line += censored.count(pos, l.start);
     pos = l.start;
     out->findings[k].rule = matched[k].first;
     find_location(l.start, l.end, censored, line, &out->findings[k]);
