@@ -34,7 +34,7 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 # FETCH_SIZE of the same command (rocprofv3 --pmc FETCH_SIZE), committed under profiles/
-PMC_FETCH_CSV = os.path.join(ROOT, "profiles", "r01", "bench_10gib_pmc_fetch_v5.csv")
+PMC_FETCH_CSV = os.path.join(ROOT, "profiles", "r01", "bench_10gib_pmc_fetch_v6.csv")
 
 
 def _dist():
@@ -160,15 +160,19 @@ def main():
     from trivy_amd import _native as N
     L = N.lib()
 
-    acc = {"k1": 0.0, "k2": 0.0, "gate": 0.0, "res": 0.0}
+    acc = {"k1": 0.0, "k2": 0.0, "gate": 0.0, "res": 0.0, "submit": 0.0, "wait": 0.0}
 
     def collect():
+        t = time.perf_counter()
         L.tsg_result_free(ctx.collect_raw())
+        acc["wait"] += (time.perf_counter() - t) * 1e3
         acc["res"] += ctx.stats()["resolve_ms"]
 
     def run(k):
         for _ in range(k):
+            t = time.perf_counter()
             ctx.submit()
+            acc["submit"] += (time.perf_counter() - t) * 1e3
             st = ctx.stats()
             acc["k1"] += st["k1_ms"]
             acc["k2"] += st["k2_ms"]
@@ -219,6 +223,8 @@ def main():
         "breakdown_ms": {"k1": round(k1_ms, 3), "gate": round(acc["gate"] / args.steps, 3),
                          "k2": round(k2_ms, 3),
                          "resolve": round(res / args.steps, 3), "aux": round(st["aux_ms"], 3),
+                         "submit_wall": round(acc["submit"] / args.steps, 3),
+                         "collect_wait": round(acc["wait"] / args.steps, 3),
                          "k2_launches": st["k2_launches"], "candidates": st["candidates"],
                          "upload_s": round(upload_s, 3), "gen_s": round(gen_s, 2),
                          "pcie_inclusive_GBps": round(info["bytes"] / (upload_s + dt / args.steps) / 1e9, 3)},
