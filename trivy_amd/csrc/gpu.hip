@@ -21,6 +21,8 @@
 // are a necessary condition of every match of the rule's GPU program (plan.cpp), so the
 // candidate set is a superset of the exact match ends; the host resolves exactly.
 #include <hip/hip_runtime.h>
+#include <malloc.h>
+#include <mutex>
 
 #include <algorithm>
 #include <chrono>
@@ -154,6 +156,21 @@ __global__ void path_allow_kernel(DevPathDFA d, const uint8_t* __restrict__ path
 // ---------------------------------------------------------------- K1
 typedef unsigned short us2 __attribute__((ext_vector_type(2)));
 
+// K1 class table in LDS.  The class word of a byte is class * 2 (low byte) | 0xFF00 if the
+// byte is in run class D | 0xFFFF0000 if in U.  The table holds it as u16 (class * 2 |
+// D << 14 | U << 15): 512 bytes, so the bytes of text hit twice fewer LDS banks per
+// dword than with a 1 KiB u32 table, and one v_perm (sign bits of bytes 1 of e and
+// e << 1) rebuilds the word.  Built with K1_CLS16; the default u32 table measured faster.
+#ifndef K1_CLS16
+typedef uint32_t k1cls_t;
+__device__ __forceinline__ uint32_t k1_class_word(uint32_t e) { return e; }
+#else
+typedef uint16_t k1cls_t;
+__device__ __forceinline__ uint32_t k1_class_word(uint32_t e) {
+  return __builtin_amdgcn_perm(e << 1, e, 0x08080A00u);
+}
+#endif
+
 // run counters: high half = U run length, low half = D run length << 8 (both saturating);
 // m (the byte's class word) keeps the halves of the classes the byte belongs to
 __device__ __forceinline__ uint32_t run_step(uint32_t cnt, uint32_t m) {
@@ -230,10 +247,12 @@ struct K1Lane {
   const DevK1& d;
   const K1Args& A;
   const uint16_t* s_tab;
-  const uint32_t* s_cls;
+  const k1cls_t* s_cls;
   const uint16_t* s_accs;
   const uint32_t* s_masks;
 
+  // the class word of byte b (see k1cls_t)
+  __device__ __forceinline__ uint32_t cls(uint32_t b) const { return k1_class_word(s_cls[b]); }
   // m's low byte is the byte's class * 2: the entry's byte offset is 2 * row + m[7:0]
   __device__ __forceinline__ uint32_t next(uint32_t s, uint32_t m) const {
     return *(const uint16_t*)((const uint8_t*)s_tab + (s + s + (m & 0xFFu)));
@@ -270,7 +289,7 @@ struct K1Lane {
   __device__ __forceinline__ void replay16(K1Chain& c, uint32_t s, const uint4 v, uint64_t p) {
 #pragma unroll 1
     for (uint32_t k = 0; k < 16; k++) {
-      s = next(s, s_cls[byte_of(v, k)]);
+      s = next(s, cls(byte_of(v, k)));
       if (s >= d.acc_row) accept(c, s, p + k);
     }
   }
@@ -291,7 +310,7 @@ struct K1Lane {
 #ifdef K1_EXP_NO_CLS  // timing experiments only: wrong results
         const uint32_t m = (byte_of(v[i], k) & 0x3Fu) * 2u;
 #else
-        const uint32_t m = s_cls[byte_of(v[i], k)];
+        const uint32_t m = cls(byte_of(v[i], k));
 #endif
 #ifdef K1_EXP_NO_TAB
         c[i].s = (c[i].s + m) & 0x3FFFu;
@@ -336,7 +355,7 @@ struct K1Lane {
       for (int k = 0; k < 16; k++)
 #pragma unroll
         for (int i = 0; i < NS; i++) {
-          const uint32_t m = s_cls[byte_of(v[i], k)];
+          const uint32_t m = cls(byte_of(v[i], k));
           c[i].s = next(c[i].s, m);
           c[i].cnt = run_step(c[i].cnt, m);
         }
@@ -411,7 +430,7 @@ struct K1Lane {
       for (int k = 0; k < 16; k++)
 #pragma unroll
         for (int i = 0; i < NS; i++) {
-          const uint32_t m = s_cls[byte_of(v[i], k)];
+          const uint32_t m = cls(byte_of(v[i], k));
           c[i].s = next(c[i].s, m);
           c[i].cnt = run_step(c[i].cnt, m);
         }
@@ -482,13 +501,20 @@ struct K1Lane {
 template <int KWW, int LDSK, int NS>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2, 8))) k1_kernel(DevK1 d, K1Args A) {
   __shared__ __attribute__((aligned(16))) uint8_t smem[LDSK * 1024];
-  uint32_t* s_cls = (uint32_t*)smem;
+  k1cls_t* s_cls = (k1cls_t*)smem;
   uint16_t* s_tab = (uint16_t*)(smem + 1024);
   {
     const uint32_t* src = (const uint32_t*)d.tab;
     uint32_t* dst = (uint32_t*)s_tab;
     for (uint32_t i = threadIdx.x; i < (d.ns * d.nc + 1) / 2; i += blockDim.x) dst[i] = src[i];
-    for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) s_cls[i] = d.cls[i];
+    for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) {
+      const uint32_t w = d.cls[i];
+#ifndef K1_CLS16
+      s_cls[i] = w;
+#else
+      s_cls[i] = (k1cls_t)((w & 0xFFu) | ((w >> 31) << 15) | (((w >> 15) & 1u) << 14));
+#endif
+    }
   }
   __syncthreads();
   K1Lane<KWW> L{d, A, s_tab, s_cls, d.accs, d.masks};
@@ -1177,6 +1203,8 @@ struct tsg_ctx {
   size_t d_items_cap = 0;
   // host mirrors
   KernelOutput ko;
+  std::vector<std::shared_ptr<KernelOutput>> ko_pool;  // outputs of submitted batches
+  std::vector<uint32_t> h_ovf;
   uint32_t* h_count = nullptr;
   tsg_stats stats{};
   int grid = 0;
@@ -1362,6 +1390,14 @@ int tsg_ctx_create(int device, const tsg_ruleset* rs, const tsg_ctx_options* opt
   if (c->opt.ext_cap == 0) c->opt.ext_cap = 1u << 16;
   if (c->opt.cand_capacity == 0) c->opt.cand_capacity = 1u << 22;
   HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+  // The per-batch host buffers (keyword bits, result vectors, serialized results) are
+  // tens of MB: keep such blocks on the heap (reused, already faulted in) instead of
+  // fresh mmap'ed pages for every batch.
+  static std::once_flag heap_once;
+  std::call_once(heap_once, [] {
+    mallopt(M_MMAP_THRESHOLD, 32 << 20);
+    mallopt(M_TRIM_THRESHOLD, 1 << 30);
+  });
   for (auto& e : c->ev) HIP_TRY(hipEventCreate(&e));
   const Plan& p = *rs->plan;
   const uint32_t W = (uint32_t)p.kw_words;
@@ -1655,13 +1691,14 @@ int tsg_batch_kernels(tsg_ctx* c) {
   uint32_t n = std::min(*c->h_count, c->opt.cand_capacity);
   c->ko.cand.resize(n);
   c->ko.kw.resize((size_t)F * W);
-  std::vector<uint32_t> ovf(F);
+  std::vector<uint32_t>& ovf = c->h_ovf;
+  ovf.resize(F);
   if (n) HIP_TRY(hipMemcpyAsync(c->ko.cand.data(), c->d_cand, sizeof(DevCand) * n, hipMemcpyDeviceToHost, st));
   if (F) {
     HIP_TRY(hipMemcpyAsync(c->ko.kw.data(), c->d_kw, sizeof(uint32_t) * (size_t)F * W, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipMemcpyAsync(ovf.data(), c->d_ovf, sizeof(uint32_t) * F, hipMemcpyDeviceToHost, st));
   }
-  c->ko.path_ok.clear();
+  if (!(F && c->has_pathdfa)) c->ko.path_ok.clear();
   if (F && c->has_pathdfa) {
     c->ko.path_ok.resize(F);
     HIP_TRY(hipMemcpyAsync(c->ko.path_ok.data(), c->d_pathok, F, hipMemcpyDeviceToHost, st));
@@ -1669,7 +1706,7 @@ int tsg_batch_kernels(tsg_ctx* c) {
   HIP_TRY(hipEventRecord(c->ev[5], st));
   HIP_TRY(hipStreamSynchronize(st));
   c->ko.kw_unknown = c->kw_unknown;
-  c->ko.overflow.assign(F, 0);
+  c->ko.overflow.resize(F);
   for (uint32_t i = 0; i < F; i++) c->ko.overflow[i] = ovf[i] ? 1 : 0;
   float t[5] = {0, 0, 0, 0, 0};
   for (int k = 0; k < 5; k++) HIP_TRY(hipEventElapsedTime(&t[k], c->ev[k], c->ev[k + 1]));
@@ -1713,8 +1750,20 @@ int tsg_batch_submit(tsg_ctx* c) {
   try {
     tsg_ctx::Pending pj;
     pj.done = std::make_shared<std::pair<double, uint64_t>>(0.0, 0);
-    auto ko = std::make_shared<KernelOutput>(std::move(c->ko));
-    c->ko = KernelOutput{};
+    // the batch's output goes to a pooled KernelOutput no pending job holds; c->ko gets
+    // that entry's buffers back, so the next batch reuses their pages (no allocation and
+    // no page faults for the tens of MB of keyword bits per batch)
+    std::shared_ptr<KernelOutput> ko;
+    for (auto& e : c->ko_pool)
+      if (e.use_count() == 1) {
+        ko = e;
+        break;
+      }
+    if (!ko) {
+      ko = std::make_shared<KernelOutput>();
+      c->ko_pool.push_back(ko);
+    }
+    std::swap(*ko, c->ko);
     BatchView b{c->h_data, c->h_off, c->nfiles, c->h_paths, c->h_poff};
     const tsg_ruleset* rs = c->rs;
     const int nt = c->opt.host_threads > 0 ? c->opt.host_threads : 16;

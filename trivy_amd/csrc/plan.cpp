@@ -1,5 +1,9 @@
 // GPU plan construction, host resolver, CPU batch path and kernel emulation.
 #include "plan.hpp"
+#include <deque>
+#include <condition_variable>
+#include <mutex>
+#include <functional>
 
 #include <algorithm>
 #include <chrono>
@@ -366,26 +370,103 @@ std::unique_ptr<Plan> build_plan(const Ruleset& rs, const PlanOptions& opt, std:
 }
 
 // ------------------------------------------------------------------ threading
+// One process-wide pool of worker threads shared by every parallel_for, so concurrent
+// batch resolutions (tsg_batch_submit pipelines them) never run more than the pool's
+// threads plus their callers, and per-thread caches (the backtracker's visited rows)
+// survive from one batch to the next.
+namespace {
+
+struct PJob {
+  std::function<void(size_t)> body;
+  size_t n = 0, grain = 64;
+  std::atomic<size_t> next{0};
+  int pending = 0;  // queued or running helper tasks (under m)
+  std::mutex m;
+  std::condition_variable cv;
+  void work() {
+    for (;;) {
+      const size_t s = next.fetch_add(grain);
+      if (s >= n) break;
+      const size_t e = std::min(n, s + grain);
+      for (size_t i = s; i < e; i++) body(i);
+    }
+  }
+};
+
+class Pool {
+ public:
+  static Pool& get() {
+    static Pool* p = new Pool;  // never destroyed: workers may still wait at exit
+    return *p;
+  }
+  // runs j on the caller and up to `helpers` pool threads; returns when all are done
+  void run(PJob& j, int helpers) {
+    grow(helpers);
+    {
+      std::lock_guard<std::mutex> g(m_);
+      j.pending = helpers;
+      for (int h = 0; h < helpers; h++) q_.push_back(&j);
+    }
+    cv_.notify_all();
+    j.work();
+    {  // helpers that have not started are not needed any more
+      std::lock_guard<std::mutex> g(m_);
+      int removed = 0;
+      for (auto it = q_.begin(); it != q_.end();)
+        if (*it == &j) {
+          it = q_.erase(it);
+          removed++;
+        } else {
+          ++it;
+        }
+      std::lock_guard<std::mutex> g2(j.m);
+      j.pending -= removed;
+    }
+    std::unique_lock<std::mutex> lk(j.m);
+    j.cv.wait(lk, [&] { return j.pending == 0; });
+  }
+
+ private:
+  void grow(int want) {
+    std::lock_guard<std::mutex> g(m_);
+    while ((int)th_.size() < want) {
+      th_.emplace_back([this] { worker(); });
+      th_.back().detach();
+    }
+  }
+  void worker() {
+    for (;;) {
+      PJob* j;
+      {
+        std::unique_lock<std::mutex> lk(m_);
+        cv_.wait(lk, [&] { return !q_.empty(); });
+        j = q_.front();
+        q_.pop_front();
+      }
+      j->work();
+      std::lock_guard<std::mutex> g(j->m);
+      if (--j->pending == 0) j->cv.notify_all();
+    }
+  }
+  std::mutex m_;
+  std::condition_variable cv_;
+  std::deque<PJob*> q_;
+  std::vector<std::thread> th_;
+};
+
+}  // namespace
+
 template <class F>
-static void parallel_for(size_t n, int nthreads, F f) {
-  if (nthreads <= 1 || n < 64) {
+static void parallel_for(size_t n, int nthreads, F f, size_t grain = 64) {
+  if (nthreads <= 1 || n < 2 * grain) {
     for (size_t i = 0; i < n; i++) f(i);
     return;
   }
-  std::atomic<size_t> next{0};
-  std::vector<std::thread> th;
-  const size_t grain = 64;
-  for (int t = 0; t < nthreads; t++) {
-    th.emplace_back([&]() {
-      for (;;) {
-        size_t s = next.fetch_add(grain);
-        if (s >= n) break;
-        size_t e = std::min(n, s + grain);
-        for (size_t i = s; i < e; i++) f(i);
-      }
-    });
-  }
-  for (auto& t : th) t.join();
+  PJob j;
+  j.body = [&f](size_t i) { f(i); };
+  j.n = n;
+  j.grain = grain;
+  Pool::get().run(j, std::min(nthreads, 256) - 1);
 }
 
 static bool path_allowed(const Ruleset& rs, const Plan* plan, const char* p, size_t n) {
@@ -494,38 +575,66 @@ void resolve_batch(const Ruleset& rs, const Plan& plan, const BatchView& b,
       kw_has_k[r] |= k.find('k') != std::string::npos;
     }
 
-  // Files that need the exact scan: candidates, empty files, kernel overflow, folding
-  // runes, or a gated rule without a GPU program.  The others only need Global.AllowPath.
-  out->status.assign(F, kNoFindings);
-  out->slot.assign(F, UINT32_MAX);
-  uint32_t nslots = 0;
-  for (uint32_t f = 0; f < F; f++) {
-    bool need = first[f] != first[f + 1] || b.offsets[f + 1] == b.offsets[f] ||
-                (!ko.overflow.empty() && ko.overflow[f]) || !hostonly.empty();
-    if (!need) {
-      const uint32_t* kw = ko.kw.data() + (size_t)f * plan.kw_words;
-      for (int k = plan.fb_kw0; k < plan.n_kw && !need; k++) need = (kw[k / 32] >> (k % 32)) & 1;
-    }
-    if (need) out->slot[f] = nslots++;
-  }
-  out->res.assign(nslots, FileResult{});
-
+  const uint64_t t_ser1 = __rdtsc();
   // Global.AllowPath (scanner.go:343-347): from the device when it decided the path
   auto path_ok = [&](uint32_t f) -> bool {
     if (!ko.path_ok.empty() && ko.path_ok[f] < 2) return ko.path_ok[f] == 1;
     return path_allowed(rs, &plan, b.paths + b.path_offsets[f], b.path_offsets[f + 1] - b.path_offsets[f]);
   };
+  // Files that need the exact scan: candidates, empty files, kernel overflow, folding
+  // runes, or a gated rule without a GPU program.  The others only need Global.AllowPath,
+  // settled here.  Two parallel passes over blocks of files: flags and counts, then slot
+  // numbers in file order.
+  out->status.resize(F);
+  out->slot.resize(F);
+  const size_t kBlk = 8192, nblk = (F + kBlk - 1) / kBlk;
+  std::vector<uint32_t> bcount(nblk + 1, 0);
+  parallel_for(nblk, nthreads, [&](size_t bi) {
+    uint32_t cnt = 0;
+    for (uint32_t f = (uint32_t)(bi * kBlk), fe = (uint32_t)std::min<size_t>(F, (bi + 1) * kBlk); f < fe; f++) {
+      bool need = first[f] != first[f + 1] || b.offsets[f + 1] == b.offsets[f] ||
+                  (!ko.overflow.empty() && ko.overflow[f]) || !hostonly.empty();
+      if (!need) {
+        const uint32_t* kw = ko.kw.data() + (size_t)f * plan.kw_words;
+        for (int k = plan.fb_kw0; k < plan.n_kw && !need; k++) need = (kw[k / 32] >> (k % 32)) & 1;
+      }
+      if (need) {
+        out->slot[f] = 0;
+        cnt++;
+      } else {
+        out->slot[f] = UINT32_MAX;
+        out->status[f] = path_ok(f) ? kPathAllowed : kNoFindings;
+      }
+    }
+    bcount[bi + 1] = cnt;
+  }, 1);
+  for (size_t bi = 0; bi < nblk; bi++) bcount[bi + 1] += bcount[bi];
+  const uint32_t nslots = bcount[nblk];
+  std::vector<uint32_t> need_files(nslots);
+  parallel_for(nblk, nthreads, [&](size_t bi) {
+    uint32_t k = bcount[bi];
+    for (uint32_t f = (uint32_t)(bi * kBlk), fe = (uint32_t)std::min<size_t>(F, (bi + 1) * kBlk); f < fe; f++)
+      if (out->slot[f] != UINT32_MAX) {
+        out->slot[f] = k;
+        need_files[k++] = f;
+      }
+  }, 1);
+  out->res.clear();
+  out->res.resize(nslots);
+
   static const bool prof = getenv("TSG_PROF") != nullptr;
-  if (prof) fprintf(stderr, "resolve: serial setup %.1f Mcyc\n", (__rdtsc() - t_ser0) / 1e6);
+  if (prof)
+    fprintf(stderr, "resolve: setup %.1f Mcyc (candidate sort %.1f; %u files to scan)\n", (__rdtsc() - t_ser0) / 1e6,
+            (t_ser1 - t_ser0) / 1e6, nslots);
   // TSG_PROF: per-thread cycle counters (no shared atomics in the loop)
   struct alignas(64) Slot {
-    uint64_t cyc[4] = {0, 0, 0, 0};  // fast files, candidate files, other files, count cand
+    uint64_t cyc[5] = {0, 0, 0, 0, 0};  // fast files, candidate files, other files, count cand, scan_file
   };
   static std::atomic<int> next_tid{0};
   std::vector<Slot> slots(prof ? 256 : 0);
   std::atomic<int64_t> n_whole{0};
   const uint64_t t_par0 = prof ? __rdtsc() : 0;
-  parallel_for(F, nthreads, [&](size_t fi) {
+  parallel_for(nslots, nthreads, [&](size_t si) {
     thread_local int tid = next_tid++ & 255;
     const uint64_t tp0 = prof ? __rdtsc() : 0;
     struct Tm {
@@ -536,7 +645,7 @@ void resolve_batch(const Ruleset& rs, const Plan& plan, const BatchView& b,
         if (on) *acc += __rdtsc() - t0;
       }
     };
-    const uint32_t f = (uint32_t)fi;
+    const uint32_t f = need_files[si];
     const bool has_cand = first[f] != first[f + 1];
     Tm tm{prof, tp0, prof ? &slots[tid].cyc[has_cand ? 1 : 2] : nullptr};
     if (prof && has_cand) slots[tid].cyc[3]++;
@@ -544,11 +653,6 @@ void resolve_batch(const Ruleset& rs, const Plan& plan, const BatchView& b,
     const size_t pn = b.path_offsets[f + 1] - b.path_offsets[f];
     const uint8_t* content = b.data + b.offsets[f];
     const int64_t n = (int64_t)(b.offsets[f + 1] - b.offsets[f]);
-    if (out->slot[f] == UINT32_MAX) {  // no match possible
-      if (prof) tm.acc = &slots[tid].cyc[0];
-      out->status[f] = path_ok(f) ? kPathAllowed : kNoFindings;
-      return;
-    }
     FileResult& res = out->res[out->slot[f]];
     struct SetStatus {
       FileResult& r;
@@ -701,15 +805,18 @@ void resolve_batch(const Ruleset& rs, const Plan& plan, const BatchView& b,
                     (int)wptr[r]->whole, wptr[r]->iv.empty() ? -1L : (long)wptr[r]->iv[0].first,
                     wptr[r]->iv.empty() ? -1L : (long)wptr[r]->iv[0].second, wptr[r]->iv.size());
         }
+    const uint64_t ts0 = prof ? __rdtsc() : 0;
     scan_file(rs, path, content, (size_t)n, &gate, &res);
+    if (prof) slots[tid].cyc[4] += __rdtsc() - ts0;
   });
   if (prof) {
-    uint64_t t[4] = {0, 0, 0, 0};
+    uint64_t t[5] = {0, 0, 0, 0, 0};
     for (const auto& sl : slots)
-      for (int k = 0; k < 4; k++) t[k] += sl.cyc[k];
+      for (int k = 0; k < 5; k++) t[k] += sl.cyc[k];
     fprintf(stderr, "resolve: parallel part %.1f Mcyc wall; thread Mcyc: no-candidate files %.1f, candidate files %.1f "
-            "(%lu files, %ld whole-prefix rule scans), other %.1f\n",
-            (__rdtsc() - t_par0) / 1e6, t[0] / 1e6, t[1] / 1e6, (unsigned long)t[3], (long)n_whole, t[2] / 1e6);
+            "(%lu files, %ld whole-prefix rule scans; scan_file %.1f), other %.1f\n",
+            (__rdtsc() - t_par0) / 1e6, t[0] / 1e6, t[1] / 1e6, (unsigned long)t[3], (long)n_whole, t[4] / 1e6,
+            t[2] / 1e6);
   }
 }
 

@@ -458,6 +458,18 @@ void find_location(int64_t start, int64_t end, const Censored& c, int64_t start_
 
 // TSG_PROF: per-phase cycle counters of scan_file (printed at exit)
 static std::atomic<uint64_t> g_ph[8];
+// per-thread phase sums in slots of their own (no shared cache line is written per lap:
+// contended atomics would distort what they measure); PhDump adds the slots up
+struct alignas(64) PhSlot {
+  uint64_t v[8];
+};
+static PhSlot g_phslot[256];
+static std::atomic<int> g_phslots{0};
+static thread_local PhSlot* t_phslot = nullptr;
+static PhSlot& ph_slot() {
+  if (!t_phslot) t_phslot = &g_phslot[g_phslots++ & 255];
+  return *t_phslot;
+}
 static std::atomic<uint64_t> g_rule_cyc[2048], g_rule_calls[2048], g_rule_bytes[2048];
 static std::string g_rule_name[2048];  // rule ids seen by the profiler (names outlive rule sets)
 static const bool g_prof = getenv("TSG_PROF") != nullptr;
@@ -465,7 +477,11 @@ struct PhDump {
   ~PhDump() {
     if (!g_prof) return;
     const char* nm[8] = {"allowpath", "rulegates", "lower", "findall", "allowmatch", "locate", "total", "nfiles"};
-    for (int i = 0; i < 8; i++) fprintf(stderr, "scan_file %-10s %.2f Mcyc\n", nm[i], g_ph[i] / 1e6);
+    for (int i = 0; i < 8; i++) {
+      uint64_t t = g_ph[i];
+      for (const auto& sl : g_phslot) t += sl.v[i];
+      fprintf(stderr, "scan_file %-10s %.2f Mcyc\n", nm[i], t / 1e6);
+    }
     std::vector<std::pair<uint64_t, size_t>> v;
     for (size_t r = 0; r < 2048; r++)
       if (g_rule_calls[r]) v.push_back({g_rule_cyc[r].load(), r});
@@ -481,7 +497,7 @@ struct PhT {
   void lap(int i) {
     if (!g_prof) return;
     uint64_t n = __rdtsc();
-    g_ph[i] += n - t;
+    ph_slot().v[i] += n - t;
     t = n;
   }
 };
@@ -489,7 +505,7 @@ struct PhT {
 void scan_file(const Ruleset& rs, const std::string& path, const uint8_t* content, size_t n,
                const FileGate* gate, FileResult* out) {
   PhT ph, tot;
-  if (g_prof) g_ph[7] += 1000000;
+  if (g_prof) ph_slot().v[7] += 1000000;
   struct TotL { PhT& t; ~TotL() { t.lap(6); } } totl{tot};
   out->findings.clear();
   out->status = kNoFindings;
