@@ -140,7 +140,7 @@ def main():
     ap.add_argument("--chunk", type=int, default=0)
     ap.add_argument("--seed", type=int, default=2)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--depth", type=int, default=2, help="pipelined scans in flight")
+    ap.add_argument("--depth", type=int, default=4, help="pipelined scans in flight")
     args = ap.parse_args()
 
     dist, rank, world, local = _dist()

@@ -439,8 +439,26 @@ std::unique_ptr<DFA> build_reverse_dfa(const Prog& prog, const DFAOptions& opt, 
   return b.run(err);
 }
 
+void DFA::pack() {
+  packed.assign(next.size(), 0);
+  for (size_t i = 0; i < next.size(); i++)
+    packed[i] = next[i] * (uint32_t)nclasses | (acc[i] ? 1u << 31 : 0u) | (dead[next[i]] ? 1u << 30 : 0u);
+}
+
 int64_t reverse_match_start(const DFA& d, const uint8_t* b, int64_t e) {
   const int nc = d.nclasses;
+  if (!d.packed.empty()) {  // one load per byte: row, accept and dead flags together
+    uint32_t row = d.anchored * (uint32_t)nc;
+    int64_t best = -1;
+    for (int64_t q = e; q > 0; q--) {
+      const uint32_t x = d.packed[row + d.cls[b[q - 1]]];
+      if (x >> 31) best = q;
+      row = x & 0x3FFFFFFFu;
+      if (x & (1u << 30)) return best;
+    }
+    if (d.eot_acc[row / (uint32_t)nc]) best = 0;
+    return best;
+  }
   uint32_t s = d.anchored;
   int64_t best = -1;
   int64_t q = e;

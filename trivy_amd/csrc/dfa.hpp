@@ -48,6 +48,10 @@ struct DFA {
   std::vector<uint8_t> noinject;     // [nstates] mode bit
   int64_t max_len = -1;              // longest match in bytes (-1 = unbounded)
   uint32_t anchored = 0;             // DFAOptions::anchored: noinject state of the start node
+  // host fast path (reverse DFAs): per transition the next state's row (state * nclasses)
+  // | 1 << 31 if the transition accepts | 1 << 30 if the next state is dead; see pack()
+  std::vector<uint32_t> packed;
+  void pack();
 
   // Host helper: accept mask (words) of regexes matching somewhere in b (MatchString).
   void match_any(const uint8_t* b, size_t n, std::vector<uint64_t>* out) const;

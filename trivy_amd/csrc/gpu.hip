@@ -59,6 +59,15 @@ constexpr int kK1Seg = 8;         // K1: consecutive chunks per chain
 constexpr int kK1Lds[3] = {52, 80, 156};
 constexpr uint32_t kK1Tab = 1024;  // K1 LDS: 256 class words, then the transition table   // independent DFA chains per lane (dense passes)
 constexpr int kBlock = 256;
+// K1 block and occupancy target: two blocks of K1_BLOCK threads share a CU's LDS (one
+// 80 KiB automaton image each); K1_WAVES waves per SIMD bounds the registers per lane
+#ifndef K1_BLOCK
+#define K1_BLOCK 256
+#endif
+#ifndef K1_WAVES
+#define K1_WAVES 2
+#endif
+constexpr int kK1Block = K1_BLOCK;
 constexpr int kPad = 256;     // zero bytes before and after the batch in HBM (>= K1 warm-up)
 constexpr int kMaxBack = 16;  // event windows up to this many chunks; larger -> whole file
 
@@ -499,7 +508,7 @@ struct K1Lane {
 // (a byte's word is at byte * 4), the transitions from 1 KiB.  Accept masks stay in
 // global memory (rare path).
 template <int KWW, int LDSK, int NS>
-__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2, 8))) k1_kernel(DevK1 d, K1Args A) {
+__global__ void __launch_bounds__(kK1Block) __attribute__((amdgpu_waves_per_eu(K1_WAVES, 8))) k1_kernel(DevK1 d, K1Args A) {
   __shared__ __attribute__((aligned(16))) uint8_t smem[LDSK * 1024];
   k1cls_t* s_cls = (k1cls_t*)smem;
   uint16_t* s_tab = (uint16_t*)(smem + 1024);
@@ -1290,11 +1299,11 @@ static const void* k1_fn(uint32_t kw_words, uint32_t lds_class, uint32_t ns) {
 static int launch_k1(tsg_ctx* c, const K1Args& A) {
   static const int gmul = getenv("TSG_K1_GRID") ? atoi(getenv("TSG_K1_GRID")) : 0;
   const uint64_t cap = (uint64_t)c->grid / 8 * (gmul > 0 ? gmul : 8);
-  const int grid = (int)std::min<uint64_t>((A.nitems + kBlock - 1) / kBlock, cap);
+  const int grid = (int)std::min<uint64_t>((A.nitems + kK1Block - 1) / kK1Block, cap);
   DevK1 d = c->k1;
   K1Args a = A;
   void* args[] = {&d, &a};
-  HIP_TRY(hipLaunchKernel(k1_fn(c->k1.kw_words, c->k1.lds_class, A.streams), dim3(grid), dim3(kBlock), args, 0,
+  HIP_TRY(hipLaunchKernel(k1_fn(c->k1.kw_words, c->k1.lds_class, A.streams), dim3(grid), dim3(kK1Block), args, 0,
                           c->stream));
   HIP_TRY(hipGetLastError());
   return TSG_OK;

@@ -350,6 +350,7 @@ std::unique_ptr<Plan> build_plan(const Ruleset& rs, const PlanOptions& opt, std:
     std::string e;
     auto t0 = std::chrono::steady_clock::now();
     p->rule_rev[r] = build_reverse_dfa(rs.rules[r].regex->prog(), o, &e);
+    if (p->rule_rev[r]) p->rule_rev[r]->pack();
     if (getenv("TSG_PROF"))
       fprintf(stderr, "rev %s: %d states %.1f ms\n", rs.rules[r].id.c_str(),
               p->rule_rev[r] ? p->rule_rev[r]->nstates : -1,
@@ -467,6 +468,10 @@ static void parallel_for(size_t n, int nthreads, F f, size_t grain = 64) {
   j.n = n;
   j.grain = grain;
   Pool::get().run(j, std::min(nthreads, 256) - 1);
+}
+
+void pool_for(size_t n, int nthreads, const std::function<void(size_t)>& f, size_t grain) {
+  parallel_for(n, nthreads, f, grain);
 }
 
 static bool path_allowed(const Ruleset& rs, const Plan* plan, const char* p, size_t n) {

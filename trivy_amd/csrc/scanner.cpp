@@ -701,12 +701,7 @@ void serialize_batch(const BatchResult& br, std::string* out, int nthreads) {
       }
     }
   };
-  auto run = [&](auto fn) {
-    std::vector<std::thread> th;
-    for (size_t t = 1; t < T; t++) th.emplace_back(fn, t);
-    fn(0);
-    for (auto& x : th) x.join();
-  };
+  auto run = [&](auto fn) { pool_for(T, (int)T, [&](size_t t) { fn(t); }, 1); };
   run(range_bytes);
   for (size_t t = 0; t < T; t++) bytes[t + 1] += bytes[t];
   out->resize(8 + bytes[T]);

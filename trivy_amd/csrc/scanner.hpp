@@ -12,6 +12,7 @@
 // bits and per-rule candidate end offsets); everything that reaches the output is
 // computed here with Go semantics.
 #pragma once
+#include <functional>
 #include <cstdint>
 #include <memory>
 #include <string>
@@ -107,6 +108,9 @@ bool match_keywords(const RuleC& r, const std::string& lowered);
 
 // Serialization of results (format documented in include/trivy_secret.h).
 void serialize_batch(const BatchResult& br, std::string* out, int nthreads = 1);
+
+// f(i) for i in [0, n) on the process-wide worker pool (plan.cpp), `grain` indices a claim
+void pool_for(size_t n, int nthreads, const std::function<void(size_t)>& f, size_t grain);
 void serialize_results(const std::vector<FileResult>& res, std::string* out);
 
 }  // namespace tsg
