@@ -1,0 +1,50 @@
+"""BASELINE configs[3] and configs[4] as parity cases: large user rule
+sets (keyword-less rules, unbounded rules, DFA state blow-up, keywords left out of the
+K1 automaton when it outgrows its LDS budget) and allow rules / exclude blocks / binary
+blobs.  The GPU algorithm (emulated here, on the device in test_gpu_configs) must give
+exactly the findings of the exact CPU path (Scanner.Scan, scanner.go:341-416).  No
+reference fixture covers these rule sets: the expected side is the exact CPU path, which
+the reference fixtures pin (test_cpu_reference.py)."""
+import numpy as np
+import pytest
+
+from trivy_amd import analyzer as A
+from trivy_amd import configs
+from trivy_amd import secret as S
+
+
+@pytest.fixture(scope="module")
+def user100():
+    doc = configs.user_rules_doc(100, seed=4)
+    return doc, S.NewScanner(S.config_from_dict(doc))
+
+
+def test_user_rules_plan_degrades_not_fails(user100):
+    """183 rules: the K1 automaton would exceed its budget; keywords are left out of it
+    instead of failing the rule-set compile (the reference has no such limit)."""
+    _, sc = user100
+    info = sc.info()
+    assert info["n_rules"] == 183 and info["kw_states"] > 0
+
+
+@pytest.mark.parametrize("chunk", [64, 256])
+def test_user_rules_emulation_vs_exact(user100, chunk):
+    doc, sc = user100
+    b = S.Batch.from_args(configs.mixed_batch(doc, 192 << 10, seed=40 + chunk))
+    want = sc.ScanBatch(b, nthreads=8)
+    assert sc.ScanBatch(b, emulate_chunk=chunk) == want
+    assert sum(len(x["Findings"] or []) for x in want) > 10
+
+
+def test_allow_exclude_binary_emulation_vs_exact():
+    doc = configs.allow_exclude_doc()
+    sc = S.NewScanner(S.config_from_dict(doc))
+    args = configs.mixed_batch(doc, 256 << 10, seed=51, plants_per_file=0.5, binary_frac=0.3)
+    # analyzer gate first (utils.IsBinary, secret.go:78-110), as the analyzer does
+    args = [a for a in args if not A.IsBinary(a.Content, len(a.Content))]
+    b = S.Batch.from_args(args)
+    want = sc.ScanBatch(b, nthreads=8)
+    assert sc.ScanBatch(b, emulate_chunk=256) == want
+    n = sum(len(x["Findings"] or []) for x in want)
+    assert n > 5
+    assert any("blob/" in x.get("FilePath", "") for x in want if x["Findings"])

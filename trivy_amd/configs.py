@@ -1,0 +1,136 @@
+"""Seeded rule-set configurations for the BASELINE parity configs beyond the builtins.
+
+    user_rules_doc(n, seed)    configs[3]: n user-defined rules in trivy-secret.yaml form
+                               (SURVEY.md §8d "Config 4"): generic-family clones with
+                               random keyword names, rules with no keywords, unbounded
+                               (?s).* rules between literals, and DFA state-blowup
+                               patterns that force the NFA / host-only fallback.  Every
+                               rule has a `secret` group (scanner.go:148-158).
+    allow_exclude_doc(seed)    configs[4]: global and per-rule allow rules (regex and
+                               path) and exclude blocks (scanner.go:50-57, :178-265).
+    plant_lines(doc, rng, k)   lines that match rules of `doc`, to mix into a corpus.
+
+The documents are plain dicts in the YAML schema of ParseConfig (scanner.go:27-47), so
+they go through trivy_amd.secret.config_from_dict exactly like a parsed file.
+"""
+import string
+
+import numpy as np
+
+_ALNUM = string.ascii_lowercase + string.digits
+
+
+def _name(rng, lo=5, hi=12):
+    n = int(rng.integers(lo, hi + 1))
+    return "".join(rng.choice(list(string.ascii_lowercase), size=n))
+
+
+def user_rules_doc(n=1000, seed=4):
+    """configs[3]: 60 % generic clones, 20 % keyword-less, 10 % unbounded, 10 % blow-up."""
+    rng = np.random.default_rng(seed)
+    rules = []
+    seen = set()
+    for i in range(n):
+        kind = i % 10
+        name = _name(rng)
+        while name in seen:
+            name = _name(rng)
+        seen.add(name)
+        rid = "user-%04d-%s" % (i, name)
+        r = {"id": rid, "category": "user", "title": "User rule %d" % i,
+             "severity": ["LOW", "MEDIUM", "HIGH", "CRITICAL", ""][i % 5],
+             "secret-group-name": "secret"}
+        if kind < 6:    # generic-family clone (builtin-rules.go generic pattern)
+            r["regex"] = (r"(?i)(?:%s)(?:[0-9a-z\-_\t .]{0,20})(?:[\s|']|[\s|\"]){0,3}"
+                          r"(?:=|>|:=|\|\|:|<=|=>|:)(?:'|\"|\s|=|\x60){0,5}"
+                          r"(?P<secret>[0-9a-z]{16,32})(?:['|\"|\n|\r|\s|\x60]|$)" % name)
+            r["keywords"] = [name]
+        elif kind < 8:  # no keywords: always scanned
+            r["regex"] = r"%s_(?P<secret>[A-Z0-9]{20})\b" % name.upper()
+        elif kind < 9:  # unbounded between two literals
+            r["regex"] = r"(?s)begin_%s(?P<secret>.*)end_%s" % (name, name)
+            r["keywords"] = ["begin_" + name]
+        else:           # DFA state blow-up: counted overlap / k-th symbol from the end
+            if i % 20 == 9:
+                r["regex"] = r"%s(?P<secret>[a-z0-9]{1,40}x[a-f0-9]{20,40})" % name
+            else:
+                r["regex"] = r"%s(?P<secret>(a|b)*a(a|b){15})" % name
+            r["keywords"] = [name]
+        rules.append(r)
+    return {"rules": rules}
+
+
+def allow_exclude_doc(seed=5):
+    """configs[4]: allow rules and exclude blocks around builtin and custom rules."""
+    return {
+        "rules": [
+            {"id": "custom-token", "category": "custom", "title": "Custom token", "severity": "HIGH",
+             "regex": r"(?i)(?P<key>(custom_token))(=|:).{0,5}['\"](?P<secret>[0-9a-zA-Z\-_=]{8,64})['\"]",
+             "secret-group-name": "secret", "keywords": ["custom_token"],
+             "allow-rules": [{"id": "skip-test-values", "regex": "TESTVALUE"},
+                             {"id": "skip-fixtures", "path": r"fixtures/"}],
+             "exclude-block": {"description": "local block",
+                               "regexes": [r"--- ignore block start ---(.|\s)*--- ignore block stop ---"]}},
+        ],
+        "allow-rules": [{"id": "global-example", "regex": "EXAMPLEKEY"},
+                        {"id": "global-docs", "path": r"\.rst$"}],
+        "exclude-block": {"description": "global block",
+                          "regexes": [r"-----BEGIN IGNORE-----(.|\s)*?-----END IGNORE-----"]},
+    }
+
+
+def plant_lines(doc, rng, k):
+    """k lines, each matching (or nearly matching) a random rule of `doc`."""
+    rules = doc.get("rules") or []
+    out = []
+    for _ in range(k):
+        r = rules[int(rng.integers(0, len(rules)))]
+        rid = r["id"]
+        name = rid.split("-", 2)[-1] if rid.startswith("user-") else "custom_token"
+        tok = "".join(rng.choice(list(_ALNUM), size=int(rng.integers(12, 36))))
+        kind = int(rng.integers(0, 6))
+        if kind == 0:
+            out.append("%s = '%s'" % (name, tok))
+        elif kind == 1:
+            out.append("%s_%s" % (name.upper(), tok.upper()[:20].ljust(20, "Q")))
+        elif kind == 2:
+            out.append("begin_%s %s\n%s end_%s" % (name, tok, tok[::-1], name))
+        elif kind == 3:
+            out.append("%s%sx%s" % (name, tok[:10], "abcdef0123456789"[:int(rng.integers(18, 30)) % 16] * 2))
+        elif kind == 4:
+            out.append("%s%s" % (name, "".join(rng.choice(["a", "b"], size=int(rng.integers(14, 30))))))
+        else:
+            out.append("custom_token: '%s' TESTVALUE" % tok if rng.random() < 0.3 else
+                       "custom_token='%s'" % tok)
+    return out
+
+
+def mixed_batch(doc, nbytes, seed, plants_per_file=0.3, binary_frac=0.0):
+    """A seeded corpus (trivy_amd.corpus) with lines of `plant_lines` mixed into files,
+    and (configs[4]) binary blobs: random bytes, half with a text-looking first 300 bytes
+    so that they pass utils.IsBinary (utils.go:71-89)."""
+    from trivy_amd import corpus
+    from trivy_amd import secret as S
+    rng = np.random.default_rng(seed)
+    base, _ = corpus.make_corpus(nbytes, seed=seed, plants_per_mib=50)
+    args = []
+    for i in range(base.nfiles):
+        c = bytes(base.data[int(base.offsets[i]):int(base.offsets[i + 1])])
+        if rng.random() < plants_per_file:
+            lines = c.split(b"\n")
+            for ln in plant_lines(doc, rng, int(rng.integers(1, 4))):
+                lines.insert(int(rng.integers(0, len(lines) + 1)), ln.encode())
+            if rng.random() < 0.05:
+                lines.insert(0, b"--- ignore block start ---")
+                lines.append(b"--- ignore block stop ---")
+            c = b"\n".join(lines)
+        path = base.path(i)
+        if rng.random() < 0.03:
+            path = "fixtures/" + path
+        args.append(S.ScanArgs(path, c))
+        if binary_frac and rng.random() < binary_frac:
+            blob = rng.integers(0, 256, size=int(rng.integers(64, 4096)), dtype=np.uint8).tobytes()
+            if rng.random() < 0.5:
+                blob = (b"custom_token='abcdefgh12345678' " * 10)[:300] + blob
+            args.append(S.ScanArgs("blob/%d.bin" % i, blob))
+    return args

@@ -282,8 +282,12 @@ std::unique_ptr<Plan> build_plan(const Ruleset& rs, const PlanOptions& opt, std:
   // ---- K1 automaton: keywords + anchor literals; literal groups share event bits
   std::vector<char> litg(p->groups.size(), 0);
   for (size_t g = 0; g < p->groups.size(); g++) litg[g] = p->groups[g].events == (1u << kEvLit0);
+  // keywords left out of K1 (table budget): a literal no ASCII text contains holds their id
+  std::vector<char> kw_dropped(kws.size(), 0);
   auto build_k1 = [&](bool with_anchors) -> bool {
     std::vector<std::string> lits = kws;
+    for (size_t k = 0; k < lits.size(); k++)
+      if (kw_dropped[k]) lits[k] = "\xff\xff";
     std::vector<uint32_t> lit_event(lits.size(), 0);
     std::map<std::string, uint32_t> lid;
     for (size_t i = 0; i < lits.size(); i++) lid.emplace(lits[i], (uint32_t)i);
@@ -335,8 +339,29 @@ std::unique_ptr<Plan> build_plan(const Ruleset& rs, const PlanOptions& opt, std:
     return true;
   };
   if (!build_k1(opt.anchors) && !build_k1(false)) {
-    if (err) *err = "keyword automaton exceeds the K1 table budget";
-    return nullptr;
+    // Too many keyword bytes for an LDS-resident automaton (large user rule sets): leave
+    // keywords out, longest first (they cost the most states), until it fits.  Their rules
+    // get the exact keyword gate on the host, and their groups are scanned on every file.
+    std::vector<int> order;
+    for (int k = 0; k < p->fb_kw0; k++) order.push_back(k);
+    std::stable_sort(order.begin(), order.end(),
+                     [&](int a, int b) { return kws[a].size() > kws[b].size(); });
+    bool ok = false;
+    for (size_t next = 0; next < order.size() && !ok;) {
+      for (size_t m = std::max<size_t>(1, order.size() / 32); m > 0 && next < order.size(); m--)
+        kw_dropped[order[next++]] = 1;
+      ok = build_k1(opt.anchors) || build_k1(false);
+    }
+    if (!ok) {
+      if (err) *err = "keyword automaton exceeds the K1 table budget";
+      return nullptr;
+    }
+    for (size_t r = 0; r < R; r++) {
+      if (p->rule_kw_mode[r] != kKwBits) continue;
+      for (uint32_t k : p->rule_kws[r])
+        if (kw_dropped[k]) p->rule_kw_mode[r] = kKwUnknown;
+    }
+    for (auto& g : p->groups) group_kwmask(g);
   }
 
   // ---- host resolver: reverse DFAs of the exact programs
