@@ -134,3 +134,64 @@ def mixed_batch(doc, nbytes, seed, plants_per_file=0.3, binary_frac=0.0):
                 blob = (b"custom_token='abcdefgh12345678' " * 10)[:300] + blob
             args.append(S.ScanArgs("blob/%d.bin" % i, blob))
     return args
+
+
+def layer_tar(nbytes, seed=3, binary_frac=0.05):
+    """configs[2] (SURVEY.md §8d "Config 3"): an uncompressed image-layer tar built from the
+    seeded corpus, with directory entries, symlinks/hardlinks (no content), whiteouts,
+    an opaque marker, a system dir (`proc/`, skipped by the walker), `.git` and
+    `node_modules` trees, binary blobs and PAX long names.  Returns the tar bytes."""
+    import io
+    import tarfile
+    from trivy_amd import corpus
+    rng = np.random.default_rng(seed)
+    base, _ = corpus.make_corpus(nbytes, seed=seed, plants_per_mib=50)
+    buf = io.BytesIO()
+    dirs = set()
+
+    def add(tf, name, typ, data=b"", link=""):
+        ti = tarfile.TarInfo(name)
+        ti.type = typ
+        ti.linkname = link
+        ti.size = len(data) if typ in (tarfile.REGTYPE, tarfile.AREGTYPE) else 0
+        tf.addfile(ti, io.BytesIO(data) if ti.size else None)
+
+    with tarfile.open(fileobj=buf, mode="w", format=tarfile.PAX_FORMAT) as tf:
+        for i in range(base.nfiles):
+            c = bytes(base.data[int(base.offsets[i]):int(base.offsets[i + 1])])
+            p = base.path(i).lstrip("/")
+            r = rng.random()
+            if r < 0.02:
+                p = "proc/%d/%s" % (i, p.rsplit("/", 1)[-1])
+            elif r < 0.03:
+                p = "srv/.git/objects/%d" % i
+            elif r < 0.04:
+                p = "app/node_modules/%s" % p
+            elif r < 0.05:
+                p = "deep/" + "/".join("d%d" % k for k in range(24)) + "/" + p
+            d = p.rsplit("/", 1)[0] if "/" in p else ""
+            parts = d.split("/") if d else []
+            for k in range(1, len(parts) + 1):
+                dd = "/".join(parts[:k])
+                if dd not in dirs:
+                    dirs.add(dd)
+                    add(tf, dd + "/", tarfile.DIRTYPE)
+            add(tf, p, tarfile.REGTYPE, c)
+            r = rng.random()
+            if r < 0.01:
+                add(tf, p + ".lnk", tarfile.SYMTYPE, link=p)
+            elif r < 0.02:
+                add(tf, p + ".hard", tarfile.LNKTYPE, link=p)
+            elif r < 0.025:
+                add(tf, (d + "/" if d else "") + ".wh." + "gone%d" % i, tarfile.REGTYPE)
+            elif r < 0.026:
+                add(tf, (d + "/" if d else "") + ".wh..wh..opq", tarfile.REGTYPE)
+            if binary_frac and rng.random() < binary_frac:
+                blob = rng.integers(0, 256, size=int(rng.integers(64, 4096)),
+                                    dtype=np.uint8).tobytes()
+                if rng.random() < 0.5:
+                    blob = c[:300].replace(b"\0", b" ") + blob
+                add(tf, "blob/%d.dat" % i, tarfile.REGTYPE, blob)
+        add(tf, "etc/.wh..wh..opq", tarfile.REGTYPE)
+        add(tf, "etc/.wh.hostname", tarfile.REGTYPE)
+    return buf.getvalue()

@@ -1,0 +1,205 @@
+"""Image-layer ingest for the secret path: trivy's layer tar walker
+(pkg/fanal/walker/tar.go, walk.go) feeding the batched analyzer.
+
+  LayerTar(skip_files, skip_dirs).Walk(layer, fn)   walker/tar.go:33-84
+  analyze_layer(analyzer, layer, ...)               walker.Walk + AnalyzerGroup.AnalyzeFile
+                                                    (analyzer.go:395-445) + SecretAnalyzer,
+                                                    with the files of a layer packed into
+                                                    large batches for the MI355X kernels
+
+The reference hands each file to a goroutine (≤5 per layer, image.go:28) that scans it
+alone.  Here every file that passes `Required` is copied once into a batch; a batch of
+`batch_bytes` is scanned in one call.  Per-file semantics are unchanged: the path passed
+to `Required` is the cleaned tar name, the path given to `Scan` gets the "/" prefix of
+image files (secret.go:90-96), and `IsBinary` uses the header size (secret.go:80).
+
+Go's path helpers (filepath.Clean / Split / Join / Rel / Base on "/" paths) are restated
+below because Python's posixpath differs on "//" prefixes, empty paths and "..".
+"""
+import tarfile
+
+from .analyzer import AnalysisInput, IsBinary, sort_secrets
+from . import secret as S
+
+OPQ = ".wh..wh..opq"   # tar.go:19
+WH = ".wh."            # tar.go:20
+APP_DIRS = [".git"]                 # walk.go:14
+SYSTEM_DIRS = ["proc", "sys", "dev"]  # walk.go:15
+THRESHOLD_SIZE = 200 << 20          # walk.go:18 (temp-file spill; no effect on results)
+
+_REG = (tarfile.REGTYPE, tarfile.AREGTYPE)  # Go's reader maps TypeRegA to TypeReg
+
+
+def clean(p):
+    """Go path.Clean (lexical)."""
+    if p == "":
+        return "."
+    rooted = p[0] == "/"
+    out = []
+    for part in p.split("/"):
+        if part == "" or part == ".":
+            continue
+        if part == "..":
+            if out and out[-1] != "..":
+                out.pop()
+            elif not rooted:
+                out.append("..")
+            continue
+        out.append(part)
+    s = "/".join(out)
+    if rooted:
+        return "/" + s
+    return s or "."
+
+
+def split(p):
+    """Go filepath.Split: dir keeps its trailing slash."""
+    i = p.rfind("/")
+    return p[:i + 1], p[i + 1:]
+
+
+def join(*elems):
+    """Go filepath.Join: empty elements are ignored, the result is cleaned."""
+    parts = [e for e in elems if e != ""]
+    return clean("/".join(parts)) if parts else ""
+
+
+def base(p):
+    """Go filepath.Base."""
+    if p == "":
+        return "."
+    p = p.rstrip("/")
+    if p == "":
+        return "/"
+    return p[p.rfind("/") + 1:]
+
+
+def rel(basepath, targpath):
+    """Go filepath.Rel on "/" paths; returns None where Go returns an error."""
+    b = clean(basepath)
+    t = clean(targpath)
+    if t == b:
+        return "."
+    if b == ".":
+        b = ""
+    if (len(b) > 0 and b[0] == "/") != (len(t) > 0 and t[0] == "/"):
+        return None
+    bl, tl = len(b), len(t)
+    b0 = bi = t0 = ti = 0
+    while True:
+        while bi < bl and b[bi] != "/":
+            bi += 1
+        while ti < tl and t[ti] != "/":
+            ti += 1
+        if t[t0:ti] != b[b0:bi]:
+            break
+        if bi < bl:
+            bi += 1
+        if ti < tl:
+            ti += 1
+        b0, t0 = bi, ti
+    if b[b0:bi] == "..":
+        return None
+    if b0 != bl:
+        seps = b[b0:bl].count("/")
+        s = ".." + "/.." * seps
+        if t0 != tl:
+            s += "/" + t[t0:]
+        return s
+    return t[t0:]
+
+
+def under_skipped_dir(file_path, skip_dirs):
+    """tar.go:100-111 (an error from Rel ends the search with False, as in Go)."""
+    for sd in skip_dirs:
+        r = rel(sd, file_path)
+        if r is None:
+            return False
+        if not r.startswith("../"):
+            return True
+    return False
+
+
+class LayerTar:
+    """walker.LayerTar (tar.go:23-31, walk.go:25-76)."""
+
+    def __init__(self, skip_files=(), skip_dirs=()):
+        self.skip_files = [clean(f).lstrip("/") for f in skip_files]
+        self.skip_dirs = [clean(d).lstrip("/") for d in list(skip_dirs) + SYSTEM_DIRS]
+
+    def should_skip_file(self, p):
+        return p.lstrip("/") in self.skip_files          # walk.go:48-54
+
+    def should_skip_dir(self, d):
+        d = d.lstrip("/")                                # walk.go:56-71
+        return base(d) in APP_DIRS or d in self.skip_dirs
+
+    def Walk(self, layer, fn):
+        """tar.go:33-84.  `layer` is a binary file object (read sequentially).
+        fn(file_path, size, read) is called for each regular file that is kept;
+        `read()` returns its content.  Returns (opq_dirs, wh_files)."""
+        opq_dirs, wh_files, skip_dirs = [], [], []
+        with tarfile.open(fileobj=layer, mode="r|", encoding="utf-8",
+                          errors="surrogateescape") as tr:
+            for hdr in tr:
+                file_path = clean(hdr.name).lstrip("/")
+                file_dir, file_name = split(file_path)
+                if file_name == OPQ:
+                    opq_dirs.append(file_dir)
+                    continue
+                if file_name.startswith(WH):
+                    wh_files.append(join(file_dir, file_name[len(WH):]))
+                    continue
+                if hdr.type == tarfile.DIRTYPE:
+                    if self.should_skip_dir(file_path):
+                        skip_dirs.append(file_path)
+                        continue
+                elif hdr.type in _REG:
+                    if self.should_skip_file(file_path):
+                        continue
+                else:
+                    continue  # links, devices, fifos, sparse/contiguous: no content
+                if under_skipped_dir(file_path, skip_dirs):
+                    continue
+                if hdr.type == tarfile.DIRTYPE:
+                    continue  # AnalyzeFile returns early for directories (analyzer.go:395)
+                fn(file_path, hdr.size, lambda h=hdr: tr.extractfile(h).read())
+        return opq_dirs, wh_files
+
+
+def analyze_layer(analyzer, layer, device=None, ctx=None, emulate_chunk=0,
+                  batch_bytes=1 << 30, skip_files=(), skip_dirs=()):
+    """Secrets of one image layer: (sorted AnalysisResult.Secrets, opq_dirs, wh_files).
+
+    Files are gated by `Required` on the cleaned path (analyzer.go:400-409) and by
+    `IsBinary` on the header size, then packed into batches of about `batch_bytes` and
+    scanned together (device/ctx: MI355X; emulate_chunk: kernel emulation; else the
+    exact CPU batch path)."""
+    scanner = analyzer.scanner
+    secrets = []
+    pending, pending_bytes = [], 0
+
+    def flush():
+        nonlocal pending, pending_bytes
+        if pending:
+            res = scanner.ScanBatch(pending, device=device, ctx=ctx, emulate_chunk=emulate_chunk)
+            secrets.extend(r for r in res if r["Findings"])
+        pending, pending_bytes = [], 0
+
+    def on_file(file_path, size, read):
+        nonlocal pending_bytes
+        clean_path = file_path.lstrip("/")
+        if not analyzer.Required(clean_path, size):
+            return
+        content = read()
+        if IsBinary(content, size):
+            return
+        inp = AnalysisInput("", file_path, content)
+        pending.append(S.ScanArgs(analyzer._scan_path(inp), content))
+        pending_bytes += len(content)
+        if pending_bytes >= batch_bytes:
+            flush()
+
+    opq, wh = LayerTar(skip_files, skip_dirs).Walk(layer, on_file)
+    flush()
+    return sort_secrets(secrets), opq, wh
