@@ -226,6 +226,33 @@ int tsg_scan_batch_emulated(const tsg_ruleset* rs, const uint8_t* data, const ui
                             uint32_t nfiles, const char* paths, const uint64_t* path_offsets,
                             uint32_t chunk, tsg_result** out);
 
+/* Layer ingest, replaces walker.LayerTar.Walk (pkg/fanal/walker/tar.go:33-84)
+ * + AnalyzerGroup.AnalyzeFile's Required gate (analyzer.go:399-409) + SecretAnalyzer.Required
+ * (analyzer/secret/secret.go:112-150) + utils.IsBinary (utils.go:71-89): walks an uncompressed
+ * layer tar held in memory and packs every file the secret analyzer would scan into one batch
+ * (paths get the "/" prefix of image files, secret.go:90-96).  skip_files / skip_dirs are the
+ * walker's --skip-files / --skip-dirs; config_path the secret config (Required skips its base
+ * name).  A malformed archive is TSG_ERR_ARG ("failed to extract the archive", tar.go:40). */
+typedef struct tsg_layer tsg_layer;
+typedef struct tsg_layer_view {
+  const uint8_t* data;           /* kept files back to back (tsg_batch_upload layout) */
+  const uint64_t* offsets;       /* [nfiles + 1] */
+  uint32_t nfiles;
+  const uint8_t* paths;          /* scan paths back to back */
+  const uint64_t* path_offsets;  /* [nfiles + 1] */
+  const char* opq;               /* opaque dirs, each NUL-terminated (tar.go:48-51) */
+  size_t opq_len;
+  const char* wh;                /* whiteout files, each NUL-terminated (tar.go:53-57) */
+  size_t wh_len;
+  uint32_t walked;               /* regular files the walker handed to the analyzers */
+} tsg_layer_view;
+int tsg_layer_pack(const tsg_ruleset* rs, const uint8_t* tar, uint64_t tar_len,
+                   const char* const* skip_files, uint32_t n_skip_files,
+                   const char* const* skip_dirs, uint32_t n_skip_dirs, const char* config_path,
+                   tsg_layer** out);
+int tsg_layer_get(const tsg_layer* layer, tsg_layer_view* out);
+void tsg_layer_free(tsg_layer* layer);
+
 #ifdef __cplusplus
 }
 #endif

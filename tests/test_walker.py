@@ -164,3 +164,53 @@ def test_seeded_layer_gpu(analyzer):
     want, _, _ = W.analyze_layer(analyzer, io.BytesIO(tar))
     assert [canon_secret(s) for s in got] == [canon_secret(s) for s in want]
     assert len(got) > 100
+
+
+@pytest.mark.parametrize("fmt", [tarfile.PAX_FORMAT, tarfile.GNU_FORMAT, tarfile.USTAR_FORMAT])
+def test_native_layer_pack_matches_walker(analyzer, fmt):
+    """tsg_layer_pack == the Python walker + Required + IsBinary, file for file."""
+    from trivy_amd import configs
+    tars = [configs.layer_tar(1 << 20, seed=7)] if fmt != tarfile.USTAR_FORMAT else []
+    if fmt != tarfile.USTAR_FORMAT:
+        tars.append(layer_bytes(fmt))
+    for tar in tars:
+        want = []
+        opq, wh = W.LayerTar(["/app/skipme.txt"]).Walk(io.BytesIO(tar), lambda p, n, rd: (
+            analyzer.Required(p, n) and not A.IsBinary(c := rd(), n) and want.append(("/" + p, c))))
+        lay = W.NativeLayer(analyzer.scanner, tar, skip_files=["/app/skipme.txt"])
+        b = lay.batch
+        got = [(b.path(i), bytes(b.data[int(b.offsets[i]):int(b.offsets[i + 1])]))
+               for i in range(b.nfiles)]
+        assert got == want
+        assert (lay.opq, lay.wh) == (opq, wh)
+
+
+def test_native_layer_scan(analyzer):
+    from trivy_amd import configs
+    tar = configs.layer_tar(2 << 20, seed=3)
+    got, opq, wh = W.analyze_layer_native(analyzer, tar, emulate_chunk=128)
+    want, opq2, wh2 = W.analyze_layer(analyzer, io.BytesIO(tar))
+    assert [canon_secret(s) for s in got] == [canon_secret(s) for s in want]
+    assert (opq, wh) == (opq2, wh2) and len(got) > 20
+
+
+def test_native_layer_errors(analyzer):
+    from trivy_amd import _native as N
+    tar = layer_bytes()
+    bad = bytearray(tar)
+    bad[148] ^= 0x7  # checksum
+    with pytest.raises(N.NativeError):
+        W.NativeLayer(analyzer.scanner, bytes(bad))
+    with pytest.raises(N.NativeError):
+        W.NativeLayer(analyzer.scanner, tar[:1000])  # truncated data
+    assert W.NativeLayer(analyzer.scanner, b"").batch.nfiles == 0
+
+
+@pytest.mark.gpu
+def test_native_layer_gpu(analyzer):
+    from trivy_amd import configs
+    tar = configs.layer_tar(16 << 20, seed=34)
+    got, _, _ = W.analyze_layer_native(analyzer, tar, device=0)
+    want, _, _ = W.analyze_layer(analyzer, io.BytesIO(tar))
+    assert [canon_secret(s) for s in got] == [canon_secret(s) for s in want]
+    assert len(got) > 100

@@ -48,6 +48,13 @@ class CtxOptions(C.Structure):
                 ("adapt_mib", C.c_uint32)]
 
 
+class LayerView(C.Structure):
+    _fields_ = [("data", C.c_void_p), ("offsets", C.POINTER(C.c_uint64)), ("nfiles", C.c_uint32),
+                ("paths", C.c_void_p), ("path_offsets", C.POINTER(C.c_uint64)),
+                ("opq", C.c_void_p), ("opq_len", C.c_size_t), ("wh", C.c_void_p),
+                ("wh_len", C.c_size_t), ("walked", C.c_uint32)]
+
+
 class Stats(C.Structure):
     _fields_ = [("k1_ms", C.c_double), ("k2_ms", C.c_double), ("aux_ms", C.c_double),
                 ("resolve_ms", C.c_double), ("bytes", C.c_uint64), ("k2_bytes", C.c_uint64),
@@ -103,6 +110,10 @@ SIGNATURES = [
                                       C.POINTER(C.c_uint32), C.c_size_t]),
     ("tsg_emulate_k1", C.c_int, [_P, _P, _U64P, C.c_uint32, C.c_uint32, C.POINTER(C.c_uint32),
                                  C.c_size_t, C.POINTER(C.c_uint32), C.c_size_t]),
+    ("tsg_layer_pack", C.c_int, [_P, _P, C.c_uint64, C.POINTER(C.c_char_p), C.c_uint32,
+                                 C.POINTER(C.c_char_p), C.c_uint32, C.c_char_p, C.POINTER(_P)]),
+    ("tsg_layer_get", C.c_int, [_P, C.POINTER(LayerView)]),
+    ("tsg_layer_free", None, [_P]),
     ("tsg_ruleset_rule_anchor", C.c_int, [_P, C.c_uint32, C.POINTER(C.c_uint32),
                                           C.POINTER(C.c_int64), C.c_char_p, C.c_size_t]),
 ]

@@ -1,0 +1,421 @@
+// Native layer-tar ingest: one pass over an uncompressed image-layer tar
+// that walks it like walker.LayerTar (pkg/fanal/walker/tar.go:33-111, walk.go:25-76),
+// gates every regular file like SecretAnalyzer.Required (analyzer/secret/secret.go:112-150)
+// and utils.IsBinary (utils.go:71-89), and packs the kept files back to back into one
+// batch (the layout tsg_batch_upload / tsg_scan_batch take), with the "/" prefix of image
+// files on their scan paths (secret.go:90-96).  The Python mirror is trivy_amd/walker.py.
+//
+// Tar decoding follows Go 1.19 archive/tar: ustar/PAX/GNU headers, PAX 'x' records
+// (path, linkpath, size), GNU 'L'/'K' long names, TypeRegA -> TypeReg (TypeDir with a
+// trailing "/"), header-only types carry no data, end = a zero block or end of input.
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <functional>
+#include <memory>
+#include <vector>
+
+#include "internal.hpp"
+
+struct tsg_layer {
+  std::unique_ptr<uint8_t[]> data;  // not zero-filled: every byte is copied in
+  std::vector<uint64_t> offsets{0};
+  std::string paths;
+  std::vector<uint64_t> path_offsets{0};
+  std::string opq, wh;  // NUL-terminated lists
+  uint32_t walked = 0;  // files handed to the analyzer (before Required / IsBinary)
+};
+
+namespace tsg {
+namespace {
+
+// Go path.Clean
+std::string clean(const std::string& p) {
+  if (p.empty()) return ".";
+  const bool rooted = p[0] == '/';
+  std::vector<std::string> out;
+  size_t i = 0;
+  while (i <= p.size()) {
+    size_t j = p.find('/', i);
+    if (j == std::string::npos) j = p.size();
+    std::string part = p.substr(i, j - i);
+    i = j + 1;
+    if (part.empty() || part == ".") continue;
+    if (part == "..") {
+      if (!out.empty() && out.back() != "..") out.pop_back();
+      else if (!rooted) out.push_back("..");
+      continue;
+    }
+    out.push_back(part);
+  }
+  std::string s;
+  for (size_t k = 0; k < out.size(); k++) {
+    if (k) s += '/';
+    s += out[k];
+  }
+  if (rooted) return "/" + s;
+  return s.empty() ? "." : s;
+}
+
+std::string trim_left_slash(const std::string& s) {
+  size_t i = 0;
+  while (i < s.size() && s[i] == '/') i++;
+  return s.substr(i);
+}
+
+std::string base(std::string p) {  // Go filepath.Base
+  if (p.empty()) return ".";
+  while (!p.empty() && p.back() == '/') p.pop_back();
+  if (p.empty()) return "/";
+  size_t k = p.rfind('/');
+  return k == std::string::npos ? p : p.substr(k + 1);
+}
+
+// Go filepath.Rel on "/" paths; false where Go returns an error
+bool rel(const std::string& basepath, const std::string& targpath, std::string* out) {
+  std::string b = clean(basepath), t = clean(targpath);
+  if (t == b) {
+    *out = ".";
+    return true;
+  }
+  if (b == ".") b.clear();
+  if ((!b.empty() && b[0] == '/') != (!t.empty() && t[0] == '/')) return false;
+  const size_t bl = b.size(), tl = t.size();
+  size_t b0 = 0, bi = 0, t0 = 0, ti = 0;
+  for (;;) {
+    while (bi < bl && b[bi] != '/') bi++;
+    while (ti < tl && t[ti] != '/') ti++;
+    if (t.compare(t0, ti - t0, b, b0, bi - b0) != 0) break;
+    if (bi < bl) bi++;
+    if (ti < tl) ti++;
+    b0 = bi;
+    t0 = ti;
+  }
+  if (b.compare(b0, bi - b0, "..") == 0) return false;
+  if (b0 != bl) {
+    size_t seps = 0;
+    for (size_t k = b0; k < bl; k++) seps += b[k] == '/';
+    std::string s = "..";
+    for (size_t k = 0; k < seps; k++) s += "/..";
+    if (t0 != tl) s += "/" + t.substr(t0);
+    *out = s;
+    return true;
+  }
+  *out = t.substr(t0);
+  return true;
+}
+
+bool starts_with(const std::string& s, const char* p) { return s.rfind(p, 0) == 0; }
+
+bool contains(const std::vector<std::string>& v, const std::string& s) {
+  for (const auto& x : v)
+    if (x == s) return true;
+  return false;
+}
+
+// tar numeric field: octal (spaces / NULs trimmed) or GNU base-256
+bool parse_num(const uint8_t* f, size_t n, int64_t* out) {
+  if (n && (f[0] & 0x80)) {
+    if (f[0] & 0x40) return false;  // negative
+    uint64_t v = f[0] & 0x7f;
+    for (size_t i = 1; i < n; i++) {
+      if (v >> 55) return false;
+      v = (v << 8) | f[i];
+    }
+    *out = (int64_t)v;
+    return true;
+  }
+  size_t a = 0, b = n;
+  while (a < b && (f[a] == ' ' || f[a] == 0)) a++;
+  while (b > a && (f[b - 1] == ' ' || f[b - 1] == 0)) b--;
+  uint64_t v = 0;
+  for (size_t i = a; i < b; i++) {
+    if (f[i] < '0' || f[i] > '7') return false;
+    v = v * 8 + (f[i] - '0');
+  }
+  *out = (int64_t)v;
+  return true;
+}
+
+std::string cstr(const uint8_t* f, size_t n) {
+  size_t k = 0;
+  while (k < n && f[k]) k++;
+  return std::string((const char*)f, k);
+}
+
+bool checksum_ok(const uint8_t* h) {
+  int64_t want;
+  if (!parse_num(h + 148, 8, &want)) return false;
+  int64_t u = 0, s = 0;
+  for (int i = 0; i < 512; i++) {
+    const uint8_t c = (i >= 148 && i < 156) ? ' ' : h[i];
+    u += c;
+    s += (int8_t)c;
+  }
+  return want == u || want == s;
+}
+
+bool header_only(char t) {  // archive/tar isHeaderOnlyType
+  return t == '1' || t == '2' || t == '3' || t == '4' || t == '5' || t == '6';
+}
+
+// PAX records "len key=value\n"
+bool parse_pax(const uint8_t* p, size_t n, std::vector<std::pair<std::string, std::string>>* recs) {
+  size_t i = 0;
+  while (i < n) {
+    size_t sp = i;
+    uint64_t len = 0;
+    while (sp < n && p[sp] >= '0' && p[sp] <= '9') len = len * 10 + (p[sp++] - '0');
+    if (sp >= n || p[sp] != ' ' || len == 0 || i + len > n || p[i + len - 1] != '\n') return false;
+    std::string rec((const char*)p + sp + 1, i + len - 1 - (sp + 1));
+    size_t eq = rec.find('=');
+    if (eq == std::string::npos) return false;
+    recs->emplace_back(rec.substr(0, eq), rec.substr(eq + 1));
+    i += len;
+  }
+  return true;
+}
+
+struct Gate {  // SecretAnalyzer.Required (secret.go:112-150) + walker skip lists
+  const Ruleset& rs;
+  const Plan* plan;
+  std::string config_base;
+  std::vector<std::string> skip_files, skip_dirs;
+
+  bool required(const std::string& fp, int64_t size) const {
+    static const std::vector<std::string> kSkipFiles = {
+        "go.mod", "go.sum", "package-lock.json", "yarn.lock", "pnpm-lock.yaml", "Pipfile.lock",
+        "Gemfile.lock"};  // secret.go:27-35
+    static const std::vector<std::string> kSkipDirs = {".git", "node_modules"};  // :36
+    static const std::vector<std::string> kSkipExts = {
+        ".jpg", ".png", ".gif", ".doc", ".pdf", ".bin", ".svg", ".socket", ".deb", ".rpm",
+        ".zip", ".gz", ".gzip", ".tar", ".pyc"};  // :37-40
+    if (size < 10) return false;
+    const size_t k = fp.rfind('/');
+    const std::string dir = k == std::string::npos ? "" : fp.substr(0, k + 1);
+    const std::string name = k == std::string::npos ? fp : fp.substr(k + 1);
+    size_t i = 0;
+    for (;;) {  // strings.Split(dir, "/")
+      size_t j = dir.find('/', i);
+      const std::string part = dir.substr(i, j == std::string::npos ? std::string::npos : j - i);
+      if (contains(kSkipDirs, part)) return false;
+      if (j == std::string::npos) break;
+      i = j + 1;
+    }
+    if (contains(kSkipFiles, name)) return false;
+    if (config_base == fp) return false;
+    std::string ext;
+    for (size_t e = name.size(); e-- > 0;)
+      if (name[e] == '.') {
+        ext = name.substr(e);
+        break;
+      }
+    if (contains(kSkipExts, ext)) return false;
+    return !path_allowed(rs, plan, fp.data(), fp.size());
+  }
+};
+
+bool is_binary(const uint8_t* p, int64_t n) {  // utils.go:71-89
+  const int64_t h = n < 300 ? n : 300;
+  for (int64_t i = 0; i < h; i++) {
+    const uint8_t b = p[i];
+    if (b < 7 || b == 11 || (13 < b && b < 27) || (27 < b && b < 0x20) || b == 0x7f) return true;
+  }
+  return false;
+}
+
+}  // namespace
+}  // namespace tsg
+
+using namespace tsg;
+
+extern "C" int tsg_layer_pack(const tsg_ruleset* rs, const uint8_t* tar, uint64_t tar_len,
+                              const char* const* skip_files, uint32_t n_skip_files,
+                              const char* const* skip_dirs, uint32_t n_skip_dirs,
+                              const char* config_path, tsg_layer** out) {
+  if (!rs || !out || (!tar && tar_len)) return fail(TSG_ERR_ARG, "bad argument");
+  *out = nullptr;
+  try {
+    Gate g{rs->rs, rs->plan.get(), base(config_path ? config_path : ""), {}, {}};
+    for (uint32_t i = 0; i < n_skip_files; i++)  // walk.go:25-33
+      g.skip_files.push_back(trim_left_slash(clean(skip_files[i])));
+    std::vector<std::string> sd;
+    for (uint32_t i = 0; i < n_skip_dirs; i++) sd.push_back(skip_dirs[i]);
+    for (const char* s : {"proc", "sys", "dev"}) sd.push_back(s);  // walk.go:15
+    for (const auto& s : sd) g.skip_dirs.push_back(trim_left_slash(clean(s)));
+
+    const auto t0 = std::chrono::steady_clock::now();
+    auto L = std::make_unique<tsg_layer>();
+    struct Walked {
+      uint64_t dpos, size;
+      std::string fp;
+    };
+    std::vector<Walked> walked;
+    std::vector<std::string> skipped;  // tar.go:35 skipDirs
+    std::string long_name;
+    bool have_long = false;
+    std::vector<std::pair<std::string, std::string>> pax;
+    uint64_t pos = 0;
+    auto bad = [&](const char* what) {
+      return fail(TSG_ERR_ARG, std::string("failed to extract the archive: ") + what);
+    };
+    auto zero_block = [&](uint64_t p) {
+      for (int i = 0; i < 512; i++)
+        if (tar[p + i]) return false;
+      return true;
+    };
+    for (;;) {  // archive/tar Reader.readHeader
+      if (pos == tar_len) break;
+      if (tar_len - pos < 512) return bad("unexpected EOF");
+      const uint8_t* h = tar + pos;
+      if (zero_block(pos)) {  // end: two zero blocks (or one, then end of input)
+        const uint64_t p2 = pos + 512;
+        if (p2 == tar_len) break;
+        if (tar_len - p2 < 512) return bad("unexpected EOF");
+        if (zero_block(p2)) break;
+        return bad("invalid header");
+      }
+      if (!checksum_ok(h)) return bad("invalid header");
+      int64_t size;
+      if (!parse_num(h + 124, 12, &size) || size < 0) return bad("invalid size");
+      char type = (char)h[156];
+      const bool ustar = std::memcmp(h + 257, "ustar\0" "00", 8) == 0;
+      std::string name = cstr(h, 100);
+      if (ustar) {
+        const std::string prefix = cstr(h + 345, 155);
+        if (!prefix.empty()) name = prefix + "/" + name;
+      }
+      const uint64_t dpos = pos + 512;
+      if (type == 'x' || type == 'L' || type == 'K') {
+        if (dpos + (uint64_t)size > tar_len) return bad("unexpected EOF");
+        if (type == 'x') {
+          if (!parse_pax(tar + dpos, (size_t)size, &pax)) return bad("invalid PAX record");
+        } else if (type == 'L') {
+          long_name = cstr(tar + dpos, (size_t)size);
+          have_long = true;
+        }
+        pos = dpos + (((uint64_t)size + 511) & ~511ull);
+        continue;
+      }
+      if (have_long) name = long_name;
+      for (const auto& kv : pax) {
+        if (kv.first == "path") name = kv.second;
+        else if (kv.first == "size") {
+          int64_t v = 0;
+          for (char c : kv.second) {
+            if (c < '0' || c > '9') return bad("invalid PAX size");
+            v = v * 10 + (c - '0');
+          }
+          size = v;
+        }
+      }
+      pax.clear();
+      have_long = false;
+      if (type == 0) type = (!name.empty() && name.back() == '/') ? '5' : '0';
+      const uint64_t dlen = header_only(type) ? 0 : (uint64_t)size;
+      if (dpos + dlen > tar_len) return bad("unexpected EOF");
+      pos = dpos + ((dlen + 511) & ~511ull);
+
+      // tar.go:45-84
+      const std::string fp = trim_left_slash(clean(name));
+      const size_t k = fp.rfind('/');
+      const std::string fdir = k == std::string::npos ? "" : fp.substr(0, k + 1);
+      const std::string fname = k == std::string::npos ? fp : fp.substr(k + 1);
+      if (fname == ".wh..wh..opq") {
+        L->opq += fdir;
+        L->opq += '\0';
+        continue;
+      }
+      if (starts_with(fname, ".wh.")) {
+        std::string j = fdir + fname.substr(4);
+        L->wh += j.empty() ? j : clean(j);
+        L->wh += '\0';
+        continue;
+      }
+      if (type == '5') {
+        const std::string d = trim_left_slash(fp);
+        if (base(d) == ".git" || contains(g.skip_dirs, d)) {  // walk.go:56-71
+          skipped.push_back(fp);
+          continue;
+        }
+      } else if (type == '0') {
+        if (contains(g.skip_files, trim_left_slash(fp))) continue;
+      } else {
+        continue;  // links, devices, fifos, sparse, contiguous: no content
+      }
+      bool under = false;  // tar.go:100-111
+      for (const auto& s : skipped) {
+        std::string r;
+        if (!rel(s, fp, &r)) break;
+        if (!starts_with(r, "../")) {
+          under = true;
+          break;
+        }
+      }
+      if (under || type == '5') continue;
+      L->walked++;
+      walked.push_back({dpos, (uint64_t)size, fp});
+    }
+    // AnalyzerGroup.AnalyzeFile (analyzer.go:399-409) + SecretAnalyzer.Analyze: the gates of
+    // the walked files in parallel (Required's AllowPath is the costly part), then the
+    // kept files copied into the batch in parallel
+    auto now = [] { return std::chrono::steady_clock::now(); };
+    const bool prof = getenv("TSG_LAYER_PROF") != nullptr;
+    auto t1 = now();
+    const size_t n = walked.size();
+    const int T = 16;  // the process-wide host pool (plan.cpp)
+    std::vector<uint8_t> keep(n);
+    auto par = [&](const std::function<void(size_t)>& fn) { pool_for(n, T, fn, 64); };
+    par([&](size_t i) {
+      const Walked& w = walked[i];
+      keep[i] = g.required(w.fp, (int64_t)w.size) && !is_binary(tar + w.dpos, (int64_t)w.size);
+    });
+    auto t2 = now();
+    std::vector<uint64_t> dst(n);
+    uint64_t total = 0;
+    for (size_t i = 0; i < n; i++)
+      if (keep[i]) {
+        dst[i] = total;
+        total += walked[i].size;
+        L->offsets.push_back(total);
+        L->paths += '/';
+        L->paths += walked[i].fp;
+        L->path_offsets.push_back(L->paths.size());
+      }
+    L->data.reset(new uint8_t[total ? total : 1]);
+    par([&](size_t i) {
+      if (keep[i] && walked[i].size) std::memcpy(L->data.get() + dst[i], tar + walked[i].dpos, walked[i].size);
+    });
+    if (prof)
+      fprintf(stderr, "layer: walk %.1f ms, gates %.1f ms, pack %.1f ms (%d threads)\n",
+              std::chrono::duration<double, std::milli>(t1 - t0).count(),
+              std::chrono::duration<double, std::milli>(t2 - t1).count(),
+              std::chrono::duration<double, std::milli>(now() - t2).count(), T);
+    *out = L.release();
+    return TSG_OK;
+  } catch (const std::bad_alloc&) {
+    return fail(TSG_ERR_NOMEM, "out of memory");
+  } catch (const std::exception& e) {
+    return fail(TSG_ERR_INTERNAL, e.what());
+  }
+}
+
+extern "C" int tsg_layer_get(const tsg_layer* L, tsg_layer_view* v) {
+  if (!L || !v) return fail(TSG_ERR_ARG, "bad argument");
+  v->data = L->offsets.back() ? L->data.get() : nullptr;
+  v->offsets = L->offsets.data();
+  v->nfiles = (uint32_t)(L->offsets.size() - 1);
+  v->paths = (const uint8_t*)L->paths.data();
+  v->path_offsets = L->path_offsets.data();
+  v->opq = L->opq.data();
+  v->opq_len = L->opq.size();
+  v->wh = L->wh.data();
+  v->wh_len = L->wh.size();
+  v->walked = L->walked;
+  return TSG_OK;
+}
+
+extern "C" void tsg_layer_free(tsg_layer* L) { delete L; }

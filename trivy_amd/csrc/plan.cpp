@@ -499,7 +499,7 @@ void pool_for(size_t n, int nthreads, const std::function<void(size_t)>& f, size
   parallel_for(n, nthreads, f, grain);
 }
 
-static bool path_allowed(const Ruleset& rs, const Plan* plan, const char* p, size_t n) {
+bool path_allowed(const Ruleset& rs, const Plan* plan, const char* p, size_t n) {
   if (plan && plan->allow_path_dfa) {
     bool ascii = true;
     for (size_t i = 0; i < n && ascii; i++) ascii = (uint8_t)p[i] < 0x80;

@@ -111,6 +111,9 @@ void serialize_batch(const BatchResult& br, std::string* out, int nthreads = 1);
 
 // f(i) for i in [0, n) on the process-wide worker pool (plan.cpp), `grain` indices a claim
 void pool_for(size_t n, int nthreads, const std::function<void(size_t)>& f, size_t grain);
+// Global.AllowPath (scanner.go:55-57): the plan's path DFA for ASCII paths, else the exact VM
+struct Plan;
+bool path_allowed(const Ruleset& rs, const Plan* plan, const char* p, size_t n);
 void serialize_results(const std::vector<FileResult>& res, std::string* out);
 
 }  // namespace tsg

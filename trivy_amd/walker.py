@@ -2,6 +2,8 @@
 (pkg/fanal/walker/tar.go, walk.go) feeding the batched analyzer.
 
   LayerTar(skip_files, skip_dirs).Walk(layer, fn)   walker/tar.go:33-84
+  NativeLayer(scanner, tar_bytes, ...)             the same walk + Required + IsBinary in C++
+                                                    (tsg_layer_pack), packed into one batch
   analyze_layer(analyzer, layer, ...)               walker.Walk + AnalyzerGroup.AnalyzeFile
                                                     (analyzer.go:395-445) + SecretAnalyzer,
                                                     with the files of a layer packed into
@@ -16,8 +18,12 @@ image files (secret.go:90-96), and `IsBinary` uses the header size (secret.go:80
 Go's path helpers (filepath.Clean / Split / Join / Rel / Base on "/" paths) are restated
 below because Python's posixpath differs on "//" prefixes, empty paths and "..".
 """
+import ctypes as C
 import tarfile
 
+import numpy as np
+
+from . import _native as N
 from .analyzer import AnalysisInput, IsBinary, sort_secrets
 from . import secret as S
 
@@ -203,3 +209,51 @@ def analyze_layer(analyzer, layer, device=None, ctx=None, emulate_chunk=0,
     opq, wh = LayerTar(skip_files, skip_dirs).Walk(layer, on_file)
     flush()
     return sort_secrets(secrets), opq, wh
+
+
+class NativeLayer:
+    """tsg_layer_pack: the walk, `Required` and `IsBinary` of a whole in-memory layer tar in
+    one native pass; `.batch` views the packed files without a copy (valid while this
+    object lives).  `.opq` / `.wh` are the walker's opaque dirs and whiteout files."""
+
+    def __init__(self, scanner, tar, skip_files=(), skip_dirs=(), config_path=""):
+        L = N.lib()
+        self._h = None
+        self._tar = np.frombuffer(tar, dtype=np.uint8) if len(tar) else np.zeros(1, np.uint8)
+        enc = lambda xs: (C.c_char_p * max(1, len(xs)))(
+            *[x.encode("utf-8", "surrogateescape") for x in xs])
+        sf, sd = enc(list(skip_files)), enc(list(skip_dirs))
+        h = C.c_void_p()
+        N.check(L.tsg_layer_pack(scanner.handle, C.c_void_p(self._tar.ctypes.data), len(tar),
+                                 sf, len(skip_files), sd, len(skip_dirs),
+                                 config_path.encode("utf-8", "surrogateescape"), C.byref(h)))
+        self._h = h
+        v = N.LayerView()
+        N.check(L.tsg_layer_get(h, C.byref(v)))
+        n = v.nfiles
+        as_u64 = lambda p: np.ctypeslib.as_array(p, shape=(n + 1,))
+        offs, poffs = as_u64(v.offsets), as_u64(v.path_offsets)
+        as_u8 = lambda p, k: (np.ctypeslib.as_array(C.cast(p, C.POINTER(C.c_uint8)), shape=(k,))
+                              if p and k else np.zeros(1, np.uint8))
+        self.batch = S.Batch(as_u8(v.data, int(offs[-1])), offs, as_u8(v.paths, int(poffs[-1])),
+                             poffs)
+        self.batch._owner = self
+        lst = lambda p, k: [x.decode("utf-8", "surrogateescape")
+                            for x in C.string_at(p, k).split(b"\0")[:-1]] if k else []
+        self.opq = lst(v.opq, v.opq_len)
+        self.wh = lst(v.wh, v.wh_len)
+        self.walked = v.walked
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            N.lib().tsg_layer_free(self._h)
+            self._h = None
+
+
+def analyze_layer_native(analyzer, tar, device=None, ctx=None, emulate_chunk=0,
+                         skip_files=(), skip_dirs=()):
+    """analyze_layer over an in-memory tar with the native ingest (one batch per layer)."""
+    lay = NativeLayer(analyzer.scanner, tar, skip_files, skip_dirs, analyzer.configPath)
+    res = analyzer.scanner.ScanBatch(lay.batch, device=device, ctx=ctx,
+                                     emulate_chunk=emulate_chunk) if lay.batch.nfiles else []
+    return sort_secrets([r for r in res if r["Findings"]]), lay.opq, lay.wh
