@@ -63,3 +63,41 @@ def test_two_ranks_gloo(tmp_path):
     outs = [p.communicate(timeout=300)[0] for p in procs]
     assert all(p.returncode == 0 for p in procs), outs
     assert "OK" in outs[0]
+
+
+LAYER_WORKER = textwrap.dedent("""
+    import io, sys
+    sys.path.insert(0, %(root)r)
+    import torch.distributed as dist
+    from tests.helpers import canon_secret
+    from trivy_amd import analyzer as A, configs, secret as S, walker as W
+    from trivy_amd.shard import scan_layer_sharded
+    dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%(port)d",
+                            rank=int(sys.argv[1]), world_size=2)
+    tar = configs.layer_tar(1 << 20, seed=21)
+    an = A.SecretAnalyzer(S.NewScanner(None), "")
+    out = scan_layer_sharded(an, tar, dist.get_rank(), 2, dist=dist, emulate_chunk=64)
+    if dist.get_rank() == 0:
+        got, opq, wh = out
+        want, opq2, wh2 = W.analyze_layer(an, io.BytesIO(tar))
+        assert [canon_secret(s) for s in got] == [canon_secret(s) for s in want]
+        assert (opq, wh) == (opq2, wh2) and len(got) > 10
+        print("OK", len(got))
+    else:
+        assert out is None
+    dist.destroy_process_group()
+""")
+
+
+def test_two_ranks_layer_gloo(tmp_path):
+    """configs[2]: one layer's files sharded over 2 ranks == the single-process layer scan."""
+    port = _free_port()
+    script = tmp_path / "wl.py"
+    script.write_text(LAYER_WORKER % {"root": ROOT, "port": port})
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    procs = [subprocess.Popen([sys.executable, str(script), str(r)], cwd=ROOT, env=env,
+                              stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+             for r in range(2)]
+    outs = [p.communicate(timeout=300)[0] for p in procs]
+    assert all(p.returncode == 0 for p in procs), outs
+    assert "OK" in outs[0]

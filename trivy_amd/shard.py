@@ -47,10 +47,30 @@ def scan_sharded(scanner, args, rank, world, dist=None, device=None, emulate_chu
     return res
 
 
+def scan_layer_sharded(analyzer, tar, rank, world, dist=None, device=None, emulate_chunk=0,
+                       skip_files=(), skip_dirs=()):
+    """BASELINE configs[2]: one image layer's files sharded over `world` ranks.
+
+    Every rank walks the (same) in-memory layer tar natively (tsg_layer_pack: the walk,
+    `Required`, `IsBinary`), takes its LPT share of the kept files by bytes and scans it;
+    rank 0 returns (sorted AnalysisResult.Secrets, opq_dirs, wh_files), others None."""
+    from .walker import NativeLayer
+    lay = NativeLayer(analyzer.scanner, tar, skip_files, skip_dirs, analyzer.configPath)
+    b = lay.batch
+    offs = [int(x) for x in b.offsets]
+    args = [S.ScanArgs(b.path(i), b.data[offs[i]:offs[i + 1]].tobytes())
+            for i in range(b.nfiles)]
+    res = scan_sharded(analyzer.scanner, args, rank, world, dist=dist, device=device,
+                       emulate_chunk=emulate_chunk)
+    if res is None:
+        return None
+    return findings_sorted(res), lay.opq, lay.wh
+
+
 def findings_sorted(results):
     """The secrets of AnalysisResult after Sort: files with findings, by path."""
     from .analyzer import sort_secrets
     return sort_secrets([r for r in results if r and r["Findings"]])
 
 
-__all__ = ["lpt_shards", "scan_sharded", "findings_sorted", "S"]
+__all__ = ["lpt_shards", "scan_sharded", "scan_layer_sharded", "findings_sorted", "S"]
