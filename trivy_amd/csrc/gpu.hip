@@ -1049,15 +1049,36 @@ struct K1Host {  // host copies of the K1 tables (adaptation rebuilds the device
   std::vector<uint16_t> tab, accs;
   std::vector<uint32_t> masks;
   std::vector<uint32_t> order;  // device state id -> automaton state
+  uint32_t stride = 0;          // row stride of tab (>= the class count)
 };
 
 // Device numbering of the K1 automaton: states whose arrival is reported (they end a
 // literal, and are not `quiet`) last; rows = id * nc.
+// Row stride (u16 entries) of the K1 table: the class count padded to 2 mod 4, so a row is
+// an odd number of dwords and equal classes of different rows fall in different LDS banks
+// (ds_read_u16 banks are dword mod 32).  Padding is skipped when it would need a larger LDS
+// image or overflow the 16-bit rows.  TSG_K1_STRIDE=0 turns it off (measurements).
+static size_t k1_stride(size_t nc, size_t ns) {
+  const char* e = getenv("TSG_K1_STRIDE");
+  if (e && atoi(e) == 0) return nc;
+  size_t rs = nc;
+  while (rs % 4 != 2) rs++;
+  auto lds_class = [&](size_t r) {
+    for (int k = 0; k < 3; k++)
+      if (ns * r * 2 + 2 + 1024 <= (size_t)kK1Lds[k] * 1024) return k;
+    return 3;
+  };
+  if ((ns - 1) * rs > 0xFFFF || lds_class(rs) != lds_class(nc)) return nc;
+  return rs;
+}
+
 static int k1_tables(const Plan& p, const std::vector<uint8_t>& quiet, K1Host* h, uint32_t* start_row,
                      uint32_t* acc_row) {
   const DFA& d = *p.kw_dfa;
   const size_t nc = d.nclasses, ns = d.nstates;
-  if ((ns - 1) * nc > 0xFFFF) return fail(TSG_ERR_INTERNAL, "keyword automaton too large for 16-bit rows");
+  const size_t rs = k1_stride(nc, ns);
+  h->stride = (uint32_t)rs;
+  if ((ns - 1) * rs > 0xFFFF) return fail(TSG_ERR_INTERNAL, "keyword automaton too large for 16-bit rows");
   std::vector<uint32_t> newid(ns);
   h->order.clear();
   for (int pass = 0; pass < 2; pass++)
@@ -1076,15 +1097,15 @@ static int k1_tables(const Plan& p, const std::vector<uint8_t>& quiet, K1Host* h
       break;
     }
   }
-  h->tab.assign(ns * nc + (ns * nc & 1), 0);  // the kernel stages whole dwords
+  h->tab.assign(ns * rs + (ns * rs & 1), 0);  // the kernel stages whole dwords
   h->accs.assign(ns, 0);
   for (size_t i = 0; i < ns; i++) {
     const uint32_t st = h->order[i];
     h->accs[i] = (uint16_t)d.eot_acc[st];
-    for (size_t c = 0; c < nc; c++) h->tab[i * nc + c] = (uint16_t)(newid[d.next[st * nc + c]] * nc);
+    for (size_t c = 0; c < nc; c++) h->tab[i * rs + c] = (uint16_t)(newid[d.next[st * nc + c]] * rs);
   }
-  *start_row = newid[d.start[kCtxBOT]] * (uint32_t)nc;
-  *acc_row = first_rep * (uint32_t)nc;
+  *start_row = newid[d.start[kCtxBOT]] * (uint32_t)rs;
+  *acc_row = first_rep * (uint32_t)rs;
   return TSG_OK;
 }
 
@@ -1113,7 +1134,7 @@ static int make_device_k1(const Plan& p, DevK1* out, std::vector<void*>* allocs,
   if ((rc = upload_vec(cls, &v.cls, allocs))) return rc;
   if ((rc = upload_vec(host->accs, &v.accs, allocs))) return rc;
   if ((rc = upload_vec(masks, &v.masks, allocs))) return rc;
-  v.nc = (uint32_t)nc;
+  v.nc = host->stride;  // the kernel's row stride
   v.ns = (uint32_t)d.nstates;
   v.nmasks = (uint32_t)d.masks.size();
   v.mw = mw;
