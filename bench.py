@@ -34,7 +34,7 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 # FETCH_SIZE of the same command (rocprofv3 --pmc FETCH_SIZE), committed under profiles/
-PMC_FETCH_CSV = os.path.join(ROOT, "profiles", "r01", "bench_10gib_pmc_fetch_v8.csv")
+PMC_FETCH_CSV = os.path.join(ROOT, "profiles", "r01", "bench_10gib_pmc_fetch_v9.csv")
 
 
 def _dist():
