@@ -141,6 +141,8 @@ def main():
     ap.add_argument("--seed", type=int, default=2)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--depth", type=int, default=4, help="pipelined scans in flight")
+    ap.add_argument("--host-threads", type=int, default=0,
+                    help="host resolution pool threads (0: library default, 16)")
     args = ap.parse_args()
 
     dist, rank, world, local = _dist()
@@ -153,7 +155,7 @@ def main():
     gen_s = time.perf_counter() - t0
     sc = S.NewScanner(None)
     dev = local if world > 1 else 0
-    ctx = S.GpuContext(sc, dev, chunk_bytes=args.chunk)
+    ctx = S.GpuContext(sc, dev, chunk_bytes=args.chunk, host_threads=args.host_threads)
     t0 = time.perf_counter()
     ctx.upload(batch)
     upload_s = time.perf_counter() - t0
