@@ -34,7 +34,7 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 # FETCH_SIZE of the same command (rocprofv3 --pmc FETCH_SIZE), committed under profiles/
-PMC_FETCH_CSV = os.path.join(ROOT, "profiles", "r01", "bench_10gib_pmc_fetch_v9.csv")
+PMC_FETCH_CSV = os.path.join(ROOT, "profiles", "r01", "bench_10gib_pmc_fetch_v10.csv")
 
 
 def _dist():
@@ -134,8 +134,8 @@ def cpu_native(sc, batch, max_bytes=256 << 20, nthreads=16):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--gb", type=float, default=10.0, help="GiB of corpus per rank")
     ap.add_argument("--chunk", type=int, default=0)
     ap.add_argument("--seed", type=int, default=2)
