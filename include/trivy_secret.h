@@ -117,6 +117,14 @@ int tsg_scan_cpu_batch(const tsg_ruleset* rs, const uint8_t* data, const uint64_
                        int nthreads, tsg_result** out);
 
 const uint8_t* tsg_result_data(const tsg_result* r, size_t* len);
+
+/* sort.Slice with Go 1.19's pdqsort_func (unstable; ties ordered exactly as Go orders them)
+ * of n items by (key bytes as a Go string, then secondary if not NULL): perm[k] = index of
+ * the k-th item.  Replaces the secret part of AnalysisResult.Sort
+ * (pkg/fanal/analyzer/analyzer.go:212-223): files by FilePath, findings by (RuleID,
+ * StartLine). */
+int tsg_go_sort_perm(const uint8_t* keys, const uint64_t* key_offsets, const int64_t* secondary,
+                     uint32_t n, uint32_t* perm);
 void tsg_result_free(tsg_result* r);
 
 /* ---- GPU (one context per device; one process per GPU) ---- */

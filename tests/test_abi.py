@@ -64,3 +64,21 @@ def test_bad_arguments():
     assert L.tsg_batch_scan(None, None) == N.TSG_ERR_ARG
     assert L.tsg_batch_collect(None, None) == N.TSG_ERR_ARG
     assert L.tsg_batch_pending(None) == N.TSG_ERR_ARG
+
+
+def test_go_sort_perm_matches_oracle_with_ties():
+    """tsg_go_sort_perm (the product's AnalysisResult.Sort) against the oracle's restated
+    Go 1.19 pdqsort_func on findings with many (RuleID, StartLine) ties, where an unstable
+    sort's order depends on the algorithm."""
+    import random
+    from oracle import secret as O
+    from trivy_amd import analyzer as A
+    rnd = random.Random(5)
+    for n in (3, 13, 40, 200):
+        fs = [{"RuleID": rnd.choice(["a", "b", "aws", "aws-x"]), "StartLine": rnd.randint(1, 3),
+               "Match": "m%d" % i} for i in range(n)]
+        mine = [{"FilePath": "p%d" % (n - i), "Findings": [dict(f) for f in fs]} for i in range(3)]
+        want = [{"FilePath": "p%d" % (n - i), "Findings": [dict(f) for f in fs]} for i in range(3)]
+        A.sort_secrets(mine)
+        O.sort_secrets(want)
+        assert mine == want

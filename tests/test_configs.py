@@ -48,3 +48,39 @@ def test_allow_exclude_binary_emulation_vs_exact():
     n = sum(len(x["Findings"] or []) for x in want)
     assert n > 5
     assert any("blob/" in x.get("FilePath", "") for x in want if x["Findings"])
+
+
+def _vs_oracle(doc, args, got):
+    from oracle import secret as O
+    from tests.helpers import canon_secret
+    osc = O.NewScanner(O.config_from_dict(doc))
+    n = 0
+    for a, g in zip(args, got):
+        want = canon_secret(osc.Scan(a.FilePath, a.Content))
+        assert canon_secret(g) == want, a.FilePath
+        n += len(want["Findings"] or [])
+    return n
+
+
+@pytest.fixture(scope="module")
+def user1000():
+    doc = configs.user_rules_doc(1000, seed=4)
+    return doc, S.NewScanner(S.config_from_dict(doc))
+
+
+def test_user_rules_1000_emulation_vs_oracle(user1000):
+    """configs[3] at its stated size (1,000 user rules): the GPU algorithm, emulated,
+    file by file against the oracle (not the product's own CPU path)."""
+    doc, sc = user1000
+    args = configs.mixed_batch(doc, 128 << 10, seed=71, plants_per_file=0.6)
+    got = sc.ScanBatch(args, emulate_chunk=256)
+    assert _vs_oracle(doc, args, got) > 10
+
+
+def test_allow_exclude_binary_emulation_vs_oracle():
+    doc = configs.allow_exclude_doc()
+    sc = S.NewScanner(S.config_from_dict(doc))
+    args = configs.mixed_batch(doc, 192 << 10, seed=72, plants_per_file=0.5, binary_frac=0.3)
+    args = [a for a in args if not A.IsBinary(a.Content, len(a.Content))]
+    got = sc.ScanBatch(args, emulate_chunk=64)
+    assert _vs_oracle(doc, args, got) > 5

@@ -16,9 +16,6 @@ from tests.helpers import canon_secret
 from trivy_amd import corpus
 from trivy_amd import secret as S
 
-FOLD = {ord("k"): "K", ord("K"): "K", ord("s"): "ſ", ord("S"): "ſ",
-        ord("i"): "İ", ord("I"): "İ"}
-
 
 @pytest.fixture(scope="module")
 def builtin():
@@ -26,37 +23,7 @@ def builtin():
 
 
 def fold_corpus(seed, nbytes=1 << 20, plants=300, frac=0.3):
-    """Seeded corpus; in `frac` of the files some k/s/i letters become folding runes,
-    mostly inside and around planted secrets and keywords."""
-    rng = np.random.default_rng(seed)
-    b, _ = corpus.make_corpus(nbytes, seed=seed, plants_per_mib=plants)
-    args = []
-    for i in range(b.nfiles):
-        c = bytes(b.data[int(b.offsets[i]):int(b.offsets[i + 1])])
-        if rng.random() < frac and len(c) > 0:
-            t = bytearray()
-            p = float(rng.choice([0.002, 0.02, 0.2]))
-            for ch in c:
-                if ch in FOLD and rng.random() < p:
-                    t += FOLD[ch].encode()
-                else:
-                    t.append(ch)
-            c = bytes(t)
-        args.append(S.ScanArgs(b.path(i), c))
-    # hand-made files: a fold rune inside the secret / keyword of common rules
-    hand = [
-        "aws_secret_access_Key = \"12ASD34qwe56CXZ78tyH10Tna543VBokN85RHCas\"\n",
-        "AWS_ſECRET_ACCESS_KEY=12ASD34qwe56CXZ78tyH10Tna543VBokN85RHCas\n",
-        "ghp_0123456789abcdefghijKlmnopqrstuvwxyz\n",
-        "İntercom_api_token = \"" + "a" * 60 + "\"\n",
-        "gitlab_ſecret glpat-0123456789abcdefghij\n",
-        "-----BEGIN RSA PRIVATE KEY-----\nMIIEabc\n-----END RSA PRIVATE KEY-----\n",
-        "twitch_api_Key = '" + "x" * 30 + "'\n",
-        "facebook_token = '" + "a" * 31 + "K'\n",
-    ]
-    for j, h in enumerate(hand):
-        args.append(S.ScanArgs("hand/f%d.txt" % j, h.encode()))
-    return S.Batch.from_args(args)
+    return corpus.fold_runes_batch(seed, nbytes=nbytes, plants=plants, frac=frac)
 
 
 @pytest.mark.parametrize("chunk", [16, 64, 256])

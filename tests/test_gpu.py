@@ -182,3 +182,57 @@ def test_stats_report_kernels(builtin):
     st = ctx.stats()
     ctx.close()
     assert st["k1_ms"] > 0 and st["k2_ms"] > 0 and st["bytes"] == batch.data.size - 16
+
+
+def test_fold_runes_gpu_vs_oracle(builtin):
+    """U+0130 / U+212A / U+017F (bytes C4 B0, E2 84 AA, C5 BF) through K1's fallback flags
+    on the device, file by file against the oracle.  Derived behaviour (Go 1.19's
+    unicode.SimpleFold / unicode.ToLower), not pinned by a
+    reference fixture."""
+    from oracle import secret as O
+    batch = corpus.fold_runes_batch(3, nbytes=128 << 10, plants=400, frac=0.6)
+    data = bytes(batch.data[:int(batch.offsets[-1])])
+    for rune in ("\u0130", "\u212a", "\u017f"):
+        assert data.count(rune.encode()) > 5, rune
+    got = builtin.ScanBatch(batch, device=0)
+    osc = O.NewScanner(None)
+    nf = 0
+    for i in range(batch.nfiles):
+        c = bytes(batch.data[int(batch.offsets[i]):int(batch.offsets[i + 1])])
+        want = canon_secret(osc.Scan(batch.path(i), c))
+        assert canon_secret(got[i]) == want, batch.path(i)
+        nf += len(want["Findings"] or [])
+    assert nf > 10
+
+
+@pytest.mark.parametrize("chunk", [64, 256])
+def test_fold_runes_gpu_vs_exact(builtin, chunk):
+    batch = corpus.fold_runes_batch(5 + chunk, nbytes=2 << 20, plants=200, frac=0.3)
+    ctx = S.GpuContext(builtin, 0, chunk_bytes=chunk)
+    ctx.upload(batch)
+    got = ctx.scan()
+    ctx.close()
+    assert got == builtin.ScanBatch(batch, nthreads=16)
+    assert got == builtin.ScanBatch(batch, emulate_chunk=chunk)
+
+
+def test_analyzer_cases_gpu():
+    """The reference's SecretAnalyzer cases (analyzer/secret/secret_test.go: fs path, image
+    "/" prefix, .doc skip, no config, binary skip) through AnalyzeBatch(device=0)."""
+    from trivy_amd import analyzer as A
+    adir = os.path.join(GOLDEN, "reference", "analyzer")
+    old = os.getcwd()
+    os.chdir(adir)
+    try:
+        for case in CASES["analyzer_cases"]:
+            a = A.SecretAnalyzer()
+            a.Init(case["config"])
+            content = open(case["input"], "rb").read()
+            inp = A.AnalysisInput(Dir=case["dir"], FilePath=case["input"], Content=content)
+            got = a.AnalyzeBatch([inp], device=0)
+            if case["want"] is None:
+                assert got == [], case["name"]
+            else:
+                assert [canon_secret(x) for x in got] == case["want"]["Secrets"], case["name"]
+    finally:
+        os.chdir(old)

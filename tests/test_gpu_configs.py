@@ -1,7 +1,10 @@
-"""configs[3] / configs[4] parity on the device (see test_configs.py): HIP kernels +
-host resolution == the exact CPU path, through the C ABI."""
+"""configs[3] / configs[4] parity on the device: HIP kernels + host resolution through the
+C ABI, file by file against the oracle (oracle/secret.py, a restatement of scanner.go) and
+against the exact CPU path on larger batches.  No reference fixture covers these rule
+sets; the oracle is pinned by the reference fixtures (test_oracle_reference.py)."""
 import pytest
 
+from tests.helpers import canon_secret
 from trivy_amd import analyzer as A
 from trivy_amd import configs
 from trivy_amd import secret as S
@@ -9,19 +12,58 @@ from trivy_amd import secret as S
 pytestmark = pytest.mark.gpu
 
 
-def test_user_rules_gpu_vs_exact():
-    doc = configs.user_rules_doc(100, seed=4)
-    sc = S.NewScanner(S.config_from_dict(doc))
-    b = S.Batch.from_args(configs.mixed_batch(doc, 512 << 10, seed=61))
+@pytest.fixture(scope="module")
+def user1000():
+    doc = configs.user_rules_doc(1000, seed=4)
+    return doc, S.NewScanner(S.config_from_dict(doc))
+
+
+def _vs_oracle(doc, args, got):
+    from oracle import secret as O
+    osc = O.NewScanner(O.config_from_dict(doc))
+    n = 0
+    for a, g in zip(args, got):
+        want = canon_secret(osc.Scan(a.FilePath, a.Content))
+        assert canon_secret(g) == want, a.FilePath
+        n += len(want["Findings"] or [])
+    return n
+
+
+def test_user_rules_1000_compile(user1000):
+    """configs[3] at its stated size: 1,000 user rules + 83 builtins compile into a plan."""
+    _, sc = user1000
+    info = sc.info()
+    assert info["n_rules"] == 1083 and info["n_groups"] > 0
+
+
+def test_user_rules_1000_gpu_vs_oracle(user1000):
+    doc, sc = user1000
+    args = configs.mixed_batch(doc, 256 << 10, seed=61, plants_per_file=0.6)
+    got = sc.ScanBatch(args, device=0)
+    assert _vs_oracle(doc, args, got) > 10
+
+
+def test_user_rules_1000_gpu_vs_exact(user1000):
+    doc, sc = user1000
+    b = S.Batch.from_args(configs.mixed_batch(doc, 2 << 20, seed=63))
     want = sc.ScanBatch(b, nthreads=16)
     assert sc.ScanBatch(b, device=0) == want
     assert sum(len(x["Findings"] or []) for x in want) > 10
 
 
+def test_allow_exclude_binary_gpu_vs_oracle():
+    doc = configs.allow_exclude_doc()
+    sc = S.NewScanner(S.config_from_dict(doc))
+    args = configs.mixed_batch(doc, 256 << 10, seed=62, plants_per_file=0.5, binary_frac=0.3)
+    args = [a for a in args if not A.IsBinary(a.Content, len(a.Content))]
+    got = sc.ScanBatch(args, device=0)
+    assert _vs_oracle(doc, args, got) > 5
+
+
 def test_allow_exclude_binary_gpu_vs_exact():
     doc = configs.allow_exclude_doc()
     sc = S.NewScanner(S.config_from_dict(doc))
-    args = configs.mixed_batch(doc, 512 << 10, seed=62, plants_per_file=0.5, binary_frac=0.3)
+    args = configs.mixed_batch(doc, 2 << 20, seed=64, plants_per_file=0.5, binary_frac=0.3)
     args = [a for a in args if not A.IsBinary(a.Content, len(a.Content))]
     b = S.Batch.from_args(args)
     want = sc.ScanBatch(b, nthreads=16)

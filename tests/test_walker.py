@@ -214,3 +214,37 @@ def test_native_layer_gpu(analyzer):
     want, _, _ = W.analyze_layer(analyzer, io.BytesIO(tar))
     assert [canon_secret(s) for s in got] == [canon_secret(s) for s in want]
     assert len(got) > 100
+
+
+def _pax_tar(records):
+    """A tar whose first member carries a hand-made PAX 'x' header block."""
+    def hdr(name, size, typ):
+        h = bytearray(512)
+        h[0:len(name)] = name
+        h[100:108] = b"0000644\0"
+        h[124:136] = b"%011o\0" % size
+        h[156] = ord(typ)
+        h[257:265] = b"ustar\x0000"
+        h[148:156] = b" " * 8
+        h[148:156] = b"%06o\0 " % sum(h)
+        return bytes(h)
+    pad = lambda b: b + b"\0" * (-len(b) % 512)
+    body = b"export GITHUB_TOKEN=%s\n" % GHP.encode()
+    return (hdr(b"PaxHeaders/x", len(records), "x") + pad(records) +
+            hdr(b"etc/app.env", len(body), "0") + pad(body) + b"\0" * 1024)
+
+
+def test_native_layer_malformed_pax(analyzer):
+    """Untrusted layers: a PAX size or record length that overflows int64 is an error
+    (archive/tar's strconv.ParseInt fails: ErrHeader), never a wrap-around that moves
+    the walk backwards."""
+    from trivy_amd import _native as N
+    ok = _pax_tar(b"20 path=etc/app.env\n")
+    assert W.NativeLayer(analyzer.scanner, ok).batch.nfiles == 1
+    for rec in [b"39 size=99999999999999999999999999999\n",     # int64 overflow
+                b"29 size=18446744073709551104\n",              # wraps to -512 as uint64
+                b"30 size=9223372036854775807\n",               # past the end of the archive
+                b"99999999999999999999999 path=a\n",           # record length overflow
+                b"5 a=b\n"]:                                     # record shorter than its text
+        with pytest.raises(N.NativeError):
+            W.NativeLayer(analyzer.scanner, _pax_tar(rec))

@@ -114,6 +114,7 @@ SIGNATURES = [
                                  C.POINTER(C.c_char_p), C.c_uint32, C.c_char_p, C.POINTER(_P)]),
     ("tsg_layer_get", C.c_int, [_P, C.POINTER(LayerView)]),
     ("tsg_layer_free", None, [_P]),
+    ("tsg_go_sort_perm", C.c_int, [_P, _U64P, _I64P, C.c_uint32, C.POINTER(C.c_uint32)]),
     ("tsg_ruleset_rule_anchor", C.c_int, [_P, C.c_uint32, C.POINTER(C.c_uint32),
                                           C.POINTER(C.c_int64), C.c_char_p, C.c_size_t]),
 ]

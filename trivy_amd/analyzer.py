@@ -106,13 +106,33 @@ class SecretAnalyzer:
         return sort_secrets(secrets)
 
 
+def _go_sort(items, key, secondary=None):
+    """sort.Slice (Go 1.19 pdqsort_func, unstable) of `items` in place by (key bytes,
+    secondary): the native restatement in libtrivy_secret.so (tsg_go_sort_perm)."""
+    import ctypes as C
+    import numpy as np
+    from . import _native as N
+    n = len(items)
+    if n < 2:
+        return
+    ks = [key(x) for x in items]
+    offs = np.zeros(n + 1, dtype=np.uint64)
+    np.cumsum([len(k) for k in ks], out=offs[1:])
+    blob = np.frombuffer(b"".join(ks) or b"\0", dtype=np.uint8)
+    sec = None if secondary is None else np.array([secondary(x) for x in items], dtype=np.int64)
+    perm = np.zeros(n, dtype=np.uint32)
+    N.check(N.lib().tsg_go_sort_perm(C.c_void_p(blob.ctypes.data),
+                                     offs.ctypes.data_as(C.POINTER(C.c_uint64)),
+                                     None if sec is None else sec.ctypes.data_as(C.POINTER(C.c_int64)),
+                                     n, perm.ctypes.data_as(C.POINTER(C.c_uint32))))
+    items[:] = [items[int(i)] for i in perm]
+
+
 def sort_secrets(secrets):
-    """AnalysisResult.Sort, secrets part (analyzer.go:212-223); Go sort.Slice is unstable
-    but file paths are unique and per-file findings are already in scan order."""
-    from ._gosort import sort_slice
-    sort_slice(secrets, lambda a, b: a["FilePath"].encode() < b["FilePath"].encode())
+    """AnalysisResult.Sort, secrets part (analyzer.go:212-223): files by FilePath, then each
+    file's findings by (RuleID, StartLine), both with Go's unstable sort.Slice."""
+    _go_sort(secrets, lambda s: s["FilePath"].encode("utf-8", "surrogateescape"))
     for s in secrets:
-        sort_slice(s["Findings"], lambda a, b: (a["RuleID"].encode() < b["RuleID"].encode()
-                                                if a["RuleID"] != b["RuleID"]
-                                                else a["StartLine"] < b["StartLine"]))
+        _go_sort(s["Findings"], lambda f: f["RuleID"].encode("utf-8", "surrogateescape"),
+                 lambda f: f["StartLine"])
     return secrets

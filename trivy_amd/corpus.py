@@ -126,6 +126,19 @@ def _base_text(nbytes, rng):
     return text[:nbytes]
 
 
+# The three runes that change keyword gates or (?i) matching:
+# U+017F (s under (?i)), U+212A (k under (?i); bytes.ToLower -> 'k'), U+0130
+# (bytes.ToLower -> 'i').  Each line is planted whole, so some are real findings.
+FOLD_PLANTS = [
+    "ſecret=\"abcdefgh12\" KEY",
+    "aws_secret_access_\u212aey = \"12ASD34qwe56CXZ78tyH10Tna543VBokN85RHCas\"",
+    "A\u0130DA token \u0130ntercom_api_token = \"" + "b" * 60 + "\"",
+    "\u212aEY=\"9f8e7d6c5b4a39281706\" aws_account_id: 1234-5678-9012",
+]
+
+FOLD = {ord("k"): "\u212a", ord("K"): "\u212a", ord("s"): "\u017f", ord("S"): "\u017f",
+        ord("i"): "\u0130", ord("I"): "\u0130"}
+
 EXTS = ["go", "py", "js", "ts", "yaml", "json", "sh", "env", "tf", "ini", "txt", "conf", "rb",
         "java", "md"]
 DIRS = ["src", "pkg", "lib", "app", "cmd", "internal", "config", "deploy", "scripts", "web",
@@ -192,9 +205,9 @@ def make_corpus(total_bytes, seed=1, plants_per_mib=1.0, median=6 * 1024, sigma=
             fs, fe = int(offsets[f]), int(offsets[f + 1])
             if fe - fs > 4:
                 data[fs + int(rng.integers(0, fe - fs))] = int(rng.integers(0x80, 0x100))
-        for f in rng.choice(nfiles, size=max(1, nfiles // 10000), replace=False):
+        for k, f in enumerate(rng.choice(nfiles, size=max(3, nfiles // 10000), replace=False)):
             fs, fe = int(offsets[f]), int(offsets[f + 1])
-            w = "ſecret=\"abcdefgh12\" KEY".encode()
+            w = FOLD_PLANTS[k % len(FOLD_PLANTS)].encode()
             if fe - fs > len(w) + 2:
                 at = fs + int(rng.integers(0, fe - fs - len(w)))
                 data[at:at + len(w)] = np.frombuffer(w, dtype=np.uint8)
@@ -224,3 +237,39 @@ def make_corpus(total_bytes, seed=1, plants_per_mib=1.0, median=6 * 1024, sigma=
     paths = np.frombuffer(b"".join(pb), dtype=np.uint8)
     batch = Batch(data, offsets, paths, poffs)
     return batch, {"files": nfiles, "bytes": total, "planted": planted, "seed": seed}
+
+
+def fold_runes_batch(seed, nbytes=1 << 20, plants=300, frac=0.3):
+    """Seeded corpus in which `frac` of the files have some k/s/i letters turned into the
+    folding runes (U+212A, U+017F, U+0130), mostly inside and around planted secrets and
+    keywords, plus hand-made files with a folding rune inside the secret or keyword of
+    common rules.  Stresses the one place where the kernels' anchors are not exact."""
+    from .secret import ScanArgs
+    rng = np.random.default_rng(seed)
+    b, _ = make_corpus(nbytes, seed=seed, plants_per_mib=plants)
+    args = []
+    for i in range(b.nfiles):
+        c = bytes(b.data[int(b.offsets[i]):int(b.offsets[i + 1])])
+        if rng.random() < frac and len(c) > 0:
+            t = bytearray()
+            p = float(rng.choice([0.002, 0.02, 0.2]))
+            for ch in c:
+                if ch in FOLD and rng.random() < p:
+                    t += FOLD[ch].encode()
+                else:
+                    t.append(ch)
+            c = bytes(t)
+        args.append(ScanArgs(b.path(i), c))
+    hand = [
+        "aws_secret_access_\u212aey = \"12ASD34qwe56CXZ78tyH10Tna543VBokN85RHCas\"\n",
+        "AWS_\u017fECRET_ACCESS_KEY=12ASD34qwe56CXZ78tyH10Tna543VBokN85RHCas\n",
+        "ghp_0123456789abcdefghij\u212almnopqrstuvwxyz\n",
+        "\u0130ntercom_api_token = \"" + "a" * 60 + "\"\n",
+        "gitlab_\u017fecret glpat-0123456789abcdefghij\n",
+        "-----BEGIN RSA PRIVATE KEY-----\nMIIEabc\n-----END RSA PRIVATE KEY-----\n",
+        "twitch_api_\u212aey = '" + "x" * 30 + "'\n",
+        "facebook_token = '" + "a" * 31 + "\u212a'\n",
+    ] + [w + "\n" for w in FOLD_PLANTS]
+    for j, h in enumerate(hand):
+        args.append(ScanArgs("hand/f%d.txt" % j, h.encode()))
+    return Batch.from_args(args)

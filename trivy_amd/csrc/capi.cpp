@@ -250,30 +250,42 @@ int tsg_emulate_candidate_stats(const tsg_ruleset* rs, const uint8_t* data,
                                 const uint64_t* offsets, uint32_t nfiles, uint32_t chunk,
                                 uint64_t* cand_per_rule, uint64_t* gated_bytes_per_group) {
   if (!rs || !offsets || chunk == 0) return fail(TSG_ERR_ARG, "bad argument");
-  std::vector<uint64_t> poff(nfiles + 1, 0);
-  BatchView b{data, offsets, nfiles, "", poff.data()};
-  KernelOutput ko;
-  std::vector<uint64_t> gib;
-  emulate_kernels(*rs->plan, b, chunk, 1u << 16, &ko, &gib);
-  if (cand_per_rule) {
-    std::fill(cand_per_rule, cand_per_rule + rs->rs.rules.size(), 0);
-    for (const auto& c : ko.cand) cand_per_rule[c.rule]++;
+  try {
+    std::vector<uint64_t> poff(nfiles + 1, 0);
+    BatchView b{data, offsets, nfiles, "", poff.data()};
+    KernelOutput ko;
+    std::vector<uint64_t> gib;
+    emulate_kernels(*rs->plan, b, chunk, 1u << 16, &ko, &gib);
+    if (cand_per_rule) {
+      std::fill(cand_per_rule, cand_per_rule + rs->rs.rules.size(), 0);
+      for (const auto& c : ko.cand) cand_per_rule[c.rule]++;
+    }
+    if (gated_bytes_per_group) std::copy(gib.begin(), gib.end(), gated_bytes_per_group);
+    return TSG_OK;
+  } catch (const std::bad_alloc&) {
+    return fail(TSG_ERR_NOMEM, "out of memory");
+  } catch (const std::exception& ex) {
+    return fail(TSG_ERR_INTERNAL, ex.what());
   }
-  if (gated_bytes_per_group) std::copy(gib.begin(), gib.end(), gated_bytes_per_group);
-  return TSG_OK;
 }
 
 int tsg_emulate_k1(const tsg_ruleset* rs, const uint8_t* data, const uint64_t* offsets,
                    uint32_t nfiles, uint32_t chunk, uint32_t* kw, size_t kw_len, uint32_t* ev,
                    size_t ev_len) {
   if (!rs || !offsets || chunk == 0) return fail(TSG_ERR_ARG, "bad argument");
-  std::vector<uint64_t> poff(nfiles + 1, 0);
-  BatchView b{data, offsets, nfiles, "", poff.data()};
-  std::vector<uint32_t> k, e;
-  k1_reference(*rs->plan, b, chunk, &k, &e);
-  if (kw) std::memcpy(kw, k.data(), sizeof(uint32_t) * std::min(kw_len, k.size()));
-  if (ev) std::memcpy(ev, e.data(), sizeof(uint32_t) * std::min(ev_len, e.size()));
-  return TSG_OK;
+  try {
+    std::vector<uint64_t> poff(nfiles + 1, 0);
+    BatchView b{data, offsets, nfiles, "", poff.data()};
+    std::vector<uint32_t> k, e;
+    k1_reference(*rs->plan, b, chunk, &k, &e);
+    if (kw) std::memcpy(kw, k.data(), sizeof(uint32_t) * std::min(kw_len, k.size()));
+    if (ev) std::memcpy(ev, e.data(), sizeof(uint32_t) * std::min(ev_len, e.size()));
+    return TSG_OK;
+  } catch (const std::bad_alloc&) {
+    return fail(TSG_ERR_NOMEM, "out of memory");
+  } catch (const std::exception& ex) {
+    return fail(TSG_ERR_INTERNAL, ex.what());
+  }
 }
 
 int tsg_ruleset_rule_plan(const tsg_ruleset* rs, uint32_t rule, int32_t* group, int32_t* relax,
@@ -294,6 +306,17 @@ int tsg_ruleset_rule_anchor(const tsg_ruleset* rs, uint32_t rule, uint32_t* even
   if (evdist) *evdist = p.rule_evdist[rule];
   copy_err(p.rule_anchor[rule], desc, desc_len);
   return TSG_OK;
+}
+
+int tsg_go_sort_perm(const uint8_t* keys, const uint64_t* key_offsets, const int64_t* secondary,
+                     uint32_t n, uint32_t* perm) {
+  if ((n && (!keys || !key_offsets || !perm))) return fail(TSG_ERR_ARG, "bad argument");
+  try {
+    go_sort_perm(keys, key_offsets, secondary, n, perm);
+    return TSG_OK;
+  } catch (const std::bad_alloc&) {
+    return fail(TSG_ERR_NOMEM, "out of memory");
+  }
 }
 
 const uint8_t* tsg_result_data(const tsg_result* r, size_t* len) {

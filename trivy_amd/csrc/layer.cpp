@@ -8,6 +8,7 @@
 // Tar decoding follows Go 1.19 archive/tar: ustar/PAX/GNU headers, PAX 'x' records
 // (path, linkpath, size), GNU 'L'/'K' long names, TypeRegA -> TypeReg (TypeDir with a
 // trailing "/"), header-only types carry no data, end = a zero block or end of input.
+#include <cstdint>
 #include <algorithm>
 #include <chrono>
 #include <cstdio>
@@ -168,8 +169,12 @@ bool parse_pax(const uint8_t* p, size_t n, std::vector<std::pair<std::string, st
   while (i < n) {
     size_t sp = i;
     uint64_t len = 0;
-    while (sp < n && p[sp] >= '0' && p[sp] <= '9') len = len * 10 + (p[sp++] - '0');
-    if (sp >= n || p[sp] != ' ' || len == 0 || i + len > n || p[i + len - 1] != '\n') return false;
+    while (sp < n && p[sp] >= '0' && p[sp] <= '9') {
+      if (len > (n - i) / 10) return false;  // longer than the rest of the block (or overflow)
+      len = len * 10 + (p[sp++] - '0');
+    }
+    if (sp >= n || p[sp] != ' ' || len == 0 || len > n - i || p[i + len - 1] != '\n' || sp + 1 > i + len - 1)
+      return false;
     std::string rec((const char*)p + sp + 1, i + len - 1 - (sp + 1));
     size_t eq = rec.find('=');
     if (eq == std::string::npos) return false;
@@ -289,8 +294,9 @@ extern "C" int tsg_layer_pack(const tsg_ruleset* rs, const uint8_t* tar, uint64_
         if (!prefix.empty()) name = prefix + "/" + name;
       }
       const uint64_t dpos = pos + 512;
+      if (dpos > tar_len) return bad("unexpected EOF");
       if (type == 'x' || type == 'L' || type == 'K') {
-        if (dpos + (uint64_t)size > tar_len) return bad("unexpected EOF");
+        if ((uint64_t)size > tar_len - dpos) return bad("unexpected EOF");
         if (type == 'x') {
           if (!parse_pax(tar + dpos, (size_t)size, &pax)) return bad("invalid PAX record");
         } else if (type == 'L') {
@@ -304,9 +310,11 @@ extern "C" int tsg_layer_pack(const tsg_ruleset* rs, const uint8_t* tar, uint64_
       for (const auto& kv : pax) {
         if (kv.first == "path") name = kv.second;
         else if (kv.first == "size") {
+          // strconv.ParseInt(v, 10, 64) in archive/tar: digits only, no overflow
           int64_t v = 0;
+          if (kv.second.empty()) return bad("invalid PAX size");
           for (char c : kv.second) {
-            if (c < '0' || c > '9') return bad("invalid PAX size");
+            if (c < '0' || c > '9' || v > (INT64_MAX - (c - '0')) / 10) return bad("invalid PAX size");
             v = v * 10 + (c - '0');
           }
           size = v;
@@ -316,8 +324,8 @@ extern "C" int tsg_layer_pack(const tsg_ruleset* rs, const uint8_t* tar, uint64_
       have_long = false;
       if (type == 0) type = (!name.empty() && name.back() == '/') ? '5' : '0';
       const uint64_t dlen = header_only(type) ? 0 : (uint64_t)size;
-      if (dpos + dlen > tar_len) return bad("unexpected EOF");
-      pos = dpos + ((dlen + 511) & ~511ull);
+      if (dlen > tar_len - dpos) return bad("unexpected EOF");
+      pos = dpos + ((dlen + 511) & ~511ull);  // > the header's position: the walk always advances
 
       // tar.go:45-84
       const std::string fp = trim_left_slash(clean(name));

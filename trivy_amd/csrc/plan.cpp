@@ -11,6 +11,7 @@
 #include <cstdlib>
 #include <atomic>
 #include <map>
+#include <set>
 #include <thread>
 #include <x86intrin.h>
 
@@ -103,6 +104,47 @@ Anchor choose_anchor(const Regexp& re, const Plan& p) {
   return best;
 }
 
+// Inject-mode states of the union of two DFAs' searches, counted as the reachable pairs
+// of their product (each union state is a pair of component states), up to `cap`.  A
+// lower bound on the states a subset construction of the merged programs builds, so
+// "> cap" rejects a merge without building it.
+size_t product_states(const DFA& a, const DFA& b, size_t cap) {
+  std::vector<uint8_t> seen((size_t)a.nstates * b.nstates, 0);
+  std::vector<std::pair<uint32_t, uint32_t>> stack;
+  uint16_t pcls[256][2];
+  int np = 0;
+  {
+    std::map<std::pair<int, int>, int> idx;
+    for (int c = 0; c < 256; c++) {
+      auto k = std::make_pair((int)a.cls[c], (int)b.cls[c]);
+      if (!idx.count(k)) idx[k] = np++;
+      pcls[c][0] = (uint16_t)a.cls[c];
+      pcls[c][1] = (uint16_t)b.cls[c];
+    }
+  }
+  std::vector<int> rep;  // one byte per joint class
+  {
+    std::set<std::pair<int, int>> done;
+    for (int c = 0; c < 256; c++)
+      if (done.insert({pcls[c][0], pcls[c][1]}).second) rep.push_back(c);
+  }
+  size_t n = 0;
+  auto push = [&](uint32_t x, uint32_t y) {
+    uint8_t& v = seen[(size_t)x * b.nstates + y];
+    if (v) return;
+    v = 1;
+    n++;
+    stack.push_back({x, y});
+  };
+  for (int c = 0; c < 4; c++) push(a.start[c], b.start[c]);
+  while (!stack.empty() && n <= cap) {
+    auto [x, y] = stack.back();
+    stack.pop_back();
+    for (int c : rep) push(a.next[(size_t)x * a.nclasses + pcls[c][0]], b.next[(size_t)y * b.nclasses + pcls[c][1]]);
+  }
+  return n;
+}
+
 }  // namespace
 
 std::unique_ptr<Plan> build_plan(const Ruleset& rs, const PlanOptions& opt, std::string* err) {
@@ -172,10 +214,13 @@ std::unique_ptr<Plan> build_plan(const Ruleset& rs, const PlanOptions& opt, std:
   p->rule_winback.assign(R, -1);
   p->rule_prog.assign(R, Prog{});
   std::vector<std::unique_ptr<DFA>> single(R);
+  const auto t_rules0 = std::chrono::steady_clock::now();
   std::vector<Anchor> anchor(R);
-  for (size_t r = 0; r < R; r++) {
+  // rules are independent here: build their programs on the shared pool
+  const int plan_threads = (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+  pool_for(R, plan_threads, [&](size_t r) {
     const RuleC& rule = rs.rules[r];
-    if (!rule.regex) continue;
+    if (!rule.regex) return;
     p->rule_maxlen[r] = max_match_len(rule.regex->prog());
     if (opt.anchors) anchor[r] = choose_anchor(*rule.regex, *p);
     const int fa = anchor[r].first_atom;
@@ -208,7 +253,7 @@ std::unique_ptr<Plan> build_plan(const Ruleset& rs, const PlanOptions& opt, std:
     }
     if (!single[r]) {
       p->rule_hostonly[r] = 1;
-      continue;
+      return;
     }
     // where a GPU end offset e lets the exact match start
     if (fa > 0) {
@@ -222,8 +267,15 @@ std::unique_ptr<Plan> build_plan(const Ruleset& rs, const PlanOptions& opt, std:
     p->rule_evdist[r] = anchor[r].evdist;
     p->rule_first_atom[r] = fa;
     p->rule_anchor[r] = anchor[r].desc;
-  }
+  }, 1);
 
+  const bool tprof = getenv("TSG_PROF") != nullptr;
+  auto tnow = [] { return std::chrono::steady_clock::now(); };
+  auto tms = [](std::chrono::steady_clock::time_point a) {
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - a).count();
+  };
+  auto tp = tnow();
+  if (tprof) fprintf(stderr, "plan: per-rule DFAs %.1f ms\n", tms(t_rules0));
   // ---- K2 rule groups: greedy packing under the state / table caps, among rules with
   // the same kind of event (their windows coincide)
   auto group_kwmask = [&](GroupPlan& g) {
@@ -262,11 +314,24 @@ std::unique_ptr<Plan> build_plan(const Ruleset& rs, const PlanOptions& opt, std:
         cur_dfa = std::move(single[r]);
         continue;
       }
+      // two programs whose DFAs together exceed the cap have not merged under it on any
+      // rule set measured (unanchored searches share few states): skip the construction
+      if (cur_dfa->nstates + single[r]->nstates > opt.max_group_states ||
+          product_states(*cur_dfa, *single[r], opt.max_group_states) > (size_t)opt.max_group_states) {
+        flush();
+        cur.push_back((uint32_t)r);
+        cur_dfa = std::move(single[r]);
+        continue;
+      }
       std::vector<const Prog*> progs;
       for (uint32_t q : cur) progs.push_back(&p->rule_prog[q]);
       progs.push_back(&p->rule_prog[r]);
       std::string e;
       auto merged = build_dfa(progs, one, &e);
+      if (getenv("TSG_PROF2"))
+        fprintf(stderr, "merge %d+%d (nc %d,%d) -> %d %s\n", cur_dfa->nstates, single[r]->nstates,
+                cur_dfa->nclasses, single[r]->nclasses, merged ? merged->nstates : -1,
+                merged && fits(*merged, cur.size() + 1) ? "ok" : "FAIL");
       if (merged && fits(*merged, cur.size() + 1)) {
         cur.push_back((uint32_t)r);
         cur_dfa = std::move(merged);
@@ -279,6 +344,8 @@ std::unique_ptr<Plan> build_plan(const Ruleset& rs, const PlanOptions& opt, std:
     flush();
   }
 
+  if (tprof) fprintf(stderr, "plan: grouping %.1f ms (%zu groups)\n", tms(tp), p->groups.size());
+  tp = tnow();
   // ---- K1 automaton: keywords + anchor literals; literal groups share event bits
   std::vector<char> litg(p->groups.size(), 0);
   for (size_t g = 0; g < p->groups.size(); g++) litg[g] = p->groups[g].events == (1u << kEvLit0);
@@ -338,7 +405,29 @@ std::unique_ptr<Plan> build_plan(const Ruleset& rs, const PlanOptions& opt, std:
     p->kw_dfa = std::move(d);
     return true;
   };
-  if (!build_k1(opt.anchors) && !build_k1(false)) {
+  // table bytes of an automaton over the keywords (and anchors): its states are the
+  // literals' distinct prefixes, its classes at most the distinct bytes + 1
+  auto k1_estimate = [&](bool with_anchors) {
+    std::set<std::string> pre;
+    bool bytes[256] = {false};
+    auto add = [&](const std::string& s) {
+      for (size_t i = 1; i <= s.size(); i++) pre.insert(s.substr(0, i));
+      for (unsigned char ch : s) bytes[ch] = true;
+    };
+    for (size_t k = 0; k < kws.size(); k++)
+      if (!kw_dropped[k]) add(kws[k]);
+    if (with_anchors)
+      for (size_t r = 0; r < R; r++)
+        if (!anchor[r].lit.empty()) add(anchor[r].lit);
+    size_t ncls = 1;
+    for (int c = 0; c < 256; c++) ncls += bytes[c];
+    return (pre.size() + 1) * ncls * 2;
+  };
+  // (an estimate far over the budget skips the exact build)
+  auto try_k1 = [&](bool with_anchors) {
+    return k1_estimate(with_anchors) <= 4 * (size_t)opt.max_kw_table_bytes && build_k1(with_anchors);
+  };
+  if (!(opt.anchors && try_k1(true)) && !try_k1(false)) {
     // Too many keyword bytes for an LDS-resident automaton (large user rule sets): leave
     // keywords out, longest first (they cost the most states), until it fits.  Their rules
     // get the exact keyword gate on the host, and their groups are scanned on every file.
@@ -346,8 +435,14 @@ std::unique_ptr<Plan> build_plan(const Ruleset& rs, const PlanOptions& opt, std:
     for (int k = 0; k < p->fb_kw0; k++) order.push_back(k);
     std::stable_sort(order.begin(), order.end(),
                      [&](int a, int b) { return kws[a].size() > kws[b].size(); });
-    bool ok = false;
-    for (size_t next = 0; next < order.size() && !ok;) {
+    // Estimate first, so the exact build runs once or twice.
+    size_t next = 0;
+    while (next < order.size() && k1_estimate(false) > (size_t)opt.max_kw_table_bytes) {
+      const size_t m = std::max<size_t>(1, (order.size() - next) / 8);
+      for (size_t k = 0; k < m && next < order.size(); k++) kw_dropped[order[next++]] = 1;
+    }
+    bool ok = (opt.anchors && try_k1(true)) || build_k1(false);
+    while (next < order.size() && !ok) {
       for (size_t m = std::max<size_t>(1, order.size() / 32); m > 0 && next < order.size(); m--)
         kw_dropped[order[next++]] = 1;
       ok = build_k1(opt.anchors) || build_k1(false);
@@ -364,6 +459,8 @@ std::unique_ptr<Plan> build_plan(const Ruleset& rs, const PlanOptions& opt, std:
     for (auto& g : p->groups) group_kwmask(g);
   }
 
+  if (tprof) fprintf(stderr, "plan: K1 %.1f ms\n", tms(tp));
+  tp = tnow();
   // ---- host resolver: reverse DFAs of the exact programs
   p->rule_rev.resize(R);
   // (only where the forward bound is loose: unbounded or long windows; the subset
@@ -382,6 +479,7 @@ std::unique_ptr<Plan> build_plan(const Ruleset& rs, const PlanOptions& opt, std:
               std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
   }
 
+  if (tprof) fprintf(stderr, "plan: reverse DFAs %.1f ms\n", tms(tp));
   // ---- Global.AllowPath automaton (exact on ASCII paths)
   std::vector<const Prog*> paths;
   for (const auto& a : rs.allow)
@@ -783,7 +881,8 @@ void resolve_batch(const Ruleset& rs, const Plan& plan, const BatchView& b,
       // U+212A / U+017F join ASCII letters under (?i), which the K1 anchors (literal
       // automaton, token-run counters) do not see: a match the kernels may have missed
       // contains one of them, so its start lies within rule_maxlen bytes before it.  A
-      // rule without that bound runs its K2 DFA (which does fold them) over the file here.
+      // rule without that bound runs its K2 DFA over the file here when its GPU program is
+      // exact (relaxed programs leave these runes out of their sets), else the whole file.
       std::vector<int64_t> fold;
       for (int64_t q = 0; q + 1 < n; q++) {
         if (content[q] == 0xC5 && content[q + 1] == 0xBF) fold.push_back(q);
@@ -796,7 +895,9 @@ void resolve_batch(const Ruleset& rs, const Plan& plan, const BatchView& b,
         const int64_t ml = plan.rule_maxlen[r];
         if (ml >= 0) {
           for (int64_t q : fold) w.iv.push_back({align_rune(content, n, std::max<int64_t>(0, q - ml)), q});
-        } else if (plan.rule_group[r] >= 0) {
+        } else if (plan.rule_group[r] >= 0 && plan.rule_relax[r] < 0) {
+          // only an unrelaxed GPU program keeps U+017F / U+212A in its (?i) sets (relaxed
+          // ones drop them, goregex.cpp Compiler::rune): a relaxed rule is resolved whole
           const GroupPlan& g = plan.groups[plan.rule_group[r]];
           size_t local = 0;
           while (g.rules[local] != r) local++;
@@ -821,6 +922,13 @@ void resolve_batch(const Ruleset& rs, const Plan& plan, const BatchView& b,
         wins[r].whole = true;
         wptr[r] = &wins[r];
       }
+    if (getenv("TSG_DEBUG_RESOLVE"))
+      for (size_t r = 0; r < R; r++)
+        if (wptr[r]) {
+          fprintf(stderr, "file %u rule %s kws %d whole %d:", f, rs.rules[r].id.c_str(), kws[r], (int)wptr[r]->whole);
+          for (auto& iv : wptr[r]->iv) fprintf(stderr, " [%ld,%ld]", (long)iv.first, (long)iv.second);
+          fprintf(stderr, "\n");
+        }
     FileGate gate;
     gate.kw_state = kws.data();
     gate.windows = wptr.data();

@@ -304,6 +304,25 @@ void sort_slice(std::vector<T>& x, L less) {
 
 }  // namespace gosort
 
+void go_sort_perm(const uint8_t* keys, const uint64_t* key_offsets, const int64_t* secondary, uint32_t n,
+                  uint32_t* perm) {
+  std::vector<uint32_t> x(n);
+  for (uint32_t i = 0; i < n; i++) x[i] = i;
+  auto key = [&](uint32_t i, size_t* len) {
+    *len = key_offsets[i + 1] - key_offsets[i];
+    return keys + key_offsets[i];
+  };
+  gosort::sort_slice(x, [&](uint32_t a, uint32_t b) {
+    size_t la, lb;
+    const uint8_t* ka = key(a, &la);
+    const uint8_t* kb = key(b, &lb);
+    const int c = std::memcmp(ka, kb, std::min(la, lb));
+    if (c != 0 || la != lb) return c != 0 ? c < 0 : la < lb;  // Go string <
+    return secondary ? secondary[a] < secondary[b] : false;
+  });
+  std::memcpy(perm, x.data(), sizeof(uint32_t) * n);
+}
+
 // ------------------------------------------------------------------ materialise
 namespace {
 

@@ -115,5 +115,9 @@ void pool_for(size_t n, int nthreads, const std::function<void(size_t)>& f, size
 struct Plan;
 bool path_allowed(const Ruleset& rs, const Plan* plan, const char* p, size_t n);
 void serialize_results(const std::vector<FileResult>& res, std::string* out);
+// sort.Slice (Go 1.19 pdqsort_func) of n items by (key bytes, then secondary): the order
+// as a permutation (perm[k] = original index of the k-th item)
+void go_sort_perm(const uint8_t* keys, const uint64_t* key_offsets, const int64_t* secondary, uint32_t n,
+                  uint32_t* perm);
 
 }  // namespace tsg
