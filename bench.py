@@ -4,24 +4,30 @@
     python bench.py [--gpus N] [--steps K] [--warmup W] [--gb G]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
 
-Workload (per rank, weak scaling): builtin rules over a seeded synthetic corpus of
+Workload (per rank, weak scaling): the 83 builtin rules over a seeded synthetic corpus of
 --gb GiB (default 10: BASELINE configs[1]) of mixed code/config text files with planted
-secrets.  The batch is uploaded to HBM once (outside the timed region); one step =
-one scan of the resident batch: K1 keyword automaton, gates, K2 rule-group DFAs,
-candidate download (tsg_batch_submit), then exact host resolution of every finding (Go
-semantics) and serialization of all per-file results (tsg_batch_collect).  Steps are
-pipelined two deep: the device part of step i+1 runs while the host resolves step i.
-The timed region ends when every step's results have been collected.
-value = content bytes of all ranks x steps / max-over-ranks wall time.
+secrets.  The corpus is packed once, before timing, into the context's pinned host slots
+(--batch-mib each; the ingest of SURVEY.md §8f writes files straight into such slots).
+One step = one scan of the whole corpus from host memory: for every slot, H2D into HBM,
+K1 keyword automaton, gates, device-side item layout, K2 rule-group DFAs, outputs back to
+pinned host memory, then exact host resolution of every finding (Go semantics) and
+serialization of every per-file result.  Batches are pipelined across two device lanes
+(the H2D of one overlaps the kernels of the other) and --depth batches in flight; every
+byte crosses PCIe in every step.  value = content bytes of all ranks x steps / max-over-
+ranks wall time of the timed steps.
 
-Rank 0 prints ONE JSON line with, in addition to the contract fields:
-  roofline      the dominant kernel's algorithmic bytes / its mean HIP-event duration
-                (events recorded on the context's stream around each launch) vs 8 TB/s
-  cpu_baseline  the oracle (Python restatement of the reference's algorithm) timed on a
-                bounded sample of the same corpus on this host, 1 core
-  cpu_native    the product library's exact CPU path (C++ restatement of the same
-                algorithm: per-rule keyword gate, Go-semantics Pike VM over whole files),
-                16 threads, on a bounded sample -- the closer stand-in for Go's speed
+Rank 0 prints ONE JSON line with, besides the contract fields:
+  roofline       K1 (the dominant kernel): algorithmic bytes per launch / mean HIP-event
+                 duration of its launches (events on the lane stream around each launch)
+                 vs 8 TB/s; traffic = FETCH_SIZE bytes per launch from the committed PMC
+                 pass of the same command (profiles/r02/)
+  kernels        K1, K2 (on the bytes it reads) and K1+gates+K2 GB/s (HIP events)
+  pipeline       H2D GB/s, per-batch stage times, resolution time
+  cpu_baseline   the library's exact C++ CPU path (the reference algorithm restated:
+                 per-rule keyword gate on bytes.ToLower, Go-semantics regexp over whole
+                 files) on this host's cores, on a bounded sample of the same corpus
+  cpu_optimised  the GPU algorithm (K1 automaton + K2 DFAs + the same exact resolution)
+                 emulated on the same cores and sample
 """
 import argparse
 import json
@@ -34,7 +40,7 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 # FETCH_SIZE of the same command (rocprofv3 --pmc FETCH_SIZE), committed under profiles/
-PMC_FETCH_CSV = os.path.join(ROOT, "profiles", "r01", "bench_10gib_pmc_fetch_v10.csv")
+PMC_FETCH_CSV = os.path.join(ROOT, "profiles", "r02", "bench_pmc_fetch.csv")
 
 
 def _dist():
@@ -48,8 +54,8 @@ def _dist():
 
 
 def _barrier(dist):
-    """Barrier + device sync (the scans run on the library's own HIP stream and each
-    submit waits for it; torch's synchronize covers anything else on the device)."""
+    """Barrier + device sync (every batch runs on the library's own lane streams and is
+    collected inside the timed region; torch's synchronize covers anything else)."""
     if dist is not None:
         dist.barrier()
     try:
@@ -60,94 +66,130 @@ def _barrier(dist):
         pass
 
 
-def _max(dist, v):
+def _reduce(dist, v, op):
     if dist is None:
         return v
     import torch
     t = torch.tensor([v], dtype=torch.float64)
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dist.all_reduce(t, op=getattr(dist.ReduceOp, op))
     return float(t.item())
 
 
-def _sum(dist, v):
-    if dist is None:
-        return v
-    import torch
-    t = torch.tensor([v], dtype=torch.float64)
-    dist.all_reduce(t, op=dist.ReduceOp.SUM)
-    return float(t.item())
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
 
 
-def cpu_baseline(batch, budget_s=12.0):
-    """Oracle (reference algorithm restated in Python) on a bounded prefix of the corpus."""
-    from oracle import secret as O
-    osc = O.NewScanner(None)
-    done = 0
-    nfiles = 0
-    t0 = time.perf_counter()
-    for i in range(batch.nfiles):
-        c = bytes(batch.data[int(batch.offsets[i]):int(batch.offsets[i + 1])])
-        osc.Scan(batch.path(i), c)
-        done += len(c)
-        nfiles += 1
-        if time.perf_counter() - t0 > budget_s:
-            break
-    dt = time.perf_counter() - t0
-    return {"value": done / dt / 1e9, "unit": "GB/s", "cores": 1, "kind": "port",
-            "sample": "first %d files (%.2f MB) of the same corpus, oracle/secret.py "
-                      "(Go regexp restated over Python `regex`), %.1f s" % (nfiles, done / 1e6, dt)}
-
-
-def _traffic(dom, gb):
-    """HBM bytes per launch of the dominant kernel from the committed PMC pass (same
-    10 GiB workload; null for other sizes or when the file is absent)."""
-    if abs(gb - 10.0) > 1e-9 or not os.path.exists(PMC_FETCH_CSV):
-        return None
-    sys.path.insert(0, os.path.join(ROOT, "tools"))
-    from pmc_traffic import traffic
-    t = traffic(PMC_FETCH_CSV, "k1_kernel" if dom.startswith("K1") else "k2_")
-    return None if t is None else int(t)
-
-
-def cpu_native(sc, batch, max_bytes=256 << 20, nthreads=16):
-    """Exact CPU batch path of libtrivy_secret.so on the first files of the corpus."""
-    from trivy_amd import _native as N
-    import ctypes as C
+def _sub_batch(batch, max_bytes):
+    from trivy_amd.secret import Batch
     nf = 0
     while nf < batch.nfiles and int(batch.offsets[nf + 1]) <= max_bytes:
         nf += 1
     nf = max(nf, 1)
-    from trivy_amd.secret import Batch
-    sub = Batch(batch.data[:int(batch.offsets[nf])], batch.offsets[:nf + 1],
-                batch.paths[:int(batch.path_offsets[nf])], batch.path_offsets[:nf + 1])
+    return Batch(batch.data[:int(batch.offsets[nf])], batch.offsets[:nf + 1],
+                 batch.paths[:int(batch.path_offsets[nf])], batch.path_offsets[:nf + 1]), nf
+
+
+def cpu_baselines(sc, batch, max_bytes, nthreads):
+    """The exact CPU path (the reference algorithm, restated in C++) and the optimised CPU
+    path (the GPU algorithm emulated), both on `nthreads` threads over the same prefix."""
+    from trivy_amd import _native as N
+    import ctypes as C
+    sub, nf = _sub_batch(batch, max_bytes)
+    nb = int(sub.offsets[-1])
     out = C.c_void_p()
     t0 = time.perf_counter()
     N.check(N.lib().tsg_scan_cpu_batch(sc.handle, *sub.ptrs(), nthreads, C.byref(out)))
     dt = time.perf_counter() - t0
     N.lib().tsg_result_free(out)
-    nb = int(batch.offsets[nf])
-    return {"value": nb / dt / 1e9, "unit": "GB/s", "cores": nthreads, "kind": "port",
-            "sample": "first %d files (%.1f MB) of the same corpus, exact CPU path of "
-                      "libtrivy_secret.so (tsg_scan_cpu_batch), %.1f s" % (nf, nb / 1e6, dt)}
+    model = cpu_model()
+    exact = {"value": round(nb / dt / 1e9, 4), "unit": "GB/s", "cores": nthreads, "kind": "port",
+             "cpu": model,
+             "sample": "first %d files (%.0f MB) of the same corpus; exact CPU path of "
+                       "libtrivy_secret.so (tsg_scan_cpu_batch: per-rule bytes.ToLower keyword "
+                       "gate + Go-semantics regexp, scanner.go:341-416 restated), %.1f s"
+                       % (nf, nb / 1e6, dt)}
+    from trivy_amd.secret import GpuContext
+    ctx = GpuContext(sc, 0, emulate=True, host_threads=nthreads)
+    t0 = time.perf_counter()
+    ctx.upload(sub)
+    ctx.submit()
+    N.lib().tsg_result_free(ctx.collect_raw())
+    dt2 = time.perf_counter() - t0
+    ctx.close()
+    opt = {"value": round(nb / dt2 / 1e9, 4), "unit": "GB/s", "cores": nthreads, "kind": "port",
+           "cpu": model,
+           "sample": "same %.0f MB; the GPU algorithm (K1 automaton, gates, K2 DFAs) emulated "
+                     "on the CPU + the same exact resolution (TSG_CTX_EMULATE), %.1f s"
+                     % (nb / 1e6, dt2)}
+    return exact, opt
+
+
+def _traffic_per_launch(batch_bytes):
+    """K1 HBM bytes per launch from the committed FETCH_SIZE pass (None when absent or for
+    another batch size)."""
+    if not os.path.exists(PMC_FETCH_CSV):
+        return None
+    meta = PMC_FETCH_CSV.replace(".csv", ".json")
+    if os.path.exists(meta):
+        m = json.load(open(meta))
+        if int(m.get("batch_bytes", -1)) != int(batch_bytes):
+            return None
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    from pmc_traffic import traffic
+    t = traffic(PMC_FETCH_CSV, "k1_kernel")
+    return None if t is None else int(t)
+
+
+def fill_slots(ctx, batch, batch_bytes):
+    """Pack the corpus into pinned slots of about batch_bytes each (outside timing)."""
+    import numpy as np
+    slots = []
+    f0 = 0
+    while f0 < batch.nfiles:
+        base = int(batch.offsets[f0])
+        f1 = int(np.searchsorted(batch.offsets, base + batch_bytes, side="right")) - 1
+        f1 = max(f1, f0 + 1)
+        f1 = min(f1, batch.nfiles)
+        nb = int(batch.offsets[f1]) - base
+        pbase = int(batch.path_offsets[f0])
+        npb = int(batch.path_offsets[f1]) - pbase
+        sid, data, offs, paths, poffs = ctx.acquire_slot(nb, f1 - f0, npb)
+        data[:nb] = batch.data[base:base + nb]
+        offs[:f1 - f0 + 1] = batch.offsets[f0:f1 + 1] - np.uint64(base)
+        paths[:npb] = batch.paths[pbase:pbase + npb]
+        poffs[:f1 - f0 + 1] = batch.path_offsets[f0:f1 + 1] - np.uint64(pbase)
+        slots.append((sid, f1 - f0, nb))
+        f0 = f1
+    return slots
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--gb", type=float, default=10.0, help="GiB of corpus per rank")
+    ap.add_argument("--batch-mib", type=int, default=1024, help="bytes per pinned slot / batch")
     ap.add_argument("--chunk", type=int, default=0)
     ap.add_argument("--seed", type=int, default=2)
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--depth", type=int, default=4, help="pipelined scans in flight")
+    ap.add_argument("--depth", type=int, default=4, help="batches in flight")
     ap.add_argument("--host-threads", type=int, default=0,
                     help="host resolution pool threads (0: library default, 16)")
+    ap.add_argument("--cpu-mib", type=int, default=1024, help="CPU baseline sample")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
     dist, rank, world, local = _dist()
     from trivy_amd import corpus
     from trivy_amd import secret as S
+    from trivy_amd import _native as N
+    L = N.lib()
 
     nbytes = int(args.gb * (1 << 30))
     t0 = time.perf_counter()
@@ -155,51 +197,40 @@ def main():
     gen_s = time.perf_counter() - t0
     sc = S.NewScanner(None)
     dev = local if world > 1 else 0
-    ctx = S.GpuContext(sc, dev, chunk_bytes=args.chunk, host_threads=args.host_threads)
+    batch_bytes = args.batch_mib << 20
+    nslots = -(-nbytes // batch_bytes) + 2
+    ctx = S.GpuContext(sc, dev, chunk_bytes=args.chunk, host_threads=args.host_threads,
+                       max_slots=nslots + 2)
     t0 = time.perf_counter()
-    ctx.upload(batch)
-    upload_s = time.perf_counter() - t0
-    from trivy_amd import _native as N
-    L = N.lib()
+    slots = fill_slots(ctx, batch, batch_bytes)
+    pack_s = time.perf_counter() - t0
 
-    acc = {"k1": 0.0, "k2": 0.0, "gate": 0.0, "res": 0.0, "submit": 0.0, "wait": 0.0}
-
-    def collect():
-        t = time.perf_counter()
-        L.tsg_result_free(ctx.collect_raw())
-        acc["wait"] += (time.perf_counter() - t) * 1e3
-        acc["res"] += ctx.stats()["resolve_ms"]
-
-    def run(k):
-        for _ in range(k):
-            t = time.perf_counter()
-            ctx.submit()
-            acc["submit"] += (time.perf_counter() - t) * 1e3
-            st = ctx.stats()
-            acc["k1"] += st["k1_ms"]
-            acc["k2"] += st["k2_ms"]
-            acc["gate"] += st["gate_ms"]
-            while ctx.pending() >= args.depth:
-                collect()
+    def run(steps):
+        for _ in range(steps):
+            for sid, nf, _ in slots:
+                ctx.submit_slot(sid, nf)
+                while ctx.pending() >= args.depth:
+                    L.tsg_result_free(ctx.collect_raw())
         while ctx.pending():
-            collect()
+            L.tsg_result_free(ctx.collect_raw())
 
     run(args.warmup)
-    for k in acc:
-        acc[k] = 0.0
+    st0 = ctx.stats()
     _barrier(dist)
     t0 = time.perf_counter()
     run(args.steps)
     _barrier(dist)
     dt = time.perf_counter() - t0
-    dt = _max(dist, dt)
-    k1, k2, res = acc["k1"], acc["k2"], acc["res"]
-    total_bytes = _sum(dist, float(info["bytes"])) * args.steps
     st = ctx.stats()
-    k1_ms, k2_ms = k1 / args.steps, k2 / args.steps
-    dom = "K1 keyword automaton" if k1_ms >= k2_ms else "K2 rule-group DFAs (all launches)"
-    dom_ms = max(k1_ms, k2_ms)
-    achieved = info["bytes"] / (dom_ms / 1e3) / 1e9
+    dt = _reduce(dist, dt, "MAX")
+    total_bytes = _reduce(dist, float(info["bytes"]), "SUM") * args.steps
+    d = {k: st[k] - st0[k] for k in ("batches", "sum_bytes", "sum_k1_ms", "sum_gate_ms", "sum_k2_ms",
+                                      "sum_h2d_ms", "sum_d2h_ms", "sum_resolve_ms")}
+    nbat = max(1, d["batches"])
+    k1_gbs = d["sum_bytes"] / (d["sum_k1_ms"] / 1e3) / 1e9
+    dev_ms = d["sum_k1_ms"] + d["sum_gate_ms"] + d["sum_k2_ms"]
+    launch_bytes = d["sum_bytes"] / nbat
+    k2_read = st["k2_bytes"]  # last batch: chunk bytes K2 read
     line = {
         "metric": "secret-scan GB/s (builtin rules) at 1/2/4/8 MI355X; % of HBM peak",
         "value": round(total_bytes / dt / 1e9, 3),
@@ -212,28 +243,41 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "u8",
-        "data": "synthetic (seeded corpus, trivy_amd/corpus.py; resident in HBM)",
+        "data": "synthetic (seeded corpus, trivy_amd/corpus.py) in pinned host memory; every "
+                "step moves every byte host->HBM (H2D inside the timed region)",
         "config": {"workload": "builtin rules over %.1f GiB synthetic text corpus per GPU "
                                "(BASELINE configs[1])" % args.gb,
                    "files_per_gpu": info["files"], "bytes_per_gpu": info["bytes"],
+                   "batches_per_step": len(slots), "batch_bytes": batch_bytes,
                    "rules": 83, "parallelism": "file-sharded x%d, no collective" % world},
-        "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1),
-                     "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": _traffic(dom, args.gb),
-                     "algorithmic_bytes": info["bytes"],
+        "roofline": {"bound": "hbm", "kernel": "K1 keyword automaton (k1_kernel)",
+                     "achieved": round(k1_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(k1_gbs / HBM_PEAK_GBS, 4),
+                     "traffic": _traffic_per_launch(launch_bytes),
+                     "algorithmic_bytes_per_launch": int(launch_bytes),
                      "traffic_source": os.path.relpath(PMC_FETCH_CSV, ROOT)},
-        "breakdown_ms": {"k1": round(k1_ms, 3), "gate": round(acc["gate"] / args.steps, 3),
-                         "k2": round(k2_ms, 3),
-                         "resolve": round(res / args.steps, 3), "aux": round(st["aux_ms"], 3),
-                         "submit_wall": round(acc["submit"] / args.steps, 3),
-                         "collect_wait": round(acc["wait"] / args.steps, 3),
-                         "k2_launches": st["k2_launches"], "candidates": st["candidates"],
-                         "upload_s": round(upload_s, 3), "gen_s": round(gen_s, 2),
-                         "pcie_inclusive_GBps": round(info["bytes"] / (upload_s + dt / args.steps) / 1e9, 3)},
+        "kernels": {"k1_GBps": round(k1_gbs, 1),
+                    "k2_GBps_on_item_bytes": round(k2_read / (st["k2_ms"] / 1e3) / 1e9, 1)
+                    if st["k2_ms"] else None,
+                    "k1_gates_k2_GBps": round(d["sum_bytes"] / (dev_ms / 1e3) / 1e9, 1),
+                    "k1_ms_per_batch": round(d["sum_k1_ms"] / nbat, 3),
+                    "gates_ms_per_batch": round(d["sum_gate_ms"] / nbat, 3),
+                    "k2_ms_per_batch": round(d["sum_k2_ms"] / nbat, 3),
+                    "k2_item_bytes_last_batch": k2_read, "k2_entries_last_batch": st["k2_launches"],
+                    "candidates_last_batch": st["candidates"],
+                    "groups_skipped_last_batch": st["groups_skipped"]},
+        "pipeline": {"h2d_GBps": round(d["sum_bytes"] / (d["sum_h2d_ms"] / 1e3) / 1e9, 2),
+                     "h2d_ms_per_batch": round(d["sum_h2d_ms"] / nbat, 3),
+                     "d2h_ms_per_batch": round(d["sum_d2h_ms"] / nbat, 3),
+                     "resolve_ms_per_batch": round(d["sum_resolve_ms"] / nbat, 3),
+                     "depth": args.depth, "lanes": 2,
+                     "gen_s": round(gen_s, 2), "pack_into_pinned_s": round(pack_s, 2)},
     }
     if rank == 0 and not args.no_cpu_baseline:
-        line["cpu_baseline"] = cpu_baseline(batch)
-        line["cpu_native"] = cpu_native(sc, batch)
+        nt = args.host_threads or 16
+        line["cpu_baseline"], line["cpu_optimised"] = cpu_baselines(sc, batch, args.cpu_mib << 20, nt)
+    for sid, _, _ in slots:
+        ctx.release_slot(sid)
     ctx.close()
     if rank == 0:
         print(json.dumps(line), flush=True)

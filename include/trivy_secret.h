@@ -14,17 +14,15 @@
  *       scanner.go:55-57 (used by SecretAnalyzer.Required, analyzer/secret/secret.go:145)
  *   (*Scanner).Scan(ScanArgs) types.Secret            tsg_scan_cpu (one file, exact CPU)
  *       scanner.go:341-416                            tsg_scan_batch (many files, GPU)
- *   SecretAnalyzer.Analyze per-file goroutines        tsg_scan_batch: the batching boundary
- *       analyzer/secret/secret.go:78-110, analyzer.go:419-443
+ *   SecretAnalyzer.Analyze per-file goroutines        tsg_queue_scan (concurrent callers
+ *       analyzer/secret/secret.go:78-110,               coalesced into pinned batches),
+ *       analyzer.go:419-443                             tsg_slot_* / tsg_scan_batch (batches)
  *
  * Error convention: every call returns TSG_OK (0) or a negative TSG_ERR_*; the
  * message of the last failing call on this thread is tsg_last_error().  No C++
- * exception crosses the ABI.  All entry points are thread-safe for distinct
- * tsg_ctx objects; a tsg_ruleset is immutable and may be shared by any number of
- * threads and contexts.  The library never retains caller pointers past a call,
- * except that tsg_batch_upload's host buffers must stay valid until the next
- * tsg_batch_upload / tsg_ctx_destroy on that context (they are read by the host
- * resolution step of tsg_batch_scan).
+ * exception crosses the ABI.  Every entry point is thread-safe; a tsg_ruleset is
+ * immutable and may be shared by any number of threads and contexts.  The library never
+ * retains a caller pointer past a call.
  *
  * Result format (tsg_result_data), little endian:
  *   u32 magic 'TSG1' (0x31475354), u32 nfiles, then per file:
@@ -127,59 +125,117 @@ int tsg_go_sort_perm(const uint8_t* keys, const uint64_t* key_offsets, const int
                      uint32_t n, uint32_t* perm);
 void tsg_result_free(tsg_result* r);
 
-/* ---- GPU (one context per device; one process per GPU) ---- */
+/* ---- GPU (one context per device; one process per GPU) ----
+ *
+ * A context owns the rule tables on one device, two lanes (HIP stream + HBM buffers: the
+ * H2D of one batch overlaps the kernels of the other), a pool of pinned host slots that
+ * batches are staged in, and the host resolvers of batches in flight.  Every entry point
+ * is thread-safe; the library never retains a caller pointer past a call (batch bytes are
+ * copied into, or written directly by the caller into, library-owned pinned slots). */
 typedef struct tsg_ctx_options {
   uint32_t chunk_bytes;      /* bytes per lane (multiple of 16); 0 = default */
   uint32_t ext_cap;          /* max bytes a lane follows a match past its chunk; 0 = default */
   uint32_t cand_capacity;    /* candidate records per batch; 0 = default */
-  int32_t host_threads;      /* resolver threads; <= 0 = hardware */
+  int32_t host_threads;      /* resolver threads; <= 0 = 16 */
   uint32_t adapt_mib;        /* first batch of at least this many MiB samples K1's literal
                                 frequencies and stops reporting the frequent ones (their
                                 keyword gates are then checked on the host); 0 = 64,
                                 0xFFFFFFFF = never */
+  uint32_t flags;            /* TSG_CTX_* */
+  uint32_t slot_mib;         /* default capacity of a pinned slot (tsg_queue batches); 0 = 256 */
+  uint32_t max_slots;        /* pinned slots a context may hold; 0 = 16 */
 } tsg_ctx_options;
+
+/* Test mode: no HIP device is touched; the kernels' algorithm is emulated on the CPU over
+ * the same slots, lanes and queue logic (tests of the pipeline and of tsg_queue on hosts
+ * without a GPU).  Never chosen implicitly. */
+#define TSG_CTX_EMULATE 1u
 
 int tsg_ctx_create(int device, const tsg_ruleset* rs, const tsg_ctx_options* opt,
                    tsg_ctx** out);
+/* Waits for every batch in flight, then frees the context. */
 void tsg_ctx_destroy(tsg_ctx* ctx);
 
-/* Copy a batch into device memory (HBM). Host buffers must stay valid until the next
- * upload (the exact host resolution reads them). */
+/* -- Zero-copy staging: the caller packs files straight into a pinned slot -------------
+ * Replaces the per-file io.ReadAll copy of SecretAnalyzer.Analyze
+ * (pkg/fanal/analyzer/secret/secret.go:85): ingest writes file bytes into the slot,
+ * offsets[i] / path_offsets[i] describe file i exactly as for tsg_batch_upload. */
+typedef struct tsg_slot_view {
+  uint32_t id;
+  uint8_t* data;            /* data_cap bytes */
+  uint64_t data_cap;
+  uint64_t* offsets;        /* files_cap + 1 */
+  uint32_t files_cap;
+  char* paths;              /* paths_cap bytes */
+  uint64_t paths_cap;
+  uint64_t* path_offsets;   /* files_cap + 1 */
+} tsg_slot_view;
+/* A free slot with at least these capacities (allocated or grown if needed). */
+int tsg_slot_acquire(tsg_ctx* ctx, uint64_t data_bytes, uint32_t nfiles, uint64_t path_bytes,
+                     tsg_slot_view* out);
+/* Submit the slot's first nfiles files (the device part runs asynchronously, the host
+ * resolution follows it on the resolver pool); collect with tsg_batch_collect.  The slot
+ * stays the caller's: it may be submitted again (same bytes) once earlier submissions are
+ * collected or immediately (they only read it), and must not be written until they are. */
+int tsg_slot_submit(tsg_ctx* ctx, uint32_t slot_id, uint32_t nfiles);
+/* Give the slot back to the context (it becomes free when its submissions are collected). */
+int tsg_slot_release(tsg_ctx* ctx, uint32_t slot_id);
+
+/* -- Copying staging (compatibility): the batch is copied into a context-owned slot ----- */
 int tsg_batch_upload(tsg_ctx* ctx, const uint8_t* data, const uint64_t* offsets,
                      uint32_t nfiles, const char* paths, const uint64_t* path_offsets);
-/* K1 + K2 on the device-resident batch, candidates back to the host, exact resolution. */
-int tsg_batch_scan(tsg_ctx* ctx, tsg_result** out);
-/* Only the device part of tsg_batch_scan (kernels + candidate download), no resolution. */
+/* The device part of a scan of the last uploaded batch, synchronously, no resolution
+ * (test hook: tsg_batch_k1_output then reads its keyword bits / chunk events). */
 int tsg_batch_kernels(tsg_ctx* ctx);
-/* Pipelined form of tsg_batch_scan: submit runs the device part synchronously and starts
- * the host resolution of that batch in the background; collect returns the results of
- * the oldest submitted batch (waiting for its resolution).  The device work of the next
- * submit overlaps the host resolution of the previous ones.  The host buffers of a batch
- * must stay valid until its results are collected. */
+/* Submit the last uploaded batch (it may be submitted again). */
 int tsg_batch_submit(tsg_ctx* ctx);
+/* Results of the oldest submitted batch (slot or upload), waiting for its resolution. */
 int tsg_batch_collect(tsg_ctx* ctx, tsg_result** out);
 /* number of submitted, uncollected batches */
 int tsg_batch_pending(const tsg_ctx* ctx);
+/* submit + collect of the last uploaded batch */
+int tsg_batch_scan(tsg_ctx* ctx, tsg_result** out);
 /* upload + scan */
 int tsg_scan_batch(tsg_ctx* ctx, const uint8_t* data, const uint64_t* offsets, uint32_t nfiles,
                    const char* paths, const uint64_t* path_offsets, tsg_result** out);
 
 typedef struct tsg_stats {
-  double k1_ms;          /* K1 literal automaton + run counters, last batch (HIP events) */
-  double k2_ms;          /* all rule-group (K2) launches, last batch */
-  double aux_ms;         /* memsets + candidate/keyword downloads */
+  double k1_ms;          /* K1 literal automaton + run counters, last collected batch (HIP events) */
+  double k2_ms;          /* K2 rule-group DFAs (the persistent work-list launch) */
+  double aux_ms;         /* D2H of the outputs */
   double resolve_ms;     /* host exact resolution (wall) */
   uint64_t bytes;        /* content bytes of the batch */
-  uint64_t k2_bytes;     /* chunk bytes K2 scans (sum over groups of item bytes) */
+  uint64_t k2_bytes;     /* chunk bytes K2 scans (items listed x chunk) */
   uint64_t candidates;   /* candidate records produced */
-  uint64_t files_resolved;  /* files that needed exact host work */
-  uint32_t k2_launches;
+  uint64_t files_resolved;  /* files with findings */
+  uint32_t k2_launches;  /* K2 work-list entries */
   uint32_t overflow;     /* 1 if the candidate buffer overflowed (files resolved whole) */
-  double gate_ms;        /* keyword gates + K2 item lists (incl. one host round trip) */
-  uint64_t k2_items;     /* (file, chunk) items of the sparse K2 launch */
+  double gate_ms;        /* keyword gates + items + device-side layout */
+  uint64_t k2_items;     /* (file, chunk) items K2 scanned */
   uint32_t k1_hot_states;  /* K1 automaton states no longer reported (adaptation) */
+  double h2d_ms;         /* H2D of the batch (pinned slot -> HBM) */
+  uint32_t groups_skipped; /* rule groups K2 left to the host (item capacity) */
+  uint64_t batches;      /* batches collected so far, and their sums: */
+  uint64_t sum_bytes;
+  double sum_k1_ms, sum_gate_ms, sum_k2_ms, sum_h2d_ms, sum_d2h_ms, sum_resolve_ms;
 } tsg_stats;
 int tsg_ctx_get_stats(const tsg_ctx* ctx, tsg_stats* out);
+
+/* -- Submission queue for concurrent per-file callers ----------------------------------
+ * The analyzer framework calls Analyze -> Scan from one goroutine per file
+ * (pkg/fanal/analyzer/analyzer.go:419-443).  tsg_queue_scan is that Scan: any number of
+ * threads call it at once; their files are packed into the open slot, a slot is submitted
+ * when full or flush_us after its first file, and each call returns its own file's result
+ * (tsg_result, one file, the format above) once its batch is resolved.  Files too large
+ * for a slot are scanned by the exact CPU path (same results). */
+typedef struct tsg_queue tsg_queue;
+int tsg_queue_create(tsg_ctx* ctx, uint32_t flush_us, tsg_queue** out);
+int tsg_queue_scan(tsg_queue* q, const char* path, size_t path_len, const uint8_t* content,
+                   size_t len, tsg_result** out);
+/* submit the open slot now */
+int tsg_queue_flush(tsg_queue* q);
+/* waits for every call in flight */
+void tsg_queue_destroy(tsg_queue* q);
 
 /* K1 output of the last tsg_batch_kernels: keyword bits [nfiles * kw_words] and chunk
  * event bits [ceil(bytes / chunk_bytes)] (test hook; either pointer may be NULL). */

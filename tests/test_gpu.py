@@ -240,3 +240,63 @@ def test_analyzer_cases_gpu():
                 assert [canon_secret(x) for x in got] == case["want"]["Secrets"], case["name"]
     finally:
         os.chdir(old)
+
+
+def test_pipelined_batches_gpu(builtin):
+    """Different batches in flight on both lanes at once (H2D of one overlapping the
+    kernels of the other), each collected with its own results."""
+    batches = [corpus.make_corpus(n, seed=s, plants_per_mib=60)[0]
+               for n, s in [(8 << 20, 41), (3 << 20, 42), (5 << 20, 43), (1 << 20, 44)]]
+    ctx = S.GpuContext(builtin, 0)
+    for b in batches:
+        ctx.upload(b)
+        ctx.submit()
+    got = [ctx.collect() for _ in batches]
+    st = ctx.stats()
+    ctx.close()
+    assert got == [builtin.ScanBatch(b, nthreads=16) for b in batches]
+    assert st["batches"] == 4 and st["sum_k1_ms"] > 0 and st["sum_h2d_ms"] > 0
+
+
+def test_zero_copy_slots_gpu(builtin):
+    b, _ = corpus.make_corpus(16 << 20, seed=45, plants_per_mib=20)
+    ctx = S.GpuContext(builtin, 0)
+    sid, data, offs, paths, poffs = ctx.acquire_slot(int(b.offsets[-1]), b.nfiles,
+                                                     int(b.path_offsets[-1]))
+    data[:int(b.offsets[-1])] = b.data[:int(b.offsets[-1])]
+    offs[:b.nfiles + 1] = b.offsets
+    paths[:int(b.path_offsets[-1])] = b.paths[:int(b.path_offsets[-1])]
+    poffs[:b.nfiles + 1] = b.path_offsets
+    for _ in range(3):
+        ctx.submit_slot(sid, b.nfiles, paths_of=b)
+    want = builtin.ScanBatch(b, nthreads=16)
+    assert [ctx.collect() for _ in range(3)] == [want] * 3
+    ctx.release_slot(sid)
+    ctx.close()
+
+
+def test_queue_concurrent_callers_gpu(builtin):
+    """tsg_queue on the device: 16 threads share one context; per-file results equal
+    Scanner.Scan (analyzer.go:419-443)."""
+    import threading
+    b = corpus.fold_runes_batch(12, nbytes=4 << 20, plants=100, frac=0.1)
+    args = [S.ScanArgs(b.path(i), bytes(b.data[int(b.offsets[i]):int(b.offsets[i + 1])]))
+            for i in range(b.nfiles)]
+    ctx = S.GpuContext(builtin, 0, slot_mib=1, max_slots=6)
+    q = S.ScanQueue(ctx, flush_us=1000)
+    got = [None] * len(args)
+
+    def worker(k):
+        for i in range(k, len(args), 16):
+            got[i] = q.Scan(args[i])
+
+    ts = [threading.Thread(target=worker, args=(k,)) for k in range(16)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    q.close()
+    st = ctx.stats()
+    ctx.close()
+    assert got == [builtin.Scan(a) for a in args]
+    assert st["batches"] >= 3

@@ -42,10 +42,21 @@ class RulesetInfo(C.Structure):
                 ("kw_classes", C.c_uint32)]
 
 
+TSG_CTX_EMULATE = 1
+
+
 class CtxOptions(C.Structure):
     _fields_ = [("chunk_bytes", C.c_uint32), ("ext_cap", C.c_uint32),
                 ("cand_capacity", C.c_uint32), ("host_threads", C.c_int32),
-                ("adapt_mib", C.c_uint32)]
+                ("adapt_mib", C.c_uint32), ("flags", C.c_uint32), ("slot_mib", C.c_uint32),
+                ("max_slots", C.c_uint32)]
+
+
+class SlotView(C.Structure):
+    _fields_ = [("id", C.c_uint32), ("data", C.c_void_p), ("data_cap", C.c_uint64),
+                ("offsets", C.POINTER(C.c_uint64)), ("files_cap", C.c_uint32),
+                ("paths", C.c_void_p), ("paths_cap", C.c_uint64),
+                ("path_offsets", C.POINTER(C.c_uint64))]
 
 
 class LayerView(C.Structure):
@@ -61,7 +72,12 @@ class Stats(C.Structure):
                 ("candidates", C.c_uint64), ("files_resolved", C.c_uint64),
                 ("k2_launches", C.c_uint32), ("overflow", C.c_uint32),
                 ("gate_ms", C.c_double), ("k2_items", C.c_uint64),
-                ("k1_hot_states", C.c_uint32)]
+                ("k1_hot_states", C.c_uint32), ("h2d_ms", C.c_double),
+                ("groups_skipped", C.c_uint32), ("batches", C.c_uint64),
+                ("sum_bytes", C.c_uint64), ("sum_k1_ms", C.c_double),
+                ("sum_gate_ms", C.c_double), ("sum_k2_ms", C.c_double),
+                ("sum_h2d_ms", C.c_double), ("sum_d2h_ms", C.c_double),
+                ("sum_resolve_ms", C.c_double)]
 
 
 # (name, restype, argtypes) -- every symbol include/trivy_secret.h declares
@@ -91,6 +107,14 @@ SIGNATURES = [
     ("tsg_batch_pending", C.c_int, [_P]),
     ("tsg_scan_batch", C.c_int, [_P, _P, _U64P, C.c_uint32, _P, _U64P, C.POINTER(_P)]),
     ("tsg_ctx_get_stats", C.c_int, [_P, C.POINTER(Stats)]),
+    ("tsg_slot_acquire", C.c_int, [_P, C.c_uint64, C.c_uint32, C.c_uint64, C.POINTER(SlotView)]),
+    ("tsg_slot_submit", C.c_int, [_P, C.c_uint32, C.c_uint32]),
+    ("tsg_slot_release", C.c_int, [_P, C.c_uint32]),
+    ("tsg_queue_create", C.c_int, [_P, C.c_uint32, C.POINTER(_P)]),
+    ("tsg_queue_scan", C.c_int, [_P, C.c_char_p, C.c_size_t, C.c_char_p, C.c_size_t,
+                                 C.POINTER(_P)]),
+    ("tsg_queue_flush", C.c_int, [_P]),
+    ("tsg_queue_destroy", None, [_P]),
     ("tsg_last_error", C.c_char_p, []),
     ("tsg_regex_compile", C.c_int, [C.c_char_p, C.POINTER(_P), C.c_char_p, C.c_size_t]),
     ("tsg_regex_free", None, [_P]),

@@ -227,7 +227,7 @@ int tsg_scan_batch_emulated(const tsg_ruleset* rs, const uint8_t* data, const ui
     }
     auto t1 = std::chrono::steady_clock::now();
     BatchResult res;
-    resolve_batch(rs->rs, *rs->plan, b, ko, hw_threads(0), &res);
+    resolve_batch(rs->rs, *rs->plan, b, ko.view(), hw_threads(0), &res);
     auto t2 = std::chrono::steady_clock::now();
     auto r = std::make_unique<tsg_result>();
     serialize_batch(res, &r->buf, hw_threads(0));

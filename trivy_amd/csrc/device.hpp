@@ -1,0 +1,80 @@
+// Host interface of the gfx950 kernels (kernels.hip) for the batch pipeline (pipeline.cpp).
+//
+// One DeviceRules per device holds the compiled rule set's tables in HBM (K1 literal
+// automaton, K2 rule-group DFAs, the Global.AllowPath DFA, gates).  A batch runs on one
+// DeviceLane (its own HIP stream and HBM buffers); enqueue_scan puts the whole device part
+// of a batch on that stream with no host round trip:
+//
+//   H2D (pinned slot -> HBM)  chunk->file map  K1  path gate  keyword gates  event-chunk
+//   compaction  item counts  item layout (device-side)  item lists  K2  candidate copy-out
+//   (to pinned, mapped host memory)  D2H of keyword bits / overflow / path / skip flags
+//
+// and records the batch's completion event.  Two lanes per device let the H2D of one batch
+// overlap the kernels of the other.
+#pragma once
+#include <hip/hip_runtime_api.h>
+
+#include <cstdint>
+#include <memory>
+#include <vector>
+
+#include "plan.hpp"
+
+namespace tsg {
+
+struct DeviceRules;
+
+// Pinned host memory of one batch's device outputs (written by the lane's stream).
+struct HostOut {
+  uint32_t* kw = nullptr;       // [files_cap * kw_words]
+  uint8_t* ovf = nullptr;       // [files_cap] 1 = resolve the file whole
+  uint8_t* pathok = nullptr;    // [files_cap] Global.AllowPath: 0 / 1 / 2 = host decides
+  uint8_t* gskip = nullptr;     // [groups] 1 = K2 skipped the group (item capacity)
+  Candidate* cand = nullptr;    // [cand_cap] host-mapped: K2 candidates copied out
+  Candidate* cand_dev = nullptr;  // device address of `cand`
+  uint32_t* counts = nullptr;   // [8] host-mapped: 0 candidates, 1 items, 2 K2 entries,
+                                //      3 skipped groups, 4 event chunks
+  uint32_t* counts_dev = nullptr;
+  uint32_t files_cap = 0, cand_cap = 0, groups = 0, kw_words = 0;
+  // stage boundaries of the batch on its lane's stream: H2D | K1 | gates | K2 | D2H; ev[5]
+  // completes the batch (its outputs are in these buffers)
+  hipEvent_t ev[6] = {};
+};
+
+struct ScanInput {
+  const uint8_t* data;       // pinned host, `total` bytes
+  const uint64_t* off;       // [nfiles + 1]
+  uint32_t nfiles;
+  uint64_t total;
+  const char* paths;         // pinned host
+  const uint64_t* poff;      // [nfiles + 1]
+};
+
+struct ScanTimes {  // HIP-event milliseconds of one batch on its lane
+  float h2d = 0, k1 = 0, gates = 0, k2 = 0, d2h = 0;
+};
+
+struct LaneState;  // HBM buffers + stream + events of one lane
+
+int device_rules_create(int device, const Plan& plan, uint32_t chunk, uint32_t ext_cap,
+                        uint32_t adapt_mib, DeviceRules** out);
+void device_rules_destroy(DeviceRules* d);
+// keyword bits K1 no longer reports after its adaptation (null before / without it)
+std::shared_ptr<const std::vector<uint8_t>> device_rules_kw_unknown(const DeviceRules* d);
+uint32_t device_rules_hot_states(const DeviceRules* d);
+
+int lane_create(DeviceRules* d, LaneState** out);
+void lane_destroy(LaneState* l);
+hipStream_t lane_stream(LaneState* l);
+
+int host_out_alloc(const DeviceRules* d, uint32_t files_cap, HostOut* out);
+void host_out_free(HostOut* o);
+
+// The device part of one batch on lane `l`, asynchronously; out->ev[5] completes it.
+int enqueue_scan(DeviceRules* d, LaneState* l, const ScanInput& in, HostOut* out);
+// after out->ev[5]: the HIP-event times of that batch's stages
+int batch_times(const HostOut* out, ScanTimes* t);
+// K1 output of the lane's last batch (test hook): chunk events [nchunks]
+int lane_events(LaneState* l, uint32_t* ev, size_t n);
+
+}  // namespace tsg

@@ -1,40 +1,41 @@
-// MI355X (gfx950) device path of the secret engine over a device-resident batch of file
-// blobs packed back to back in one HBM stream (chunk c = bytes [c*C, (c+1)*C)).
+// MI355X (gfx950) kernels of the secret engine over a batch of file blobs packed back to
+// back in one HBM stream (chunk c = bytes [c*C, (c+1)*C)), and the host code that builds
+// their tables and enqueues one batch on a lane (device.hpp).
 //
 //   K1   one dense pass over every byte: the Aho-Corasick automaton of the rule set's
 //        literals (keywords of Rule.MatchKeywords + anchor literals) stepped from LDS,
 //        fused with two saturating run counters (class U = token bytes, class D = digits).
-//        Outputs per-file keyword bits and per-chunk event bits (plan.hpp kEv*).  A lane
-//        owns kStreams consecutive chunks of one file and steps them as independent
-//        chains; each chain first replays `warm` bytes of the chunk before it, so every
-//        literal / run that ends inside the chunk is seen without state from other lanes.
-//   gate per file: which K2 groups the keyword bits switch on; per chunk: which of those
+//        Outputs per-file keyword bits and per-chunk event bits (plan.hpp kEv*).  The
+//        automaton runs over the batch as one byte stream; each chain first replays `warm`
+//        bytes before its segment, so every literal / run ending inside it is seen.
+//   gates per file: which K2 groups the keyword bits switch on; per chunk: which of those
 //        groups have an event within `back` chunks after it -> (file, chunk) items,
-//        counted, then appended into per-group regions.
-//   K2   per rule group, its DFA (LDS-resident) over the group's items: one fused launch
-//        for all sparse groups (a block per (group, item range)), a dense launch for a
-//        group whose items cover a large share of the batch.  A lane runs its chunk in
-//        inject mode and then follows the threads that started in it until they die
-//        (noinject), so every match end is found by the lane that owns its start.
-//        Accepts append {file, rule, end} candidate records.
+//        counted; a one-block layout kernel turns the counts into item regions and K2's
+//        work list on the device (no host round trip); the items are then written.
+//   K2   a persistent grid over the work list: each entry is up to 512 items of one rule
+//        group (two DFA chains per lane, quad-transposed loads) or a dense range of the
+//        batch; the group's DFA stays staged in LDS across consecutive entries.  A lane
+//        runs its chunk in inject mode and then follows the threads that started in it
+//        until they die (noinject), so every match end is found by the lane that owns its
+//        start.  Accepts append {file, rule, end} candidates (wave-aggregated atomics).
 // Exactness: K1 keyword bits are exact (files with folding runes are flagged), events
 // are a necessary condition of every match of the rule's GPU program (plan.cpp), so the
 // candidate set is a superset of the exact match ends; the host resolves exactly.
 #include <hip/hip_runtime.h>
-#include <malloc.h>
-#include <mutex>
 
 #include <algorithm>
-#include <chrono>
 #include <cstdlib>
 #include <cstring>
-#include <deque>
-#include <future>
+#include <memory>
 #include <vector>
 
+#include "device.hpp"
 #include "internal.hpp"
 
 namespace tsg {
+
+// how K2 covers a rule group in one batch (layout_kernel)
+enum : uint8_t { kGroupNone = 0, kGroupList = 1, kGroupDense = 2, kGroupSkip = 3 };
 
 #define HIP_TRY(x)                                                                    \
   do {                                                                                \
@@ -676,66 +677,204 @@ __device__ __forceinline__ void gen_items(const ItemArgs& A, uint64_t t, V visit
   }
 }
 
+// Both item passes run a fixed grid over the work units t in [0, nev + F) (nev is read on
+// the device, so the host never waits for it), each block visiting the same units twice.
 // count pass: items per group (block totals in LDS, one global atomic per group and block)
 __global__ void __launch_bounds__(kBlock) items_count_kernel(ItemArgs A) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   uint32_t* s_count = (uint32_t*)smem;
   for (uint32_t g = threadIdx.x; g < A.G; g += blockDim.x) s_count[g] = 0;
   __syncthreads();
-  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  gen_items(A, t, [&](uint32_t, uint32_t g, uint64_t lo, uint64_t hi) { atomicAdd(&s_count[g], (uint32_t)(hi - lo + 1)); });
+  const uint64_t nt = (uint64_t)*A.nev + A.F, stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < nt; t += stride)
+    gen_items(A, t, [&](uint32_t, uint32_t g, uint64_t lo, uint64_t hi) { atomicAdd(&s_count[g], (uint32_t)(hi - lo + 1)); });
   __syncthreads();
   for (uint32_t g = threadIdx.x; g < A.G; g += blockDim.x)
     if (s_count[g]) atomicAdd(&A.count[g], s_count[g]);
 }
 
-// emit pass: the block counts its items again, reserves one range per group with a single
-// global atomic, then writes its items into it
+// emit pass: the block counts its items of listed groups again, reserves one range per
+// group with a single global atomic, then writes its items into it
 __global__ void __launch_bounds__(kBlock) items_emit_kernel(ItemArgs A) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   uint32_t* s_count = (uint32_t*)smem;
   uint32_t* s_base = s_count + A.G;
   for (uint32_t g = threadIdx.x; g < A.G; g += blockDim.x) s_count[g] = 0;
   __syncthreads();
-  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  gen_items(A, t, [&](uint32_t, uint32_t g, uint64_t lo, uint64_t hi) {
-    if (A.listed[g]) atomicAdd(&s_count[g], (uint32_t)(hi - lo + 1));
-  });
+  const uint64_t nt = (uint64_t)*A.nev + A.F, stride = (uint64_t)gridDim.x * blockDim.x;
+  const uint64_t t0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (uint64_t t = t0; t < nt; t += stride)
+    gen_items(A, t, [&](uint32_t, uint32_t g, uint64_t lo, uint64_t hi) {
+      if (A.listed[g] == kGroupList) atomicAdd(&s_count[g], (uint32_t)(hi - lo + 1));
+    });
   __syncthreads();
   for (uint32_t g = threadIdx.x; g < A.G; g += blockDim.x) {
     s_base[g] = s_count[g] ? (uint32_t)A.base[g] + atomicAdd(&A.cursor[g], s_count[g]) : 0;
     s_count[g] = 0;
   }
   __syncthreads();
-  gen_items(A, t, [&](uint32_t f, uint32_t g, uint64_t lo, uint64_t hi) {
-    if (!A.listed[g]) return;
-    const uint32_t n = (uint32_t)(hi - lo + 1);
-    uint32_t at = s_base[g] + atomicAdd(&s_count[g], n);
-    for (uint64_t c = lo; c <= hi; c++) A.items[at++] = make_uint2(f, (uint32_t)c);
-  });
+  for (uint64_t t = t0; t < nt; t += stride)
+    gen_items(A, t, [&](uint32_t f, uint32_t g, uint64_t lo, uint64_t hi) {
+      if (A.listed[g] != kGroupList) return;
+      const uint32_t n = (uint32_t)(hi - lo + 1);
+      uint32_t at = s_base[g] + atomicAdd(&s_count[g], n);
+      for (uint64_t c = lo; c <= hi; c++) A.items[at++] = make_uint2(f, (uint32_t)c);
+    });
+}
+
+// ---------------------------------------------------------------- device-side item layout
+// One block decides, from the item counts, how K2 covers each group and writes K2's work
+// list, so the host never reads the counts back:
+//   list   (kGroupList)  its items go to a region of the item array; K2 entries of up to
+//                        kEntryItems items
+//   dense  (kGroupDense) its items cover more than half the batch: K2 entries of
+//                        kEntryChunks consecutive chunks of the whole batch, gated per file
+//   skip   (kGroupSkip)  over the item capacity or the dense budget: K2 does not scan it
+//                        and the host resolves its rules like rules without a GPU program
+// Groups are taken in id order, so the outcome is deterministic.
+struct LayoutArgs {
+  const uint32_t* gcount;  // [G]
+  uint32_t G;
+  uint64_t nchunks, items_cap;
+  uint32_t max_dense;
+  uint8_t* kind;      // [G]
+  uint64_t* base;     // [G] first item of a list group
+  uint4* entries;     // K2 work list: {group, first, n, kind}
+  uint32_t* nentries;
+  uint8_t* gskip;     // [G] (to the host)
+  uint32_t* stats;    // [1] items listed, [2] entries, [3] skipped groups
+};
+
+// exclusive prefix sum of v over the block (blockDim.x = kLayoutBlock); returns the total
+template <class T>
+__device__ T block_exclusive_scan(T v, T* out, T* s_wave) {
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  T x = v;
+  for (int o = 1; o < 64; o <<= 1) {
+    const T y = __shfl_up(x, o);
+    if (lane >= (uint32_t)o) x += y;
+  }
+  if (lane == 63) s_wave[wave] = x;
+  __syncthreads();
+  T before = 0, total = 0;
+  for (uint32_t w = 0; w < nw; w++) {
+    before += w < wave ? s_wave[w] : 0;
+    total += s_wave[w];
+  }
+  *out = before + x - v;
+  __syncthreads();
+  return total;
+}
+
+constexpr int kLayoutBlock = 1024;
+constexpr uint32_t kEntryItems = 2 * kBlock;    // two chains per lane
+constexpr uint32_t kEntryChunks = kStreams * kBlock;
+
+__global__ void __launch_bounds__(kLayoutBlock) layout_kernel(LayoutArgs A) {
+  __shared__ unsigned long long s_wave64[kLayoutBlock / 64];
+  __shared__ unsigned long long s_carry[4];  // items, entries, dense groups, skipped groups
+  if (threadIdx.x < 4) s_carry[threadIdx.x] = 0;
+  __syncthreads();
+  for (uint32_t g0 = 0; g0 < A.G; g0 += blockDim.x) {
+    const uint32_t g = g0 + threadIdx.x;
+    const uint64_t cnt = g < A.G ? A.gcount[g] : 0;
+    const bool dense_want = cnt * 2 > A.nchunks;
+    // dense budget first (in group order), then the item capacity for list groups
+    unsigned long long dpre;
+    const unsigned long long dtot = block_exclusive_scan<unsigned long long>(dense_want ? 1 : 0, &dpre, s_wave64);
+    const bool dense = dense_want && s_carry[2] + dpre < A.max_dense;
+    const bool want_list = cnt && !dense_want;
+    unsigned long long ipre;
+    const unsigned long long itot = block_exclusive_scan<unsigned long long>(want_list ? cnt : 0, &ipre, s_wave64);
+    const bool list = want_list && s_carry[0] + ipre + cnt <= A.items_cap;
+    // items of groups that fit are placed at their prefix position (a skipped group's
+    // range stays unused: the regions keep group order)
+    const uint64_t nent = list ? (cnt + kEntryItems - 1) / kEntryItems
+                               : dense ? (A.nchunks + kEntryChunks - 1) / kEntryChunks : 0;
+    unsigned long long epre;
+    const unsigned long long etot = block_exclusive_scan<unsigned long long>(nent, &epre, s_wave64);
+    const bool skip = cnt && !list && !dense;
+    unsigned long long spre;
+    const unsigned long long stot = block_exclusive_scan<unsigned long long>(skip ? 1 : 0, &spre, s_wave64);
+    // (entries_cap covers every list entry the item capacity allows plus max_dense dense
+    // groups, so the work list always fits)
+    const uint64_t e0 = s_carry[1] + epre;
+    if (g < A.G) {
+      const uint8_t k = !cnt ? kGroupNone : list ? kGroupList : dense ? kGroupDense : kGroupSkip;
+      A.kind[g] = k;
+      A.gskip[g] = k == kGroupSkip ? 1 : 0;
+      A.base[g] = s_carry[0] + ipre;
+      if (k == kGroupList)
+        for (uint64_t i = 0; i < nent; i++) {
+          const uint32_t first = (uint32_t)(i * kEntryItems);
+          A.entries[e0 + i] = make_uint4(g, (uint32_t)(s_carry[0] + ipre) + first,
+                                         (uint32_t)min<uint64_t>(kEntryItems, cnt - first), kGroupList);
+        }
+      else if (k == kGroupDense)
+        for (uint64_t i = 0; i < nent; i++) {
+          const uint64_t first = i * kEntryChunks;
+          A.entries[e0 + i] = make_uint4(g, (uint32_t)first,
+                                         (uint32_t)min<uint64_t>(kEntryChunks, A.nchunks - first), kGroupDense);
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      s_carry[0] += itot;
+      s_carry[1] += etot;
+      s_carry[2] += dtot;
+      s_carry[3] += stot;
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    *A.nentries = (uint32_t)s_carry[1];
+    A.stats[1] = (uint32_t)min<unsigned long long>(s_carry[0], 0xFFFFFFFFull);
+    A.stats[2] = (uint32_t)s_carry[1];
+    A.stats[3] = (uint32_t)s_carry[3];
+  }
 }
 
 // ---------------------------------------------------------------- K2
-struct ScanArgsDev {
+struct K2Args {
   const uint8_t* data;
   const uint64_t* off;
   const uint32_t* chunk_file;
-  uint64_t total, nitems;
+  uint64_t total, nchunks;
   uint32_t chunk, ext_cap;
   const uint32_t* kw;
   uint32_t kw_words;
-  const uint32_t* gmask;  // dense: this group's keyword mask [kw_words]
-  uint32_t galways;
-  const uint2* items;     // list mode
+  const uint32_t* gmask;    // [G * kw_words] keyword gate of each group (dense entries)
+  const uint32_t* galways;  // [G]
+  const uint2* items;       // list entries: (file, chunk)
+  const uint4* entries;     // {group, first, n, kind} (layout_kernel)
+  const uint32_t* nentries;
   DevCand* cand;
   uint32_t* cand_count;
   uint32_t cand_cap;
-  uint32_t* ovf;
+  uint8_t* ovf;
 };
+
+// Candidate emission, wave-aggregated: the lanes that reach an accept together reserve
+// their records with ONE atomic (ballot, popcount prefix, broadcast of the base).  A record
+// past the capacity flags its file for whole-file host resolution instead.
+__device__ __forceinline__ void emit_cand(const K2Args& A, uint32_t file, uint32_t rule, uint64_t end) {
+  const unsigned long long m = __ballot(1);
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t leader = (uint32_t)__builtin_ctzll(m);
+  uint32_t base = 0;
+  if (lane == leader) base = atomicAdd(A.cand_count, (uint32_t)__popcll(m));
+  base = __shfl(base, (int)leader);
+  const uint32_t idx = base + (uint32_t)__popcll(m & ((1ull << lane) - 1));
+  if (idx < A.cand_cap) {
+    A.cand[idx] = DevCand{file, rule, (uint32_t)end};
+  } else {
+    A.ovf[file] = 1;
+  }
+}
 
 struct Lane {
   const DevDFA& d;
-  const ScanArgsDev& A;
+  const K2Args& A;
   const uint16_t* s_tab;
   const uint8_t* s_cls;
   const uint16_t* s_accs;
@@ -747,19 +886,9 @@ struct Lane {
   // the accept bits of 16 transitions and replay the word through step() when one is set
   __device__ __forceinline__ void emit(uint32_t mi, uint64_t pos) {
     const uint64_t* m = (d.state_acc && mi < d.nmasks) ? s_masks + (size_t)mi * d.mw : d.masks + (size_t)mi * d.mw;
-    uint64_t v = m[0];
-    while (v) {
-      uint32_t k = __builtin_ctzll(v);
-      v &= v - 1;
-      uint32_t idx = atomicAdd(A.cand_count, 1u);
-      if (idx < A.cand_cap) {
-        A.cand[idx].file = file;
-        A.cand[idx].rule = d.rules[k];
-        A.cand[idx].end = (uint32_t)(pos - fs);
-      } else {
-        A.ovf[file] = 1;
-      }
-    }
+    for (uint32_t w = 0; w < d.mw; w++)
+      for (uint64_t v = m[w]; v; v &= v - 1)
+        emit_cand(A, file, d.rules[w * 64 + __builtin_ctzll(v)], pos - fs);
   }
 
   __device__ __forceinline__ uint32_t step(uint32_t s, uint32_t byte, uint64_t pos) {
@@ -898,69 +1027,184 @@ __device__ __forceinline__ void stage_dfa(const DevDFA& d, uint8_t* smem) {
   __syncthreads();
 }
 
-// dense: every chunk of the batch, lanes skip the pieces of files the group is not gated on
-__global__ void __launch_bounds__(kBlock) k2_dense_kernel(DevDFA d, ScanArgsDev A) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  stage_dfa(d, smem);
-  Lane L{d, A, (const uint16_t*)smem, smem + d.o_cls, (const uint16_t*)(smem + d.o_accs),
-         (const uint64_t*)(smem + d.o_masks), 0, 0};
-  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-  for (uint64_t it = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; it < A.nitems; it += stride) {
-    uint64_t a = it * kStreams * A.chunk;
-    const uint64_t b = min(a + (uint64_t)kStreams * A.chunk, A.total);
-    uint32_t f = A.chunk_file[it * kStreams];
-    {
-      const uint64_t fs = A.off[f], fe = A.off[f + 1];
-      if (b == a + (uint64_t)kStreams * A.chunk && b <= fe) {  // common case: one file
-        if (group_gated(A.kw + (size_t)f * A.kw_words, A.gmask, A.kw_words, A.galways)) {
-          L.file = f;
-          L.fs = fs;
-          L.template streams<kStreams>(fe, a, A.chunk);
-        }
-        continue;
-      }
+// One list entry: up to kEntryItems (file, chunk) items of group d, two per lane, stepped
+// as two interleaved DFA chains.  Items are whole chunks of the batch stream (aligned to
+// the chunk size, a multiple of 64), so the loads are quad-transposed like K1's: the four
+// lanes of a quad fetch 64 contiguous bytes of one lane's chunk per instruction.  Bytes of
+// a chunk outside the item's file are stepped as no-ops (the file's first byte starts
+// from the start state of its context, its end stops the chain).
+struct K2Item {
+  uint32_t s, file;
+  uint64_t fs, fe, a, b, base;
+};
+
+__device__ __forceinline__ void k2_list_entry(const DevDFA& d, const K2Args& A, const uint16_t* s_tab,
+                                              const uint8_t* s_cls, const uint16_t* s_accs,
+                                              const uint64_t* s_masks, uint4 en) {
+  const uint32_t C = A.chunk;
+  const uint32_t lane = threadIdx.x & 63, q = lane & 3;
+  const bool b0 = q & 1, b1 = (q >> 1) & 1;
+  K2Item it[2];
+  bool live[2];
+#pragma unroll
+  for (int i = 0; i < 2; i++) {
+    const uint32_t k = threadIdx.x + (uint32_t)i * kBlock;
+    live[i] = k < en.z;
+    const uint2 item = A.items[en.y + (live[i] ? k : 0)];
+    it[i].file = item.x;
+    it[i].fs = A.off[item.x];
+    it[i].fe = A.off[item.x + 1];
+    it[i].base = (uint64_t)item.y * C;
+    it[i].a = max(it[i].fs, it[i].base);
+    it[i].b = min(it[i].fe, it[i].base + C);
+    if (!live[i]) it[i].b = it[i].a;  // a ghost steps nothing and emits nothing
+    it[i].s = it[i].a == it[i].fs ? d.start[0] : d.start[ctx_of(A.data[it[i].a - 1])];
+  }
+  // word q of quad lane t's chunk, for each chain
+  const uint8_t* src[2][4];
+#pragma unroll
+  for (int i = 0; i < 2; i++)
+#pragma unroll
+    for (int t = 0; t < 4; t++) {
+      const uint64_t bt = __shfl((unsigned long long)it[i].base, (int)((lane & ~3u) + t));
+      src[i][t] = A.data + bt + 16u * q;
     }
-    while (a < b) {
-      const uint64_t fs = A.off[f], fe = A.off[f + 1];
-      if (fe == fs) {
-        f++;
-        continue;
+  Lane L{d, A, s_tab, s_cls, s_accs, s_masks, 0, 0};
+  auto word = [&](int i, uint64_t wb, const uint4 v) __attribute__((always_inline)) {
+    // bytes [wb, wb + 16) of chain i, stepped where they lie in [a, b)
+    const int32_t lo = (int32_t)max<int64_t>(0, min<int64_t>(16, (int64_t)it[i].a - (int64_t)wb));
+    const int32_t hi = (int32_t)max<int64_t>(0, min<int64_t>(16, (int64_t)it[i].b - (int64_t)wb));
+    uint32_t s = it[i].s, any = 0;
+    const uint32_t s0 = s;
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+      const uint32_t e = s_tab[s * d.nc + s_cls[byte_of(v, k)]];
+      const bool in = k >= lo && k < hi;
+      any |= in ? e : 0u;
+      s = in ? (e & 0x7FFFu) : s;
+    }
+    if (__builtin_expect(any & 0x8000u, 0)) {  // an accept: replay the word, emitting
+      L.file = it[i].file;
+      L.fs = it[i].fs;
+      uint32_t r = s0;
+      for (int k = lo; k < hi; k++) r = L.step(r, byte_of(v, k), wb + k);
+    }
+    it[i].s = s;
+  };
+  auto block = [&](uint64_t j, uint4 (&r)[2][4]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < 2; i++) quad_transpose4(r[i], b0, b1);
+#pragma unroll
+    for (int w = 0; w < 4; w++)
+#pragma unroll
+      for (int i = 0; i < 2; i++) word(i, it[i].base + j + 16u * w, r[i][w]);
+  };
+  auto load = [&](uint4 (&r)[2][4], uint64_t j) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < 2; i++)
+#pragma unroll
+      for (int t = 0; t < 4; t++) r[i][t] = *(const uint4*)(src[i][t] + j);
+  };
+  if (C & 63) {  // chunk sizes that are not whole 64-byte blocks (tests): lane by lane
+#pragma unroll
+    for (int i = 0; i < 2; i++)
+      if (live[i]) {
+        L.file = it[i].file;
+        L.fs = it[i].fs;
+        L.piece(it[i].fe, it[i].a, it[i].b);
       }
-      // the lane owns every match start in [item start, b): pieces may span chunks
-      const uint64_t se = min(b, fe);
-      if (group_gated(A.kw + (size_t)f * A.kw_words, A.gmask, A.kw_words, A.galways)) {
+    return;
+  }
+  uint4 r0[2][4], r1[2][4];
+  load(r0, 0);
+  for (uint64_t j = 0; j < C; j += 128) {
+    const bool two = j + 64 < C;
+    if (two) load(r1, j + 64);
+    block(j, r0);
+    if (j + 128 < C) load(r0, j + 128);
+    if (two) block(j + 64, r1);
+  }
+  // matches that started in the chunk and run past it (inside the file): follow them
+#pragma unroll
+  for (int i = 0; i < 2; i++)
+    if (live[i]) {
+      L.file = it[i].file;
+      L.fs = it[i].fs;
+      L.tail(it[i].s, it[i].fe, it[i].b);
+    }
+}
+
+// One dense entry: chunks [first, first + n) of the batch, kStreams consecutive chunks per
+// lane, every file piece scanned where the group is gated for its file.
+__device__ __forceinline__ void k2_dense_entry(const DevDFA& d, const K2Args& A, uint32_t g, const uint16_t* s_tab,
+                                               const uint8_t* s_cls, const uint16_t* s_accs,
+                                               const uint64_t* s_masks, uint4 en) {
+  Lane L{d, A, s_tab, s_cls, s_accs, s_masks, 0, 0};
+  const uint32_t* gm = A.gmask + (size_t)g * A.kw_words;
+  const uint32_t always = A.galways[g];
+  const uint64_t c0 = en.y + (uint64_t)threadIdx.x * kStreams;
+  if (c0 >= (uint64_t)en.y + en.z) return;
+  uint64_t a = c0 * A.chunk;
+  const uint64_t b = min((c0 + kStreams) * A.chunk, A.total);
+  uint32_t f = A.chunk_file[c0];
+  {
+    const uint64_t fs = A.off[f], fe = A.off[f + 1];
+    if (b == a + (uint64_t)kStreams * A.chunk && a >= fs && b <= fe) {  // common case: one file
+      if (group_gated(A.kw + (size_t)f * A.kw_words, gm, A.kw_words, always)) {
         L.file = f;
         L.fs = fs;
-        L.piece(fe, a, se);
+        L.template streams<kStreams>(fe, a, A.chunk);
       }
-      a = se;
-      f++;
+      return;
     }
+  }
+  while (a < b) {
+    const uint64_t fs = A.off[f], fe = A.off[f + 1];
+    if (fe <= a) {
+      f++;
+      continue;
+    }
+    const uint64_t se = min(b, fe);
+    if (group_gated(A.kw + (size_t)f * A.kw_words, gm, A.kw_words, always)) {
+      L.file = f;
+      L.fs = fs;
+      L.piece(fe, a, se);
+    }
+    a = se;
+    f++;
   }
 }
 
-// list: block b scans items [first, first + n) of group g; blkmap[b] = (g, first, n)
-__global__ void __launch_bounds__(kBlock) k2_list_kernel(const DevDFA* __restrict__ dfas,
-                                                         const uint4* __restrict__ blkmap,
-                                                         ScanArgsDev A) {
+// K2: a persistent grid over the work list.  Block b takes a contiguous range of entries,
+// so consecutive entries mostly share a group and its DFA stays staged in LDS.
+__global__ void __launch_bounds__(kBlock) k2_kernel(const DevDFA* __restrict__ dfas, K2Args A) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  const uint4 bm = blkmap[blockIdx.x];
-  const DevDFA d = dfas[__builtin_amdgcn_readfirstlane(bm.x)];
-  stage_dfa(d, smem);
-  Lane L{d, A, (const uint16_t*)smem, smem + d.o_cls, (const uint16_t*)(smem + d.o_accs),
-         (const uint64_t*)(smem + d.o_masks), 0, 0};
-  for (uint32_t i = threadIdx.x; i < bm.z; i += blockDim.x) {
-    const uint2 item = A.items[bm.y + i];
-    const uint32_t f = item.x;
-    const uint64_t fs = A.off[f], fe = A.off[f + 1];
-    const uint64_t a = max(fs, (uint64_t)item.y * A.chunk);
-    const uint64_t b = min(fe, (uint64_t)(item.y + 1) * A.chunk);
-    if (a < b) {
-      L.file = f;
-      L.fs = fs;
-      L.piece(fe, a, b);
+  const uint32_t E = *A.nentries;
+  const uint32_t e0 = (uint32_t)((uint64_t)E * blockIdx.x / gridDim.x);
+  const uint32_t e1 = (uint32_t)((uint64_t)E * (blockIdx.x + 1) / gridDim.x);
+  uint32_t staged = 0xFFFFFFFFu;
+  for (uint32_t e = e0; e < e1; e++) {
+    const uint4 en = A.entries[e];
+    const uint32_t g = __builtin_amdgcn_readfirstlane(en.x);
+    const DevDFA d = dfas[g];
+    if (g != staged) {
+      __syncthreads();  // every lane is done with the previous table
+      stage_dfa(d, smem);
+      staged = g;
     }
+    const uint16_t* s_tab = (const uint16_t*)smem;
+    if (__builtin_amdgcn_readfirstlane(en.w) == kGroupList)
+      k2_list_entry(d, A, s_tab, smem + d.o_cls, (const uint16_t*)(smem + d.o_accs), (const uint64_t*)(smem + d.o_masks), en);
+    else
+      k2_dense_entry(d, A, g, s_tab, smem + d.o_cls, (const uint16_t*)(smem + d.o_accs), (const uint64_t*)(smem + d.o_masks), en);
   }
+}
+
+// the candidates of a batch to pinned, mapped host memory (their count is only known here)
+__global__ void cand_copy_kernel(const DevCand* __restrict__ src, const uint32_t* __restrict__ count, uint32_t cap,
+                                 DevCand* __restrict__ dst) {
+  const uint32_t n = min(*count, cap);
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) dst[i] = src[i];
 }
 
 // ---------------------------------------------------------------- host side
@@ -1161,129 +1405,96 @@ static int make_device_k1(const Plan& p, DevK1* out, std::vector<void*>* allocs,
   return TSG_OK;
 }
 
-}  // namespace tsg
-
-using namespace tsg;
-
-struct tsg_ctx {
+// ---------------------------------------------------------------- rule tables on a device
+struct DeviceRules {
   int device = 0;
-  const tsg_ruleset* rs = nullptr;
-  tsg_ctx_options opt{};
-  hipStream_t stream = nullptr;
-  hipEvent_t ev[8];
-  std::vector<void*> tables;        // every rule-table allocation
+  const Plan* plan = nullptr;
+  uint32_t chunk = 256, ext_cap = 1u << 16, adapt_mib = 0;
+  int grid = 0;          // 8 blocks per CU
+  int cus = 0;
+  std::vector<void*> tables;
   DevK1 k1{};
   K1Host k1h;
-  uint32_t* d_hits = nullptr;       // [K1 states] (adaptation sample)
+  uint32_t* d_hits = nullptr;
   bool adapted = false;
   uint32_t hot_states = 0;
-  std::vector<uint8_t> kw_unknown;  // [n_kw] keywords K1 stopped reporting
+  std::shared_ptr<const std::vector<uint8_t>> kw_unknown;
   std::vector<uint32_t> h_galways, h_gevents;
   std::vector<unsigned long long> h_gofbit;
   std::vector<DevDFA> groups;
-  DevDFA* d_groups = nullptr;       // [G] (list kernel)
+  DevDFA* d_groups = nullptr;
   DevPathDFA pathdfa{};
   bool has_pathdfa = false;
-  uint8_t* d_paths = nullptr;       // the batch's paths
-  size_t d_paths_cap = 0;
-  uint64_t* d_poff = nullptr;
-  size_t d_poff_cap = 0;
-  uint8_t* d_pathok = nullptr;      // [F] path_allow_kernel output
-  size_t d_pathok_cap = 0;
-  uint32_t* d_gmask = nullptr;      // [G * W]
-  uint32_t* d_galways = nullptr;    // [G]
-  uint32_t* d_gevents = nullptr;    // [G]
-  uint32_t* d_gback = nullptr;      // [G]
-  unsigned long long* d_gofbit = nullptr;  // [32 * GW]
+  uint32_t* d_gmask = nullptr;
+  uint32_t* d_galways = nullptr;
+  uint32_t* d_gevents = nullptr;
+  uint32_t* d_gback = nullptr;
+  unsigned long long* d_gofbit = nullptr;
   std::vector<uint32_t> gback;
-  uint32_t GW = 1, maxback = 0;
-  // batch
-  const uint8_t* h_data = nullptr;
-  const uint64_t* h_off = nullptr;
-  const char* h_paths = nullptr;
-  const uint64_t* h_poff = nullptr;
-  uint32_t nfiles = 0;
-  uint64_t total = 0;
-  uint8_t* d_data_alloc = nullptr;  // kPad | batch | kPad
-  uint8_t* d_data = nullptr;
-  size_t d_data_cap = 0;
-  uint64_t* d_off = nullptr;
-  size_t d_off_cap = 0;
-  uint32_t* d_chunk_file = nullptr;
-  size_t d_chunk_cap = 0;
-  uint32_t* d_ev = nullptr;
-  size_t d_ev_cap = 0;
-  uint32_t* d_evlist = nullptr;  // chunks with events
-  size_t d_evlist_cap = 0;
-  uint32_t* d_kw = nullptr;
-  size_t d_kw_cap = 0;
-  unsigned long long* d_ggate = nullptr;
-  size_t d_ggate_cap = 0;
-  uint32_t* d_ovf = nullptr;
-  size_t d_ovf_cap = 0;
-  DevCand* d_cand = nullptr;
-  uint32_t* d_count = nullptr;      // [0] candidates
-  uint32_t* d_gcount = nullptr;     // [G] items per group
-  uint32_t* d_cursor = nullptr;     // [G]
-  uint64_t* d_base = nullptr;       // [G]
-  uint8_t* d_listed = nullptr;      // [G]
-  uint4* d_blkmap = nullptr;
-  size_t d_blkmap_cap = 0;
-  uint2* d_items = nullptr;
-  size_t d_items_cap = 0;
-  // host mirrors
-  KernelOutput ko;
-  std::vector<std::shared_ptr<KernelOutput>> ko_pool;  // outputs of submitted batches
-  std::vector<uint32_t> h_ovf;
-  uint32_t* h_count = nullptr;
-  tsg_stats stats{};
-  int grid = 0;
-  bool uploaded = false;
-  // host resolutions of submitted batches, oldest first (tsg_batch_submit / collect)
-  struct Pending {
-    std::future<std::unique_ptr<tsg_result>> res;
-    std::shared_ptr<std::pair<double, uint64_t>> done;  // resolve ms, files with findings
-  };
-  std::deque<Pending> pending;
-
-  ~tsg_ctx() {
-    for (auto& pj : pending)
-      if (pj.res.valid()) pj.res.wait();
+  uint32_t GW = 1, maxback = 0, max_lds = 0;
+  ~DeviceRules() {
     (void)hipSetDevice(device);
     for (auto* p : tables) (void)hipFree(p);
     (void)hipFree(d_hits);
-    (void)hipFree(d_data_alloc);
-    (void)hipFree(d_off);
-    (void)hipFree(d_chunk_file);
-    (void)hipFree(d_ev);
-    (void)hipFree(d_evlist);
-    (void)hipFree(d_kw);
-    (void)hipFree(d_ggate);
-    (void)hipFree(d_ovf);
-    (void)hipFree(d_cand);
-    (void)hipFree(d_count);
-    (void)hipFree(d_gcount);
-    (void)hipFree(d_cursor);
-    (void)hipFree(d_base);
-    (void)hipFree(d_listed);
-    (void)hipFree(d_blkmap);
-    (void)hipFree(d_items);
-    (void)hipFree(d_paths);
-    (void)hipFree(d_poff);
-    (void)hipFree(d_pathok);
-    if (h_count) hipHostFree(h_count);
-    for (auto& e : ev)
-      if (e) (void)hipEventDestroy(e);
-    if (stream) hipStreamDestroy(stream);
+  }
+};
+
+// HBM buffers, stream and events of one lane (one batch in flight on the device).
+struct LaneState {
+  DeviceRules* d = nullptr;
+  hipStream_t st = nullptr;
+  uint8_t* data_alloc = nullptr;  // kPad | batch | tail
+  size_t data_cap = 0;
+  uint64_t* off = nullptr;
+  size_t off_cap = 0;
+  uint32_t* chunk_file = nullptr;
+  size_t chunk_cap = 0;
+  uint32_t* ev_bits = nullptr;
+  size_t ev_cap = 0;
+  uint32_t* evlist = nullptr;
+  size_t evlist_cap = 0;
+  uint32_t* kw = nullptr;
+  size_t kw_cap = 0;
+  unsigned long long* ggate = nullptr;
+  size_t ggate_cap = 0;
+  uint8_t* ovf = nullptr;
+  size_t ovf_cap = 0;
+  uint8_t* paths = nullptr;
+  size_t paths_cap = 0;
+  uint64_t* poff = nullptr;
+  size_t poff_cap = 0;
+  uint8_t* pathok = nullptr;
+  size_t pathok_cap = 0;
+  uint2* items = nullptr;
+  size_t items_cap = 0;
+  uint4* entries = nullptr;
+  size_t entries_cap = 0;
+  DevCand* cand = nullptr;
+  uint32_t cand_cap = 0;
+  uint32_t* counts = nullptr;   // [8] 0 candidates, 1 event chunks, 2 K2 entries
+  uint32_t* gcount = nullptr;   // [G]
+  uint32_t* cursor = nullptr;   // [G]
+  uint64_t* base = nullptr;     // [G]
+  uint8_t* kind = nullptr;      // [G]
+  uint8_t* gskip = nullptr;     // [G]
+  uint64_t nchunks = 0;         // last batch
+  ~LaneState() {
+    if (!d) return;
+    (void)hipSetDevice(d->device);
+    if (st) (void)hipStreamSynchronize(st);
+    void* bufs[] = {data_alloc, off, chunk_file, ev_bits, evlist, kw, ggate, ovf, paths, poff, pathok,
+                    items, entries, cand, counts, gcount, cursor, base, kind, gskip};
+    for (void* b : bufs) (void)hipFree(b);
+    if (st) (void)hipStreamDestroy(st);
   }
 };
 
 template <class T>
 static int ensure(T** p, size_t* cap, size_t n) {
   if (*cap >= n && *p) return TSG_OK;
-  if (*p) HIP_TRY(hipFree(*p));
+  if (*p) HIP_TRY(hipFree(*p));  // (hipFree waits for the device)
   *p = nullptr;
-  size_t alloc = std::max<size_t>(n, 16);
+  const size_t alloc = std::max<size_t>(n + n / 8, 16);
   HIP_TRY(hipMalloc((void**)p, alloc * sizeof(T)));
   *cap = alloc;
   return TSG_OK;
@@ -1309,554 +1520,420 @@ static const void* k1_fn_ns(uint32_t kw_words, uint32_t lds_class) {
 // independent K1 chains per lane: 2 (quad-transposed loads keep two 64-byte blocks per
 // chain in registers), or 4 with TSG_K1_NS=4 (measurements)
 static uint32_t k1_streams() {
-  const char* e = getenv("TSG_K1_NS");
-  return (e && atoi(e) == 4) ? 4u : 2u;
+  static const uint32_t ns = (getenv("TSG_K1_NS") && atoi(getenv("TSG_K1_NS")) == 4) ? 4u : 2u;
+  return ns;
 }
 
 static const void* k1_fn(uint32_t kw_words, uint32_t lds_class, uint32_t ns) {
   return ns == 2 ? k1_fn_ns<2>(kw_words, lds_class) : k1_fn_ns<4>(kw_words, lds_class);
 }
 
-static int launch_k1(tsg_ctx* c, const K1Args& A) {
+static int launch_k1(DeviceRules* r, const K1Args& A, hipStream_t st) {
   static const int gmul = getenv("TSG_K1_GRID") ? atoi(getenv("TSG_K1_GRID")) : 0;
-  const uint64_t cap = (uint64_t)c->grid / 8 * (gmul > 0 ? gmul : 8);
+  const uint64_t cap = (uint64_t)r->grid / 8 * (gmul > 0 ? gmul : 8);
   const int grid = (int)std::min<uint64_t>((A.nitems + kK1Block - 1) / kK1Block, cap);
-  DevK1 d = c->k1;
+  DevK1 d = r->k1;
   K1Args a = A;
   void* args[] = {&d, &a};
-  HIP_TRY(hipLaunchKernel(k1_fn(c->k1.kw_words, c->k1.lds_class, A.streams), dim3(grid), dim3(kK1Block), args, 0,
-                          c->stream));
+  HIP_TRY(hipLaunchKernel(k1_fn(r->k1.kw_words, r->k1.lds_class, A.streams), dim3(grid), dim3(kK1Block), args, 0, st));
   HIP_TRY(hipGetLastError());
   return TSG_OK;
 }
 
-// K1 adaptation (once per context, on the first large batch): a sampling pass counts the
+// K1 adaptation (once per device, on the first large batch): a sampling pass counts the
 // arrivals in every accepting state; the most frequent states stop raising the accept
 // flag until the rest arrive at most once per 4 KiB.  The literals those states end are
-// then unknown per file: their keyword gates open (host checks them exactly), their
+// then unknown per file: their keyword gates open (the host checks them exactly), their
 // anchor events fire everywhere.  Results are unchanged; K1 stops paying per-occurrence
-// accepts for words like "key" that occur in most files anyway.
-static int adapt_k1(tsg_ctx* c, uint64_t nchunks, uint64_t k1_items) {
-  const Plan& p = *c->rs->plan;
-  const uint32_t ns = c->k1.ns, W = c->k1.kw_words, mw = c->k1.mw, G = (uint32_t)c->groups.size();
+// accepts for words like "key" that occur in most files anyway.  The device is idle
+// while the shared tables change (every lane is synchronized first).
+static int adapt_k1(DeviceRules* r, LaneState* l, uint64_t total, uint32_t nfiles, uint64_t nchunks, uint64_t k1_items) {
+  const Plan& p = *r->plan;
+  HIP_TRY(hipDeviceSynchronize());
+  const uint32_t ns = r->k1.ns, W = r->k1.kw_words, mw = r->k1.mw, G = (uint32_t)r->groups.size();
   const uint64_t step = std::max<uint64_t>(1, k1_items / 16384);
   const uint64_t nsamp = (k1_items + step - 1) / step;
-  HIP_TRY(hipMemsetAsync(c->d_hits, 0, sizeof(uint32_t) * ns, c->stream));
-  K1Args A{c->d_data, c->d_off, c->d_chunk_file, c->total, nchunks, nsamp, step, c->opt.chunk_bytes,
-           c->nfiles, c->d_kw, c->d_ev, c->d_hits, k1_streams(), (uint32_t)kK1Seg};
+  HIP_TRY(hipMemsetAsync(r->d_hits, 0, sizeof(uint32_t) * ns, l->st));
+  K1Args A{l->data_alloc + kPad, l->off, l->chunk_file, total, nchunks, nsamp, step, r->chunk,
+           nfiles, l->kw, l->ev_bits, r->d_hits, k1_streams(), (uint32_t)kK1Seg};
   int rc;
-  if ((rc = launch_k1(c, A))) return rc;
+  if ((rc = launch_k1(r, A, l->st))) return rc;
   std::vector<uint32_t> hits(ns);
-  HIP_TRY(hipMemcpyAsync(hits.data(), c->d_hits, sizeof(uint32_t) * ns, hipMemcpyDeviceToHost, c->stream));
-  HIP_TRY(hipStreamSynchronize(c->stream));
-  c->adapted = true;
-  const uint64_t sample_bytes = nsamp * A.streams * A.seg * c->opt.chunk_bytes;
-  uint64_t total = 0;
+  HIP_TRY(hipMemcpyAsync(hits.data(), r->d_hits, sizeof(uint32_t) * ns, hipMemcpyDeviceToHost, l->st));
+  HIP_TRY(hipStreamSynchronize(l->st));
+  r->adapted = true;
+  const uint64_t sample_bytes = nsamp * A.streams * A.seg * r->chunk;
+  uint64_t tot = 0;
   std::vector<uint32_t> order;
   for (uint32_t s = 0; s < ns; s++)
     if (hits[s]) {
-      total += hits[s];
+      tot += hits[s];
       order.push_back(s);
     }
   std::sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return hits[a] > hits[b]; });
   const uint64_t budget = sample_bytes / 4096;
   std::vector<uint8_t> hot(p.kw_dfa->nstates, 0);  // automaton states that stop reporting
-  std::vector<uint8_t> kw_unknown(p.n_kw, 0);
+  auto kw_unknown = std::make_shared<std::vector<uint8_t>>(p.n_kw, 0);
   uint32_t ev_hot = 0, nhot = 0;
   for (uint32_t s : order) {  // s: device state id
-    if (total <= budget) break;
-    const uint32_t* m = c->k1h.masks.data() + (size_t)c->k1h.accs[s] * mw;
+    if (tot <= budget) break;
+    const uint32_t* m = r->k1h.masks.data() + (size_t)r->k1h.accs[s] * mw;
     bool fallback = false;  // folding-rune literals must stay exact (they force host resolution)
     for (int k = p.fb_kw0; k < p.n_kw; k++) fallback |= (m[k / 32] >> (k % 32)) & 1;
     if (fallback) continue;
-    hot[c->k1h.order[s]] = 1;
+    hot[r->k1h.order[s]] = 1;
     nhot++;
-    total -= hits[s];
+    tot -= hits[s];
     for (int k = 0; k < p.n_kw; k++)
-      if ((m[k / 32] >> (k % 32)) & 1) kw_unknown[k] = 1;
+      if ((m[k / 32] >> (k % 32)) & 1) (*kw_unknown)[k] = 1;
     ev_hot |= m[W];
   }
-  c->hot_states = nhot;
+  r->hot_states = nhot;
   if (!nhot) return TSG_OK;
-  int rc2;
-  if ((rc2 = k1_tables(p, hot, &c->k1h, &c->k1.start, &c->k1.acc_row))) return rc2;
-  HIP_TRY(hipMemcpy((void*)c->k1.tab, c->k1h.tab.data(), c->k1h.tab.size() * sizeof(uint16_t), hipMemcpyHostToDevice));
-  HIP_TRY(hipMemcpy((void*)c->k1.accs, c->k1h.accs.data(), c->k1h.accs.size() * sizeof(uint16_t), hipMemcpyHostToDevice));
+  if ((rc = k1_tables(p, hot, &r->k1h, &r->k1.start, &r->k1.acc_row))) return rc;
+  HIP_TRY(hipMemcpy((void*)r->k1.tab, r->k1h.tab.data(), r->k1h.tab.size() * sizeof(uint16_t), hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy((void*)r->k1.accs, r->k1h.accs.data(), r->k1h.accs.size() * sizeof(uint16_t), hipMemcpyHostToDevice));
   // gates of groups with an unknown keyword open; events of hot anchor literals fire everywhere
-  std::vector<uint32_t> galways = c->h_galways, gevents = c->h_gevents;
-  std::vector<unsigned long long> gofbit = c->h_gofbit;
+  std::vector<uint32_t> galways = r->h_galways, gevents = r->h_gevents;
+  std::vector<unsigned long long> gofbit = r->h_gofbit;
   for (uint32_t g = 0; g < G; g++) {
-    for (uint32_t r : p.groups[g].rules)
-      if (p.rule_kw_mode[r] == kKwBits)
-        for (uint32_t k : p.rule_kws[r])
-          if (kw_unknown[k]) galways[g] = 1;
+    for (uint32_t q : p.groups[g].rules)
+      if (p.rule_kw_mode[q] == kKwBits)
+        for (uint32_t k : p.rule_kws[q])
+          if ((*kw_unknown)[k]) galways[g] = 1;
     if (gevents[g] & ev_hot) {
       gevents[g] |= kEvAlways;
-      gofbit[31 * c->GW + g / 64] |= 1ull << (g % 64);
+      gofbit[31 * r->GW + g / 64] |= 1ull << (g % 64);
     }
   }
-  HIP_TRY(hipMemcpy(c->d_galways, galways.data(), sizeof(uint32_t) * G, hipMemcpyHostToDevice));
-  HIP_TRY(hipMemcpy(c->d_gevents, gevents.data(), sizeof(uint32_t) * G, hipMemcpyHostToDevice));
-  HIP_TRY(hipMemcpy(c->d_gofbit, gofbit.data(), sizeof(unsigned long long) * gofbit.size(), hipMemcpyHostToDevice));
-  c->kw_unknown = kw_unknown;
+  HIP_TRY(hipMemcpy(r->d_galways, galways.data(), sizeof(uint32_t) * G, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(r->d_gevents, gevents.data(), sizeof(uint32_t) * G, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(r->d_gofbit, gofbit.data(), sizeof(unsigned long long) * gofbit.size(), hipMemcpyHostToDevice));
+  r->kw_unknown = kw_unknown;
   return TSG_OK;
 }
 
-extern "C" {
-
-int tsg_ctx_create(int device, const tsg_ruleset* rs, const tsg_ctx_options* opt, tsg_ctx** out) {
-  if (!rs || !out) return fail(TSG_ERR_ARG, "bad argument");
+int device_rules_create(int device, const Plan& p, uint32_t chunk, uint32_t ext_cap, uint32_t adapt_mib,
+                        DeviceRules** out) {
   int ndev = 0;
   HIP_TRY(hipGetDeviceCount(&ndev));
   if (device < 0 || device >= ndev) return fail(TSG_ERR_GPU, "no such HIP device");
   HIP_TRY(hipSetDevice(device));
-  auto c = std::make_unique<tsg_ctx>();
-  std::memset(c->ev, 0, sizeof(c->ev));
-  c->device = device;
-  c->rs = rs;
-  if (opt) c->opt = *opt;
-  if (c->opt.chunk_bytes == 0) c->opt.chunk_bytes = 256;
-  if (c->opt.chunk_bytes % 16) return fail(TSG_ERR_ARG, "chunk_bytes must be a multiple of 16");
-  if (c->opt.ext_cap == 0) c->opt.ext_cap = 1u << 16;
-  if (c->opt.cand_capacity == 0) c->opt.cand_capacity = 1u << 22;
-  HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
-  // The per-batch host buffers (keyword bits, result vectors, serialized results) are
-  // tens of MB: keep such blocks on the heap (reused, already faulted in) instead of
-  // fresh mmap'ed pages for every batch.
-  static std::once_flag heap_once;
-  std::call_once(heap_once, [] {
-    mallopt(M_MMAP_THRESHOLD, 32 << 20);
-    mallopt(M_TRIM_THRESHOLD, 1 << 30);
-  });
-  for (auto& e : c->ev) HIP_TRY(hipEventCreate(&e));
-  const Plan& p = *rs->plan;
-  const uint32_t W = (uint32_t)p.kw_words;
-  const uint32_t chunk = c->opt.chunk_bytes;
+  auto r = std::make_unique<DeviceRules>();
+  r->device = device;
+  r->plan = &p;
+  r->chunk = chunk;
+  r->ext_cap = ext_cap;
+  r->adapt_mib = adapt_mib;
   if (p.warm > kPad) return fail(TSG_ERR_CONFIG, "a keyword is longer than the K1 warm-up window");
   int rc;
-  if ((rc = make_device_k1(p, &c->k1, &c->tables, &c->k1h))) return rc;
-  HIP_TRY(hipMalloc((void**)&c->d_hits, sizeof(uint32_t) * c->k1.ns));
+  if ((rc = make_device_k1(p, &r->k1, &r->tables, &r->k1h))) return rc;
+  HIP_TRY(hipMalloc((void**)&r->d_hits, sizeof(uint32_t) * r->k1.ns));
   if (const DFA* pd = p.allow_path_dfa.get()) {
     const uint32_t* t = nullptr;
-    if ((rc = upload_vec(pd->next, &t, &c->tables))) return rc;
-    c->pathdfa.next = t;
-    if ((rc = upload_vec(pd->acc, &t, &c->tables))) return rc;
-    c->pathdfa.acc = t;
-    if ((rc = upload_vec(pd->eot_acc, &t, &c->tables))) return rc;
-    c->pathdfa.eot = t;
+    if ((rc = upload_vec(pd->next, &t, &r->tables))) return rc;
+    r->pathdfa.next = t;
+    if ((rc = upload_vec(pd->acc, &t, &r->tables))) return rc;
+    r->pathdfa.acc = t;
+    if ((rc = upload_vec(pd->eot_acc, &t, &r->tables))) return rc;
+    r->pathdfa.eot = t;
     const uint8_t* cl = nullptr;
-    if ((rc = upload_vec(std::vector<uint8_t>(pd->cls, pd->cls + 256), &cl, &c->tables))) return rc;
-    c->pathdfa.cls = cl;
-    c->pathdfa.nc = (uint32_t)pd->nclasses;
-    c->pathdfa.start = pd->start[kCtxBOT];
-    c->has_pathdfa = true;
+    if ((rc = upload_vec(std::vector<uint8_t>(pd->cls, pd->cls + 256), &cl, &r->tables))) return rc;
+    r->pathdfa.cls = cl;
+    r->pathdfa.nc = (uint32_t)pd->nclasses;
+    r->pathdfa.start = pd->start[kCtxBOT];
+    r->has_pathdfa = true;
   }
   const uint32_t G = (uint32_t)p.groups.size();
-  c->GW = std::max<uint32_t>(1, (G + 63) / 64);
+  r->GW = std::max<uint32_t>(1, (G + 63) / 64);
   std::vector<uint32_t> gmask, galways, gevents;
-  std::vector<unsigned long long> gofbit(32 * c->GW, 0);
-  uint32_t max_lds = 0;
+  std::vector<unsigned long long> gofbit(32 * r->GW, 0);
   for (uint32_t g = 0; g < G; g++) {
     const auto& gp = p.groups[g];
     DevDFA dd{};
-    if ((rc = make_device_dfa(*gp.dfa, gp.rules, &dd, &c->tables))) return rc;
-    max_lds = std::max(max_lds, dd.lds_bytes);
-    c->groups.push_back(dd);
+    if ((rc = make_device_dfa(*gp.dfa, gp.rules, &dd, &r->tables))) return rc;
+    r->max_lds = std::max(r->max_lds, dd.lds_bytes);
+    r->groups.push_back(dd);
     gmask.insert(gmask.end(), gp.kwmask.begin(), gp.kwmask.end());
     galways.push_back(gp.always ? 1 : 0);
     gevents.push_back(gp.events);
     uint32_t back = group_back(gp, chunk);
     if (back > (uint32_t)kMaxBack) back = kMaxBack + 1;
-    c->gback.push_back(back);
-    if (back <= (uint32_t)kMaxBack) c->maxback = std::max(c->maxback, back);
+    r->gback.push_back(back);
+    if (back <= (uint32_t)kMaxBack) r->maxback = std::max(r->maxback, back);
     for (int b = 0; b < 32; b++)
-      if (((gp.events >> b) & 1) || back > (uint32_t)kMaxBack) gofbit[b * c->GW + g / 64] |= 1ull << (g % 64);
+      if (((gp.events >> b) & 1) || back > (uint32_t)kMaxBack) gofbit[b * r->GW + g / 64] |= 1ull << (g % 64);
   }
-  if (max_lds > 64 * 1024) {
-    HIP_TRY(hipFuncSetAttribute((const void*)k2_list_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)max_lds));
-    HIP_TRY(hipFuncSetAttribute((const void*)k2_dense_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)max_lds));
-  }
+  if (r->max_lds > 64 * 1024)
+    HIP_TRY(hipFuncSetAttribute((const void*)k2_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)r->max_lds));
   const uint32_t* cg = nullptr;
-  if ((rc = upload_vec(gmask, &cg, &c->tables))) return rc;
-  c->d_gmask = (uint32_t*)cg;
-  if ((rc = upload_vec(galways, &cg, &c->tables))) return rc;
-  c->d_galways = (uint32_t*)cg;
-  if ((rc = upload_vec(gevents, &cg, &c->tables))) return rc;
-  c->d_gevents = (uint32_t*)cg;
-  if ((rc = upload_vec(c->gback, &cg, &c->tables))) return rc;
-  c->d_gback = (uint32_t*)cg;
+  if ((rc = upload_vec(gmask, &cg, &r->tables))) return rc;
+  r->d_gmask = (uint32_t*)cg;
+  if ((rc = upload_vec(galways, &cg, &r->tables))) return rc;
+  r->d_galways = (uint32_t*)cg;
+  if ((rc = upload_vec(gevents, &cg, &r->tables))) return rc;
+  r->d_gevents = (uint32_t*)cg;
+  if ((rc = upload_vec(r->gback, &cg, &r->tables))) return rc;
+  r->d_gback = (uint32_t*)cg;
   const unsigned long long* cb = nullptr;
-  if ((rc = upload_vec(gofbit, &cb, &c->tables))) return rc;
-  c->h_galways = galways;
-  c->h_gevents = gevents;
-  c->h_gofbit = gofbit;
-  c->d_gofbit = (unsigned long long*)cb;
+  if ((rc = upload_vec(gofbit, &cb, &r->tables))) return rc;
+  r->h_galways = galways;
+  r->h_gevents = gevents;
+  r->h_gofbit = gofbit;
+  r->d_gofbit = (unsigned long long*)cb;
   const DevDFA* cd = nullptr;
-  if ((rc = upload_vec(c->groups, &cd, &c->tables))) return rc;
-  c->d_groups = (DevDFA*)cd;
-  HIP_TRY(hipMalloc((void**)&c->d_cand, sizeof(DevCand) * c->opt.cand_capacity));
-  HIP_TRY(hipMalloc((void**)&c->d_count, sizeof(uint32_t) * 4));
-  HIP_TRY(hipMalloc((void**)&c->d_gcount, sizeof(uint32_t) * (G + 1)));
-  HIP_TRY(hipMalloc((void**)&c->d_cursor, sizeof(uint32_t) * (G + 1)));
-  HIP_TRY(hipMalloc((void**)&c->d_base, sizeof(uint64_t) * (G + 1)));
-  HIP_TRY(hipMalloc((void**)&c->d_listed, G + 1));
-  HIP_TRY(hipHostMalloc((void**)&c->h_count, sizeof(uint32_t) * 4, hipHostMallocDefault));
+  if ((rc = upload_vec(r->groups, &cd, &r->tables))) return rc;
+  r->d_groups = (DevDFA*)cd;
   hipDeviceProp_t prop;
   HIP_TRY(hipGetDeviceProperties(&prop, device));
-  c->grid = prop.multiProcessorCount * 8;
-  *out = c.release();
+  r->cus = prop.multiProcessorCount;
+  r->grid = prop.multiProcessorCount * 8;
+  *out = r.release();
   return TSG_OK;
 }
 
-void tsg_ctx_destroy(tsg_ctx* ctx) { delete ctx; }
+void device_rules_destroy(DeviceRules* d) { delete d; }
 
-int tsg_batch_upload(tsg_ctx* c, const uint8_t* data, const uint64_t* offsets, uint32_t nfiles,
-                     const char* paths, const uint64_t* path_offsets) {
-  if (!c || !offsets || !path_offsets) return fail(TSG_ERR_ARG, "bad argument");
-  HIP_TRY(hipSetDevice(c->device));
-  const uint64_t total = offsets[nfiles];
-  if (offsets[0] != 0) return fail(TSG_ERR_ARG, "offsets[0] must be 0");
-  for (uint32_t i = 0; i < nfiles; i++)
-    if (offsets[i + 1] < offsets[i]) return fail(TSG_ERR_ARG, "offsets must be non-decreasing");
-  if (total && !data) return fail(TSG_ERR_ARG, "bad argument");
-  const uint32_t chunk = c->opt.chunk_bytes;
-  if (total / chunk >= (1ull << 32) - 2) return fail(TSG_ERR_ARG, "batch too large for u32 chunk ids");
+std::shared_ptr<const std::vector<uint8_t>> device_rules_kw_unknown(const DeviceRules* d) { return d->kw_unknown; }
+uint32_t device_rules_hot_states(const DeviceRules* d) { return d->hot_states; }
+
+int lane_create(DeviceRules* d, LaneState** out) {
+  HIP_TRY(hipSetDevice(d->device));
+  auto l = std::make_unique<LaneState>();
+  l->d = d;
+  HIP_TRY(hipStreamCreateWithFlags(&l->st, hipStreamNonBlocking));
+  const uint32_t G = std::max<uint32_t>(1, (uint32_t)d->groups.size());
+  HIP_TRY(hipMalloc((void**)&l->counts, sizeof(uint32_t) * 8));
+  HIP_TRY(hipMalloc((void**)&l->gcount, sizeof(uint32_t) * G));
+  HIP_TRY(hipMalloc((void**)&l->cursor, sizeof(uint32_t) * G));
+  HIP_TRY(hipMalloc((void**)&l->base, sizeof(uint64_t) * G));
+  HIP_TRY(hipMalloc((void**)&l->kind, G));
+  HIP_TRY(hipMalloc((void**)&l->gskip, G));
+  *out = l.release();
+  return TSG_OK;
+}
+
+void lane_destroy(LaneState* l) { delete l; }
+hipStream_t lane_stream(LaneState* l) { return l->st; }
+
+int host_out_alloc(const DeviceRules* d, uint32_t files_cap, HostOut* o) {
+  HIP_TRY(hipSetDevice(d->device));
+  HostOut h;
+  h.files_cap = std::max<uint32_t>(files_cap, 1);
+  h.cand_cap = 1u << 22;
+  h.groups = std::max<uint32_t>(1, (uint32_t)d->groups.size());
+  h.kw_words = (uint32_t)d->plan->kw_words;
+  HIP_TRY(hipHostMalloc((void**)&h.kw, sizeof(uint32_t) * (size_t)h.files_cap * h.kw_words, hipHostMallocDefault));
+  HIP_TRY(hipHostMalloc((void**)&h.ovf, h.files_cap, hipHostMallocDefault));
+  HIP_TRY(hipHostMalloc((void**)&h.pathok, h.files_cap, hipHostMallocDefault));
+  HIP_TRY(hipHostMalloc((void**)&h.gskip, h.groups, hipHostMallocDefault));
+  HIP_TRY(hipHostMalloc((void**)&h.cand, sizeof(Candidate) * (size_t)h.cand_cap, hipHostMallocMapped));
+  HIP_TRY(hipHostGetDevicePointer((void**)&h.cand_dev, h.cand, 0));
+  HIP_TRY(hipHostMalloc((void**)&h.counts, sizeof(uint32_t) * 8, hipHostMallocMapped));
+  HIP_TRY(hipHostGetDevicePointer((void**)&h.counts_dev, h.counts, 0));
+  for (auto& e : h.ev) HIP_TRY(hipEventCreate(&e));
+  *o = h;
+  return TSG_OK;
+}
+
+void host_out_free(HostOut* o) {
+  void* ps[] = {o->kw, o->ovf, o->pathok, o->gskip, o->cand, o->counts};
+  for (void* p : ps)
+    if (p) (void)hipHostFree(p);
+  for (auto& e : o->ev)
+    if (e) (void)hipEventDestroy(e);
+  *o = HostOut{};
+}
+
+int enqueue_scan(DeviceRules* r, LaneState* l, const ScanInput& in, HostOut* out) {
+  const Plan& p = *r->plan;
+  HIP_TRY(hipSetDevice(r->device));
+  const uint32_t W = (uint32_t)p.kw_words;
+  const uint32_t C = r->chunk;
+  const uint32_t F = in.nfiles;
+  const uint64_t total = in.total;
+  const uint32_t G = (uint32_t)r->groups.size();
+  hipStream_t st = l->st;
+  if (F > out->files_cap) return fail(TSG_ERR_ARG, "batch has more files than its output buffers");
+  if (total / C >= (1ull << 32) - 2) return fail(TSG_ERR_ARG, "batch too large for u32 chunk ids");
+  const uint64_t nchunks = (total + C - 1) / C;
+  l->nchunks = nchunks;
   int rc;
-  // front pad: K1 warm-up reads before the first chunk; tail: whole K1 items + look-ahead
-  const size_t tail = (size_t)kK1MaxStreams * kK1Seg * chunk + kPad;
-  if (c->d_data_cap < (size_t)total + kPad + tail || !c->d_data_alloc) {
-    if (c->d_data_alloc) HIP_TRY(hipFree(c->d_data_alloc));
-    c->d_data_alloc = nullptr;
-    HIP_TRY(hipMalloc((void**)&c->d_data_alloc, (size_t)total + kPad + tail));
-    c->d_data_cap = (size_t)total + kPad + tail;
-  }
-  c->d_data = c->d_data_alloc + kPad;
-  if ((rc = ensure(&c->d_off, &c->d_off_cap, (size_t)nfiles + 1))) return rc;
-  const uint64_t nchunks = (total + chunk - 1) / chunk;
-  // K1 items are kStreams chunks: chunk-indexed arrays are padded to whole items
+  // ---- buffers (grown on demand; growing waits for the device)
+  const size_t tail = (size_t)kK1MaxStreams * kK1Seg * C + kPad;
+  if ((rc = ensure(&l->data_alloc, &l->data_cap, (size_t)total + kPad + tail))) return rc;
+  uint8_t* data = l->data_alloc + kPad;
+  if ((rc = ensure(&l->off, &l->off_cap, (size_t)F + 1))) return rc;
   const uint64_t k1_item_chunks = (uint64_t)kK1MaxStreams * kK1Seg;
   const uint64_t nchunks_pad = (nchunks + k1_item_chunks - 1) / k1_item_chunks * k1_item_chunks + 1;
-  if ((rc = ensure(&c->d_chunk_file, &c->d_chunk_cap, (size_t)nchunks_pad))) return rc;
-  if ((rc = ensure(&c->d_ev, &c->d_ev_cap, (size_t)nchunks_pad))) return rc;
-  if ((rc = ensure(&c->d_evlist, &c->d_evlist_cap, (size_t)nchunks_pad))) return rc;
-  const int W = c->rs->plan->kw_words;
-  if ((rc = ensure(&c->d_kw, &c->d_kw_cap, (size_t)nfiles * W + 1))) return rc;
-  if ((rc = ensure(&c->d_ggate, &c->d_ggate_cap, (size_t)nfiles * c->GW + 1))) return rc;
-  if ((rc = ensure(&c->d_ovf, &c->d_ovf_cap, (size_t)nfiles + 1))) return rc;
-  HIP_TRY(hipMemsetAsync(c->d_data_alloc, 0, kPad, c->stream));
-  if (total) HIP_TRY(hipMemcpyAsync(c->d_data, data, total, hipMemcpyHostToDevice, c->stream));
-  HIP_TRY(hipMemsetAsync(c->d_data + total, 0, tail, c->stream));
-  HIP_TRY(hipMemcpyAsync(c->d_off, offsets, sizeof(uint64_t) * (nfiles + 1), hipMemcpyHostToDevice, c->stream));
-  if (c->has_pathdfa && nfiles) {
-    const uint64_t pbytes = path_offsets[nfiles];
-    if ((rc = ensure(&c->d_paths, &c->d_paths_cap, (size_t)pbytes + 1))) return rc;
-    if ((rc = ensure(&c->d_poff, &c->d_poff_cap, (size_t)nfiles + 1))) return rc;
-    if ((rc = ensure(&c->d_pathok, &c->d_pathok_cap, (size_t)nfiles))) return rc;
-    if (pbytes) HIP_TRY(hipMemcpyAsync(c->d_paths, paths, pbytes, hipMemcpyHostToDevice, c->stream));
-    HIP_TRY(hipMemcpyAsync(c->d_poff, path_offsets, sizeof(uint64_t) * (nfiles + 1), hipMemcpyHostToDevice,
-                           c->stream));
+  if ((rc = ensure(&l->chunk_file, &l->chunk_cap, (size_t)nchunks_pad))) return rc;
+  if ((rc = ensure(&l->ev_bits, &l->ev_cap, (size_t)nchunks_pad))) return rc;
+  if ((rc = ensure(&l->evlist, &l->evlist_cap, (size_t)nchunks_pad))) return rc;
+  if ((rc = ensure(&l->kw, &l->kw_cap, (size_t)F * W + 1))) return rc;
+  if ((rc = ensure(&l->ggate, &l->ggate_cap, (size_t)F * r->GW + 1))) return rc;
+  if ((rc = ensure(&l->ovf, &l->ovf_cap, (size_t)F + 1))) return rc;
+  // item capacity: twice the batch's chunks (the builtin rules list ~11 % of them); over
+  // it, groups are skipped (kGroupSkip) and resolved on the host, never dropped
+  const uint64_t items_cap = std::max<uint64_t>(2 * nchunks, 1u << 16);
+  const uint32_t max_dense = 16;
+  const uint64_t entries_cap = items_cap / kEntryItems + G + 1 +
+                               (uint64_t)max_dense * ((nchunks + kEntryChunks - 1) / kEntryChunks + 1);
+  if ((rc = ensure(&l->items, &l->items_cap, (size_t)items_cap))) return rc;
+  if ((rc = ensure(&l->entries, &l->entries_cap, (size_t)entries_cap))) return rc;
+  if (!l->cand || l->cand_cap < out->cand_cap) {
+    if (l->cand) HIP_TRY(hipFree(l->cand));
+    HIP_TRY(hipMalloc((void**)&l->cand, sizeof(DevCand) * (size_t)out->cand_cap));
+    l->cand_cap = out->cand_cap;
   }
-  HIP_TRY(hipMemsetAsync(c->d_chunk_file, 0, sizeof(uint32_t) * nchunks_pad, c->stream));
-  if (nfiles) {
-    chunk_file_kernel<<<(nfiles + 255) / 256, 256, 0, c->stream>>>(c->d_off, nfiles, chunk, c->d_chunk_file);
-    HIP_TRY(hipGetLastError());
+  if (r->has_pathdfa && F) {
+    if ((rc = ensure(&l->paths, &l->paths_cap, (size_t)in.poff[F] + 1))) return rc;
+    if ((rc = ensure(&l->poff, &l->poff_cap, (size_t)F + 1))) return rc;
+    if ((rc = ensure(&l->pathok, &l->pathok_cap, (size_t)F))) return rc;
   }
-  HIP_TRY(hipStreamSynchronize(c->stream));
-  c->h_data = data;
-  c->h_off = offsets;
-  c->h_paths = paths;
-  c->h_poff = path_offsets;
-  c->nfiles = nfiles;
-  c->total = total;
-  c->uploaded = true;
-  return TSG_OK;
-}
 
-int tsg_batch_kernels(tsg_ctx* c) {
-  if (!c || !c->uploaded) return fail(TSG_ERR_ARG, "no batch uploaded");
-  HIP_TRY(hipSetDevice(c->device));
-  const Plan& p = *c->rs->plan;
-  const uint32_t W = (uint32_t)p.kw_words;
-  const uint32_t chunk = c->opt.chunk_bytes;
-  const uint64_t nchunks = (c->total + chunk - 1) / chunk;
-  const uint32_t F = c->nfiles;
-  const uint32_t G = (uint32_t)c->groups.size();
-  hipStream_t st = c->stream;
-  HIP_TRY(hipEventRecord(c->ev[0], st));
-  if (F) {
-    HIP_TRY(hipMemsetAsync(c->d_kw, 0, sizeof(uint32_t) * (size_t)F * W, st));
-    HIP_TRY(hipMemsetAsync(c->d_ovf, 0, sizeof(uint32_t) * F, st));
+  // ---- H2D from the pinned slot
+  HIP_TRY(hipEventRecord(out->ev[0], st));
+  HIP_TRY(hipMemsetAsync(l->data_alloc, 0, kPad, st));
+  if (total) HIP_TRY(hipMemcpyAsync(data, in.data, total, hipMemcpyHostToDevice, st));
+  HIP_TRY(hipMemsetAsync(data + total, 0, tail, st));
+  HIP_TRY(hipMemcpyAsync(l->off, in.off, sizeof(uint64_t) * (F + 1), hipMemcpyHostToDevice, st));
+  if (r->has_pathdfa && F) {
+    if (in.poff[F]) HIP_TRY(hipMemcpyAsync(l->paths, in.paths, in.poff[F], hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(l->poff, in.poff, sizeof(uint64_t) * (F + 1), hipMemcpyHostToDevice, st));
   }
-  HIP_TRY(hipMemsetAsync(c->d_count, 0, sizeof(uint32_t) * 4, st));
-  HIP_TRY(hipMemsetAsync(c->d_gcount, 0, sizeof(uint32_t) * (G + 1), st));
-  HIP_TRY(hipMemsetAsync(c->d_cursor, 0, sizeof(uint32_t) * (G + 1), st));
-  HIP_TRY(hipEventRecord(c->ev[1], st));
+  HIP_TRY(hipEventRecord(out->ev[1], st));
+  HIP_TRY(hipMemsetAsync(l->chunk_file, 0, sizeof(uint32_t) * nchunks_pad, st));
+  if (F) {
+    chunk_file_kernel<<<(F + 255) / 256, 256, 0, st>>>(l->off, F, C, l->chunk_file);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemsetAsync(l->kw, 0, sizeof(uint32_t) * (size_t)F * W, st));
+    HIP_TRY(hipMemsetAsync(l->ovf, 0, F, st));
+  }
+  HIP_TRY(hipMemsetAsync(l->counts, 0, sizeof(uint32_t) * 8, st));
+  if (G) {
+    HIP_TRY(hipMemsetAsync(l->gcount, 0, sizeof(uint32_t) * G, st));
+    HIP_TRY(hipMemsetAsync(l->cursor, 0, sizeof(uint32_t) * G, st));
+    HIP_TRY(hipMemsetAsync(l->gskip, 0, G, st));
+    HIP_TRY(hipMemsetAsync(l->kind, 0, G, st));
+  }
 
   // ---- K1
   const uint32_t k1s = k1_streams();
   const uint64_t k1_items = (nchunks + (uint64_t)k1s * kK1Seg - 1) / ((uint64_t)k1s * kK1Seg);
-  int rc;
-  const uint64_t adapt_bytes = c->opt.adapt_mib == 0xFFFFFFFFu ? ~0ull
-                               : (uint64_t)(c->opt.adapt_mib ? c->opt.adapt_mib : 64) << 20;
-  if (!c->adapted && k1_items >= 64 && c->total >= adapt_bytes)
-    if ((rc = adapt_k1(c, nchunks, k1_items))) return rc;
+  const uint64_t adapt_bytes = r->adapt_mib == 0xFFFFFFFFu ? ~0ull : (uint64_t)(r->adapt_mib ? r->adapt_mib : 64) << 20;
+  if (!r->adapted && k1_items >= 64 && total >= adapt_bytes)
+    if ((rc = adapt_k1(r, l, total, F, nchunks, k1_items))) return rc;
   if (k1_items) {
-    K1Args A{c->d_data, c->d_off, c->d_chunk_file, c->total, nchunks, k1_items, 1, chunk, F, c->d_kw, c->d_ev,
-             nullptr, k1s, (uint32_t)kK1Seg};
-    if ((rc = launch_k1(c, A))) return rc;
+    K1Args A{data, l->off, l->chunk_file, total, nchunks, k1_items, 1, C, F, l->kw, l->ev_bits, nullptr, k1s,
+             (uint32_t)kK1Seg};
+    if ((rc = launch_k1(r, A, st))) return rc;
   }
-  HIP_TRY(hipEventRecord(c->ev[2], st));
+  HIP_TRY(hipEventRecord(out->ev[2], st));
 
-  // ---- gate + item counts
-  std::vector<uint32_t> gcount(G, 0);
+  // ---- gates, items, device-side layout
   ItemArgs IA{};
-  IA.off = c->d_off;
-  IA.chunk_file = c->d_chunk_file;
-  IA.ev = c->d_ev;
-  IA.ggate = c->d_ggate;
-  IA.gofbit = c->d_gofbit;
-  IA.gevents = c->d_gevents;
-  IA.gback = c->d_gback;
+  IA.off = l->off;
+  IA.chunk_file = l->chunk_file;
+  IA.ev = l->ev_bits;
+  IA.ggate = l->ggate;
+  IA.gofbit = r->d_gofbit;
+  IA.gevents = r->d_gevents;
+  IA.gback = r->d_gback;
   IA.nchunks = nchunks;
   IA.F = F;
   IA.G = G;
-  IA.GW = c->GW;
-  IA.chunk = chunk;
-  IA.maxback = c->maxback;
-  IA.count = c->d_gcount;
-  IA.cursor = c->d_cursor;
-  IA.listed = c->d_listed;
-  IA.evlist = c->d_evlist;
-  IA.nev = c->d_count + 1;
-  int igrid = 0;
-  if (F && G && nchunks) {
-    if (c->has_pathdfa) {
-      path_allow_kernel<<<(F + 255) / 256, 256, 0, st>>>(c->pathdfa, c->d_paths, c->d_poff, F, c->d_pathok);
-      HIP_TRY(hipGetLastError());
-    }
-    ggate_kernel<<<(F + 255) / 256, 256, 0, st>>>(c->d_kw, F, W, c->d_gmask, c->d_galways, G, c->GW, c->d_ggate);
+  IA.GW = r->GW;
+  IA.chunk = C;
+  IA.maxback = r->maxback;
+  IA.count = l->gcount;
+  IA.cursor = l->cursor;
+  IA.listed = l->kind;
+  IA.evlist = l->evlist;
+  IA.nev = l->counts + 1;
+  IA.base = l->base;
+  IA.items = l->items;
+  const bool work = F && G && nchunks;
+  if (r->has_pathdfa && F) {
+    path_allow_kernel<<<(F + 255) / 256, 256, 0, st>>>(r->pathdfa, l->paths, l->poff, F, l->pathok);
     HIP_TRY(hipGetLastError());
-    const uint32_t cgrid = (uint32_t)std::min<uint64_t>((nchunks + kBlock - 1) / kBlock, (uint64_t)c->grid);
-    ev_compact_kernel<<<cgrid, kBlock, 0, st>>>(c->d_ev, nchunks, c->d_evlist, c->d_count + 1);
+  }
+  if (work) {
+    ggate_kernel<<<(F + 255) / 256, 256, 0, st>>>(l->kw, F, W, r->d_gmask, r->d_galways, G, r->GW, l->ggate);
     HIP_TRY(hipGetLastError());
-    HIP_TRY(hipMemcpyAsync(c->h_count + 1, c->d_count + 1, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipStreamSynchronize(st));
-    igrid = (int)(((uint64_t)c->h_count[1] + F + kBlock - 1) / kBlock);
+    const uint32_t cgrid = (uint32_t)std::min<uint64_t>((nchunks + kBlock - 1) / kBlock, (uint64_t)r->grid);
+    ev_compact_kernel<<<cgrid, kBlock, 0, st>>>(l->ev_bits, nchunks, l->evlist, l->counts + 1);
+    HIP_TRY(hipGetLastError());
+    const int igrid = r->grid;
     hipLaunchKernelGGL(items_count_kernel, dim3(igrid), dim3(kBlock), G * sizeof(uint32_t) + 16, st, IA);
     HIP_TRY(hipGetLastError());
-    HIP_TRY(hipMemcpyAsync(gcount.data(), c->d_gcount, sizeof(uint32_t) * G, hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipStreamSynchronize(st));
-  }
-  // DENSE when a group's items cover a large share of the batch, LIST otherwise
-  std::vector<uint32_t> dense;
-  std::vector<uint64_t> base(G, 0);
-  std::vector<uint8_t> listed(G, 0);
-  std::vector<uint4> blkmap;
-  uint64_t nitems = 0, k2_bytes = 0;
-  uint32_t list_lds = 0;
-  const uint32_t per_block = kBlock * 2;
-  for (uint32_t g = 0; g < G; g++) {
-    if (gcount[g] == 0) continue;
-    k2_bytes += (uint64_t)gcount[g] * chunk;
-    if ((uint64_t)gcount[g] * 2 > nchunks || nitems + gcount[g] >= (1ull << 31)) {
-      dense.push_back(g);
-      continue;
-    }
-    listed[g] = 1;
-    base[g] = nitems;
-    for (uint32_t first = 0; first < gcount[g]; first += per_block)
-      blkmap.push_back(make_uint4(g, (uint32_t)nitems + first, std::min(per_block, gcount[g] - first), 0));
-    nitems += gcount[g];
-    list_lds = std::max(list_lds, c->groups[g].lds_bytes);
-  }
-  if (nitems) {
-    if ((rc = ensure(&c->d_items, &c->d_items_cap, (size_t)nitems))) return rc;
-    if ((rc = ensure(&c->d_blkmap, &c->d_blkmap_cap, blkmap.size()))) return rc;
-    HIP_TRY(hipMemcpyAsync(c->d_base, base.data(), sizeof(uint64_t) * G, hipMemcpyHostToDevice, st));
-    HIP_TRY(hipMemcpyAsync(c->d_listed, listed.data(), G, hipMemcpyHostToDevice, st));
-    HIP_TRY(hipMemcpyAsync(c->d_blkmap, blkmap.data(), sizeof(uint4) * blkmap.size(), hipMemcpyHostToDevice, st));
-    IA.base = c->d_base;
-    IA.items = c->d_items;
+    LayoutArgs LA{l->gcount, G, nchunks, items_cap, max_dense, l->kind, l->base, l->entries, l->counts + 2,
+                  l->gskip, l->counts + 4};
+    hipLaunchKernelGGL(layout_kernel, dim3(1), dim3(kLayoutBlock), 0, st, LA);
+    HIP_TRY(hipGetLastError());
     hipLaunchKernelGGL(items_emit_kernel, dim3(igrid), dim3(kBlock), 2 * G * sizeof(uint32_t) + 16, st, IA);
     HIP_TRY(hipGetLastError());
   }
-  HIP_TRY(hipEventRecord(c->ev[3], st));
+  HIP_TRY(hipEventRecord(out->ev[3], st));
 
-  // ---- K2
-  ScanArgsDev A{};
-  A.data = c->d_data;
-  A.off = c->d_off;
-  A.chunk_file = c->d_chunk_file;
-  A.total = c->total;
-  A.chunk = chunk;
-  A.ext_cap = c->opt.ext_cap;
-  A.kw = c->d_kw;
-  A.kw_words = W;
-  A.cand = c->d_cand;
-  A.cand_count = c->d_count;
-  A.cand_cap = c->opt.cand_capacity;
-  A.ovf = c->d_ovf;
-  if (nitems) {
-    ScanArgsDev B = A;
-    B.items = c->d_items;
-    B.nitems = nitems;
-    hipLaunchKernelGGL(k2_list_kernel, dim3((uint32_t)blkmap.size()), dim3(kBlock), list_lds, st,
-                       (const DevDFA*)c->d_groups, (const uint4*)c->d_blkmap, B);
+  // ---- K2 over the work list
+  if (work) {
+    K2Args A{};
+    A.data = data;
+    A.off = l->off;
+    A.chunk_file = l->chunk_file;
+    A.total = total;
+    A.nchunks = nchunks;
+    A.chunk = C;
+    A.ext_cap = r->ext_cap;
+    A.kw = l->kw;
+    A.kw_words = W;
+    A.gmask = r->d_gmask;
+    A.galways = r->d_galways;
+    A.items = l->items;
+    A.entries = l->entries;
+    A.nentries = l->counts + 2;
+    A.cand = l->cand;
+    A.cand_count = l->counts;
+    A.cand_cap = out->cand_cap;
+    A.ovf = l->ovf;
+    const int kgrid = r->cus * std::max(1, (int)(160 * 1024 / std::max<uint32_t>(r->max_lds, 1)));
+    hipLaunchKernelGGL(k2_kernel, dim3(std::min(kgrid, r->grid)), dim3(kBlock), r->max_lds, st,
+                       (const DevDFA*)r->d_groups, A);
     HIP_TRY(hipGetLastError());
   }
-  for (uint32_t g : dense) {
-    ScanArgsDev B = A;
-    B.nitems = (nchunks + kStreams - 1) / kStreams;
-    B.gmask = c->d_gmask + (size_t)g * W;
-    B.galways = p.groups[g].always ? 1 : 0;
-    const int grid = (int)std::min<uint64_t>((B.nitems + kBlock - 1) / kBlock, (uint64_t)c->grid);
-    hipLaunchKernelGGL(k2_dense_kernel, dim3(grid), dim3(kBlock), c->groups[g].lds_bytes, st, c->groups[g], B);
-    HIP_TRY(hipGetLastError());
-  }
-  HIP_TRY(hipEventRecord(c->ev[4], st));
-  HIP_TRY(hipMemcpyAsync(c->h_count, c->d_count, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
-  HIP_TRY(hipStreamSynchronize(st));
-  uint32_t n = std::min(*c->h_count, c->opt.cand_capacity);
-  c->ko.cand.resize(n);
-  c->ko.kw.resize((size_t)F * W);
-  std::vector<uint32_t>& ovf = c->h_ovf;
-  ovf.resize(F);
-  if (n) HIP_TRY(hipMemcpyAsync(c->ko.cand.data(), c->d_cand, sizeof(DevCand) * n, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipEventRecord(out->ev[4], st));
+
+  // ---- results to the pinned host buffers
+  cand_copy_kernel<<<64, 256, 0, st>>>(l->cand, l->counts, out->cand_cap, (DevCand*)out->cand_dev);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipMemcpyAsync(out->counts, l->counts, sizeof(uint32_t) * 8, hipMemcpyDeviceToHost, st));
   if (F) {
-    HIP_TRY(hipMemcpyAsync(c->ko.kw.data(), c->d_kw, sizeof(uint32_t) * (size_t)F * W, hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipMemcpyAsync(ovf.data(), c->d_ovf, sizeof(uint32_t) * F, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(out->kw, l->kw, sizeof(uint32_t) * (size_t)F * W, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(out->ovf, l->ovf, F, hipMemcpyDeviceToHost, st));
+    if (r->has_pathdfa) HIP_TRY(hipMemcpyAsync(out->pathok, l->pathok, F, hipMemcpyDeviceToHost, st));
   }
-  if (!(F && c->has_pathdfa)) c->ko.path_ok.clear();
-  if (F && c->has_pathdfa) {
-    c->ko.path_ok.resize(F);
-    HIP_TRY(hipMemcpyAsync(c->ko.path_ok.data(), c->d_pathok, F, hipMemcpyDeviceToHost, st));
-  }
-  HIP_TRY(hipEventRecord(c->ev[5], st));
-  HIP_TRY(hipStreamSynchronize(st));
-  c->ko.kw_unknown = c->kw_unknown;
-  c->ko.overflow.resize(F);
-  for (uint32_t i = 0; i < F; i++) c->ko.overflow[i] = ovf[i] ? 1 : 0;
-  float t[5] = {0, 0, 0, 0, 0};
-  for (int k = 0; k < 5; k++) HIP_TRY(hipEventElapsedTime(&t[k], c->ev[k], c->ev[k + 1]));
-  c->stats.k1_ms = t[1];
-  c->stats.gate_ms = t[2];
-  c->stats.k2_ms = t[3];
-  c->stats.aux_ms = t[0] + t[4];
-  c->stats.bytes = c->total;
-  c->stats.k2_bytes = k2_bytes;
-  c->stats.k2_items = nitems;
-  c->stats.candidates = *c->h_count;
-  c->stats.overflow = *c->h_count > c->opt.cand_capacity ? 1 : 0;
-  c->stats.k2_launches = (uint32_t)(dense.size() + (nitems ? 1 : 0));
-  c->stats.k1_hot_states = c->hot_states;
+  if (G) HIP_TRY(hipMemcpyAsync(out->gskip, l->gskip, G, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipEventRecord(out->ev[5], st));
   return TSG_OK;
 }
 
-// Host resolution of one batch's kernel output (exact findings, serialized).
-static std::unique_ptr<tsg_result> resolve_job(const tsg_ruleset* rs, BatchView b, const KernelOutput& ko,
-                                               int nt, std::pair<double, uint64_t>* done) {
-  auto t0 = std::chrono::steady_clock::now();
-  BatchResult res;
-  resolve_batch(rs->rs, *rs->plan, b, ko, nt, &res);
-  auto t1 = std::chrono::steady_clock::now();
-  auto r = std::make_unique<tsg_result>();
-  serialize_batch(res, &r->buf, nt);
-  if (getenv("TSG_PROF"))
-    fprintf(stderr, "resolve_job: resolve_batch %.1f ms, serialize %.1f ms\n",
-            std::chrono::duration<double, std::milli>(t1 - t0).count(),
-            std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t1).count());
-  done->first = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-  done->second = 0;
-  for (uint8_t st : res.status) done->second += st == kHasFindings;
-  return r;
-}
-
-int tsg_batch_submit(tsg_ctx* c) {
-  if (!c) return fail(TSG_ERR_ARG, "bad argument");
-  int rc = tsg_batch_kernels(c);
-  if (rc) return rc;
-  try {
-    tsg_ctx::Pending pj;
-    pj.done = std::make_shared<std::pair<double, uint64_t>>(0.0, 0);
-    // the batch's output goes to a pooled KernelOutput no pending job holds; c->ko gets
-    // that entry's buffers back, so the next batch reuses their pages (no allocation and
-    // no page faults for the tens of MB of keyword bits per batch)
-    std::shared_ptr<KernelOutput> ko;
-    for (auto& e : c->ko_pool)
-      if (e.use_count() == 1) {
-        ko = e;
-        break;
-      }
-    if (!ko) {
-      ko = std::make_shared<KernelOutput>();
-      c->ko_pool.push_back(ko);
-    }
-    std::swap(*ko, c->ko);
-    BatchView b{c->h_data, c->h_off, c->nfiles, c->h_paths, c->h_poff};
-    const tsg_ruleset* rs = c->rs;
-    const int nt = c->opt.host_threads > 0 ? c->opt.host_threads : 16;
-    auto done = pj.done;
-    pj.res = std::async(std::launch::async, [rs, b, ko, nt, done]() { return resolve_job(rs, b, *ko, nt, done.get()); });
-    c->pending.push_back(std::move(pj));
-    return TSG_OK;
-  } catch (const std::bad_alloc&) {
-    return fail(TSG_ERR_NOMEM, "out of memory");
-  } catch (const std::exception& ex) {
-    return fail(TSG_ERR_INTERNAL, ex.what());
-  }
-}
-
-int tsg_batch_collect(tsg_ctx* c, tsg_result** out) {
-  if (!c || !out) return fail(TSG_ERR_ARG, "bad argument");
-  if (c->pending.empty()) return fail(TSG_ERR_ARG, "no submitted batch");
-  tsg_ctx::Pending pj = std::move(c->pending.front());
-  c->pending.pop_front();
-  try {
-    std::unique_ptr<tsg_result> r = pj.res.get();
-    c->stats.resolve_ms = pj.done->first;
-    c->stats.files_resolved = pj.done->second;
-    *out = r.release();
-    return TSG_OK;
-  } catch (const std::bad_alloc&) {
-    return fail(TSG_ERR_NOMEM, "out of memory");
-  } catch (const std::exception& ex) {
-    return fail(TSG_ERR_INTERNAL, ex.what());
-  }
-}
-
-int tsg_batch_pending(const tsg_ctx* c) { return c ? (int)c->pending.size() : TSG_ERR_ARG; }
-
-int tsg_batch_scan(tsg_ctx* c, tsg_result** out) {
-  if (!c || !out) return fail(TSG_ERR_ARG, "bad argument");
-  if (!c->pending.empty()) return fail(TSG_ERR_ARG, "collect the submitted batches first");
-  int rc = tsg_batch_submit(c);
-  if (rc) return rc;
-  return tsg_batch_collect(c, out);
-}
-
-int tsg_scan_batch(tsg_ctx* c, const uint8_t* data, const uint64_t* offsets, uint32_t nfiles,
-                   const char* paths, const uint64_t* path_offsets, tsg_result** out) {
-  int rc = tsg_batch_upload(c, data, offsets, nfiles, paths, path_offsets);
-  if (rc) return rc;
-  return tsg_batch_scan(c, out);
-}
-
-int tsg_batch_k1_output(tsg_ctx* c, uint32_t* kw, size_t kw_len, uint32_t* ev, size_t ev_len) {
-  if (!c || !c->uploaded) return fail(TSG_ERR_ARG, "no batch uploaded");
-  HIP_TRY(hipSetDevice(c->device));
-  const uint64_t nchunks = (c->total + c->opt.chunk_bytes - 1) / c->opt.chunk_bytes;
-  if (kw) std::memcpy(kw, c->ko.kw.data(), sizeof(uint32_t) * std::min(kw_len, c->ko.kw.size()));
-  if (ev && nchunks)
-    HIP_TRY(hipMemcpy(ev, c->d_ev, sizeof(uint32_t) * std::min<uint64_t>(ev_len, nchunks), hipMemcpyDeviceToHost));
+int batch_times(const HostOut* o, ScanTimes* t) {
+  float x[5] = {0, 0, 0, 0, 0};
+  for (int k = 0; k < 5; k++) HIP_TRY(hipEventElapsedTime(&x[k], o->ev[k], o->ev[k + 1]));
+  t->h2d = x[0];
+  t->k1 = x[1];
+  t->gates = x[2];
+  t->k2 = x[3];
+  t->d2h = x[4];
   return TSG_OK;
 }
 
-int tsg_ctx_get_stats(const tsg_ctx* c, tsg_stats* out) {
-  if (!c || !out) return fail(TSG_ERR_ARG, "bad argument");
-  *out = c->stats;
+int lane_events(LaneState* l, uint32_t* ev, size_t n) {
+  HIP_TRY(hipSetDevice(l->d->device));
+  HIP_TRY(hipStreamSynchronize(l->st));
+  if (n && l->nchunks)
+    HIP_TRY(hipMemcpy(ev, l->ev_bits, sizeof(uint32_t) * std::min<uint64_t>(n, l->nchunks), hipMemcpyDeviceToHost));
   return TSG_OK;
 }
 
-}  // extern "C"
+}  // namespace tsg

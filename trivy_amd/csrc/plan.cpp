@@ -676,18 +676,18 @@ bool run_segment(const DFA& d, const uint8_t* data, uint64_t fs, uint64_t fe, ui
 }  // namespace
 
 void resolve_batch(const Ruleset& rs, const Plan& plan, const BatchView& b,
-                   const KernelOutput& ko, int nthreads, BatchResult* out) {
+                   const KernelOutputView& ko, int nthreads, BatchResult* out) {
   const uint32_t F = b.nfiles;
   const size_t R = rs.rules.size();
   const uint64_t t_ser0 = __rdtsc();
   // bucket candidates by file (counting sort), then sort each file's few by (rule, end)
   std::vector<uint32_t> first(F + 1, 0);
-  for (const auto& c : ko.cand) first[c.file + 1]++;
+  for (size_t i = 0; i < ko.ncand; i++) first[ko.cand[i].file + 1]++;
   for (uint32_t f = 0; f < F; f++) first[f + 1] += first[f];
-  std::vector<Candidate> cand(ko.cand.size());
+  std::vector<Candidate> cand(ko.ncand);
   {
     std::vector<uint32_t> fill(first.begin(), first.end() - 1);
-    for (const auto& c : ko.cand) cand[fill[c.file]++] = c;
+    for (size_t i = 0; i < ko.ncand; i++) cand[fill[ko.cand[i].file]++] = ko.cand[i];
   }
   auto by_rule_end = [](const Candidate& x, const Candidate& y) {
     return x.rule != y.rule ? x.rule < y.rule : x.end < y.end;
@@ -695,7 +695,9 @@ void resolve_batch(const Ruleset& rs, const Plan& plan, const BatchView& b,
 
   std::vector<uint32_t> hostonly;
   for (size_t r = 0; r < R; r++)
-    if (plan.rule_hostonly[r]) hostonly.push_back((uint32_t)r);
+    if (plan.rule_hostonly[r] ||
+        (ko.group_skipped && plan.rule_group[r] >= 0 && ko.group_skipped[plan.rule_group[r]]))
+      hostonly.push_back((uint32_t)r);
   std::vector<uint8_t> kw_has_i(R, 0), kw_has_k(R, 0);
   for (size_t r = 0; r < R; r++)
     for (const auto& k : rs.rules[r].kw_lower) {
@@ -706,7 +708,7 @@ void resolve_batch(const Ruleset& rs, const Plan& plan, const BatchView& b,
   const uint64_t t_ser1 = __rdtsc();
   // Global.AllowPath (scanner.go:343-347): from the device when it decided the path
   auto path_ok = [&](uint32_t f) -> bool {
-    if (!ko.path_ok.empty() && ko.path_ok[f] < 2) return ko.path_ok[f] == 1;
+    if (ko.path_ok && ko.path_ok[f] < 2) return ko.path_ok[f] == 1;
     return path_allowed(rs, &plan, b.paths + b.path_offsets[f], b.path_offsets[f + 1] - b.path_offsets[f]);
   };
   // Files that need the exact scan: candidates, empty files, kernel overflow, folding
@@ -721,9 +723,9 @@ void resolve_batch(const Ruleset& rs, const Plan& plan, const BatchView& b,
     uint32_t cnt = 0;
     for (uint32_t f = (uint32_t)(bi * kBlk), fe = (uint32_t)std::min<size_t>(F, (bi + 1) * kBlk); f < fe; f++) {
       bool need = first[f] != first[f + 1] || b.offsets[f + 1] == b.offsets[f] ||
-                  (!ko.overflow.empty() && ko.overflow[f]) || !hostonly.empty();
+                  (ko.overflow && ko.overflow[f]) || !hostonly.empty();
       if (!need) {
-        const uint32_t* kw = ko.kw.data() + (size_t)f * plan.kw_words;
+        const uint32_t* kw = ko.kw + (size_t)f * plan.kw_words;
         for (int k = plan.fb_kw0; k < plan.n_kw && !need; k++) need = (kw[k / 32] >> (k % 32)) & 1;
       }
       if (need) {
@@ -791,7 +793,7 @@ void resolve_batch(const Ruleset& rs, const Plan& plan, const BatchView& b,
       scan_file(rs, std::string(pp, pn), content, 0, nullptr, &res);
       return;
     }
-    const uint32_t* kw = ko.kw.data() + (size_t)f * plan.kw_words;
+    const uint32_t* kw = ko.kw + (size_t)f * plan.kw_words;
     // folding runes present: bit 0 U+0130, bit 1 U+212A, bit 2 U+017F
     uint32_t fbbits = 0;
     for (int k = plan.fb_kw0; k < plan.n_kw; k++)
@@ -806,7 +808,7 @@ void resolve_batch(const Ruleset& rs, const Plan& plan, const BatchView& b,
         default:
           for (uint32_t k : plan.rule_kws[r])
             if ((kw[k / 32] >> (k % 32)) & 1) return 1;
-          if (!ko.kw_unknown.empty())
+          if (ko.kw_unknown)
             for (uint32_t k : plan.rule_kws[r])
               if (ko.kw_unknown[k]) return 2;  // the kernels scanned the rule's group
           // 3: uncertain and the kernels did not scan the rule (its keyword bits were clear)
@@ -815,7 +817,7 @@ void resolve_batch(const Ruleset& rs, const Plan& plan, const BatchView& b,
       }
     };
     // kernel overflow: resolve every rule over the whole file
-    const bool ovf = !ko.overflow.empty() && ko.overflow[f];
+    const bool ovf = ko.overflow && ko.overflow[f];
     bool any_host = false;
     for (uint32_t r : hostonly)
       if (kw_state(r) != 0) any_host = true;

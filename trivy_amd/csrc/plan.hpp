@@ -96,6 +96,20 @@ struct Candidate {
   uint32_t end;
 };
 
+// What the kernels hand back for one batch, wherever it lives (pinned host buffers of the
+// device pipeline, or the vectors of a CPU emulation).
+struct KernelOutputView {
+  const uint32_t* kw = nullptr;     // [nfiles * kw_words]
+  const Candidate* cand = nullptr;
+  size_t ncand = 0;
+  const uint8_t* overflow = nullptr;    // [nfiles] or null: 1 = resolve the whole file exactly
+  const uint8_t* kw_unknown = nullptr;  // [n_kw] or null: keyword bits K1 no longer reports
+  const uint8_t* path_ok = nullptr;     // [nfiles] or null: Global.AllowPath from the device
+  // [groups] or null: groups K2 did not scan in this batch (item capacity); their rules are
+  // resolved like rules without a GPU program
+  const uint8_t* group_skipped = nullptr;
+};
+
 // Everything the kernels hand back for one batch.
 struct KernelOutput {
   std::vector<uint32_t> kw;        // [nfiles * kw_words]
@@ -106,6 +120,16 @@ struct KernelOutput {
   // [nfiles] (or empty): Global.AllowPath of each path computed on the device:
   // 0 / 1, or 2 = non-ASCII path, decided on the host
   std::vector<uint8_t> path_ok;
+  KernelOutputView view() const {
+    KernelOutputView v;
+    v.kw = kw.data();
+    v.cand = cand.data();
+    v.ncand = cand.size();
+    v.overflow = overflow.empty() ? nullptr : overflow.data();
+    v.kw_unknown = kw_unknown.empty() ? nullptr : kw_unknown.data();
+    v.path_ok = path_ok.empty() ? nullptr : path_ok.data();
+    return v;
+  }
 };
 
 struct BatchView {
@@ -118,7 +142,7 @@ struct BatchView {
 
 // Host resolution: exact findings for every file of the batch.
 void resolve_batch(const Ruleset& rs, const Plan& plan, const BatchView& b,
-                   const KernelOutput& ko, int nthreads, BatchResult* out);
+                   const KernelOutputView& ko, int nthreads, BatchResult* out);
 
 // Exact CPU path for a whole batch (no GPU).
 void scan_batch_cpu(const Ruleset& rs, const BatchView& b, int nthreads,

@@ -382,17 +382,25 @@ def decode_results(buf, paths, rules):
 
 
 class GpuContext:
-    """One device context (tsg_ctx): replicated rule tables + batch buffers in HBM."""
+    """One device context (tsg_ctx): rule tables replicated in HBM, two lanes, pinned slots.
+
+    upload() copies a batch into a context-owned pinned slot (the library keeps no pointer
+    to the caller's buffers); submit()/collect() pipeline scans, each collected result is
+    decoded with the paths of the batch it was submitted for (FIFO).  emulate=True runs
+    the kernels' algorithm on the CPU over the same pipeline (tests without a GPU)."""
 
     def __init__(self, scanner, device=0, chunk_bytes=0, ext_cap=0, cand_capacity=0,
-                 host_threads=0, adapt_mib=0):
+                 host_threads=0, adapt_mib=0, emulate=False, slot_mib=0, max_slots=0):
         self._h = None
         self.scanner = scanner
-        opt = N.CtxOptions(chunk_bytes, ext_cap, cand_capacity, host_threads, adapt_mib)
+        opt = N.CtxOptions(chunk_bytes, ext_cap, cand_capacity, host_threads, adapt_mib,
+                           N.TSG_CTX_EMULATE if emulate else 0, slot_mib, max_slots)
         h = C.c_void_p()
         N.check(N.lib().tsg_ctx_create(int(device), scanner.handle, C.byref(opt), C.byref(h)))
         self._h = h
-        self._batch = None
+        self._paths = None      # paths of the last uploaded batch
+        self._nfiles = 0
+        self._fifo = []         # paths of each submitted, uncollected batch
 
     @property
     def handle(self):
@@ -400,15 +408,15 @@ class GpuContext:
 
     def upload(self, batch):
         N.check(N.lib().tsg_batch_upload(self._h, *batch.ptrs()))
-        self._batch = batch  # host buffers must outlive the scans
+        self._paths = batch
+        self._nfiles = batch.nfiles
 
     def kernels(self):
         N.check(N.lib().tsg_batch_kernels(self._h))
 
     def k1_output(self, chunk):
         """(keyword bits [nfiles, kw_words], chunk event bits) of the last kernels() call."""
-        import numpy as np
-        b = self._batch
+        b = self._paths
         W = (self.scanner.info()["n_keywords"] + 31) // 32
         kw = np.zeros(b.nfiles * W, dtype=np.uint32)
         ev = np.zeros((int(b.offsets[-1]) + chunk - 1) // chunk, dtype=np.uint32)
@@ -417,33 +425,56 @@ class GpuContext:
                                             ev.ctypes.data_as(u32p), ev.size))
         return kw.reshape(b.nfiles, W), ev
 
-    def scan_raw(self):
-        out = C.c_void_p()
-        N.check(N.lib().tsg_batch_scan(self._h, C.byref(out)))
-        return out
+    def _paths_of(self, batch):
+        return [batch.path(i) for i in range(batch.nfiles)]
 
     def submit(self):
-        """Device part of a scan now; its host resolution runs in the background."""
+        """Device part of a scan of the uploaded batch, asynchronously; its host resolution
+        follows it in the background."""
         N.check(N.lib().tsg_batch_submit(self._h))
+        self._fifo.append(self._paths)
+
+    def submit_slot(self, slot_id, nfiles, paths_of=None):
+        """Submit the first nfiles files of an acquired slot (see acquire_slot)."""
+        N.check(N.lib().tsg_slot_submit(self._h, int(slot_id), int(nfiles)))
+        self._fifo.append(paths_of)
+
+    def acquire_slot(self, data_bytes, nfiles, path_bytes):
+        """A pinned slot to fill directly: (id, data, offsets, paths, path_offsets) as
+        numpy views of the library's pinned memory."""
+        v = N.SlotView()
+        N.check(N.lib().tsg_slot_acquire(self._h, int(data_bytes), int(nfiles),
+                                         int(path_bytes), C.byref(v)))
+        data = np.ctypeslib.as_array((C.c_uint8 * v.data_cap).from_address(v.data))
+        offs = np.ctypeslib.as_array(v.offsets, shape=(v.files_cap + 1,))
+        paths = np.ctypeslib.as_array((C.c_uint8 * v.paths_cap).from_address(v.paths))
+        poffs = np.ctypeslib.as_array(v.path_offsets, shape=(v.files_cap + 1,))
+        return v.id, data, offs, paths, poffs
+
+    def release_slot(self, slot_id):
+        N.check(N.lib().tsg_slot_release(self._h, int(slot_id)))
 
     def collect_raw(self):
         """Results of the oldest submitted scan (raw tsg_result handle)."""
         out = C.c_void_p()
-        N.check(N.lib().tsg_batch_collect(self._h, C.byref(out)))
+        try:
+            N.check(N.lib().tsg_batch_collect(self._h, C.byref(out)))
+        finally:
+            if self._fifo:
+                self._last_collected = self._fifo.pop(0)
         return out
 
     def collect(self):
         out = self.collect_raw()
-        b = self._batch
-        return self.scanner.decode(out, [b.path(i) for i in range(b.nfiles)])
+        b = self._last_collected
+        return self.scanner.decode(out, self._paths_of(b))
 
     def pending(self):
         return N.lib().tsg_batch_pending(self._h)
 
     def scan(self):
-        out = self.scan_raw()
-        b = self._batch
-        return self.scanner.decode(out, [b.path(i) for i in range(b.nfiles)])
+        self.submit()
+        return self.collect()
 
     def stats(self):
         s = N.Stats()
@@ -453,6 +484,36 @@ class GpuContext:
     def close(self):
         if self._h:
             N.lib().tsg_ctx_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        self.close()
+
+
+class ScanQueue:
+    """tsg_queue: Scan(ScanArgs) for many concurrent callers sharing one context; their
+    files are coalesced into pinned batches (the analyzer's per-file goroutines,
+    pkg/fanal/analyzer/analyzer.go:419-443)."""
+
+    def __init__(self, ctx, flush_us=2000):
+        self.ctx = ctx
+        h = C.c_void_p()
+        N.check(N.lib().tsg_queue_create(ctx.handle, int(flush_us), C.byref(h)))
+        self._h = h
+
+    def Scan(self, args):
+        p = _b(args.FilePath)
+        out = C.c_void_p()
+        N.check(N.lib().tsg_queue_scan(self._h, p, len(p), bytes(args.Content),
+                                       len(args.Content), C.byref(out)))
+        return self.ctx.scanner.decode(out, [args.FilePath])[0]
+
+    def flush(self):
+        N.check(N.lib().tsg_queue_flush(self._h))
+
+    def close(self):
+        if self._h:
+            N.lib().tsg_queue_destroy(self._h)
             self._h = None
 
     def __del__(self):
