@@ -315,6 +315,13 @@ int tsg_layer_pack(const tsg_ruleset* rs, const uint8_t* tar, uint64_t tar_len,
                    const char* const* skip_dirs, uint32_t n_skip_dirs, const char* config_path,
                    tsg_layer** out);
 int tsg_layer_get(const tsg_layer* layer, tsg_layer_view* out);
+/* Filesystem ingest (configs[0], trivy fs): replaces walker.FS.Walk (pkg/fanal/walker/fs.go:25-63)
+ * + the fs artifact's relative paths (pkg/fanal/artifact/local/fs.go:83-100) + Required +
+ * IsBinary; files are read in parallel and packed in path order (paths relative to root, no
+ * "/" prefix).  Result in the same tsg_layer form (no whiteouts). */
+int tsg_fs_pack(const tsg_ruleset* rs, const char* root, const char* const* skip_files,
+                uint32_t n_skip_files, const char* const* skip_dirs, uint32_t n_skip_dirs,
+                const char* config_path, tsg_layer** out);
 void tsg_layer_free(tsg_layer* layer);
 
 #ifdef __cplusplus

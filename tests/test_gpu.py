@@ -300,3 +300,31 @@ def test_queue_concurrent_callers_gpu(builtin):
     ctx.close()
     assert got == [builtin.Scan(a) for a in args]
     assert st["batches"] >= 3
+
+
+def test_fs_json_report_gpu(tmp_path):
+    """`trivy fs` of the integration fixture through the native fs ingest and the device,
+    as the JSON report, against integration/testdata/secrets.json.golden (see
+    test_report.py for the one field the golden has that this revision does not)."""
+    import shutil
+    from trivy_amd import analyzer as A
+    from trivy_amd import report as R
+    from trivy_amd import walker as W
+    idir = os.path.join(GOLDEN, "reference", "integration")
+    root = tmp_path / "testdata" / "fixtures" / "fs" / "secrets"
+    root.mkdir(parents=True)
+    for f in ("deploy.sh", "trivy-secret.yaml"):
+        shutil.copy(os.path.join(idir, "secrets", f), root / f)
+    old = os.getcwd()
+    os.chdir(tmp_path)
+    try:
+        an = A.SecretAnalyzer()
+        an.Init("testdata/fixtures/fs/secrets/trivy-secret.yaml")
+        secrets = W.analyze_fs(an, "testdata/fixtures/fs/secrets", device=0)
+    finally:
+        os.chdir(old)
+    rep = R.fs_report("testdata/fixtures/fs/secrets",
+                      R.secrets_to_results(R.apply_layers([{"Secrets": secrets}])))
+    golden = [l for l in open(os.path.join(idir, "secrets.json.golden")).read().split("\n")
+              if l.strip() != '"Deleted": false,']
+    assert R.write_json(rep) == "\n".join(golden)

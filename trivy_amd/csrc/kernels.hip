@@ -118,14 +118,21 @@ __device__ __forceinline__ uint32_t byte_of(const uint4 v, uint32_t k) {
   return (w >> ((k & 3) * 8)) & 0xFF;
 }
 
+// chunk_file[c] = the file holding byte c*C (the last file starting at or before it; empty
+// files never hold a byte), for every chunk of the padded chunk range: one thread per
+// chunk, a binary search over the offsets (balanced, unlike a thread per file)
 __global__ void chunk_file_kernel(const uint64_t* __restrict__ off, uint32_t nfiles, uint32_t chunk,
-                                  uint32_t* __restrict__ chunk_file) {
-  uint32_t f = blockIdx.x * blockDim.x + threadIdx.x;
-  if (f >= nfiles) return;
-  uint64_t fs = off[f], fe = off[f + 1];
-  if (fe == fs) return;
-  uint64_t c0 = (fs + chunk - 1) / chunk, c1 = (fe + chunk - 1) / chunk;  // chunks starting in f
-  for (uint64_t c = c0; c < c1; c++) chunk_file[c] = f;
+                                  uint64_t nchunks_pad, uint32_t* __restrict__ chunk_file) {
+  const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= nchunks_pad) return;
+  const uint64_t p = c * chunk;
+  uint32_t lo = 0, hi = nfiles;  // invariant: off[lo] <= p (off[0] = 0), answer in [lo, hi)
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (off[mid] <= p) lo = mid;
+    else hi = mid;
+  }
+  chunk_file[c] = lo;
 }
 
 // ---------------------------------------------------------------- Global.AllowPath
@@ -739,8 +746,10 @@ struct LayoutArgs {
   uint32_t max_dense;
   uint8_t* kind;      // [G]
   uint64_t* base;     // [G] first item of a list group
-  uint4* entries;     // K2 work list: {group, first, n, kind}
+  uint4* entries;     // K2 work list of list groups: {group, first item, n, kGroupList}
   uint32_t* nentries;
+  uint4* dentries;    // ... of dense groups: {group, first chunk, n, kGroupDense}
+  uint32_t* ndentries;
   uint8_t* gskip;     // [G] (to the host)
   uint32_t* stats;    // [1] items listed, [2] entries, [3] skipped groups
 };
@@ -767,13 +776,13 @@ __device__ T block_exclusive_scan(T v, T* out, T* s_wave) {
 }
 
 constexpr int kLayoutBlock = 1024;
-constexpr uint32_t kEntryItems = 2 * kBlock;    // two chains per lane
+constexpr uint32_t kEntryItems = 4 * kBlock;    // two chains per lane, two rounds
 constexpr uint32_t kEntryChunks = kStreams * kBlock;
 
 __global__ void __launch_bounds__(kLayoutBlock) layout_kernel(LayoutArgs A) {
   __shared__ unsigned long long s_wave64[kLayoutBlock / 64];
-  __shared__ unsigned long long s_carry[4];  // items, entries, dense groups, skipped groups
-  if (threadIdx.x < 4) s_carry[threadIdx.x] = 0;
+  __shared__ unsigned long long s_carry[5];  // items, entries, dense groups, skipped groups, dense entries
+  if (threadIdx.x < 5) s_carry[threadIdx.x] = 0;
   __syncthreads();
   for (uint32_t g0 = 0; g0 < A.G; g0 += blockDim.x) {
     const uint32_t g = g0 + threadIdx.x;
@@ -789,16 +798,17 @@ __global__ void __launch_bounds__(kLayoutBlock) layout_kernel(LayoutArgs A) {
     const bool list = want_list && s_carry[0] + ipre + cnt <= A.items_cap;
     // items of groups that fit are placed at their prefix position (a skipped group's
     // range stays unused: the regions keep group order)
-    const uint64_t nent = list ? (cnt + kEntryItems - 1) / kEntryItems
-                               : dense ? (A.nchunks + kEntryChunks - 1) / kEntryChunks : 0;
-    unsigned long long epre;
+    const uint64_t nent = list ? (cnt + kEntryItems - 1) / kEntryItems : 0;
+    const uint64_t ndent = dense ? (A.nchunks + kEntryChunks - 1) / kEntryChunks : 0;
+    unsigned long long epre, dpre2;
     const unsigned long long etot = block_exclusive_scan<unsigned long long>(nent, &epre, s_wave64);
+    const unsigned long long dtot2 = block_exclusive_scan<unsigned long long>(ndent, &dpre2, s_wave64);
     const bool skip = cnt && !list && !dense;
     unsigned long long spre;
     const unsigned long long stot = block_exclusive_scan<unsigned long long>(skip ? 1 : 0, &spre, s_wave64);
     // (entries_cap covers every list entry the item capacity allows plus max_dense dense
     // groups, so the work list always fits)
-    const uint64_t e0 = s_carry[1] + epre;
+    const uint64_t e0 = s_carry[1] + epre, d0 = s_carry[4] + dpre2;
     if (g < A.G) {
       const uint8_t k = !cnt ? kGroupNone : list ? kGroupList : dense ? kGroupDense : kGroupSkip;
       A.kind[g] = k;
@@ -811,10 +821,10 @@ __global__ void __launch_bounds__(kLayoutBlock) layout_kernel(LayoutArgs A) {
                                          (uint32_t)min<uint64_t>(kEntryItems, cnt - first), kGroupList);
         }
       else if (k == kGroupDense)
-        for (uint64_t i = 0; i < nent; i++) {
+        for (uint64_t i = 0; i < ndent; i++) {
           const uint64_t first = i * kEntryChunks;
-          A.entries[e0 + i] = make_uint4(g, (uint32_t)first,
-                                         (uint32_t)min<uint64_t>(kEntryChunks, A.nchunks - first), kGroupDense);
+          A.dentries[d0 + i] = make_uint4(g, (uint32_t)first,
+                                          (uint32_t)min<uint64_t>(kEntryChunks, A.nchunks - first), kGroupDense);
         }
     }
     __syncthreads();
@@ -823,11 +833,13 @@ __global__ void __launch_bounds__(kLayoutBlock) layout_kernel(LayoutArgs A) {
       s_carry[1] += etot;
       s_carry[2] += dtot;
       s_carry[3] += stot;
+      s_carry[4] += dtot2;
     }
     __syncthreads();
   }
   if (threadIdx.x == 0) {
     *A.nentries = (uint32_t)s_carry[1];
+    *A.ndentries = (uint32_t)s_carry[4];
     A.stats[1] = (uint32_t)min<unsigned long long>(s_carry[0], 0xFFFFFFFFull);
     A.stats[2] = (uint32_t)s_carry[1];
     A.stats[3] = (uint32_t)s_carry[3];
@@ -846,8 +858,10 @@ struct K2Args {
   const uint32_t* gmask;    // [G * kw_words] keyword gate of each group (dense entries)
   const uint32_t* galways;  // [G]
   const uint2* items;       // list entries: (file, chunk)
-  const uint4* entries;     // {group, first, n, kind} (layout_kernel)
+  const uint4* entries;     // list entries {group, first item, n, kind} (layout_kernel)
   const uint32_t* nentries;
+  const uint4* dentries;    // dense entries {group, first chunk, n, kind}
+  const uint32_t* ndentries;
   DevCand* cand;
   uint32_t* cand_count;
   uint32_t cand_cap;
@@ -929,16 +943,24 @@ struct Lane {
       return;
     }
     s = d.to_ni[s];
+    // 16 bytes per load (the next word in flight), liveness checked once per word: a dead
+    // noinject state is absorbing and accepts nothing, so stepping on inside the word
+    // changes no output.  (The batch is padded, so whole-word loads past fe are safe.)
     uint64_t q = b;
+    uint64_t w = q & ~15ull;
+    uint4 cur = *(const uint4*)(data + w);
     while (q < fe && !d.dead[s]) {
       if (q - b >= A.ext_cap) {
         A.ovf[file] = 1;
         return;
       }
-      s = step(s, data[q], q);
-      q++;
+      const uint4 nxt = *(const uint4*)(data + w + 16);
+      const uint64_t e = min(fe, w + 16);
+      for (; q < e; q++) s = step(s, byte_of(cur, (uint32_t)(q - w)), q);
+      cur = nxt;
+      w += 16;
     }
-    if (q == fe && !d.dead[s]) {
+    if (q >= fe && !d.dead[s]) {
       const uint32_t m = d.eot[s];
       if (m) emit(m, fe);
     }
@@ -1027,8 +1049,8 @@ __device__ __forceinline__ void stage_dfa(const DevDFA& d, uint8_t* smem) {
   __syncthreads();
 }
 
-// One list entry: up to kEntryItems (file, chunk) items of group d, two per lane, stepped
-// as two interleaved DFA chains.  Items are whole chunks of the batch stream (aligned to
+// One list entry: up to kEntryItems (file, chunk) items of group d, in rounds of two per
+// lane stepped as two interleaved DFA chains.  Items are whole chunks of the batch stream (aligned to
 // the chunk size, a multiple of 64), so the loads are quad-transposed like K1's: the four
 // lanes of a quad fetch 64 contiguous bytes of one lane's chunk per instruction.  Bytes of
 // a chunk outside the item's file are stepped as no-ops (the file's first byte starts
@@ -1038,9 +1060,21 @@ struct K2Item {
   uint64_t fs, fe, a, b, base;
 };
 
+__device__ __forceinline__ void k2_list_pair(const DevDFA& d, const K2Args& A, const uint16_t* s_tab,
+                                             const uint8_t* s_cls, const uint16_t* s_accs,
+                                             const uint64_t* s_masks, uint32_t g, uint32_t first, uint32_t n);
+
 __device__ __forceinline__ void k2_list_entry(const DevDFA& d, const K2Args& A, const uint16_t* s_tab,
                                               const uint8_t* s_cls, const uint16_t* s_accs,
                                               const uint64_t* s_masks, uint4 en) {
+  for (uint32_t r0i = 0; r0i < en.z; r0i += 2 * kBlock)
+    k2_list_pair(d, A, s_tab, s_cls, s_accs, s_masks, en.x, en.y + r0i, min(en.z - r0i, (uint32_t)(2 * kBlock)));
+}
+
+// items [first, first + n) of an entry, n <= 2 * kBlock: two per lane
+__device__ __forceinline__ void k2_list_pair(const DevDFA& d, const K2Args& A, const uint16_t* s_tab,
+                                             const uint8_t* s_cls, const uint16_t* s_accs,
+                                             const uint64_t* s_masks, uint32_t g, uint32_t first, uint32_t n) {
   const uint32_t C = A.chunk;
   const uint32_t lane = threadIdx.x & 63, q = lane & 3;
   const bool b0 = q & 1, b1 = (q >> 1) & 1;
@@ -1049,8 +1083,8 @@ __device__ __forceinline__ void k2_list_entry(const DevDFA& d, const K2Args& A, 
 #pragma unroll
   for (int i = 0; i < 2; i++) {
     const uint32_t k = threadIdx.x + (uint32_t)i * kBlock;
-    live[i] = k < en.z;
-    const uint2 item = A.items[en.y + (live[i] ? k : 0)];
+    live[i] = k < n;
+    const uint2 item = A.items[first + (live[i] ? k : 0)];
     it[i].file = item.x;
     it[i].fs = A.off[item.x];
     it[i].fe = A.off[item.x + 1];
@@ -1175,16 +1209,16 @@ __device__ __forceinline__ void k2_dense_entry(const DevDFA& d, const K2Args& A,
   }
 }
 
-// K2: a persistent grid over the work list.  Block b takes a contiguous range of entries,
+// K2: persistent grids over the work lists.  Block b takes a contiguous range of entries,
 // so consecutive entries mostly share a group and its DFA stays staged in LDS.
-__global__ void __launch_bounds__(kBlock) k2_kernel(const DevDFA* __restrict__ dfas, K2Args A) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  const uint32_t E = *A.nentries;
+template <bool DENSE>
+__device__ __forceinline__ void k2_run(const DevDFA* __restrict__ dfas, const K2Args& A, const uint4* entries,
+                                       uint32_t E, uint8_t* smem) {
   const uint32_t e0 = (uint32_t)((uint64_t)E * blockIdx.x / gridDim.x);
   const uint32_t e1 = (uint32_t)((uint64_t)E * (blockIdx.x + 1) / gridDim.x);
   uint32_t staged = 0xFFFFFFFFu;
   for (uint32_t e = e0; e < e1; e++) {
-    const uint4 en = A.entries[e];
+    const uint4 en = entries[e];
     const uint32_t g = __builtin_amdgcn_readfirstlane(en.x);
     const DevDFA d = dfas[g];
     if (g != staged) {
@@ -1193,11 +1227,21 @@ __global__ void __launch_bounds__(kBlock) k2_kernel(const DevDFA* __restrict__ d
       staged = g;
     }
     const uint16_t* s_tab = (const uint16_t*)smem;
-    if (__builtin_amdgcn_readfirstlane(en.w) == kGroupList)
-      k2_list_entry(d, A, s_tab, smem + d.o_cls, (const uint16_t*)(smem + d.o_accs), (const uint64_t*)(smem + d.o_masks), en);
-    else
+    if (DENSE)
       k2_dense_entry(d, A, g, s_tab, smem + d.o_cls, (const uint16_t*)(smem + d.o_accs), (const uint64_t*)(smem + d.o_masks), en);
+    else
+      k2_list_entry(d, A, s_tab, smem + d.o_cls, (const uint16_t*)(smem + d.o_accs), (const uint64_t*)(smem + d.o_masks), en);
   }
+}
+
+__global__ void __launch_bounds__(kBlock) k2_kernel(const DevDFA* __restrict__ dfas, K2Args A) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  k2_run<false>(dfas, A, A.entries, *A.nentries, smem);
+}
+
+__global__ void __launch_bounds__(kBlock) k2_dense_kernel(const DevDFA* __restrict__ dfas, K2Args A) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  k2_run<true>(dfas, A, A.dentries, *A.ndentries, smem);
 }
 
 // the candidates of a batch to pinned, mapped host memory (their count is only known here)
@@ -1412,6 +1456,9 @@ struct DeviceRules {
   uint32_t chunk = 256, ext_cap = 1u << 16, adapt_mib = 0;
   int grid = 0;          // 8 blocks per CU
   int cus = 0;
+  int k2_grid = 0, k2_dense_grid = 0;  // resident blocks of the persistent K2 kernels
+  hipEvent_t kernels_done = nullptr;   // end of the kernels of the last enqueued batch
+  bool kernels_done_valid = false;
   std::vector<void*> tables;
   DevK1 k1{};
   K1Host k1h;
@@ -1434,6 +1481,7 @@ struct DeviceRules {
   uint32_t GW = 1, maxback = 0, max_lds = 0;
   ~DeviceRules() {
     (void)hipSetDevice(device);
+    if (kernels_done) (void)hipEventDestroy(kernels_done);
     for (auto* p : tables) (void)hipFree(p);
     (void)hipFree(d_hits);
   }
@@ -1469,6 +1517,8 @@ struct LaneState {
   size_t items_cap = 0;
   uint4* entries = nullptr;
   size_t entries_cap = 0;
+  uint4* dentries = nullptr;
+  size_t dentries_cap = 0;
   DevCand* cand = nullptr;
   uint32_t cand_cap = 0;
   uint32_t* counts = nullptr;   // [8] 0 candidates, 1 event chunks, 2 K2 entries
@@ -1483,7 +1533,7 @@ struct LaneState {
     (void)hipSetDevice(d->device);
     if (st) (void)hipStreamSynchronize(st);
     void* bufs[] = {data_alloc, off, chunk_file, ev_bits, evlist, kw, ggate, ovf, paths, poff, pathok,
-                    items, entries, cand, counts, gcount, cursor, base, kind, gskip};
+                    items, entries, dentries, cand, counts, gcount, cursor, base, kind, gskip};
     for (void* b : bufs) (void)hipFree(b);
     if (st) (void)hipStreamDestroy(st);
   }
@@ -1529,8 +1579,10 @@ static const void* k1_fn(uint32_t kw_words, uint32_t lds_class, uint32_t ns) {
 }
 
 static int launch_k1(DeviceRules* r, const K1Args& A, hipStream_t st) {
+  // blocks per CU: 2 = the resident blocks of the 80 KiB LDS class (a persistent grid, each
+  // block stages the automaton once); TSG_K1_GRID overrides (measurements)
   static const int gmul = getenv("TSG_K1_GRID") ? atoi(getenv("TSG_K1_GRID")) : 0;
-  const uint64_t cap = (uint64_t)r->grid / 8 * (gmul > 0 ? gmul : 8);
+  const uint64_t cap = (uint64_t)r->grid / 8 * (gmul > 0 ? gmul : 2);
   const int grid = (int)std::min<uint64_t>((A.nitems + kK1Block - 1) / kK1Block, cap);
   DevK1 d = r->k1;
   K1Args a = A;
@@ -1664,8 +1716,12 @@ int device_rules_create(int device, const Plan& p, uint32_t chunk, uint32_t ext_
     for (int b = 0; b < 32; b++)
       if (((gp.events >> b) & 1) || back > (uint32_t)kMaxBack) gofbit[b * r->GW + g / 64] |= 1ull << (g % 64);
   }
-  if (r->max_lds > 64 * 1024)
+  r->max_lds = std::max<uint32_t>(r->max_lds, 16);
+  if (r->max_lds > 64 * 1024) {
     HIP_TRY(hipFuncSetAttribute((const void*)k2_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)r->max_lds));
+    HIP_TRY(hipFuncSetAttribute((const void*)k2_dense_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)r->max_lds));
+  }
   const uint32_t* cg = nullptr;
   if ((rc = upload_vec(gmask, &cg, &r->tables))) return rc;
   r->d_gmask = (uint32_t*)cg;
@@ -1688,6 +1744,12 @@ int device_rules_create(int device, const Plan& p, uint32_t chunk, uint32_t ext_
   HIP_TRY(hipGetDeviceProperties(&prop, device));
   r->cus = prop.multiProcessorCount;
   r->grid = prop.multiProcessorCount * 8;
+  HIP_TRY(hipEventCreateWithFlags(&r->kernels_done, hipEventDisableTiming));
+  int occ = 0;
+  HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void*)k2_kernel, kBlock, r->max_lds));
+  r->k2_grid = r->cus * std::max(occ, 1);
+  HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void*)k2_dense_kernel, kBlock, r->max_lds));
+  r->k2_dense_grid = r->cus * std::max(occ, 1);
   *out = r.release();
   return TSG_OK;
 }
@@ -1776,10 +1838,11 @@ int enqueue_scan(DeviceRules* r, LaneState* l, const ScanInput& in, HostOut* out
   // it, groups are skipped (kGroupSkip) and resolved on the host, never dropped
   const uint64_t items_cap = std::max<uint64_t>(2 * nchunks, 1u << 16);
   const uint32_t max_dense = 16;
-  const uint64_t entries_cap = items_cap / kEntryItems + G + 1 +
-                               (uint64_t)max_dense * ((nchunks + kEntryChunks - 1) / kEntryChunks + 1);
+  const uint64_t entries_cap = items_cap / kEntryItems + G + 1;
+  const uint64_t dentries_cap = (uint64_t)max_dense * ((nchunks + kEntryChunks - 1) / kEntryChunks + 1);
   if ((rc = ensure(&l->items, &l->items_cap, (size_t)items_cap))) return rc;
   if ((rc = ensure(&l->entries, &l->entries_cap, (size_t)entries_cap))) return rc;
+  if ((rc = ensure(&l->dentries, &l->dentries_cap, (size_t)dentries_cap))) return rc;
   if (!l->cand || l->cand_cap < out->cand_cap) {
     if (l->cand) HIP_TRY(hipFree(l->cand));
     HIP_TRY(hipMalloc((void**)&l->cand, sizeof(DevCand) * (size_t)out->cand_cap));
@@ -1802,9 +1865,12 @@ int enqueue_scan(DeviceRules* r, LaneState* l, const ScanInput& in, HostOut* out
     HIP_TRY(hipMemcpyAsync(l->poff, in.poff, sizeof(uint64_t) * (F + 1), hipMemcpyHostToDevice, st));
   }
   HIP_TRY(hipEventRecord(out->ev[1], st));
-  HIP_TRY(hipMemsetAsync(l->chunk_file, 0, sizeof(uint32_t) * nchunks_pad, st));
+  // the kernels of consecutive batches run one after the other (each has the whole chip;
+  // their HIP-event times are the kernels' own), while this lane's H2D above overlapped
+  // the previous batch's kernels on the other lane
+  if (r->kernels_done_valid) HIP_TRY(hipStreamWaitEvent(st, r->kernels_done, 0));
   if (F) {
-    chunk_file_kernel<<<(F + 255) / 256, 256, 0, st>>>(l->off, F, C, l->chunk_file);
+    chunk_file_kernel<<<(uint32_t)((nchunks_pad + 255) / 256), 256, 0, st>>>(l->off, F, C, nchunks_pad, l->chunk_file);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipMemsetAsync(l->kw, 0, sizeof(uint32_t) * (size_t)F * W, st));
     HIP_TRY(hipMemsetAsync(l->ovf, 0, F, st));
@@ -1867,7 +1933,7 @@ int enqueue_scan(DeviceRules* r, LaneState* l, const ScanInput& in, HostOut* out
     hipLaunchKernelGGL(items_count_kernel, dim3(igrid), dim3(kBlock), G * sizeof(uint32_t) + 16, st, IA);
     HIP_TRY(hipGetLastError());
     LayoutArgs LA{l->gcount, G, nchunks, items_cap, max_dense, l->kind, l->base, l->entries, l->counts + 2,
-                  l->gskip, l->counts + 4};
+                  l->dentries, l->counts + 3, l->gskip, l->counts + 4};
     hipLaunchKernelGGL(layout_kernel, dim3(1), dim3(kLayoutBlock), 0, st, LA);
     HIP_TRY(hipGetLastError());
     hipLaunchKernelGGL(items_emit_kernel, dim3(igrid), dim3(kBlock), 2 * G * sizeof(uint32_t) + 16, st, IA);
@@ -1892,16 +1958,22 @@ int enqueue_scan(DeviceRules* r, LaneState* l, const ScanInput& in, HostOut* out
     A.items = l->items;
     A.entries = l->entries;
     A.nentries = l->counts + 2;
+    A.dentries = l->dentries;
+    A.ndentries = l->counts + 3;
     A.cand = l->cand;
     A.cand_count = l->counts;
     A.cand_cap = out->cand_cap;
     A.ovf = l->ovf;
-    const int kgrid = r->cus * std::max(1, (int)(160 * 1024 / std::max<uint32_t>(r->max_lds, 1)));
-    hipLaunchKernelGGL(k2_kernel, dim3(std::min(kgrid, r->grid)), dim3(kBlock), r->max_lds, st,
+    // one block per resident slot (the grids are persistent)
+    hipLaunchKernelGGL(k2_kernel, dim3(r->k2_grid), dim3(kBlock), r->max_lds, st, (const DevDFA*)r->d_groups, A);
+    HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL(k2_dense_kernel, dim3(r->k2_dense_grid), dim3(kBlock), r->max_lds, st,
                        (const DevDFA*)r->d_groups, A);
     HIP_TRY(hipGetLastError());
   }
   HIP_TRY(hipEventRecord(out->ev[4], st));
+  HIP_TRY(hipEventRecord(r->kernels_done, st));
+  r->kernels_done_valid = true;
 
   // ---- results to the pinned host buffers
   cand_copy_kernel<<<64, 256, 0, st>>>(l->cand, l->counts, out->cand_cap, (DevCand*)out->cand_dev);

@@ -19,6 +19,14 @@
 #include <memory>
 #include <vector>
 
+#include <cerrno>
+#include <dirent.h>
+#include <fcntl.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <algorithm>
+
 #include "internal.hpp"
 
 struct tsg_layer {
@@ -427,3 +435,116 @@ extern "C" int tsg_layer_get(const tsg_layer* L, tsg_layer_view* v) {
 }
 
 extern "C" void tsg_layer_free(tsg_layer* L) { delete L; }
+
+// ---------------------------------------------------------------- filesystem ingest
+// walker.FS.Walk (pkg/fanal/walker/fs.go:25-63) + the fs artifact's callback
+// (pkg/fanal/artifact/local/fs.go:83-100) + AnalyzerGroup.AnalyzeFile's Required gate
+// (analyzer.go:399-409) + SecretAnalyzer.Analyze's IsBinary (secret.go:78-84): walks a
+// directory tree and packs every file the secret analyzer would scan into one batch.
+// Files are read in parallel on the host pool.  The reference walks with concurrent
+// goroutines (order unspecified); here files are packed in path order.
+extern "C" int tsg_fs_pack(const tsg_ruleset* rs, const char* root, const char* const* skip_files,
+                           uint32_t n_skip_files, const char* const* skip_dirs, uint32_t n_skip_dirs,
+                           const char* config_path, tsg_layer** out) {
+  if (!rs || !root || !out) return fail(TSG_ERR_ARG, "bad argument");
+  *out = nullptr;
+  try {
+    Gate g{rs->rs, rs->plan.get(), base(config_path ? config_path : ""), {}, {}};
+    for (uint32_t i = 0; i < n_skip_files; i++)  // walk.go:25-33
+      g.skip_files.push_back(trim_left_slash(clean(skip_files[i])));
+    std::vector<std::string> sd;
+    for (uint32_t i = 0; i < n_skip_dirs; i++) sd.push_back(skip_dirs[i]);
+    for (const char* x : {"proc", "sys", "dev"}) sd.push_back(x);  // walk.go:15
+    for (const auto& x : sd) g.skip_dirs.push_back(trim_left_slash(clean(x)));
+    auto skip_dir = [&](const std::string& dir) {  // walk.go:58-75
+      const std::string d = trim_left_slash(dir);
+      return base(d) == ".git" || contains(g.skip_dirs, d);
+    };
+    const std::string r0 = clean(root);
+    struct stat st;
+    if (lstat(r0.c_str(), &st) != 0) return fail(TSG_ERR_ARG, "walk error: cannot stat " + r0);
+    // local/fs.go:86-90: a file given as the root is analyzed relative to its directory
+    std::string directory = r0;
+    if (!S_ISDIR(st.st_mode)) {
+      const size_t k = r0.rfind('/');
+      directory = k == std::string::npos ? "." : (k == 0 ? "/" : r0.substr(0, k));
+    }
+    struct Found {
+      std::string full, fp;
+      uint64_t size;
+    };
+    std::vector<Found> found;
+    uint32_t walked = 0;
+    std::vector<std::string> stack{r0};
+    while (!stack.empty()) {
+      const std::string path = stack.back();
+      stack.pop_back();
+      struct stat s2;
+      if (lstat(path.c_str(), &s2) != 0) continue;
+      if (S_ISDIR(s2.st_mode)) {
+        if (skip_dir(path)) continue;
+        DIR* d = opendir(path.c_str());
+        if (!d) {
+          if (errno == EACCES) continue;  // fs.go:48-55: permission errors are ignored
+          return fail(TSG_ERR_ARG, "walk error: cannot read " + path);
+        }
+        while (dirent* e = readdir(d)) {
+          const std::string name = e->d_name;
+          if (name == "." || name == "..") continue;
+          stack.push_back(clean(path + "/" + name));
+        }
+        closedir(d);
+        continue;
+      }
+      if (!S_ISREG(s2.st_mode)) continue;  // fs.go:37-38
+      if (contains(g.skip_files, trim_left_slash(path))) continue;
+      std::string fp;
+      if (!rel(directory, path, &fp)) fp = path;
+      walked++;
+      const std::string clean_fp = trim_left_slash(fp);
+      if (!g.required(clean_fp, (int64_t)s2.st_size)) continue;
+      found.push_back({path, fp, (uint64_t)s2.st_size});
+    }
+    std::sort(found.begin(), found.end(), [](const Found& a, const Found& b) { return a.fp < b.fp; });
+    const size_t n = found.size();
+    std::vector<uint64_t> at(n + 1, 0);
+    for (size_t i = 0; i < n; i++) at[i + 1] = at[i] + found[i].size;
+    auto L = std::make_unique<tsg_layer>();
+    L->walked = walked;
+    std::unique_ptr<uint8_t[]> buf(new uint8_t[at[n] ? at[n] : 1]);
+    std::vector<uint8_t> keep(n, 0);
+    std::vector<uint64_t> got(n, 0);
+    pool_for(n, 16, [&](size_t i) {  // io.ReadAll (secret.go:85), then utils.IsBinary
+      const int fd = open(found[i].full.c_str(), O_RDONLY);
+      if (fd < 0) return;  // analyzer.go:411-413: a permission error skips the file
+      uint64_t r = 0;
+      while (r < found[i].size) {
+        const ssize_t k = pread(fd, buf.get() + at[i] + r, found[i].size - r, (off_t)r);
+        if (k <= 0) break;
+        r += (uint64_t)k;
+      }
+      close(fd);
+      got[i] = r;  // a file that shrank since the walk is read as it is now
+      keep[i] = !is_binary(buf.get() + at[i], (int64_t)r);
+    }, 8);
+    uint64_t total = 0;
+    for (size_t i = 0; i < n; i++)
+      if (keep[i]) total += got[i];
+    L->data.reset(new uint8_t[total ? total : 1]);
+    uint64_t o = 0;
+    for (size_t i = 0; i < n; i++) {
+      if (!keep[i]) continue;
+      std::memcpy(L->data.get() + o, buf.get() + at[i], got[i]);
+      o += got[i];
+      L->offsets.push_back(o);
+      L->paths += found[i].fp;  // fs scans keep the relative path (secret.go:94-96: no "/")
+      L->path_offsets.push_back(L->paths.size());
+    }
+    *out = L.release();
+    return TSG_OK;
+  } catch (const std::bad_alloc&) {
+    return fail(TSG_ERR_NOMEM, "out of memory");
+  } catch (const std::exception& e) {
+    return fail(TSG_ERR_INTERNAL, e.what());
+  }
+}

@@ -250,6 +250,44 @@ class NativeLayer:
             self._h = None
 
 
+class NativeFS(NativeLayer):
+    """tsg_fs_pack: walker.FS.Walk + the fs artifact's relative paths + `Required` +
+    `IsBinary` over a directory tree, files read in parallel and packed in path order."""
+
+    def __init__(self, scanner, root, skip_files=(), skip_dirs=(), config_path=""):
+        L = N.lib()
+        self._h = None
+        enc = lambda xs: (C.c_char_p * max(1, len(xs)))(
+            *[x.encode("utf-8", "surrogateescape") for x in xs])
+        sf, sd = enc(list(skip_files)), enc(list(skip_dirs))
+        h = C.c_void_p()
+        N.check(L.tsg_fs_pack(scanner.handle, root.encode("utf-8", "surrogateescape"), sf,
+                              len(skip_files), sd, len(skip_dirs),
+                              config_path.encode("utf-8", "surrogateescape"), C.byref(h)))
+        self._h = h
+        v = N.LayerView()
+        N.check(L.tsg_layer_get(h, C.byref(v)))
+        n = v.nfiles
+        as_u64 = lambda p: np.ctypeslib.as_array(p, shape=(n + 1,))
+        offs, poffs = as_u64(v.offsets), as_u64(v.path_offsets)
+        as_u8 = lambda p, k: (np.ctypeslib.as_array(C.cast(p, C.POINTER(C.c_uint8)), shape=(k,))
+                              if p and k else np.zeros(1, np.uint8))
+        self.batch = S.Batch(as_u8(v.data, int(offs[-1])), offs, as_u8(v.paths, int(poffs[-1])),
+                             poffs)
+        self.batch._owner = self
+        self.opq, self.wh = [], []
+        self.walked = v.walked
+
+
+def analyze_fs(analyzer, root, device=None, ctx=None, emulate_chunk=0, skip_files=(), skip_dirs=()):
+    """`trivy fs --security-checks secret <root>`'s secret analysis (BASELINE configs[0]):
+    the native fs ingest, one batch, the sorted AnalysisResult.Secrets."""
+    fs = NativeFS(analyzer.scanner, root, skip_files, skip_dirs, analyzer.configPath)
+    res = analyzer.scanner.ScanBatch(fs.batch, device=device, ctx=ctx,
+                                     emulate_chunk=emulate_chunk) if fs.batch.nfiles else []
+    return sort_secrets([r for r in res if r["Findings"]])
+
+
 def analyze_layer_native(analyzer, tar, device=None, ctx=None, emulate_chunk=0,
                          skip_files=(), skip_dirs=()):
     """analyze_layer over an in-memory tar with the native ingest (one batch per layer)."""
