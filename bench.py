@@ -265,7 +265,9 @@ def main():
                     "k2_ms_per_batch": round(d["sum_k2_ms"] / nbat, 3),
                     "k2_item_bytes_last_batch": k2_read, "k2_entries_last_batch": st["k2_launches"],
                     "candidates_last_batch": st["candidates"],
-                    "groups_skipped_last_batch": st["groups_skipped"]},
+                    "groups_skipped_last_batch": st["groups_skipped"],
+                    "k2_diag_last_batch": {k: st[k] for k in ("k2_tail_bytes", "k2_tail_max",
+                                                               "k2_long_tails", "k2_replays")}},
         "pipeline": {"h2d_GBps": round(d["sum_bytes"] / (d["sum_h2d_ms"] / 1e3) / 1e9, 2),
                      "h2d_ms_per_batch": round(d["sum_h2d_ms"] / nbat, 3),
                      "d2h_ms_per_batch": round(d["sum_d2h_ms"] / nbat, 3),

@@ -218,6 +218,11 @@ typedef struct tsg_stats {
   uint64_t batches;      /* batches collected so far, and their sums: */
   uint64_t sum_bytes;
   double sum_k1_ms, sum_gate_ms, sum_k2_ms, sum_h2d_ms, sum_d2h_ms, sum_resolve_ms;
+  double wait_ms;        /* last batch: its kernels waiting for the previous batch's */
+  /* K2 diagnostics of the last batch (TSG_K2_DIAG=1 in the environment, else 0): bytes
+   * followed past chunk ends, the longest such tail, tails over 4 KiB, words replayed for
+   * accepts */
+  uint32_t k2_tail_bytes, k2_tail_max, k2_long_tails, k2_replays;
 } tsg_stats;
 int tsg_ctx_get_stats(const tsg_ctx* ctx, tsg_stats* out);
 

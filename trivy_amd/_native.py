@@ -77,7 +77,9 @@ class Stats(C.Structure):
                 ("sum_bytes", C.c_uint64), ("sum_k1_ms", C.c_double),
                 ("sum_gate_ms", C.c_double), ("sum_k2_ms", C.c_double),
                 ("sum_h2d_ms", C.c_double), ("sum_d2h_ms", C.c_double),
-                ("sum_resolve_ms", C.c_double)]
+                ("sum_resolve_ms", C.c_double), ("wait_ms", C.c_double),
+                ("k2_tail_bytes", C.c_uint32), ("k2_tail_max", C.c_uint32),
+                ("k2_long_tails", C.c_uint32), ("k2_replays", C.c_uint32)]
 
 
 # (name, restype, argtypes) -- every symbol include/trivy_secret.h declares

@@ -32,13 +32,20 @@ struct HostOut {
   uint8_t* gskip = nullptr;     // [groups] 1 = K2 skipped the group (item capacity)
   Candidate* cand = nullptr;    // [cand_cap] host-mapped: K2 candidates copied out
   Candidate* cand_dev = nullptr;  // device address of `cand`
-  uint32_t* counts = nullptr;   // [8] host-mapped: 0 candidates, 1 items, 2 K2 entries,
-                                //      3 skipped groups, 4 event chunks
+  uint32_t* counts = nullptr;   // [16] host-mapped: 0 candidates, 1 event chunks, 2 K2 list
+                                // entries, 3 dense entries, 5 items, 6 entries, 7 skipped
+                                // groups, 8-11 K2 diagnostics (TSG_K2_DIAG)
   uint32_t* counts_dev = nullptr;
   uint32_t files_cap = 0, cand_cap = 0, groups = 0, kw_words = 0;
-  // stage boundaries of the batch on its lane's stream: H2D | K1 | gates | K2 | D2H; ev[5]
-  // completes the batch (its outputs are in these buffers)
-  hipEvent_t ev[6] = {};
+  // stage boundaries of the batch on its lane's stream: H2D | wait for the previous
+  // batch's kernels | K1 | gates | K2 | D2H; ev[kEvDone] completes the batch
+  hipEvent_t ev[7] = {};
+};
+
+constexpr int kEvDone = 6;
+// per-batch K2 diagnostics (K2 work that is not the chunks themselves)
+struct K2Diag {
+  unsigned long long tail_bytes, tail_max, long_tails, replays;
 };
 
 struct ScanInput {
@@ -51,7 +58,7 @@ struct ScanInput {
 };
 
 struct ScanTimes {  // HIP-event milliseconds of one batch on its lane
-  float h2d = 0, k1 = 0, gates = 0, k2 = 0, d2h = 0;
+  float h2d = 0, wait = 0, k1 = 0, gates = 0, k2 = 0, d2h = 0;
 };
 
 struct LaneState;  // HBM buffers + stream + events of one lane
@@ -70,9 +77,9 @@ hipStream_t lane_stream(LaneState* l);
 int host_out_alloc(const DeviceRules* d, uint32_t files_cap, HostOut* out);
 void host_out_free(HostOut* o);
 
-// The device part of one batch on lane `l`, asynchronously; out->ev[5] completes it.
+// The device part of one batch on lane `l`, asynchronously; out->ev[kEvDone] completes it.
 int enqueue_scan(DeviceRules* d, LaneState* l, const ScanInput& in, HostOut* out);
-// after out->ev[5]: the HIP-event times of that batch's stages
+// after out->ev[kEvDone]: the HIP-event times of that batch's stages
 int batch_times(const HostOut* out, ScanTimes* t);
 // K1 output of the lane's last batch (test hook): chunk events [nchunks]
 int lane_events(LaneState* l, uint32_t* ev, size_t n);

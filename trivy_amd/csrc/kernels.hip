@@ -73,18 +73,21 @@ constexpr int kPad = 256;     // zero bytes before and after the batch in HBM (>
 constexpr int kMaxBack = 16;  // event windows up to this many chunks; larger -> whole file
 
 // ---------------------------------------------------------------- device tables
+// K2 tables name a state by its row (state * nc): next = tab[row + class] needs no
+// multiply; the per-state tables are indexed by state_of(row).
 struct DevDFA {  // K2 rule group
-  const uint16_t* tab;        // [ns * nc] next | 0x8000 if the transition accepts
+  const uint16_t* tab;        // [ns * nc] next row | 0x8000 if the transition accepts
   const uint16_t* acc;        // [ns * nc] accept-mask index (look-ahead DFAs)
   const uint16_t* acc_state;  // [ns] accept-mask index per state (state_acc DFAs)
   const uint16_t* eot;        // [ns] accept-mask index at end of text
-  const uint16_t* to_ni;      // [ns] noinject twin
+  const uint16_t* to_ni;      // [ns] row of the noinject twin
   const uint8_t* dead;        // [ns]
   const uint64_t* masks;      // [nmasks * mw]
   const uint8_t* cls;         // [256]
   const uint32_t* rules;      // group-local id -> global rule
   uint32_t nc, ns, mw, nmasks, state_acc;
-  uint32_t start[4];
+  uint32_t inv_nc;            // ceil(2^32 / nc): state_of(row) = umulhi(row, inv_nc), exact below 2^16
+  uint32_t start[4];          // start rows per previous-byte context
   uint32_t o_cls, o_accs, o_masks, lds_bytes;
 };
 
@@ -866,6 +869,7 @@ struct K2Args {
   uint32_t* cand_count;
   uint32_t cand_cap;
   uint8_t* ovf;
+  uint32_t* diag;  // null, or [4]: tail bytes, longest tail, tails over 4 KiB, word replays
 };
 
 // Candidate emission, wave-aggregated: the lanes that reach an accept together reserve
@@ -905,20 +909,21 @@ struct Lane {
         emit_cand(A, file, d.rules[w * 64 + __builtin_ctzll(v)], pos - fs);
   }
 
+  __device__ __forceinline__ uint32_t state_of(uint32_t row) const { return __umulhi(row, d.inv_nc); }
+
+  // s is a row throughout
   __device__ __forceinline__ uint32_t step(uint32_t s, uint32_t byte, uint64_t pos) {
-    const uint32_t ix = s * d.nc + s_cls[byte];
+    const uint32_t ix = s + s_cls[byte];
     const uint32_t e = s_tab[ix];
-    if (__builtin_expect(e & 0x8000u, 0)) emit(d.state_acc ? s_accs[s] : d.acc[ix], pos);
+    if (__builtin_expect(e & 0x8000u, 0)) emit(d.state_acc ? s_accs[state_of(s)] : d.acc[ix], pos);
     return e & 0x7FFFu;
   }
 
-  __device__ __forceinline__ uint32_t fast(uint32_t s, uint32_t byte) const {
-    return s_tab[s * d.nc + s_cls[byte]];
-  }
+  __device__ __forceinline__ uint32_t fast(uint32_t s, uint32_t byte) const { return s_tab[s + s_cls[byte]]; }
 
-  __device__ __forceinline__ void replay16(uint32_t s, const uint4 v, uint64_t p) {
+  __device__ __forceinline__ void replay16(uint32_t s, const uint4, uint64_t p) {
 #pragma unroll 1
-    for (uint32_t k = 0; k < 16; k++) s = step(s, byte_of(v, k), p + k);
+    for (uint32_t k = 0; k < 16; k++) s = step(s, A.data[p + k], p + k);
   }
 
   __device__ __forceinline__ uint32_t step16(uint32_t s, const uint4 v, uint64_t p) {
@@ -938,18 +943,18 @@ struct Lane {
   __device__ __forceinline__ void tail(uint32_t s, uint64_t fe, uint64_t b) {
     const uint8_t* data = A.data;
     if (b >= fe) {
-      const uint32_t m = d.eot[s];
+      const uint32_t m = d.eot[state_of(s)];
       if (m) emit(m, fe);
       return;
     }
-    s = d.to_ni[s];
+    s = d.to_ni[state_of(s)];
     // 16 bytes per load (the next word in flight), liveness checked once per word: a dead
     // noinject state is absorbing and accepts nothing, so stepping on inside the word
     // changes no output.  (The batch is padded, so whole-word loads past fe are safe.)
     uint64_t q = b;
     uint64_t w = q & ~15ull;
     uint4 cur = *(const uint4*)(data + w);
-    while (q < fe && !d.dead[s]) {
+    while (q < fe && !d.dead[state_of(s)]) {
       if (q - b >= A.ext_cap) {
         A.ovf[file] = 1;
         return;
@@ -960,8 +965,14 @@ struct Lane {
       cur = nxt;
       w += 16;
     }
-    if (q >= fe && !d.dead[s]) {
-      const uint32_t m = d.eot[s];
+    if (A.diag) {
+      const uint32_t n = (uint32_t)min<uint64_t>(q - b, 0xFFFFFFFFull);
+      atomicAdd(&A.diag[0], n);
+      atomicMax(&A.diag[1], n);
+      if (n > 4096) atomicAdd(&A.diag[2], 1u);
+    }
+    if (q >= fe && !d.dead[state_of(s)]) {
+      const uint32_t m = d.eot[state_of(s)];
       if (m) emit(m, fe);
     }
   }
@@ -1104,42 +1115,7 @@ __device__ __forceinline__ void k2_list_pair(const DevDFA& d, const K2Args& A, c
       src[i][t] = A.data + bt + 16u * q;
     }
   Lane L{d, A, s_tab, s_cls, s_accs, s_masks, 0, 0};
-  auto word = [&](int i, uint64_t wb, const uint4 v) __attribute__((always_inline)) {
-    // bytes [wb, wb + 16) of chain i, stepped where they lie in [a, b)
-    const int32_t lo = (int32_t)max<int64_t>(0, min<int64_t>(16, (int64_t)it[i].a - (int64_t)wb));
-    const int32_t hi = (int32_t)max<int64_t>(0, min<int64_t>(16, (int64_t)it[i].b - (int64_t)wb));
-    uint32_t s = it[i].s, any = 0;
-    const uint32_t s0 = s;
-#pragma unroll
-    for (int k = 0; k < 16; k++) {
-      const uint32_t e = s_tab[s * d.nc + s_cls[byte_of(v, k)]];
-      const bool in = k >= lo && k < hi;
-      any |= in ? e : 0u;
-      s = in ? (e & 0x7FFFu) : s;
-    }
-    if (__builtin_expect(any & 0x8000u, 0)) {  // an accept: replay the word, emitting
-      L.file = it[i].file;
-      L.fs = it[i].fs;
-      uint32_t r = s0;
-      for (int k = lo; k < hi; k++) r = L.step(r, byte_of(v, k), wb + k);
-    }
-    it[i].s = s;
-  };
-  auto block = [&](uint64_t j, uint4 (&r)[2][4]) __attribute__((always_inline)) {
-#pragma unroll
-    for (int i = 0; i < 2; i++) quad_transpose4(r[i], b0, b1);
-#pragma unroll
-    for (int w = 0; w < 4; w++)
-#pragma unroll
-      for (int i = 0; i < 2; i++) word(i, it[i].base + j + 16u * w, r[i][w]);
-  };
-  auto load = [&](uint4 (&r)[2][4], uint64_t j) __attribute__((always_inline)) {
-#pragma unroll
-    for (int i = 0; i < 2; i++)
-#pragma unroll
-      for (int t = 0; t < 4; t++) r[i][t] = *(const uint4*)(src[i][t] + j);
-  };
-  if (C & 63) {  // chunk sizes that are not whole 64-byte blocks (tests): lane by lane
+  if (C & 127) {  // chunk sizes that are not whole 128-byte lines (tests): lane by lane
 #pragma unroll
     for (int i = 0; i < 2; i++)
       if (live[i]) {
@@ -1149,15 +1125,57 @@ __device__ __forceinline__ void k2_list_pair(const DevDFA& d, const K2Args& A, c
       }
     return;
   }
-  uint4 r0[2][4], r1[2][4];
-  load(r0, 0);
-  for (uint64_t j = 0; j < C; j += 128) {
-    const bool two = j + 64 < C;
-    if (two) load(r1, j + 64);
-    block(j, r0);
-    if (j + 128 < C) load(r0, j + 128);
-    if (two) block(j + 64, r1);
+  // bytes [wb, wb + 16) of chain c, stepped where they lie in [a, b)
+  auto word = [&](K2Item& c, uint64_t wb, const uint4 v) __attribute__((always_inline)) {
+    // bit k of `live` = byte wb + k lies in [a, b) (the chunk's part inside its file)
+    const int64_t lo64 = (int64_t)c.a - (int64_t)wb, hi64 = (int64_t)c.b - (int64_t)wb;
+    const int32_t lo = (int32_t)max<int64_t>(0, min<int64_t>(16, lo64));
+    const int32_t hi = (int32_t)max<int64_t>(0, min<int64_t>(16, hi64));
+    const uint32_t mask = ((1u << hi) - 1u) & ~((1u << lo) - 1u);
+    uint32_t s = c.s, any = 0;
+    const uint32_t s0 = s;
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+      const uint32_t e = s_tab[s + s_cls[byte_of(v, k)]];
+      const bool in = (mask >> k) & 1u;
+      any |= in ? e : 0u;
+      s = in ? (e & 0x7FFFu) : s;
+    }
+    if (__builtin_expect(any & 0x8000u, 0)) {  // an accept: replay the word, emitting
+      if (A.diag) atomicAdd(&A.diag[3], 1u);
+      L.file = c.file;
+      L.fs = c.fs;
+      uint32_t r = s0;  // (bytes re-read from memory: no dynamic index into registers)
+      for (int k = lo; k < hi; k++) r = L.step(r, A.data[wb + k], wb + k);
+    }
+    c.s = s;
+  };
+  // two 64-byte blocks of both chains in registers (x: chain 0, y: chain 1; 0: current,
+  // 1: next), named individually so they stay in VGPRs
+  uint4 x0[4], y0[4], x1[4], y1[4];
+#define K2_LOAD(X, Y, J)                                                        \
+  _Pragma("unroll") for (int t = 0; t < 4; t++) {                              \
+    X[t] = *(const uint4*)(src[0][t] + (J));                                     \
+    Y[t] = *(const uint4*)(src[1][t] + (J));                                     \
   }
+#define K2_BLOCK(X, Y, J)                                                       \
+  quad_transpose4(X, b0, b1);                                                   \
+  quad_transpose4(Y, b0, b1);                                                   \
+  _Pragma("unroll") for (int w = 0; w < 4; w++) {                              \
+    word(it[0], it[0].base + (J) + 16u * w, X[w]);                              \
+    word(it[1], it[1].base + (J) + 16u * w, Y[w]);                              \
+  }
+  K2_LOAD(x0, y0, 0)
+  for (uint64_t j = 0; j < C; j += 128) {  // C is a multiple of 128 here
+    K2_LOAD(x1, y1, j + 64)
+    K2_BLOCK(x0, y0, j)
+    if (j + 128 < C) {
+      K2_LOAD(x0, y0, j + 128)
+    }
+    K2_BLOCK(x1, y1, j + 64)
+  }
+#undef K2_LOAD
+#undef K2_BLOCK
   // matches that started in the chunk and run past it (inside the file): follow them
 #pragma unroll
   for (int i = 0; i < 2; i++)
@@ -1220,7 +1238,7 @@ __device__ __forceinline__ void k2_run(const DevDFA* __restrict__ dfas, const K2
   for (uint32_t e = e0; e < e1; e++) {
     const uint4 en = entries[e];
     const uint32_t g = __builtin_amdgcn_readfirstlane(en.x);
-    const DevDFA d = dfas[g];
+    const DevDFA& d = dfas[g];  // (a reference: uniform fields load into SGPRs, no copy)
     if (g != staged) {
       __syncthreads();  // every lane is done with the previous table
       stage_dfa(d, smem);
@@ -1265,18 +1283,36 @@ static int upload_vec(const std::vector<T>& v, const T** dst, std::vector<void*>
 
 static uint32_t align16(uint32_t x) { return (x + 15) & ~15u; }
 
-static int make_device_dfa(const DFA& d, const std::vector<uint32_t>& rules, DevDFA* out,
+static int make_device_dfa(const DFA& dd, const std::vector<uint32_t>& rules, DevDFA* out,
                            std::vector<void*>* allocs) {
-  if (d.nstates >= 0x8000) return fail(TSG_ERR_INTERNAL, "DFA too large for u16 tables");
+  if (dd.nstates >= 0x8000) return fail(TSG_ERR_INTERNAL, "DFA too large for u16 tables");
+  // rows of at least 2 entries (state_of's reciprocal needs nc >= 2): a one-class DFA gets a
+  // duplicate column no byte maps to
+  DFA padded;
+  const DFA* dp = &dd;
+  if (dd.nclasses < 2) {
+    padded = dd;
+    padded.nclasses = 2;
+    padded.next.clear();
+    padded.acc.clear();
+    for (int st = 0; st < dd.nstates; st++)
+      for (int c = 0; c < 2; c++) {
+        padded.next.push_back(dd.next[st]);
+        padded.acc.push_back(dd.acc[st]);
+      }
+    dp = &padded;
+  }
+  const DFA& d = *dp;
   const size_t nc = d.nclasses;
   std::vector<uint16_t> tab((size_t)d.nstates * nc), acc(tab.size()), accs(d.nstates, 0);
   bool state_acc = true;
+  if ((size_t)(d.nstates - 1) * nc >= 0x8000) return fail(TSG_ERR_INTERNAL, "DFA rows do not fit 15 bits");
   for (int s = 0; s < d.nstates; s++) {
     uint32_t a0 = d.acc[(size_t)s * nc];
     for (size_t c = 0; c < nc; c++) {
       size_t i = (size_t)s * nc + c;
       if (d.acc[i] > 0xFFFF) return fail(TSG_ERR_INTERNAL, "too many accept masks");
-      tab[i] = (uint16_t)(d.next[i] | (d.acc[i] ? 0x8000u : 0u));
+      tab[i] = (uint16_t)((d.next[i] * nc) | (d.acc[i] ? 0x8000u : 0u));
       acc[i] = (uint16_t)d.acc[i];
       if (d.acc[i] != a0) state_acc = false;
     }
@@ -1285,7 +1321,7 @@ static int make_device_dfa(const DFA& d, const std::vector<uint32_t>& rules, Dev
   std::vector<uint16_t> eot(d.nstates), ni(d.nstates);
   for (int s = 0; s < d.nstates; s++) {
     eot[s] = (uint16_t)d.eot_acc[s];
-    ni[s] = (uint16_t)d.to_noinject[s];
+    ni[s] = (uint16_t)(d.to_noinject[s] * nc);
   }
   std::vector<uint8_t> dead(d.dead.begin(), d.dead.end());
   std::vector<uint64_t> masks;
@@ -1308,7 +1344,8 @@ static int make_device_dfa(const DFA& d, const std::vector<uint32_t>& rules, Dev
   v.ns = (uint32_t)d.nstates;
   v.mw = (uint32_t)d.mask_words;
   v.nmasks = (uint32_t)d.masks.size();
-  for (int k = 0; k < 4; k++) v.start[k] = d.start[k];
+  for (int k = 0; k < 4; k++) v.start[k] = d.start[k] * (uint32_t)nc;
+  v.inv_nc = (uint32_t)((0x100000000ull + nc - 1) / nc);
   // LDS layout
   uint32_t o = align16((uint32_t)(tab.size() * 2));
   v.o_cls = o;
@@ -1521,7 +1558,7 @@ struct LaneState {
   size_t dentries_cap = 0;
   DevCand* cand = nullptr;
   uint32_t cand_cap = 0;
-  uint32_t* counts = nullptr;   // [8] 0 candidates, 1 event chunks, 2 K2 entries
+  uint32_t* counts = nullptr;   // [16] 0 candidates, 1 event chunks, 2 K2 entries, ...
   uint32_t* gcount = nullptr;   // [G]
   uint32_t* cursor = nullptr;   // [G]
   uint64_t* base = nullptr;     // [G]
@@ -1765,7 +1802,7 @@ int lane_create(DeviceRules* d, LaneState** out) {
   l->d = d;
   HIP_TRY(hipStreamCreateWithFlags(&l->st, hipStreamNonBlocking));
   const uint32_t G = std::max<uint32_t>(1, (uint32_t)d->groups.size());
-  HIP_TRY(hipMalloc((void**)&l->counts, sizeof(uint32_t) * 8));
+  HIP_TRY(hipMalloc((void**)&l->counts, sizeof(uint32_t) * 16));
   HIP_TRY(hipMalloc((void**)&l->gcount, sizeof(uint32_t) * G));
   HIP_TRY(hipMalloc((void**)&l->cursor, sizeof(uint32_t) * G));
   HIP_TRY(hipMalloc((void**)&l->base, sizeof(uint64_t) * G));
@@ -1791,7 +1828,7 @@ int host_out_alloc(const DeviceRules* d, uint32_t files_cap, HostOut* o) {
   HIP_TRY(hipHostMalloc((void**)&h.gskip, h.groups, hipHostMallocDefault));
   HIP_TRY(hipHostMalloc((void**)&h.cand, sizeof(Candidate) * (size_t)h.cand_cap, hipHostMallocMapped));
   HIP_TRY(hipHostGetDevicePointer((void**)&h.cand_dev, h.cand, 0));
-  HIP_TRY(hipHostMalloc((void**)&h.counts, sizeof(uint32_t) * 8, hipHostMallocMapped));
+  HIP_TRY(hipHostMalloc((void**)&h.counts, sizeof(uint32_t) * 16, hipHostMallocMapped));
   HIP_TRY(hipHostGetDevicePointer((void**)&h.counts_dev, h.counts, 0));
   for (auto& e : h.ev) HIP_TRY(hipEventCreate(&e));
   *o = h;
@@ -1864,24 +1901,26 @@ int enqueue_scan(DeviceRules* r, LaneState* l, const ScanInput& in, HostOut* out
     if (in.poff[F]) HIP_TRY(hipMemcpyAsync(l->paths, in.paths, in.poff[F], hipMemcpyHostToDevice, st));
     HIP_TRY(hipMemcpyAsync(l->poff, in.poff, sizeof(uint64_t) * (F + 1), hipMemcpyHostToDevice, st));
   }
-  HIP_TRY(hipEventRecord(out->ev[1], st));
-  // the kernels of consecutive batches run one after the other (each has the whole chip;
-  // their HIP-event times are the kernels' own), while this lane's H2D above overlapped
-  // the previous batch's kernels on the other lane
-  if (r->kernels_done_valid) HIP_TRY(hipStreamWaitEvent(st, r->kernels_done, 0));
   if (F) {
     chunk_file_kernel<<<(uint32_t)((nchunks_pad + 255) / 256), 256, 0, st>>>(l->off, F, C, nchunks_pad, l->chunk_file);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipMemsetAsync(l->kw, 0, sizeof(uint32_t) * (size_t)F * W, st));
     HIP_TRY(hipMemsetAsync(l->ovf, 0, F, st));
   }
-  HIP_TRY(hipMemsetAsync(l->counts, 0, sizeof(uint32_t) * 8, st));
+  HIP_TRY(hipMemsetAsync(l->counts, 0, sizeof(uint32_t) * 16, st));
   if (G) {
     HIP_TRY(hipMemsetAsync(l->gcount, 0, sizeof(uint32_t) * G, st));
     HIP_TRY(hipMemsetAsync(l->cursor, 0, sizeof(uint32_t) * G, st));
     HIP_TRY(hipMemsetAsync(l->gskip, 0, G, st));
     HIP_TRY(hipMemsetAsync(l->kind, 0, G, st));
   }
+
+  HIP_TRY(hipEventRecord(out->ev[1], st));
+  // the kernels of consecutive batches run one after the other (each has the whole chip;
+  // their HIP-event times are the kernels' own), while this lane's H2D above overlapped
+  // the previous batch's kernels on the other lane
+  if (r->kernels_done_valid) HIP_TRY(hipStreamWaitEvent(st, r->kernels_done, 0));
+  HIP_TRY(hipEventRecord(out->ev[2], st));
 
   // ---- K1
   const uint32_t k1s = k1_streams();
@@ -1894,7 +1933,7 @@ int enqueue_scan(DeviceRules* r, LaneState* l, const ScanInput& in, HostOut* out
              (uint32_t)kK1Seg};
     if ((rc = launch_k1(r, A, st))) return rc;
   }
-  HIP_TRY(hipEventRecord(out->ev[2], st));
+  HIP_TRY(hipEventRecord(out->ev[3], st));
 
   // ---- gates, items, device-side layout
   ItemArgs IA{};
@@ -1939,7 +1978,7 @@ int enqueue_scan(DeviceRules* r, LaneState* l, const ScanInput& in, HostOut* out
     hipLaunchKernelGGL(items_emit_kernel, dim3(igrid), dim3(kBlock), 2 * G * sizeof(uint32_t) + 16, st, IA);
     HIP_TRY(hipGetLastError());
   }
-  HIP_TRY(hipEventRecord(out->ev[3], st));
+  HIP_TRY(hipEventRecord(out->ev[4], st));
 
   // ---- K2 over the work list
   if (work) {
@@ -1964,6 +2003,8 @@ int enqueue_scan(DeviceRules* r, LaneState* l, const ScanInput& in, HostOut* out
     A.cand_count = l->counts;
     A.cand_cap = out->cand_cap;
     A.ovf = l->ovf;
+    static const bool diag = getenv("TSG_K2_DIAG") != nullptr;
+    A.diag = diag ? l->counts + 8 : nullptr;
     // one block per resident slot (the grids are persistent)
     hipLaunchKernelGGL(k2_kernel, dim3(r->k2_grid), dim3(kBlock), r->max_lds, st, (const DevDFA*)r->d_groups, A);
     HIP_TRY(hipGetLastError());
@@ -1971,32 +2012,33 @@ int enqueue_scan(DeviceRules* r, LaneState* l, const ScanInput& in, HostOut* out
                        (const DevDFA*)r->d_groups, A);
     HIP_TRY(hipGetLastError());
   }
-  HIP_TRY(hipEventRecord(out->ev[4], st));
+  HIP_TRY(hipEventRecord(out->ev[5], st));
   HIP_TRY(hipEventRecord(r->kernels_done, st));
   r->kernels_done_valid = true;
 
   // ---- results to the pinned host buffers
   cand_copy_kernel<<<64, 256, 0, st>>>(l->cand, l->counts, out->cand_cap, (DevCand*)out->cand_dev);
   HIP_TRY(hipGetLastError());
-  HIP_TRY(hipMemcpyAsync(out->counts, l->counts, sizeof(uint32_t) * 8, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipMemcpyAsync(out->counts, l->counts, sizeof(uint32_t) * 16, hipMemcpyDeviceToHost, st));
   if (F) {
     HIP_TRY(hipMemcpyAsync(out->kw, l->kw, sizeof(uint32_t) * (size_t)F * W, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipMemcpyAsync(out->ovf, l->ovf, F, hipMemcpyDeviceToHost, st));
     if (r->has_pathdfa) HIP_TRY(hipMemcpyAsync(out->pathok, l->pathok, F, hipMemcpyDeviceToHost, st));
   }
   if (G) HIP_TRY(hipMemcpyAsync(out->gskip, l->gskip, G, hipMemcpyDeviceToHost, st));
-  HIP_TRY(hipEventRecord(out->ev[5], st));
+  HIP_TRY(hipEventRecord(out->ev[kEvDone], st));
   return TSG_OK;
 }
 
 int batch_times(const HostOut* o, ScanTimes* t) {
-  float x[5] = {0, 0, 0, 0, 0};
-  for (int k = 0; k < 5; k++) HIP_TRY(hipEventElapsedTime(&x[k], o->ev[k], o->ev[k + 1]));
+  float x[6] = {0, 0, 0, 0, 0, 0};
+  for (int k = 0; k < 6; k++) HIP_TRY(hipEventElapsedTime(&x[k], o->ev[k], o->ev[k + 1]));
   t->h2d = x[0];
-  t->k1 = x[1];
-  t->gates = x[2];
-  t->k2 = x[3];
-  t->d2h = x[4];
+  t->wait = x[1];
+  t->k1 = x[2];
+  t->gates = x[3];
+  t->k2 = x[4];
+  t->d2h = x[5];
   return TSG_OK;
 }
 

@@ -72,7 +72,7 @@ struct Batch {
   std::unique_ptr<tsg_result> res;
   BatchResult br;
   ScanTimes t;
-  uint32_t counts[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  uint32_t counts[16] = {};
   double resolve_ms = 0;
   uint64_t files_found = 0;
 };
@@ -258,6 +258,11 @@ void update_stats(tsg_ctx* c, const Batch& b) {
   s.k2_launches = b.counts[6];
   s.groups_skipped = b.counts[7];
   s.files_resolved = b.files_found;
+  s.wait_ms = b.t.wait;
+  s.k2_tail_bytes = b.counts[8];
+  s.k2_tail_max = b.counts[9];
+  s.k2_long_tails = b.counts[10];
+  s.k2_replays = b.counts[11];
   s.k1_hot_states = c->dr ? device_rules_hot_states(c->dr) : 0;
   s.batches++;
   s.sum_bytes += b.bytes;
@@ -281,7 +286,7 @@ void run_job(tsg_ctx* c, std::shared_ptr<Batch> b, BatchView view, HostOut ho,
       kv = emu.view();
       b->counts[0] = (uint32_t)std::min<size_t>(emu.cand.size(), 0xFFFFFFFFu);
     } else {
-      if (hipEventSynchronize(ho.ev[5]) != hipSuccess) throw std::runtime_error("device batch failed");
+      if (hipEventSynchronize(ho.ev[kEvDone]) != hipSuccess) throw std::runtime_error("device batch failed");
       (void)batch_times(&ho, &b->t);
       std::memcpy(b->counts, ho.counts, sizeof(b->counts));
       // counts from the device: 0 candidates, 1 event chunks, 2 K2 entries; layout stats
@@ -682,7 +687,7 @@ int tsg_batch_kernels(tsg_ctx* c) {
     c->kernels_nfiles = F;
     HostOut ho = c->outs[oi];
     lk.unlock();
-    HIP_TRY(hipEventSynchronize(ho.ev[5]));
+    HIP_TRY(hipEventSynchronize(ho.ev[kEvDone]));
     Batch b;
     (void)batch_times(&ho, &b.t);
     std::memcpy(b.counts, ho.counts, sizeof(b.counts));
