@@ -240,6 +240,183 @@ bool is_binary(const uint8_t* p, int64_t n) {  // utils.go:71-89
   return false;
 }
 
+// One member of a tar stream after archive/tar's header processing: extended headers
+// ('x' PAX records, 'L' GNU long names, 'K' long link names) are applied to the entry
+// they precede.  type is the header's typeflag ('\0' kept as is).
+struct TarEntry {
+  uint64_t hdr;   // position of the entry's own header
+  uint64_t dpos;  // its data
+  uint64_t size;  // data bytes (0 for header-only types)
+  char type;
+  std::string name;
+};
+
+bool zero_block(const uint8_t* tar, uint64_t p) {
+  for (int i = 0; i < 512; i++)
+    if (tar[p + i]) return false;
+  return true;
+}
+
+// archive/tar Reader.Next from header position `pos`: appends entries while the position
+// of the next entry group (its first extended header, or its header) is < stop.  Returns
+// the position of the first group at or past stop (its headers unread), tar_len when the
+// archive ended, or (uint64_t)-1 with *err on a malformed archive.  `groups` (optional)
+// receives the position at which each appended entry's group starts.
+uint64_t walk_tar(const uint8_t* tar, uint64_t tar_len, uint64_t pos, uint64_t stop, std::vector<TarEntry>* out,
+                  std::vector<uint64_t>* groups, std::string* err) {
+  std::string long_name;
+  bool have_long = false;
+  std::vector<std::pair<std::string, std::string>> pax;
+  uint64_t group = pos;
+  auto bad = [&](const char* what) {
+    *err = what;
+    return ~0ull;
+  };
+  for (;;) {  // archive/tar Reader.readHeader
+    if (!have_long && pax.empty()) {
+      group = pos;
+      if (pos >= stop) return pos;
+    }
+    if (pos == tar_len) return have_long || !pax.empty() ? bad("unexpected EOF") : tar_len;
+    if (tar_len - pos < 512) return bad("unexpected EOF");
+    const uint8_t* h = tar + pos;
+    if (zero_block(tar, pos)) {  // end: two zero blocks (or one, then end of input)
+      const uint64_t p2 = pos + 512;
+      if (p2 == tar_len) return tar_len;
+      if (tar_len - p2 < 512) return bad("unexpected EOF");
+      if (zero_block(tar, p2)) return tar_len;
+      return bad("invalid header");
+    }
+    if (!checksum_ok(h)) return bad("invalid header");
+    int64_t size;
+    if (!parse_num(h + 124, 12, &size) || size < 0) return bad("invalid size");
+    char type = (char)h[156];
+    const bool ustar = std::memcmp(h + 257, "ustar\0" "00", 8) == 0;
+    std::string name = cstr(h, 100);
+    if (ustar) {
+      const std::string prefix = cstr(h + 345, 155);
+      if (!prefix.empty()) name = prefix + "/" + name;
+    }
+    const uint64_t dpos = pos + 512;
+    if (dpos > tar_len) return bad("unexpected EOF");
+    if (type == 'x' || type == 'L' || type == 'K') {
+      if ((uint64_t)size > tar_len - dpos) return bad("unexpected EOF");
+      if (type == 'x') {
+        if (!parse_pax(tar + dpos, (size_t)size, &pax)) return bad("invalid PAX record");
+        if (pax.empty()) pax.emplace_back("", "");  // (an empty record set still binds)
+      } else if (type == 'L') {
+        long_name = cstr(tar + dpos, (size_t)size);
+        have_long = true;
+      }
+      pos = dpos + (((uint64_t)size + 511) & ~511ull);
+      continue;
+    }
+    if (have_long) name = long_name;
+    for (const auto& kv : pax) {
+      if (kv.first == "path") name = kv.second;
+      else if (kv.first == "size") {
+        // strconv.ParseInt(v, 10, 64) in archive/tar: digits only, no overflow
+        int64_t v = 0;
+        if (kv.second.empty()) return bad("invalid PAX size");
+        for (char c : kv.second) {
+          if (c < '0' || c > '9' || v > (INT64_MAX - (c - '0')) / 10) return bad("invalid PAX size");
+          v = v * 10 + (c - '0');
+        }
+        size = v;
+      }
+    }
+    pax.clear();
+    have_long = false;
+    const uint64_t dlen = header_only(type == 0 && !name.empty() && name.back() == '/' ? '5' : type) ? 0 : (uint64_t)size;
+    if (dlen > tar_len - dpos) return bad("unexpected EOF");
+    out->push_back({pos, dpos, dlen, type, std::move(name)});
+    if (groups) groups->push_back(group);
+    pos = dpos + ((dlen + 511) & ~511ull);  // > the header's position: the walk always advances
+  }
+}
+
+// The index of a whole tar stream.  The header chain is inherently sequential (each size
+// gives the next header), so large archives are walked speculatively in parallel: range
+// k starts at the first block past its start that checksums as a ustar header and walks
+// to the end of its range; the true chain, from 0, then continues into range k exactly
+// where range k-1's walk left it.  If range k's walk passed that position at the start
+// of an entry group, its entries from there on ARE the true chain's (a tar walk from a
+// given group position is deterministic); otherwise range k is walked again from the true
+// position.  Errors count only on the true chain, so the result (entries or the first
+// error) is that of one sequential walk.
+bool index_tar(const uint8_t* tar, uint64_t tar_len, std::vector<TarEntry>* out, std::string* err) {
+  // ranges of at least 64 MiB (TSG_TAR_RANGE_KIB lowers it: tests of the stitching)
+  static const uint64_t kMinRange =
+      getenv("TSG_TAR_RANGE_KIB") ? std::max(1ull, strtoull(getenv("TSG_TAR_RANGE_KIB"), nullptr, 10)) << 10
+                                  : 64ull << 20;
+  const int T = (int)std::min<uint64_t>(16, std::max<uint64_t>(1, tar_len / kMinRange));
+  if (T == 1) return walk_tar(tar, tar_len, 0, tar_len, out, nullptr, err) != ~0ull;
+  struct Part {
+    uint64_t lo = 0, hi = 0, start = 0, end = 0;
+    std::vector<TarEntry> e;
+    std::vector<uint64_t> groups;
+    std::string err;
+  };
+  std::vector<Part> parts(T);
+  for (int k = 0; k < T; k++) {
+    parts[k].lo = (tar_len * k / T) & ~511ull;
+    parts[k].hi = k + 1 == T ? tar_len : ((tar_len * (k + 1) / T) & ~511ull);
+  }
+  pool_for((size_t)T, T, [&](size_t k) {
+    Part& P = parts[k];
+    uint64_t c = P.lo;
+    if (k > 0) {  // first plausible header of the range
+      while (c + 512 <= P.hi &&
+             !(std::memcmp(tar + c + 257, "ustar", 5) == 0 && checksum_ok(tar + c)))
+        c += 512;
+      if (c + 512 > P.hi) {
+        P.start = ~0ull;  // none: the true chain crosses the range inside one member
+        return;
+      }
+    }
+    P.start = c;
+    P.end = walk_tar(tar, tar_len, c, P.hi, &P.e, &P.groups, &P.err);
+  }, 1);
+  uint64_t pos = 0;
+  for (int k = 0; k < T; k++) {
+    Part& P = parts[k];
+    if (pos >= P.hi && k + 1 < T) continue;  // the previous member spans this range
+    size_t first = 0;
+    bool synced = false;
+    if (k == 0) {
+      synced = true;
+    } else if (P.start != ~0ull) {
+      auto it = std::lower_bound(P.groups.begin(), P.groups.end(), pos);
+      if (it != P.groups.end() && *it == pos) {
+        synced = true;
+        first = (size_t)(it - P.groups.begin());
+      } else if (P.end == pos && P.end != ~0ull) {
+        synced = true;  // the walk reached the true position exactly at its stop
+        first = P.e.size();
+      }
+    }
+    if (!synced) {  // walk the range again from the true position
+      P.e.clear();
+      P.groups.clear();
+      P.err.clear();
+      P.end = walk_tar(tar, tar_len, pos, P.hi, &P.e, &P.groups, &P.err);
+      first = 0;
+    }
+    for (size_t i = first; i < P.e.size(); i++) out->push_back(std::move(P.e[i]));
+    if (P.end == ~0ull) {
+      *err = P.err;
+      return false;
+    }
+    if (P.end == tar_len && (k + 1 == T || P.end >= P.hi)) {
+      // the archive ended (or its last member reaches the end): done once the chain has
+      // consumed the rest
+      if (P.end == tar_len) return true;
+    }
+    pos = P.end;
+  }
+  return true;
+}
+
 }  // namespace
 }  // namespace tsg
 
@@ -268,73 +445,18 @@ extern "C" int tsg_layer_pack(const tsg_ruleset* rs, const uint8_t* tar, uint64_
     };
     std::vector<Walked> walked;
     std::vector<std::string> skipped;  // tar.go:35 skipDirs
-    std::string long_name;
-    bool have_long = false;
-    std::vector<std::pair<std::string, std::string>> pax;
-    uint64_t pos = 0;
-    auto bad = [&](const char* what) {
-      return fail(TSG_ERR_ARG, std::string("failed to extract the archive: ") + what);
-    };
-    auto zero_block = [&](uint64_t p) {
-      for (int i = 0; i < 512; i++)
-        if (tar[p + i]) return false;
-      return true;
-    };
-    for (;;) {  // archive/tar Reader.readHeader
-      if (pos == tar_len) break;
-      if (tar_len - pos < 512) return bad("unexpected EOF");
-      const uint8_t* h = tar + pos;
-      if (zero_block(pos)) {  // end: two zero blocks (or one, then end of input)
-        const uint64_t p2 = pos + 512;
-        if (p2 == tar_len) break;
-        if (tar_len - p2 < 512) return bad("unexpected EOF");
-        if (zero_block(p2)) break;
-        return bad("invalid header");
-      }
-      if (!checksum_ok(h)) return bad("invalid header");
-      int64_t size;
-      if (!parse_num(h + 124, 12, &size) || size < 0) return bad("invalid size");
-      char type = (char)h[156];
-      const bool ustar = std::memcmp(h + 257, "ustar\0" "00", 8) == 0;
-      std::string name = cstr(h, 100);
-      if (ustar) {
-        const std::string prefix = cstr(h + 345, 155);
-        if (!prefix.empty()) name = prefix + "/" + name;
-      }
-      const uint64_t dpos = pos + 512;
-      if (dpos > tar_len) return bad("unexpected EOF");
-      if (type == 'x' || type == 'L' || type == 'K') {
-        if ((uint64_t)size > tar_len - dpos) return bad("unexpected EOF");
-        if (type == 'x') {
-          if (!parse_pax(tar + dpos, (size_t)size, &pax)) return bad("invalid PAX record");
-        } else if (type == 'L') {
-          long_name = cstr(tar + dpos, (size_t)size);
-          have_long = true;
-        }
-        pos = dpos + (((uint64_t)size + 511) & ~511ull);
-        continue;
-      }
-      if (have_long) name = long_name;
-      for (const auto& kv : pax) {
-        if (kv.first == "path") name = kv.second;
-        else if (kv.first == "size") {
-          // strconv.ParseInt(v, 10, 64) in archive/tar: digits only, no overflow
-          int64_t v = 0;
-          if (kv.second.empty()) return bad("invalid PAX size");
-          for (char c : kv.second) {
-            if (c < '0' || c > '9' || v > (INT64_MAX - (c - '0')) / 10) return bad("invalid PAX size");
-            v = v * 10 + (c - '0');
-          }
-          size = v;
-        }
-      }
-      pax.clear();
-      have_long = false;
+    std::vector<TarEntry> entries;
+    {
+      std::string err;
+      if (!index_tar(tar, tar_len, &entries, &err))
+        return fail(TSG_ERR_ARG, std::string("failed to extract the archive: ") + err);
+    }
+    for (const TarEntry& te : entries) {
+      char type = te.type;
+      const std::string& name = te.name;
       if (type == 0) type = (!name.empty() && name.back() == '/') ? '5' : '0';
-      const uint64_t dlen = header_only(type) ? 0 : (uint64_t)size;
-      if (dlen > tar_len - dpos) return bad("unexpected EOF");
-      pos = dpos + ((dlen + 511) & ~511ull);  // > the header's position: the walk always advances
-
+      const uint64_t dpos = te.dpos;
+      const int64_t size = (int64_t)te.size;
       // tar.go:45-84
       const std::string fp = trim_left_slash(clean(name));
       const size_t k = fp.rfind('/');
