@@ -248,3 +248,41 @@ def test_native_layer_malformed_pax(analyzer):
                 b"5 a=b\n"]:                                     # record shorter than its text
         with pytest.raises(N.NativeError):
             W.NativeLayer(analyzer.scanner, _pax_tar(rec))
+
+
+@pytest.mark.parametrize("range_kib", [1, 3, 17, 1 << 20])
+def test_native_layer_parallel_index_matches_sequential(analyzer, monkeypatch, range_kib):
+    """The speculative parallel tar index (ranges walked from the first plausible header,
+    stitched to the true chain) gives exactly the sequential walk: PAX / GNU long-name
+    groups straddling range borders, and members whose data holds tar headers (a tar
+    inside the layer) that a range may start from."""
+    import io
+    import tarfile
+    inner = layer_bytes(tarfile.USTAR_FORMAT)
+    buf = io.BytesIO()
+    with tarfile.open(fileobj=buf, mode="w", format=tarfile.PAX_FORMAT) as tf:
+        for i in range(60):
+            _reg(tf, "d%d/" % i + "x" * (90 + i) + "/f.env",
+                 ("k=%d\nexport GITHUB_TOKEN=%s\n" % (i, GHP)).encode() * (1 + i % 7))
+            if i % 9 == 0:
+                _reg(tf, "nested/layer%d.tar.txt" % i, inner)  # headers inside file data
+    tar = buf.getvalue()
+    monkeypatch.delenv("TSG_TAR_RANGE_KIB", raising=False)
+    seq = W.NativeLayer(analyzer.scanner, tar)
+    monkeypatch.setenv("TSG_TAR_RANGE_KIB", str(range_kib))
+    par = W.NativeLayer(analyzer.scanner, tar)
+    b1, b2 = seq.batch, par.batch
+    assert b1.nfiles == b2.nfiles >= 60 and par.walked == seq.walked
+    assert [b1.path(i) for i in range(b1.nfiles)] == [b2.path(i) for i in range(b2.nfiles)]
+    assert bytes(b1.data[:int(b1.offsets[-1])]) == bytes(b2.data[:int(b2.offsets[-1])])
+    def outcome(t):
+        try:
+            lay = W.NativeLayer(analyzer.scanner, t)
+            return ("ok", lay.batch.nfiles, lay.walked)
+        except Exception as e:
+            return ("error", str(e))
+    for cut in (len(tar) // 2, len(tar) // 2 + 100, len(tar) // 3 + 700, len(tar) - 700):
+        monkeypatch.delenv("TSG_TAR_RANGE_KIB")
+        want = outcome(tar[:cut])
+        monkeypatch.setenv("TSG_TAR_RANGE_KIB", str(range_kib))
+        assert outcome(tar[:cut]) == want, cut

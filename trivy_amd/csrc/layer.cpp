@@ -346,7 +346,7 @@ uint64_t walk_tar(const uint8_t* tar, uint64_t tar_len, uint64_t pos, uint64_t s
 // error) is that of one sequential walk.
 bool index_tar(const uint8_t* tar, uint64_t tar_len, std::vector<TarEntry>* out, std::string* err) {
   // ranges of at least 64 MiB (TSG_TAR_RANGE_KIB lowers it: tests of the stitching)
-  static const uint64_t kMinRange =
+  const uint64_t kMinRange =
       getenv("TSG_TAR_RANGE_KIB") ? std::max(1ull, strtoull(getenv("TSG_TAR_RANGE_KIB"), nullptr, 10)) << 10
                                   : 64ull << 20;
   const int T = (int)std::min<uint64_t>(16, std::max<uint64_t>(1, tar_len / kMinRange));
