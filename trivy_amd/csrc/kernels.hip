@@ -779,7 +779,7 @@ __device__ T block_exclusive_scan(T v, T* out, T* s_wave) {
 }
 
 constexpr int kLayoutBlock = 1024;
-constexpr uint32_t kEntryItems = 4 * kBlock;    // two chains per lane, two rounds
+constexpr uint32_t kEntryItems = 2 * kBlock;    // two chains per lane
 constexpr uint32_t kEntryChunks = kStreams * kBlock;
 
 __global__ void __launch_bounds__(kLayoutBlock) layout_kernel(LayoutArgs A) {
@@ -870,6 +870,7 @@ struct K2Args {
   uint32_t cand_cap;
   uint8_t* ovf;
   uint32_t* diag;  // null, or [4]: tail bytes, longest tail, tails over 4 KiB, word replays
+  uint32_t* claim;  // [2] next list / dense entry (zeroed per batch)
 };
 
 // Candidate emission, wave-aggregated: the lanes that reach an accept together reserve
@@ -1227,20 +1228,24 @@ __device__ __forceinline__ void k2_dense_entry(const DevDFA& d, const K2Args& A,
   }
 }
 
-// K2: persistent grids over the work lists.  Block b takes a contiguous range of entries,
-// so consecutive entries mostly share a group and its DFA stays staged in LDS.
+// K2: persistent grids over the work lists.  Blocks claim entries dynamically (one
+// atomic per entry), so blocks that drew light entries take more; a block restages the
+// DFA only when its next entry belongs to another group.
 template <bool DENSE>
 __device__ __forceinline__ void k2_run(const DevDFA* __restrict__ dfas, const K2Args& A, const uint4* entries,
-                                       uint32_t E, uint8_t* smem) {
-  const uint32_t e0 = (uint32_t)((uint64_t)E * blockIdx.x / gridDim.x);
-  const uint32_t e1 = (uint32_t)((uint64_t)E * (blockIdx.x + 1) / gridDim.x);
+                                       uint32_t E, uint32_t* claim, uint8_t* smem) {
+  __shared__ uint32_t s_e;
   uint32_t staged = 0xFFFFFFFFu;
-  for (uint32_t e = e0; e < e1; e++) {
+  for (;;) {
+    if (threadIdx.x == 0) s_e = atomicAdd(claim, 1u);
+    __syncthreads();
+    const uint32_t e = s_e;
+    __syncthreads();  // every lane has read s_e (and is done with the previous entry)
+    if (e >= E) break;
     const uint4 en = entries[e];
     const uint32_t g = __builtin_amdgcn_readfirstlane(en.x);
     const DevDFA& d = dfas[g];  // (a reference: uniform fields load into SGPRs, no copy)
     if (g != staged) {
-      __syncthreads();  // every lane is done with the previous table
       stage_dfa(d, smem);
       staged = g;
     }
@@ -1254,12 +1259,12 @@ __device__ __forceinline__ void k2_run(const DevDFA* __restrict__ dfas, const K2
 
 __global__ void __launch_bounds__(kBlock) k2_kernel(const DevDFA* __restrict__ dfas, K2Args A) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  k2_run<false>(dfas, A, A.entries, *A.nentries, smem);
+  k2_run<false>(dfas, A, A.entries, *A.nentries, A.claim, smem);
 }
 
 __global__ void __launch_bounds__(kBlock) k2_dense_kernel(const DevDFA* __restrict__ dfas, K2Args A) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  k2_run<true>(dfas, A, A.dentries, *A.ndentries, smem);
+  k2_run<true>(dfas, A, A.dentries, *A.ndentries, A.claim + 1, smem);
 }
 
 // the candidates of a batch to pinned, mapped host memory (their count is only known here)
@@ -2005,6 +2010,7 @@ int enqueue_scan(DeviceRules* r, LaneState* l, const ScanInput& in, HostOut* out
     A.ovf = l->ovf;
     static const bool diag = getenv("TSG_K2_DIAG") != nullptr;
     A.diag = diag ? l->counts + 8 : nullptr;
+    A.claim = l->counts + 12;
     // one block per resident slot (the grids are persistent)
     hipLaunchKernelGGL(k2_kernel, dim3(r->k2_grid), dim3(kBlock), r->max_lds, st, (const DevDFA*)r->d_groups, A);
     HIP_TRY(hipGetLastError());
