@@ -71,14 +71,14 @@ def test_slot_layout_errors(builtin):
     ctx.close()
 
 
-@pytest.mark.parametrize("nthreads", [1, 8, 32])
-def test_queue_concurrent_callers(builtin, nthreads):
+@pytest.mark.parametrize("nthreads,max_slots", [(1, 4), (8, 4), (32, 4), (32, 2)])
+def test_queue_concurrent_callers(builtin, nthreads, max_slots):
     """Many threads call Scan on one shared queue; each gets its own file's result."""
     b = corpus.fold_runes_batch(11, nbytes=2 << 20, plants=150, frac=0.2)
     args = [S.ScanArgs(b.path(i), bytes(b.data[int(b.offsets[i]):int(b.offsets[i + 1])]))
             for i in range(b.nfiles)]
     args += [S.ScanArgs("empty/%d" % i, b"") for i in range(5)]
-    ctx = S.GpuContext(builtin, 0, emulate=True, slot_mib=1, max_slots=4)
+    ctx = S.GpuContext(builtin, 0, emulate=True, slot_mib=1, max_slots=max_slots)
     q = S.ScanQueue(ctx, flush_us=500)
     got = [None] * len(args)
     errors = []

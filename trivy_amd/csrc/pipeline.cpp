@@ -201,7 +201,11 @@ int slot_take(tsg_ctx* c, std::unique_lock<std::mutex>& lk, int owner, uint64_t 
       *id = (uint32_t)pick;
       return TSG_OK;
     }
-    if (c->jobs == 0) return fail(TSG_ERR_ARG, "every pinned slot is held by the caller");
+    // nothing will free a slot if no job is running and no queue batch is being filled
+    // (a queue batch's slot is submitted as soon as its last writer is done)
+    bool queue_held = false;
+    for (const auto& sl : c->slots) queue_held |= sl->owner == kQueue;
+    if (c->jobs == 0 && !queue_held) return fail(TSG_ERR_ARG, "every pinned slot is held by the caller");
     c->cv.wait(lk);
   }
 }
