@@ -19,8 +19,9 @@ ranks wall time of the timed steps.
 Rank 0 prints ONE JSON line with, besides the contract fields:
   roofline       K1 (the dominant kernel): algorithmic bytes per launch / mean HIP-event
                  duration of its launches (events on the lane stream around each launch)
-                 vs 8 TB/s; traffic = FETCH_SIZE bytes per launch from the committed PMC
-                 pass of the same command (profiles/r02/)
+                 vs 8 TB/s; traffic = HBM bytes per launch from the committed FETCH_SIZE
+                 pass of the same command (profiles/r02/), converted with the factor
+                 calibrated for K1's access pattern (tools/fetch_calib.hip)
   kernels        K1, K2 (on the bytes it reads) and K1+gates+K2 GB/s (HIP events)
   pipeline       H2D GB/s, per-batch stage times, resolution time
   cpu_baseline   the library's exact C++ CPU path (the reference algorithm restated:
@@ -255,7 +256,9 @@ def main():
                      "frac": round(k1_gbs / HBM_PEAK_GBS, 4),
                      "traffic": _traffic_per_launch(launch_bytes),
                      "algorithmic_bytes_per_launch": int(launch_bytes),
-                     "traffic_source": os.path.relpath(PMC_FETCH_CSV, ROOT)},
+                     "traffic_source": os.path.relpath(PMC_FETCH_CSV, ROOT),
+                     "traffic_calibration": "FETCH_SIZE KiB x 1024 / 0.922 (K1's quad-transposed "
+                                            "64-B loads; profiles/r02/fetch_calib.json)"},
         "kernels": {"k1_GBps": round(k1_gbs, 1),
                     "k2_GBps_on_item_bytes": round(k2_read / (st["k2_ms"] / 1e3) / 1e9, 1)
                     if st["k2_ms"] else None,

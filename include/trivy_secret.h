@@ -319,6 +319,15 @@ int tsg_layer_pack(const tsg_ruleset* rs, const uint8_t* tar, uint64_t tar_len,
                    const char* const* skip_files, uint32_t n_skip_files,
                    const char* const* skip_dirs, uint32_t n_skip_dirs, const char* config_path,
                    tsg_layer** out);
+/* Rank `rank` of `world`'s share of the same layer (configs[2], one layer sharded across the
+ * GPUs of a node): the header chain, whiteouts, opaque dirs and skip-dir logic are those of
+ * the whole layer (every rank returns the same opq / wh / walked); the walked regular files
+ * are cut into `world` contiguous runs of about equal bytes in archive order, and only this
+ * rank's run is gated and packed.  The union over ranks equals tsg_layer_pack's batch. */
+int tsg_layer_pack_shard(const tsg_ruleset* rs, const uint8_t* tar, uint64_t tar_len,
+                         const char* const* skip_files, uint32_t n_skip_files,
+                         const char* const* skip_dirs, uint32_t n_skip_dirs, const char* config_path,
+                         uint32_t rank, uint32_t world, tsg_layer** out);
 int tsg_layer_get(const tsg_layer* layer, tsg_layer_view* out);
 /* Filesystem ingest (configs[0], trivy fs): replaces walker.FS.Walk (pkg/fanal/walker/fs.go:25-63)
  * + the fs artifact's relative paths (pkg/fanal/artifact/local/fs.go:83-100) + Required +

@@ -12,6 +12,7 @@ import pytest
 from tests.helpers import canon_secret
 from trivy_amd import analyzer as A
 from trivy_amd import secret as S
+from trivy_amd import configs
 from trivy_amd import walker as W
 
 GHP = "ghp_" + "aB3dE5fG7hI9jK1lM3nO5pQ7rS9tU1vW3xY5"
@@ -286,3 +287,27 @@ def test_native_layer_parallel_index_matches_sequential(analyzer, monkeypatch, r
         want = outcome(tar[:cut])
         monkeypatch.setenv("TSG_TAR_RANGE_KIB", str(range_kib))
         assert outcome(tar[:cut]) == want, cut
+
+
+@pytest.mark.parametrize("world", [2, 3, 8])
+def test_native_layer_shards_partition_the_layer(analyzer, world):
+    """tsg_layer_pack_shard: the ranks' contiguous runs, concatenated in rank order, are
+    tsg_layer_pack's batch file for file (paths and bytes), with byte-balanced runs, and every
+    rank returns the whole layer's whiteouts / opaque dirs (configs[2], one layer over 8 GPUs)."""
+    tar = configs.layer_tar(2 << 20, seed=23)
+    whole = W.NativeLayer(analyzer.scanner, tar)
+    wb = whole.batch
+    paths, blobs, sizes = [], [], []
+    for r in range(world):
+        lay = W.NativeLayer(analyzer.scanner, tar, rank=r, world=world)
+        b = lay.batch
+        assert (lay.opq, lay.wh, lay.walked) == (whole.opq, whole.wh, whole.walked)
+        sizes.append(int(b.offsets[-1]))
+        for i in range(b.nfiles):
+            paths.append(b.path(i))
+            blobs.append(bytes(b.data[int(b.offsets[i]):int(b.offsets[i + 1])]))
+    assert paths == [wb.path(i) for i in range(wb.nfiles)]
+    assert blobs == [bytes(wb.data[int(wb.offsets[i]):int(wb.offsets[i + 1])]) for i in range(wb.nfiles)]
+    assert max(sizes) < 2 * (sum(sizes) / world) + (1 << 20)
+    with pytest.raises(Exception):
+        W.NativeLayer(analyzer.scanner, tar, rank=world, world=world)

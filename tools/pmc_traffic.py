@@ -3,13 +3,28 @@
 
     python tools/pmc_traffic.py <counter_collection.csv> [kernel-substring]
 
-FETCH_SIZE is in KiB and, on gfx950, counts half the bytes of a 16-B-per-lane streaming
-read (MI355X_MICROARCH.md, HBM section): bytes = FETCH_SIZE * 1024 * 2.  Launches with a
-grid below 1/4 of the largest launch of the same kernel (the K1 sampling pass) are skipped.
+FETCH_SIZE is in KiB and counts memory-side read requests x 64 B (MI355X_MICROARCH.md, HBM
+section), so how many bytes one KiB stands for depends on the request width of the access
+pattern: exactly 1/2 for 16-B-per-lane streaming reads, 0.92 for K1/K2's quad-transposed
+64-B segment loads.  The factor per kernel comes from profiles/r02/fetch_calib.json (a
+calibration run on a known byte count, tools/fetch_calib.hip).  Launches with a grid below
+1/4 of the largest launch of the same kernel (the K1 sampling pass) are skipped.
 """
 import csv
 import json
+import os
 import sys
+
+CALIB = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "profiles", "r02", "fetch_calib.json")
+
+
+def fetch_factor(kernel):
+    """FETCH_SIZE bytes per byte read for the kernel's access pattern."""
+    c = json.load(open(CALIB))
+    for k, pat in c["kernels"].items():
+        if k in kernel:
+            return c[pat]
+    return c["stream16"]
 
 
 def traffic(path, kernel="k1_kernel"):
@@ -19,7 +34,7 @@ def traffic(path, kernel="k1_kernel"):
         return None
     gmax = max(int(r["Grid_Size"]) for r in rows)
     vals = [float(r["Counter_Value"]) for r in rows if int(r["Grid_Size"]) * 4 >= gmax]
-    return sum(vals) / len(vals) * 1024 * 2
+    return sum(vals) / len(vals) * 1024 / fetch_factor(kernel)
 
 
 if __name__ == "__main__":

@@ -138,6 +138,9 @@ SIGNATURES = [
                                  C.c_size_t, C.POINTER(C.c_uint32), C.c_size_t]),
     ("tsg_layer_pack", C.c_int, [_P, _P, C.c_uint64, C.POINTER(C.c_char_p), C.c_uint32,
                                  C.POINTER(C.c_char_p), C.c_uint32, C.c_char_p, C.POINTER(_P)]),
+    ("tsg_layer_pack_shard", C.c_int, [_P, _P, C.c_uint64, C.POINTER(C.c_char_p), C.c_uint32,
+                                       C.POINTER(C.c_char_p), C.c_uint32, C.c_char_p, C.c_uint32,
+                                       C.c_uint32, C.POINTER(_P)]),
     ("tsg_layer_get", C.c_int, [_P, C.POINTER(LayerView)]),
     ("tsg_fs_pack", C.c_int, [_P, C.c_char_p, C.POINTER(C.c_char_p), C.c_uint32,
                               C.POINTER(C.c_char_p), C.c_uint32, C.c_char_p, C.POINTER(_P)]),

@@ -426,7 +426,21 @@ extern "C" int tsg_layer_pack(const tsg_ruleset* rs, const uint8_t* tar, uint64_
                               const char* const* skip_files, uint32_t n_skip_files,
                               const char* const* skip_dirs, uint32_t n_skip_dirs,
                               const char* config_path, tsg_layer** out) {
-  if (!rs || !out || (!tar && tar_len)) return fail(TSG_ERR_ARG, "bad argument");
+  return tsg_layer_pack_shard(rs, tar, tar_len, skip_files, n_skip_files, skip_dirs, n_skip_dirs,
+                              config_path, 0, 1, out);
+}
+
+// One rank's share of a layer (SURVEY.md §8e, configs[2]): every rank indexes the header
+// chain (headers only, parallel), and applies the walker's whiteout / skip-dir logic, which
+// needs the whole chain; the walked files are then cut into `world` contiguous runs of
+// about equal bytes, and only this rank's run is gated (Required, IsBinary) and packed.
+extern "C" int tsg_layer_pack_shard(const tsg_ruleset* rs, const uint8_t* tar, uint64_t tar_len,
+                                    const char* const* skip_files, uint32_t n_skip_files,
+                                    const char* const* skip_dirs, uint32_t n_skip_dirs,
+                                    const char* config_path, uint32_t rank, uint32_t world,
+                                    tsg_layer** out) {
+  if (!rs || !out || (!tar && tar_len) || world == 0 || rank >= world)
+    return fail(TSG_ERR_ARG, "bad argument");
   *out = nullptr;
   try {
     Gate g{rs->rs, rs->plan.get(), base(config_path ? config_path : ""), {}, {}};
@@ -496,6 +510,19 @@ extern "C" int tsg_layer_pack(const tsg_ruleset* rs, const uint8_t* tar, uint64_
       if (under || type == '5') continue;
       L->walked++;
       walked.push_back({dpos, (uint64_t)size, fp});
+    }
+    if (world > 1) {  // this rank's contiguous run of the walked files, by bytes
+      uint64_t all = 0;
+      for (const Walked& w : walked) all += w.size;
+      std::vector<Walked> mine;
+      uint64_t p = 0;
+      for (size_t i = 0; i < walked.size(); i++) {
+        // owner of the file's first byte (zero-length files: of their position)
+        const uint64_t r = all ? (uint64_t)((unsigned __int128)p * world / all) : i * world / walked.size();
+        if (r == rank) mine.push_back(std::move(walked[i]));
+        p += walked[i].size;
+      }
+      walked.swap(mine);
     }
     // AnalyzerGroup.AnalyzeFile (analyzer.go:399-409) + SecretAnalyzer.Analyze: the gates of
     // the walked files in parallel (Required's AllowPath is the costly part), then the

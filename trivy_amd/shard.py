@@ -51,20 +51,28 @@ def scan_layer_sharded(analyzer, tar, rank, world, dist=None, device=None, emula
                        skip_files=(), skip_dirs=()):
     """BASELINE configs[2]: one image layer's files sharded over `world` ranks.
 
-    Every rank walks the (same) in-memory layer tar natively (tsg_layer_pack: the walk,
-    `Required`, `IsBinary`), takes its LPT share of the kept files by bytes and scans it;
-    rank 0 returns (sorted AnalysisResult.Secrets, opq_dirs, wh_files), others None."""
+    Each rank indexes the layer's header chain and packs only its own contiguous byte run
+    of the walked files (tsg_layer_pack_shard: `Required`, `IsBinary` and the copy for that
+    run only), scans it, and the findings are gathered on rank 0; rank 0 returns (sorted
+    AnalysisResult.Secrets, opq_dirs, wh_files), the others None."""
     from .walker import NativeLayer
-    lay = NativeLayer(analyzer.scanner, tar, skip_files, skip_dirs, analyzer.configPath)
+    lay = NativeLayer(analyzer.scanner, tar, skip_files, skip_dirs, analyzer.configPath,
+                      rank=rank, world=world)
     b = lay.batch
-    offs = [int(x) for x in b.offsets]
-    args = [S.ScanArgs(b.path(i), b.data[offs[i]:offs[i + 1]].tobytes())
-            for i in range(b.nfiles)]
-    res = scan_sharded(analyzer.scanner, args, rank, world, dist=dist, device=device,
-                       emulate_chunk=emulate_chunk)
-    if res is None:
+    if b.nfiles == 0:
+        local = []
+    elif device is not None or emulate_chunk:
+        local = analyzer.scanner.ScanBatch(b, device=device, emulate_chunk=emulate_chunk)
+    else:
+        local = analyzer.scanner.ScanBatch(b, nthreads=16)
+    mine = [r for r in local if r and r["Findings"]]
+    if world == 1 or dist is None:
+        return findings_sorted(mine), lay.opq, lay.wh
+    gathered = [None] * world if rank == 0 else None
+    dist.gather_object(mine, gathered, dst=0)
+    if rank != 0:
         return None
-    return findings_sorted(res), lay.opq, lay.wh
+    return findings_sorted([r for part in gathered for r in part]), lay.opq, lay.wh
 
 
 def findings_sorted(results):

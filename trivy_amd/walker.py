@@ -214,9 +214,11 @@ def analyze_layer(analyzer, layer, device=None, ctx=None, emulate_chunk=0,
 class NativeLayer:
     """tsg_layer_pack: the walk, `Required` and `IsBinary` of a whole in-memory layer tar in
     one native pass; `.batch` views the packed files without a copy (valid while this
-    object lives).  `.opq` / `.wh` are the walker's opaque dirs and whiteout files."""
+    object lives).  `.opq` / `.wh` are the walker's opaque dirs and whiteout files.  With
+    world > 1 the batch holds only rank's contiguous byte run of the walked files
+    (tsg_layer_pack_shard); opq / wh / walked are the whole layer's."""
 
-    def __init__(self, scanner, tar, skip_files=(), skip_dirs=(), config_path=""):
+    def __init__(self, scanner, tar, skip_files=(), skip_dirs=(), config_path="", rank=0, world=1):
         L = N.lib()
         self._h = None
         self._tar = np.frombuffer(tar, dtype=np.uint8) if len(tar) else np.zeros(1, np.uint8)
@@ -224,9 +226,11 @@ class NativeLayer:
             *[x.encode("utf-8", "surrogateescape") for x in xs])
         sf, sd = enc(list(skip_files)), enc(list(skip_dirs))
         h = C.c_void_p()
-        N.check(L.tsg_layer_pack(scanner.handle, C.c_void_p(self._tar.ctypes.data), len(tar),
-                                 sf, len(skip_files), sd, len(skip_dirs),
-                                 config_path.encode("utf-8", "surrogateescape"), C.byref(h)))
+        # rank/world: tsg_layer_pack_shard, this rank's contiguous byte run of the layer
+        N.check(L.tsg_layer_pack_shard(scanner.handle, C.c_void_p(self._tar.ctypes.data), len(tar),
+                                       sf, len(skip_files), sd, len(skip_dirs),
+                                       config_path.encode("utf-8", "surrogateescape"), rank, world,
+                                       C.byref(h)))
         self._h = h
         v = N.LayerView()
         N.check(L.tsg_layer_get(h, C.byref(v)))
