@@ -147,6 +147,34 @@ def _traffic_per_launch(batch_bytes):
     return None if t is None else int(t)
 
 
+def rule_set(name):
+    """(scanner, extra plant lines, binary fraction, workload text, rule count)."""
+    from trivy_amd import configs
+    from trivy_amd import secret as S
+    import numpy as np
+    if name == "builtin":
+        return (S.NewScanner(None), None, 0.0,
+                "builtin rules over %.1f GiB synthetic text corpus per GPU (BASELINE configs[1])", 83)
+    if name == "user1000":
+        doc = configs.user_rules_doc(1000, seed=4)
+        sc = S.NewScanner(S.config_from_dict(doc))
+        extra = configs.plant_lines(doc, np.random.default_rng(4), 4096)
+        return (sc, extra, 0.0,
+                "83 builtin + 1,000 user rules (generic clones, keyword-less, unbounded, DFA "
+                "blow-up; configs.user_rules_doc) over %.1f GiB synthetic text corpus per GPU "
+                "(BASELINE configs[3])", len(sc.Rules))
+    doc = configs.allow_exclude_doc()
+    sc = S.NewScanner(S.config_from_dict(doc))
+    extra = configs.plant_lines(doc, np.random.default_rng(5), 4096)
+    extra += ["--- ignore block start ---\nAKIAQWERTYUIOPASDFGH\n--- ignore block stop ---",
+              "-----BEGIN IGNORE-----\nglpat-abcdefghij0123456789\n-----END IGNORE-----",
+              "aws_access_key_id = AKIAQWERTYUIOPEXAMPLEKEY"]
+    return (sc, extra, 0.15,
+            "builtin + custom rules with global / per-rule allow rules and exclude blocks over "
+            "%.1f GiB per GPU of text files and binary blobs that pass IsBinary (15%% of files; "
+            "BASELINE configs[4] shape)", len(sc.Rules))
+
+
 def fill_slots(ctx, batch, batch_bytes):
     """Pack the corpus into pinned slots of about batch_bytes each (outside timing)."""
     import numpy as np
@@ -184,6 +212,13 @@ def main():
                     help="host resolution pool threads (0: library default, 16)")
     ap.add_argument("--cpu-mib", type=int, default=1024, help="CPU baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--strong", action="store_true",
+                    help="strong scaling: --gb is the whole job's corpus, split over the ranks "
+                         "(each rank generates and scans its 1/N share); default: --gb per rank")
+    ap.add_argument("--rules", default="builtin", choices=["builtin", "user1000", "allow-exclude"],
+                    help="rule set: builtin (configs[1]), builtin + 1,000 user rules "
+                         "(configs[3]), allow rules + exclude blocks over text and binary "
+                         "blobs (configs[4])")
     args = ap.parse_args()
 
     dist, rank, world, local = _dist()
@@ -192,11 +227,15 @@ def main():
     from trivy_amd import _native as N
     L = N.lib()
 
-    nbytes = int(args.gb * (1 << 30))
+    nbytes = int(args.gb * (1 << 30) / (world if args.strong else 1))
     t0 = time.perf_counter()
-    batch, info = corpus.make_corpus(nbytes, seed=args.seed + 1000 * rank, plants_per_mib=1.0)
+    sc, extra, binary_frac, workload, nrules = rule_set(args.rules)
+    compile_s = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    batch, info = corpus.make_corpus(nbytes, seed=args.seed + 1000 * rank, plants_per_mib=1.0,
+                                     extra_plants=extra, extra_per_mib=2.0 if extra else 0.0,
+                                     binary_frac=binary_frac)
     gen_s = time.perf_counter() - t0
-    sc = S.NewScanner(None)
     dev = local if world > 1 else 0
     batch_bytes = args.batch_mib << 20
     nslots = -(-nbytes // batch_bytes) + 2
@@ -241,16 +280,18 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(dt / args.steps * 1e3, 3),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if args.strong else "weak",
         "vs_baseline": None,
         "dtype": "u8",
         "data": "synthetic (seeded corpus, trivy_amd/corpus.py) in pinned host memory; every "
                 "step moves every byte host->HBM (H2D inside the timed region)",
-        "config": {"workload": "builtin rules over %.1f GiB synthetic text corpus per GPU "
-                               "(BASELINE configs[1])" % args.gb,
+        "config": {"workload": workload % (nbytes / (1 << 30)) + (
+                       "; strong scaling: a %.1f GiB job split over %d ranks" % (args.gb, world)
+                       if args.strong else ""),
                    "files_per_gpu": info["files"], "bytes_per_gpu": info["bytes"],
+                   "job_bytes": int(total_bytes / args.steps),
                    "batches_per_step": len(slots), "batch_bytes": batch_bytes,
-                   "rules": 83, "parallelism": "file-sharded x%d, no collective" % world},
+                   "rules": nrules, "parallelism": "file-sharded x%d, no collective" % world},
         "roofline": {"bound": "hbm", "kernel": "K1 keyword automaton (k1_kernel)",
                      "achieved": round(k1_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(k1_gbs / HBM_PEAK_GBS, 4),
@@ -276,7 +317,8 @@ def main():
                      "d2h_ms_per_batch": round(d["sum_d2h_ms"] / nbat, 3),
                      "resolve_ms_per_batch": round(d["sum_resolve_ms"] / nbat, 3),
                      "depth": args.depth, "lanes": 2,
-                     "gen_s": round(gen_s, 2), "pack_into_pinned_s": round(pack_s, 2)},
+                     "gen_s": round(gen_s, 2), "pack_into_pinned_s": round(pack_s, 2),
+                     "rule_compile_s": round(compile_s, 2)},
     }
     if rank == 0 and not args.no_cpu_baseline:
         nt = args.host_threads or 16

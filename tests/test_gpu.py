@@ -328,3 +328,29 @@ def test_fs_json_report_gpu(tmp_path):
     golden = [l for l in open(os.path.join(idir, "secrets.json.golden")).read().split("\n")
               if l.strip() != '"Deleted": false,']
     assert R.write_json(rep) == "\n".join(golden)
+
+
+def test_source_tree_config0_gpu(tmp_path):
+    """configs[0] (8 MiB tree): `trivy fs` secret analysis on the device through the native
+    fs ingest == the exact CPU path on every file and the oracle on every 32nd file (the
+    Python oracle runs at 15-60 KB/s), and the sorted AnalysisResult == the CPU path's."""
+    from oracle import secret as O
+    from trivy_amd import analyzer as A
+    from trivy_amd import configs
+    from trivy_amd import walker as W
+    root = str(tmp_path / "tree")
+    configs.source_tree(root, 8 << 20, seed=0)
+    an = A.SecretAnalyzer()
+    an.Init("")
+    fs = W.NativeFS(an.scanner, root)
+    got = an.scanner.ScanBatch(fs.batch, device=0)
+    assert got == an.scanner.ScanBatch(fs.batch, nthreads=16)
+    osc = O.NewScanner(None)
+    n = 0
+    for i in range(0, fs.batch.nfiles, 32):
+        c = bytes(fs.batch.data[int(fs.batch.offsets[i]):int(fs.batch.offsets[i + 1])])
+        want = canon_secret(osc.Scan(fs.batch.path(i), c))
+        assert canon_secret(got[i]) == want, fs.batch.path(i)
+        n += len(want["Findings"] or [])
+    assert n > 5
+    assert W.analyze_fs(an, root, device=0) == W.analyze_fs(an, root)

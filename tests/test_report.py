@@ -127,3 +127,30 @@ def test_go_json_string_rules():
     assert R._go_string(" ") == '"\\u2028"'
     assert json.loads(R.write_json({"a": [1, None, {"b": True}], "c": {}, "d": []})) == \
         {"a": [1, None, {"b": True}], "c": {}, "d": []}
+
+
+def test_source_tree_config0(tmp_path):
+    """configs[0] at 6 MiB: the seeded source tree through the native fs ingest, scanned with
+    the kernels' algorithm (emulated) == the exact CPU path, a file sample == the oracle; the
+    .git dir, node_modules, lockfiles and the <10-byte file never reach Scan."""
+    from oracle import secret as O
+    from tests.helpers import canon_secret
+    from trivy_amd import configs
+    root = str(tmp_path / "tree")
+    info = configs.source_tree(root, 6 << 20, seed=0)
+    an = A.SecretAnalyzer()
+    an.Init("")
+    fs = W.NativeFS(an.scanner, root)
+    paths = [fs.batch.path(i) for i in range(fs.batch.nfiles)]
+    # the builtin global allow paths (tests, examples, vendor, docs, ...) drop more files
+    assert 0 < fs.batch.nfiles < info["files"] - 5 and paths == sorted(paths)
+    assert not any(p.startswith((".git/", "node_modules/")) or p in ("package-lock.json", "go.sum",
+                                                                      "src/tiny.txt") for p in paths)
+    emu = an.scanner.ScanBatch(fs.batch, emulate_chunk=256)
+    assert emu == an.scanner.ScanBatch(fs.batch, nthreads=8)
+    osc = O.NewScanner(None)
+    for i in range(0, fs.batch.nfiles, 29):
+        c = bytes(fs.batch.data[int(fs.batch.offsets[i]):int(fs.batch.offsets[i + 1])])
+        assert canon_secret(emu[i]) == canon_secret(osc.Scan(paths[i], c)), paths[i]
+    rules = {f["RuleID"] for r in emu if r["Findings"] for f in r["Findings"]}
+    assert {"aws-access-key-id", "github-pat", "slack-access-token"} <= rules

@@ -195,3 +195,49 @@ def layer_tar(nbytes, seed=3, binary_frac=0.05):
         add(tf, "etc/.wh..wh..opq", tarfile.REGTYPE)
         add(tf, "etc/.wh.hostname", tarfile.REGTYPE)
     return buf.getvalue()
+
+
+def source_tree(root, nbytes=200 << 20, seed=0):
+    """configs[0] (SURVEY.md §8d "Config 1"): a seeded source tree on disk for `trivy fs
+    --scanners secret`.  Files come from the corpus generator (log-normal sizes, median
+    6 KiB; every builtin rule planted, near misses included; md/test/vendor/example/docs
+    paths that the builtin allow rules cover), plus explicit AWS / GitHub / Slack tokens,
+    and entries the walker or `Required` skips: a .git dir, node_modules, lockfiles, a
+    tiny file.  Returns {"files": written regular files, "bytes": their total}."""
+    import os
+    from trivy_amd import corpus
+    rng = np.random.default_rng(seed)
+    aws = ["aws_access_key_id = AKIA%s" % "".join(rng.choice(list(string.ascii_uppercase + "234567"), size=16))
+           for _ in range(8)]
+    aws += ["aws_secret_access_key = \"%s\"" % "".join(rng.choice(list(_ALNUM + "ABCDEFGHIJ/+"), size=40))
+            for _ in range(8)]
+    gh = ["token: %s_%s" % (p, "".join(rng.choice(list(_ALNUM + "ABCDEFGHIJKLMNOP"), size=36)))
+          for p in ("ghp", "gho", "ghu", "ghs", "ghr") for _ in range(3)]
+    slack = ["SLACK_TOKEN=xoxb-%d-%d-%s" % (rng.integers(10 ** 9, 10 ** 10), rng.integers(10 ** 9, 10 ** 10),
+                                           "".join(rng.choice(list(_ALNUM), size=24))) for _ in range(8)]
+    slack += ["https://hooks.slack.com/services/T%s/B%s/%s" % (
+        "".join(rng.choice(list(string.ascii_uppercase + string.digits), size=8)),
+        "".join(rng.choice(list(string.ascii_uppercase + string.digits), size=8)),
+        "".join(rng.choice(list(_ALNUM), size=24))) for _ in range(4)]
+    extra = [x for t in zip(aws, gh, slack) for x in t] + aws[8:] + gh[8:] + slack[8:]
+    b, info = corpus.make_corpus(nbytes, seed=seed, plants_per_mib=5.0,
+                                 extra_plants=extra, extra_per_mib=8.0)
+    nfiles, total = 0, 0
+    for i in range(b.nfiles):
+        p = os.path.join(root, b.path(i))
+        os.makedirs(os.path.dirname(p), exist_ok=True)
+        data = b.data[int(b.offsets[i]):int(b.offsets[i + 1])]
+        with open(p, "wb") as f:
+            f.write(data.tobytes())
+        nfiles += 1
+        total += len(data)
+    planted = "\n".join(aws[:2] + gh[:2] + slack[:2]).encode()
+    for rel in (".git/config", "node_modules/pkg/index.js", "package-lock.json", "go.sum",
+                "src/tiny.txt"):
+        p = os.path.join(root, rel)
+        os.makedirs(os.path.dirname(p), exist_ok=True)
+        with open(p, "wb") as f:
+            f.write(planted if rel != "src/tiny.txt" else b"AKIA")
+        nfiles += 1
+        total += len(planted) if rel != "src/tiny.txt" else 4
+    return {"files": nfiles, "bytes": total, "planted": info["planted"], "seed": seed}

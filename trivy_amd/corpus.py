@@ -146,8 +146,14 @@ DIRS = ["src", "pkg", "lib", "app", "cmd", "internal", "config", "deploy", "scri
 
 
 def make_corpus(total_bytes, seed=1, plants_per_mib=1.0, median=6 * 1024, sigma=1.2,
-                min_size=10, max_size=2 * 1024 * 1024, base_bytes=None, special=True):
-    """Return (Batch, info).  Deterministic in `seed`."""
+                min_size=10, max_size=2 * 1024 * 1024, base_bytes=None, special=True,
+                extra_plants=None, extra_per_mib=0.0, binary_frac=0.0):
+    """Return (Batch, info).  Deterministic in `seed`.
+
+    extra_plants / extra_per_mib: lines (e.g. configs.plant_lines of a user rule set) planted
+    at that rate on top of the builtin plants (configs[3]).  binary_frac: that fraction of
+    the files becomes random bytes behind a text-looking first 300 bytes, i.e. binary blobs
+    that pass utils.IsBinary and reach Scan (configs[4])."""
     rng = np.random.default_rng(seed)
     base_bytes = base_bytes or int(min(total_bytes, 64 << 20))
     base = _base_text(base_bytes, rng)
@@ -199,6 +205,23 @@ def make_corpus(total_bytes, seed=1, plants_per_mib=1.0, median=6 * 1024, sigma=
         at = fs + int(rng.integers(0, fe - fs - len(line)))
         data[at:at + len(line)] = np.frombuffer(line, dtype=np.uint8)
         planted += 1
+    if extra_plants:
+        nx = int(extra_per_mib * total / (1 << 20))
+        xf = rng.integers(0, nfiles, size=nx)
+        for i in range(nx):
+            f = int(xf[i])
+            fs, fe = int(offsets[f]), int(offsets[f + 1])
+            line = ("\n" + extra_plants[i % len(extra_plants)] + "\n").encode()
+            if fe - fs < len(line) + 1:
+                continue
+            at = fs + int(rng.integers(0, fe - fs - len(line)))
+            data[at:at + len(line)] = np.frombuffer(line, dtype=np.uint8)
+            planted += 1
+    if binary_frac:
+        for f in np.flatnonzero(rng.random(nfiles) < binary_frac):
+            fs, fe = int(offsets[f]), int(offsets[f + 1])
+            if fe - fs > 300:
+                data[fs + 300:fe] = rng.integers(0, 256, size=fe - fs - 300, dtype=np.uint8)
     if special and nfiles > 100:
         # invalid bytes (0.1%), folding runes (0.01%), long lines (5%), PEM blocks (0.5%)
         for f in rng.choice(nfiles, size=max(1, nfiles // 1000), replace=False):
