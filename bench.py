@@ -221,6 +221,7 @@ def main():
                          "blobs (configs[4])")
     args = ap.parse_args()
 
+    T0 = time.perf_counter()
     dist, rank, world, local = _dist()
     from trivy_amd import corpus
     from trivy_amd import secret as S
@@ -245,8 +246,15 @@ def main():
     slots = fill_slots(ctx, batch, batch_bytes)
     pack_s = time.perf_counter() - t0
 
+    def log(msg):
+        print("[bench rank %d %.1fs] %s" % (rank, time.perf_counter() - T0, msg), file=sys.stderr, flush=True)
+
+    log("corpus %.2f GiB (%d files) in %.1fs, rules compiled in %.1fs, packed in %.1fs"
+        % (info["bytes"] / (1 << 30), info["files"], gen_s, compile_s, pack_s))
+
     def run(steps):
-        for _ in range(steps):
+        for k in range(steps):
+            log("step %d/%d" % (k + 1, steps))
             for sid, nf, _ in slots:
                 ctx.submit_slot(sid, nf)
                 while ctx.pending() >= args.depth:
@@ -320,6 +328,7 @@ def main():
                      "gen_s": round(gen_s, 2), "pack_into_pinned_s": round(pack_s, 2),
                      "rule_compile_s": round(compile_s, 2)},
     }
+    log("timed %d steps: %.3f s" % (args.steps, dt))
     if rank == 0 and not args.no_cpu_baseline:
         nt = args.host_threads or 16
         line["cpu_baseline"], line["cpu_optimised"] = cpu_baselines(sc, batch, args.cpu_mib << 20, nt)

@@ -101,6 +101,7 @@ typedef struct tsg_ruleset_info {
   uint32_t max_group_states;
   uint64_t table_bytes;     /* all device tables */
   uint32_t kw_classes;      /* K1 automaton byte classes */
+  uint32_t k1x_literals;    /* literals of the hashed prefilter (K1X; large rule sets) */
 } tsg_ruleset_info;
 int tsg_ruleset_get_info(const tsg_ruleset* rs, tsg_ruleset_info* out);
 

@@ -20,11 +20,37 @@ def user100():
 
 
 def test_user_rules_plan_degrades_not_fails(user100):
-    """183 rules: the K1 automaton would exceed its budget; keywords are left out of it
-    instead of failing the rule-set compile (the reference has no such limit)."""
+    """183 rules: the K1 automaton would exceed its LDS budget; the keywords and anchors of
+    >= 4 bytes move to the hashed prefilter (K1X) instead of failing the rule-set compile
+    (the reference has no such limit), and no keyword becomes unknown."""
     _, sc = user100
     info = sc.info()
-    assert info["n_rules"] == 183 and info["kw_states"] > 0
+    assert info["n_rules"] == 183 and info["kw_states"] > 0 and info["k1x_literals"] > 50
+
+
+def test_k1x_reference_matches_bruteforce(user100):
+    """k1_reference's keyword bits for a K1X rule set (most keywords hashed) == a brute-force
+    search of every keyword in every ASCII-lowercased file.  Keyword ids follow the plan's
+    numbering: first appearance over the rules' keywords (plan.cpp build_plan)."""
+    doc, sc = user100
+    b = S.Batch.from_args(configs.mixed_batch(doc, 64 << 10, seed=77, plants_per_file=0.9))
+    kw, _ = sc.k1_reference(b, 256)
+    ids = {}
+    for r in sc.Rules:
+        ks = [k.lower() for k in (r.Keywords or [])]
+        if not all(k.isascii() for k in ks):
+            continue
+        for k in ks:
+            ids.setdefault(k, len(ids))
+    hits = 0
+    for f in range(b.nfiles):
+        low = bytes(b.data[int(b.offsets[f]):int(b.offsets[f + 1])]).lower()
+        for k, i in ids.items():
+            want = k.encode() in low
+            got = bool((int(kw[f, i // 32]) >> (i % 32)) & 1)
+            assert got == want, (f, k)
+            hits += want
+    assert hits > 20
 
 
 @pytest.mark.parametrize("chunk", [64, 256])

@@ -36,6 +36,24 @@ def test_user_rules_1000_compile(user1000):
     assert info["n_rules"] == 1083 and info["n_groups"] > 0
 
 
+def test_user_rules_1000_k1_vs_reference(user1000):
+    """configs[3]'s keywords and anchors do not fit K1's automaton: the long ones go to the
+    hashed prefilter (K1X).  K1 + K1X keyword bits and chunk events == k1_reference."""
+    import numpy as np
+    doc, sc = user1000
+    assert sc.info()["k1x_literals"] > 800
+    b = S.Batch.from_args(configs.mixed_batch(doc, 1 << 20, seed=65, plants_per_file=0.8))
+    for chunk in (64, 256):
+        ctx = S.GpuContext(sc, 0, chunk_bytes=chunk, adapt_mib=0xFFFFFFFF)
+        ctx.upload(b)
+        ctx.kernels()
+        kw, ev = ctx.k1_output(chunk)
+        ctx.close()
+        rkw, rev = sc.k1_reference(b, chunk)
+        assert np.array_equal(kw, rkw)
+        assert np.array_equal(ev, rev)
+
+
 def test_user_rules_1000_gpu_vs_oracle(user1000):
     doc, sc = user1000
     args = configs.mixed_batch(doc, 256 << 10, seed=61, plants_per_file=0.6)

@@ -39,7 +39,7 @@ class RulesetInfo(C.Structure):
     _fields_ = [("n_rules", C.c_uint32), ("n_keywords", C.c_uint32), ("n_groups", C.c_uint32),
                 ("n_hostonly", C.c_uint32), ("kw_states", C.c_uint32),
                 ("max_group_states", C.c_uint32), ("table_bytes", C.c_uint64),
-                ("kw_classes", C.c_uint32)]
+                ("kw_classes", C.c_uint32), ("k1x_literals", C.c_uint32)]
 
 
 TSG_CTX_EMULATE = 1

@@ -156,6 +156,7 @@ int tsg_ruleset_get_info(const tsg_ruleset* rs, tsg_ruleset_info* o) {
   for (uint8_t h : p.rule_hostonly) o->n_hostonly += h;
   o->kw_states = (uint32_t)p.kw_dfa->nstates;
   o->kw_classes = (uint32_t)p.kw_dfa->nclasses;
+  o->k1x_literals = (uint32_t)p.x_lits.size();
   uint64_t tb = (uint64_t)p.kw_dfa->nstates * p.kw_dfa->nclasses * 2;
   for (const auto& g : p.groups) {
     o->max_group_states = std::max<uint32_t>(o->max_group_states, (uint32_t)g.dfa->nstates);

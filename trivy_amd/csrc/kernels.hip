@@ -24,6 +24,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <map>
 #include <cstdlib>
 #include <cstring>
 #include <memory>
@@ -551,6 +552,160 @@ __global__ void __launch_bounds__(kK1Block) __attribute__((amdgpu_waves_per_eu(K
 #endif
 }
 
+// ---------------------------------------------------------------- K1X
+// Literals K1's automaton has no room for (Plan::x_lits: the keywords and anchors of
+// >= 4 bytes of a large user rule set).  k1x_kernel slides a 4-byte window over the
+// batch, ASCII case folded, and tests the window's hash against an LDS bitmap of the
+// literals' prefixes (x_hash, 2^20 bits); each 16-byte word with a hit is listed
+// (one record per lane-word, a 16-bit mask of hit positions).  k1x_verify_kernel then
+// checks every listed position exactly against the literals with that 4-byte prefix
+// (an open-addressing table) and sets keyword bits (the whole literal inside the file
+// holding its last byte, K1's accept rule) and chunk event bits (chunk of the last
+// byte) with atomics.  A lane whose record does not fit the list verifies inline.
+struct DevK1X {
+  const uint32_t* bitmap;  // [2^kXBits / 32]
+  const uint4* slots;      // [mask + 1] {prefix, first literal, count, 0}; count 0 = empty
+  uint32_t mask;
+  const uint32_t* lits;    // literal indices of the slots, back to back
+  const uint8_t* bytes;    // literal bytes, back to back
+  const uint32_t* off;     // [n + 1]
+  const int32_t* kwid;     // [n] keyword id or -1
+  const uint32_t* ev;      // [n] event bits
+  uint32_t kw_words;
+};
+
+struct K1XArgs {
+  const uint8_t* data;
+  const uint64_t* off;
+  const uint32_t* chunk_file;
+  uint64_t total;
+  uint32_t chunk, nfiles;
+  uint32_t* kw;
+  uint32_t* ev;
+  uint2* list;      // {word index, hit mask}, one slice per k1x_kernel block
+  uint32_t* count;  // [blocks] records in each slice
+  uint32_t cap;     // records in all slices
+};
+
+__device__ __forceinline__ uint32_t x_lower4(uint32_t x) {
+  // ASCII 'A'..'Z' -> +0x20, every other byte unchanged (bytes >= 0x80 keep bit 7)
+  const uint32_t t = x & 0x7F7F7F7Fu;
+  const uint32_t ge_a = t + 0x3F3F3F3Fu;  // bit 7 set: byte >= 0x41
+  const uint32_t gt_z = t + 0x25252525u;  // bit 7 set: byte >= 0x5B
+  const uint32_t up = (ge_a & ~gt_z) & ~x & 0x80808080u;
+  return x | (up >> 2);
+}
+
+__device__ __forceinline__ uint32_t x_hash_dev(uint32_t w) { return (w * 2654435761u) >> (32 - kXBits); }
+
+__device__ __forceinline__ uint32_t x_low_byte(uint8_t c) { return (c >= 'A' && c <= 'Z') ? c + 32u : c; }
+
+// exact check of the literals starting at batch byte p (window w = its 4 lowercased bytes)
+__device__ void k1x_verify_at(const DevK1X& x, const K1XArgs& A, uint64_t p, uint32_t w) {
+  uint32_t h = (w * 0x85EBCA6Bu) & x.mask;
+  for (;;) {
+    const uint4 sl = x.slots[h];
+    if (sl.z == 0) return;  // no literal with this prefix
+    if (sl.x == w) {
+      for (uint32_t j = 0; j < sl.z; j++) {
+        const uint32_t i = x.lits[sl.y + j];
+        const uint32_t a = x.off[i], len = x.off[i + 1] - a;
+        if (p + len > A.total) continue;
+        uint32_t t = 4;
+        while (t < len && x_low_byte(A.data[p + t]) == x.bytes[a + t]) t++;
+        if (t < len) continue;
+        const uint64_t q = p + len - 1;
+        if (x.ev[i]) atomicOr(&A.ev[q / A.chunk], x.ev[i]);
+        const int32_t k = x.kwid[i];
+        if (k >= 0) {
+          uint32_t f = A.chunk_file[q / A.chunk];
+          while (A.off[f + 1] <= q) f++;
+          if (p >= A.off[f]) atomicOr(&A.kw[(size_t)f * x.kw_words + k / 32], 1u << (k % 32));
+        }
+      }
+      return;
+    }
+    h = (h + 1) & x.mask;
+  }
+}
+
+constexpr int kK1XBlock = 512;
+
+__device__ __forceinline__ uint32_t k1x_hits(const uint32_t* s_bm, const uint32_t (&d)[5]) {
+  uint32_t hits = 0;
+#pragma unroll
+  for (int k = 0; k < 16; k++) {
+    const uint32_t w = (k & 3) ? __builtin_amdgcn_alignbyte(d[k / 4 + 1], d[k / 4], k & 3) : d[k / 4];
+    const uint32_t h = x_hash_dev(w);
+    hits |= ((s_bm[h >> 5] >> (h & 31)) & 1u) << k;
+  }
+  return hits;
+}
+
+// Each block lists its hit records in its own slice of A.list (an LDS counter, no global
+// atomics); a record past the slice is verified inline.  A.count[block] = records kept.
+__global__ void __launch_bounds__(kK1XBlock) k1x_kernel(DevK1X x, K1XArgs A) {
+  extern __shared__ uint32_t s_bm[];  // 2^kXBits bits, then the block's record counter
+  uint32_t* s_n = s_bm + (1u << kXBits) / 32;
+  for (uint32_t i = threadIdx.x; i < (1u << kXBits) / 32; i += blockDim.x) s_bm[i] = x.bitmap[i];
+  if (threadIdx.x == 0) *s_n = 0;
+  __syncthreads();
+  const uint32_t slice = A.cap / gridDim.x;
+  uint2* list = A.list + (size_t)blockIdx.x * slice;
+  const uint64_t nwords = (A.total + 15) / 16;
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  uint64_t wi = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  // one word ahead in registers (the batch is padded with zero bytes past its end)
+  uint4 v = make_uint4(0, 0, 0, 0);
+  uint32_t nx = 0;
+  if (wi < nwords) {
+    v = *(const uint4*)(A.data + wi * 16);
+    nx = *(const uint32_t*)(A.data + wi * 16 + 16);
+  }
+  for (; wi < nwords; wi += stride) {
+    const uint32_t d[5] = {x_lower4(v.x), x_lower4(v.y), x_lower4(v.z), x_lower4(v.w), x_lower4(nx)};
+    if (wi + stride < nwords) {
+      v = *(const uint4*)(A.data + (wi + stride) * 16);
+      nx = *(const uint32_t*)(A.data + (wi + stride) * 16 + 16);
+    }
+    uint32_t hits = k1x_hits(s_bm, d);
+    // positions past the batch end never count (their window holds pad bytes)
+    const uint64_t p0 = wi * 16;
+    if (p0 + 16 > A.total) hits &= (1u << (uint32_t)(A.total - p0)) - 1u;
+    if (__builtin_expect(hits != 0, 0)) {
+      const uint32_t slot = atomicAdd(s_n, 1u);
+      if (slot < slice) {
+        list[slot] = make_uint2((uint32_t)wi, hits);
+      } else {
+        for (uint32_t t = hits; t; t &= t - 1) {
+          const int k = __builtin_ctz(t);
+          const uint32_t w = (k & 3) ? __builtin_amdgcn_alignbyte(d[k / 4 + 1], d[k / 4], k & 3) : d[k / 4];
+          k1x_verify_at(x, A, p0 + k, w);
+        }
+      }
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) A.count[blockIdx.x] = min(*s_n, slice);
+}
+
+__global__ void __launch_bounds__(kBlock) k1x_verify_kernel(DevK1X x, K1XArgs A, uint32_t nblocks) {
+  const uint32_t slice = A.cap / nblocks;
+  const uint64_t n = (uint64_t)slice * nblocks;
+  for (uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t b = (uint32_t)(e / slice), j = (uint32_t)(e % slice);
+    if (j >= A.count[b]) continue;
+    const uint2 r = A.list[e];
+    const uint64_t p0 = (uint64_t)r.x * 16;
+    for (uint32_t t = r.y; t; t &= t - 1) {
+      const uint64_t p = p0 + __builtin_ctz(t);
+      const uint32_t w = x_low_byte(A.data[p]) | x_low_byte(A.data[p + 1]) << 8 | x_low_byte(A.data[p + 2]) << 16 |
+                         x_low_byte(A.data[p + 3]) << 24;
+      k1x_verify_at(x, A, p, w);
+    }
+  }
+}
+
 // ---------------------------------------------------------------- gate + items
 __device__ __forceinline__ bool group_gated(const uint32_t* __restrict__ kwf, const uint32_t* __restrict__ gm,
                                             uint32_t W, uint32_t always) {
@@ -560,18 +715,31 @@ __device__ __forceinline__ bool group_gated(const uint32_t* __restrict__ kwf, co
   return false;
 }
 
-// per file: bit g of ggate[f * GW + g / 64] = group g gated (Rule.MatchKeywords may pass)
+// per file: bit g of ggate[f * GW + g / 64] = group g gated (Rule.MatchKeywords may pass):
+// the always-gated groups, ORed with the groups of every keyword bit the file has (a file
+// holds few keywords, so the cost is its set bits x GW, not groups x keyword words)
 __global__ void ggate_kernel(const uint32_t* __restrict__ kw, uint32_t F, uint32_t W,
-                             const uint32_t* __restrict__ gmask, const uint32_t* __restrict__ galways,
-                             uint32_t G, uint32_t GW, unsigned long long* __restrict__ ggate) {
+                             const unsigned long long* __restrict__ kwg,
+                             const unsigned long long* __restrict__ galw, uint32_t GW,
+                             unsigned long long* __restrict__ ggate) {
   const uint32_t f = blockIdx.x * blockDim.x + threadIdx.x;
   if (f >= F) return;
   const uint32_t* kwf = kw + (size_t)f * W;
-  for (uint32_t w = 0; w < GW; w++) {
-    unsigned long long bits = 0;
-    for (uint32_t g = w * 64; g < min(G, w * 64 + 64); g++)
-      if (group_gated(kwf, gmask + (size_t)g * W, W, galways[g])) bits |= 1ull << (g - w * 64);
-    ggate[(size_t)f * GW + w] = bits;
+  for (uint32_t w0 = 0; w0 < GW; w0 += 8) {
+    const uint32_t n = min(8u, GW - w0);
+    unsigned long long acc[8];
+#pragma unroll
+    for (uint32_t j = 0; j < 8; j++) acc[j] = j < n ? galw[w0 + j] : 0ull;
+    for (uint32_t i = 0; i < W; i++)
+      for (uint32_t bits = kwf[i]; bits; bits &= bits - 1) {
+        const unsigned long long* row = kwg + (size_t)(i * 32 + __builtin_ctz(bits)) * GW + w0;
+#pragma unroll
+        for (uint32_t j = 0; j < 8; j++)
+          if (j < n) acc[j] |= row[j];
+      }
+#pragma unroll
+    for (uint32_t j = 0; j < 8; j++)
+      if (j < n) ggate[(size_t)f * GW + w0 + j] = acc[j];
   }
 }
 
@@ -1439,6 +1607,51 @@ static int k1_tables(const Plan& p, const std::vector<uint8_t>& quiet, K1Host* h
   return TSG_OK;
 }
 
+// K1X tables: the prefix bitmap, the prefix -> literals table and the literals
+static int make_device_k1x(const Plan& p, DevK1X* out, std::vector<void*>* allocs) {
+  *out = DevK1X{};
+  out->kw_words = (uint32_t)p.kw_words;
+  if (p.x_lits.empty()) return TSG_OK;
+  const size_t n = p.x_lits.size();
+  std::vector<uint32_t> bitmap((1u << kXBits) / 32, 0);
+  std::map<uint32_t, std::vector<uint32_t>> by4;
+  std::vector<uint8_t> bytes;
+  std::vector<uint32_t> off{0}, ev(n);
+  std::vector<int32_t> kwid(n);
+  for (size_t i = 0; i < n; i++) {
+    const std::string& L = p.x_lits[i];
+    if (L.size() < 4) return fail(TSG_ERR_INTERNAL, "K1X literal shorter than 4 bytes");
+    const uint32_t w = x_prefix4((const uint8_t*)L.data());
+    const uint32_t h = x_hash(w);
+    bitmap[h >> 5] |= 1u << (h & 31);
+    by4[w].push_back((uint32_t)i);
+    bytes.insert(bytes.end(), L.begin(), L.end());
+    off.push_back((uint32_t)bytes.size());
+    ev[i] = p.x_event[i];
+    kwid[i] = p.x_kw[i];
+  }
+  uint32_t nslots = 16;
+  while (nslots < 2 * by4.size()) nslots *= 2;
+  std::vector<uint4> slots(nslots, make_uint4(0, 0, 0, 0));
+  std::vector<uint32_t> lits;
+  for (const auto& kv : by4) {
+    uint32_t h = (kv.first * 0x85EBCA6Bu) & (nslots - 1);
+    while (slots[h].z) h = (h + 1) & (nslots - 1);
+    slots[h] = make_uint4(kv.first, (uint32_t)lits.size(), (uint32_t)kv.second.size(), 0);
+    lits.insert(lits.end(), kv.second.begin(), kv.second.end());
+  }
+  int rc;
+  if ((rc = upload_vec(bitmap, &out->bitmap, allocs))) return rc;
+  if ((rc = upload_vec(slots, &out->slots, allocs))) return rc;
+  if ((rc = upload_vec(lits, &out->lits, allocs))) return rc;
+  if ((rc = upload_vec(bytes, &out->bytes, allocs))) return rc;
+  if ((rc = upload_vec(off, &out->off, allocs))) return rc;
+  if ((rc = upload_vec(kwid, &out->kwid, allocs))) return rc;
+  if ((rc = upload_vec(ev, &out->ev, allocs))) return rc;
+  out->mask = nslots - 1;
+  return TSG_OK;
+}
+
 static int make_device_k1(const Plan& p, DevK1* out, std::vector<void*>* allocs, K1Host* host) {
   const DFA& d = *p.kw_dfa;
   const size_t nc = d.nclasses;
@@ -1504,6 +1717,8 @@ struct DeviceRules {
   std::vector<void*> tables;
   DevK1 k1{};
   K1Host k1h;
+  DevK1X k1x{};
+  bool has_k1x = false;
   uint32_t* d_hits = nullptr;
   bool adapted = false;
   uint32_t hot_states = 0;
@@ -1516,6 +1731,8 @@ struct DeviceRules {
   bool has_pathdfa = false;
   uint32_t* d_gmask = nullptr;
   uint32_t* d_galways = nullptr;
+  unsigned long long* d_kwg = nullptr;   // [n_kw * GW] groups each keyword bit gates
+  unsigned long long* d_galw = nullptr;  // [GW] always-gated groups (d_galways as bits)
   uint32_t* d_gevents = nullptr;
   uint32_t* d_gback = nullptr;
   unsigned long long* d_gofbit = nullptr;
@@ -1541,6 +1758,10 @@ struct LaneState {
   size_t chunk_cap = 0;
   uint32_t* ev_bits = nullptr;
   size_t ev_cap = 0;
+  uint2* xlist = nullptr;  // K1X hit records
+  size_t xlist_cap = 0;
+  uint32_t* xcount = nullptr;  // K1X records per block
+  size_t xcount_cap = 0;
   uint32_t* evlist = nullptr;
   size_t evlist_cap = 0;
   uint32_t* kw = nullptr;
@@ -1574,7 +1795,7 @@ struct LaneState {
     if (!d) return;
     (void)hipSetDevice(d->device);
     if (st) (void)hipStreamSynchronize(st);
-    void* bufs[] = {data_alloc, off, chunk_file, ev_bits, evlist, kw, ggate, ovf, paths, poff, pathok,
+    void* bufs[] = {data_alloc, off, chunk_file, ev_bits, xlist, xcount, evlist, kw, ggate, ovf, paths, poff, pathok,
                     items, entries, dentries, cand, counts, gcount, cursor, base, kind, gskip};
     for (void* b : bufs) (void)hipFree(b);
     if (st) (void)hipStreamDestroy(st);
@@ -1703,6 +1924,12 @@ static int adapt_k1(DeviceRules* r, LaneState* l, uint64_t total, uint32_t nfile
     }
   }
   HIP_TRY(hipMemcpy(r->d_galways, galways.data(), sizeof(uint32_t) * G, hipMemcpyHostToDevice));
+  {
+    std::vector<unsigned long long> galw(r->GW, 0);
+    for (uint32_t g = 0; g < G; g++)
+      if (galways[g]) galw[g / 64] |= 1ull << (g % 64);
+    HIP_TRY(hipMemcpy(r->d_galw, galw.data(), sizeof(unsigned long long) * galw.size(), hipMemcpyHostToDevice));
+  }
   HIP_TRY(hipMemcpy(r->d_gevents, gevents.data(), sizeof(uint32_t) * G, hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(r->d_gofbit, gofbit.data(), sizeof(unsigned long long) * gofbit.size(), hipMemcpyHostToDevice));
   r->kw_unknown = kw_unknown;
@@ -1724,6 +1951,11 @@ int device_rules_create(int device, const Plan& p, uint32_t chunk, uint32_t ext_
   if (p.warm > kPad) return fail(TSG_ERR_CONFIG, "a keyword is longer than the K1 warm-up window");
   int rc;
   if ((rc = make_device_k1(p, &r->k1, &r->tables, &r->k1h))) return rc;
+  if ((rc = make_device_k1x(p, &r->k1x, &r->tables))) return rc;
+  r->has_k1x = !p.x_lits.empty();
+  if (r->has_k1x)  // the 128 KiB prefix bitmap is dynamic LDS
+    HIP_TRY(hipFuncSetAttribute((const void*)k1x_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (1 << kXBits) / 8 + 16));
   HIP_TRY(hipMalloc((void**)&r->d_hits, sizeof(uint32_t) * r->k1.ns));
   if (const DFA* pd = p.allow_path_dfa.get()) {
     const uint32_t* t = nullptr;
@@ -1777,6 +2009,20 @@ int device_rules_create(int device, const Plan& p, uint32_t chunk, uint32_t ext_
   r->d_gback = (uint32_t*)cg;
   const unsigned long long* cb = nullptr;
   if ((rc = upload_vec(gofbit, &cb, &r->tables))) return rc;
+  {  // the gate kernel's tables: keyword -> groups, always-gated groups as bits
+    const uint32_t nkw = (uint32_t)p.kw_words * 32;
+    std::vector<unsigned long long> kwg((size_t)nkw * r->GW, 0), galw(r->GW, 0);
+    for (uint32_t g = 0; g < G; g++) {
+      for (uint32_t k = 0; k < nkw; k++)
+        if ((gmask[(size_t)g * p.kw_words + k / 32] >> (k % 32)) & 1) kwg[(size_t)k * r->GW + g / 64] |= 1ull << (g % 64);
+      if (galways[g]) galw[g / 64] |= 1ull << (g % 64);
+    }
+    const unsigned long long* c64 = nullptr;
+    if ((rc = upload_vec(kwg, &c64, &r->tables))) return rc;
+    r->d_kwg = (unsigned long long*)c64;
+    if ((rc = upload_vec(galw, &c64, &r->tables))) return rc;
+    r->d_galw = (unsigned long long*)c64;
+  }
   r->h_galways = galways;
   r->h_gevents = gevents;
   r->h_gofbit = gofbit;
@@ -1874,6 +2120,9 @@ int enqueue_scan(DeviceRules* r, LaneState* l, const ScanInput& in, HostOut* out
   const uint64_t nchunks_pad = (nchunks + k1_item_chunks - 1) / k1_item_chunks * k1_item_chunks + 1;
   if ((rc = ensure(&l->chunk_file, &l->chunk_cap, (size_t)nchunks_pad))) return rc;
   if ((rc = ensure(&l->ev_bits, &l->ev_cap, (size_t)nchunks_pad))) return rc;
+  // K1X hit records: one per 256 bytes (a lane-word with a hit past that verifies inline)
+  if (r->has_k1x && (rc = ensure(&l->xlist, &l->xlist_cap, (size_t)(total / 256 + 65536)))) return rc;
+  if (r->has_k1x && (rc = ensure(&l->xcount, &l->xcount_cap, (size_t)std::max(r->cus, 1)))) return rc;
   if ((rc = ensure(&l->evlist, &l->evlist_cap, (size_t)nchunks_pad))) return rc;
   if ((rc = ensure(&l->kw, &l->kw_cap, (size_t)F * W + 1))) return rc;
   if ((rc = ensure(&l->ggate, &l->ggate_cap, (size_t)F * r->GW + 1))) return rc;
@@ -1940,6 +2189,16 @@ int enqueue_scan(DeviceRules* r, LaneState* l, const ScanInput& in, HostOut* out
              (uint32_t)kK1Seg};
     if ((rc = launch_k1(r, A, st))) return rc;
   }
+  if (r->has_k1x && total) {  // the hashed literals of a large rule set, after K1's stores
+    const int xg = (int)std::max<uint64_t>(1, std::min<uint64_t>((total / 16 + kK1XBlock - 1) / kK1XBlock,
+                                                                   (uint64_t)r->cus));
+    K1XArgs X{data, l->off, l->chunk_file, total, C, F, l->kw, l->ev_bits, l->xlist, l->xcount,
+              (uint32_t)std::min<size_t>(l->xlist_cap, 0xFFFFFFFFu)};
+    k1x_kernel<<<xg, kK1XBlock, (1u << kXBits) / 8 + 16, st>>>(r->k1x, X);
+    HIP_TRY(hipGetLastError());
+    k1x_verify_kernel<<<r->grid, kBlock, 0, st>>>(r->k1x, X, (uint32_t)xg);
+    HIP_TRY(hipGetLastError());
+  }
   HIP_TRY(hipEventRecord(out->ev[3], st));
 
   // ---- gates, items, device-side layout
@@ -1970,7 +2229,7 @@ int enqueue_scan(DeviceRules* r, LaneState* l, const ScanInput& in, HostOut* out
     HIP_TRY(hipGetLastError());
   }
   if (work) {
-    ggate_kernel<<<(F + 255) / 256, 256, 0, st>>>(l->kw, F, W, r->d_gmask, r->d_galways, G, r->GW, l->ggate);
+    ggate_kernel<<<(F + 255) / 256, 256, 0, st>>>(l->kw, F, W, r->d_kwg, r->d_galw, r->GW, l->ggate);
     HIP_TRY(hipGetLastError());
     const uint32_t cgrid = (uint32_t)std::min<uint64_t>((nchunks + kBlock - 1) / kBlock, (uint64_t)r->grid);
     ev_compact_kernel<<<cgrid, kBlock, 0, st>>>(l->ev_bits, nchunks, l->evlist, l->counts + 1);

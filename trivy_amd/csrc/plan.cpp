@@ -11,11 +11,18 @@
 #include <cstdlib>
 #include <atomic>
 #include <map>
+#include <unordered_map>
 #include <set>
 #include <thread>
 #include <x86intrin.h>
 
 namespace tsg {
+
+static std::string ascii_lower(std::string s) {
+  for (char& c : s)
+    if (c >= 'A' && c <= 'Z') c = (char)(c + 32);
+  return s;
+}
 
 static bool is_ascii(const std::string& s) {
   for (unsigned char c : s)
@@ -287,7 +294,9 @@ std::unique_ptr<Plan> build_plan(const Ruleset& rs, const PlanOptions& opt, std:
       }
       for (uint32_t k : p->rule_kws[r]) g.kwmask[k / 32] |= 1u << (k % 32);
     }
-    for (int k = p->fb_kw0; k < p->n_kw; k++) g.kwmask[k / 32] |= 1u << (k % 32);
+    // (the folding-rune pseudo keywords gate nothing here: a file holding one is always
+    // resolved on the host, which scans its uncertain-keyword rules whole and adds windows
+    // before the runes that (?i) folds, whatever K2 found)
   };
   for (uint32_t kind : {kEvRunU, kEvRunD, 1u << kEvLit0, kEvAlways}) {
     std::vector<uint32_t> cur;
@@ -351,10 +360,16 @@ std::unique_ptr<Plan> build_plan(const Ruleset& rs, const PlanOptions& opt, std:
   for (size_t g = 0; g < p->groups.size(); g++) litg[g] = p->groups[g].events == (1u << kEvLit0);
   // keywords left out of K1 (table budget): a literal no ASCII text contains holds their id
   std::vector<char> kw_dropped(kws.size(), 0);
+  // hashed mode (K1X): keywords and anchors of >= 4 bytes leave the automaton
+  std::vector<char> kw_hashed(kws.size(), 0);
+  bool anchors_hashed = false;
   auto build_k1 = [&](bool with_anchors) -> bool {
     std::vector<std::string> lits = kws;
     for (size_t k = 0; k < lits.size(); k++)
-      if (kw_dropped[k]) lits[k] = "\xff\xff";
+      if (kw_dropped[k] || kw_hashed[k]) lits[k] = "\xff\xff";
+    std::map<std::string, std::pair<int32_t, uint32_t>> xl;  // K1X literal -> keyword id, events
+    for (size_t k = 0; k < kws.size(); k++)
+      if (kw_hashed[k]) xl[ascii_lower(kws[k])] = {(int32_t)k, 0u};
     std::vector<uint32_t> lit_event(lits.size(), 0);
     std::map<std::string, uint32_t> lid;
     for (size_t i = 0; i < lits.size(); i++) lid.emplace(lits[i], (uint32_t)i);
@@ -372,6 +387,12 @@ std::unique_ptr<Plan> build_plan(const Ruleset& rs, const PlanOptions& opt, std:
       for (uint32_t r : g.rules) {
         p->rule_event[r] = bit;
         const std::string& s = anchor[r].lit;
+        if (anchors_hashed && s.size() >= 4) {
+          auto xi = xl.find(ascii_lower(s));
+          if (xi == xl.end()) xl[ascii_lower(s)] = {-1, bit};
+          else xi->second.second |= bit;
+          continue;
+        }
         auto it = lid.find(s);
         uint32_t id;
         if (it == lid.end()) {
@@ -403,6 +424,14 @@ std::unique_ptr<Plan> build_plan(const Ruleset& rs, const PlanOptions& opt, std:
     int w = (int)std::max<size_t>(longest, (size_t)std::max(p->run_k[0], p->run_k[1]));
     p->warm = (w - 1 + 15) / 16 * 16;
     p->kw_dfa = std::move(d);
+    p->x_lits.clear();
+    p->x_kw.clear();
+    p->x_event.clear();
+    for (const auto& kv : xl) {
+      p->x_lits.push_back(kv.first);
+      p->x_kw.push_back(kv.second.first);
+      p->x_event.push_back(kv.second.second);
+    }
     return true;
   };
   // table bytes of an automaton over the keywords (and anchors): its states are the
@@ -415,10 +444,10 @@ std::unique_ptr<Plan> build_plan(const Ruleset& rs, const PlanOptions& opt, std:
       for (unsigned char ch : s) bytes[ch] = true;
     };
     for (size_t k = 0; k < kws.size(); k++)
-      if (!kw_dropped[k]) add(kws[k]);
+      if (!kw_dropped[k] && !kw_hashed[k]) add(kws[k]);
     if (with_anchors)
       for (size_t r = 0; r < R; r++)
-        if (!anchor[r].lit.empty()) add(anchor[r].lit);
+        if (!anchor[r].lit.empty() && !(anchors_hashed && anchor[r].lit.size() >= 4)) add(anchor[r].lit);
     size_t ncls = 1;
     for (int c = 0; c < 256; c++) ncls += bytes[c];
     return (pre.size() + 1) * ncls * 2;
@@ -427,7 +456,20 @@ std::unique_ptr<Plan> build_plan(const Ruleset& rs, const PlanOptions& opt, std:
   auto try_k1 = [&](bool with_anchors) {
     return k1_estimate(with_anchors) <= 4 * (size_t)opt.max_kw_table_bytes && build_k1(with_anchors);
   };
-  if (!(opt.anchors && try_k1(true)) && !try_k1(false)) {
+  bool k1_ok = (opt.anchors && try_k1(true)) || try_k1(false);
+  if (!k1_ok && !getenv("TSG_NO_K1X")) {
+    // Too many literal bytes for an LDS-resident automaton (large user rule sets): the
+    // keywords and anchors of >= 4 bytes go to the hashed prefilter (K1X), the short
+    // ones stay in the automaton.  Keyword bits stay exact, anchors keep their events.
+    for (int k = 0; k < p->fb_kw0; k++) kw_hashed[k] = kws[k].size() >= 4;
+    anchors_hashed = true;
+    k1_ok = (opt.anchors && try_k1(true)) || try_k1(false);
+    if (!k1_ok) {
+      std::fill(kw_hashed.begin(), kw_hashed.end(), 0);
+      anchors_hashed = false;
+    }
+  }
+  if (!k1_ok) {
     // Too many keyword bytes for an LDS-resident automaton (large user rule sets): leave
     // keywords out, longest first (they cost the most states), until it fits.  Their rules
     // get the exact keyword gate on the host, and their groups are scanned on every file.
@@ -993,6 +1035,37 @@ void k1_reference(const Plan& plan, const BatchView& bv, uint32_t chunk, std::ve
     if ((int)cu >= plan.run_k[0]) e |= kEvRunU;
     if ((int)cd >= plan.run_k[1]) e |= kEvRunD;
     (*ev)[p / chunk] |= e;
+  }
+  k1x_reference(plan, bv, chunk, kw, ev);
+}
+
+// K1X semantics (the hashed literals of large rule sets): every occurrence of a literal in
+// the ASCII-lowercased stream ending at byte q sets its event bits on chunk q / chunk, and
+// its keyword bit for the file holding q when the whole literal lies inside that file.
+void k1x_reference(const Plan& plan, const BatchView& bv, uint32_t chunk, std::vector<uint32_t>* kw,
+                   std::vector<uint32_t>* ev) {
+  if (plan.x_lits.empty()) return;
+  const uint64_t total = bv.offsets[bv.nfiles];
+  std::unordered_map<uint32_t, std::vector<uint32_t>> by4;
+  for (size_t i = 0; i < plan.x_lits.size(); i++) by4[x_prefix4((const uint8_t*)plan.x_lits[i].data())].push_back((uint32_t)i);
+  auto low = [](uint8_t c) -> uint8_t { return (c >= 'A' && c <= 'Z') ? (uint8_t)(c + 32) : c; };
+  for (uint64_t p = 0; p + 4 <= total; p++) {
+    const uint8_t b4[4] = {low(bv.data[p]), low(bv.data[p + 1]), low(bv.data[p + 2]), low(bv.data[p + 3])};
+    auto it = by4.find(x_prefix4(b4));
+    if (it == by4.end()) continue;
+    for (uint32_t i : it->second) {
+      const std::string& L = plan.x_lits[i];
+      if (p + L.size() > total) continue;
+      size_t t = 4;
+      while (t < L.size() && low(bv.data[p + t]) == (uint8_t)L[t]) t++;
+      if (t < L.size()) continue;
+      const uint64_t q = p + L.size() - 1;
+      (*ev)[q / chunk] |= plan.x_event[i];
+      if (plan.x_kw[i] >= 0) {
+        const uint32_t f = (uint32_t)(std::upper_bound(bv.offsets, bv.offsets + bv.nfiles + 1, q) - bv.offsets) - 1;
+        if (p >= bv.offsets[f]) (*kw)[(size_t)f * plan.kw_words + plan.x_kw[i] / 32] |= 1u << (plan.x_kw[i] % 32);
+      }
+    }
   }
 }
 

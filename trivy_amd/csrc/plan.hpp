@@ -52,6 +52,13 @@ struct Plan {
   std::vector<uint32_t> kw_mask_events;
   std::vector<uint32_t> lit_event;     // [n_lit] event bits of each literal
   std::vector<uint16_t> kw_len;        // [n_kw] byte length of each keyword literal
+  // K1X: literals of >= 4 bytes that K1's LDS-resident automaton has no room for (large
+  // user rule sets) -- keywords, and anchor literals with their event bits -- found by a
+  // hashed 4-gram prefilter and exact verification (k1x_kernel).  Same semantics as
+  // K1's: ASCII case folded, one stream, a keyword counts only inside one file.
+  std::vector<std::string> x_lits;     // ASCII-lowercased literal bytes
+  std::vector<int32_t> x_kw;           // keyword id, or -1 (anchor only)
+  std::vector<uint32_t> x_event;       // event bits (0: keyword only)
   // run classes for kEvRunU / kEvRunD: byte -> membership bit 0 (U) / 1 (D)
   uint8_t run_cls[256] = {0};
   int run_k[2] = {32, 12};
@@ -162,6 +169,17 @@ void emulate_kernels(const Plan& plan, const BatchView& b, uint32_t chunk, uint3
 // lies inside f (its length is checked against the bytes of f before its last byte).
 void k1_reference(const Plan& plan, const BatchView& b, uint32_t chunk,
                   std::vector<uint32_t>* kw, std::vector<uint32_t>* ev);
+// The K1X part of k1_reference (Plan::x_lits), ORed into kw / ev.
+void k1x_reference(const Plan& plan, const BatchView& b, uint32_t chunk,
+                   std::vector<uint32_t>* kw, std::vector<uint32_t>* ev);
+
+// K1X: the 4-byte little-endian prefix word of a (lowercased) literal or window
+inline uint32_t x_prefix4(const uint8_t* b) {
+  return (uint32_t)b[0] | (uint32_t)b[1] << 8 | (uint32_t)b[2] << 16 | (uint32_t)b[3] << 24;
+}
+// K1X prefilter hash: bit of the 2^kXBits-bit LDS bitmap
+constexpr int kXBits = 20;
+inline uint32_t x_hash(uint32_t w) { return (w * 2654435761u) >> (32 - kXBits); }
 
 // Chunks of file f that K2 scans for group g (given the K1 output): chunk c of the file
 // is an item iff the group is gated for f and a chunk in [c, c + back] (inside f)
