@@ -48,8 +48,10 @@ struct Anchor {
 
 // The event every match of a rule must contain, preferring long class runs (the secret
 // part of nearly every rule) over literals: the keyword gate already handles rare
-// literals, and common ones ("key", "sk", "-----") would put events everywhere.
-Anchor choose_anchor(const Regexp& re, const Plan& p) {
+// literals, and common ones ("key", "sk", "-----") would put events everywhere.  A rule
+// without keywords (every file gated) takes a long literal first when it has one (score
+// >= 6, e.g. a 5-byte name): token runs are common, its literal is not.
+Anchor choose_anchor(const Regexp& re, const Plan& p, bool literal_first) {
   const std::vector<AtomInfo> at = re.Atoms();
   const int n = (int)at.size();
   std::vector<int64_t> B(n + 1, 0);
@@ -71,6 +73,37 @@ Anchor choose_anchor(const Regexp& re, const Plan& p) {
              std::to_string(t) + (a.first_atom ? " (suffix)" : "");
     return a;
   };
+  double best_score = 0;
+  auto best_literal = [&]() {
+    for (int i = 0; i < n;) {
+      if (at[i].lit < 0) {
+        i++;
+        continue;
+      }
+      int j = i;
+      std::string s;
+      double score = 0;
+      while (j < n && at[j].lit >= 0) {
+        int c = at[j].lit;
+        if (s.size() < 24) {
+          s.push_back((char)c);
+          score += (c >= 'a' && c <= 'z') ? 1.0 : (c >= '0' && c <= '9') ? 1.3 : 1.6;
+        }
+        j++;
+      }
+      if (score >= 3.0 && score > best_score) {
+        best_score = score;
+        best = take(1u << kEvLit0, i, (int64_t)s.size(), s, "literal");
+      }
+      i = j;
+    }
+  };
+  if (literal_first) {
+    best_literal();
+    if (best_score >= 6.0) return best;
+    best = Anchor();
+    best_score = 0;
+  }
   for (int bit = 0; bit < 2; bit++) {
     const int k = p.run_k[bit];
     for (int i = 0; i < n;) {
@@ -85,29 +118,7 @@ Anchor choose_anchor(const Regexp& re, const Plan& p) {
       i = j;
     }
   }
-  double best_score = 0;
-  for (int i = 0; i < n;) {
-    if (at[i].lit < 0) {
-      i++;
-      continue;
-    }
-    int j = i;
-    std::string s;
-    double score = 0;
-    while (j < n && at[j].lit >= 0) {
-      int c = at[j].lit;
-      if (s.size() < 24) {
-        s.push_back((char)c);
-        score += (c >= 'a' && c <= 'z') ? 1.0 : (c >= '0' && c <= '9') ? 1.3 : 1.6;
-      }
-      j++;
-    }
-    if (score >= 3.0 && score > best_score) {
-      best_score = score;
-      best = take(1u << kEvLit0, i, (int64_t)s.size(), s, "literal");
-    }
-    i = j;
-  }
+  best_literal();
   return best;
 }
 
@@ -229,7 +240,7 @@ std::unique_ptr<Plan> build_plan(const Ruleset& rs, const PlanOptions& opt, std:
     const RuleC& rule = rs.rules[r];
     if (!rule.regex) return;
     p->rule_maxlen[r] = max_match_len(rule.regex->prog());
-    if (opt.anchors) anchor[r] = choose_anchor(*rule.regex, *p);
+    if (opt.anchors) anchor[r] = choose_anchor(*rule.regex, *p, rule.kw_lower.empty());
     const int fa = anchor[r].first_atom;
     // exact program first, then ever stronger relaxations of counted repetitions, then
     // ever shorter prefixes of the top-level concatenation

@@ -71,6 +71,64 @@ bool contains_fold_ascii(const uint8_t* s, size_t n, const std::string& kw) {
   return false;
 }
 
+// bytes.Contains(bytes.ToLower(s), kw) for an ASCII lowercase keyword kw, for any s.
+// bytes.ToLower maps exactly two non-ASCII runes to ASCII: U+0130 (C4 B0) -> 'i' and
+// U+212A (E2 84 AA) -> 'k'; every other rune, and every invalid byte (U+FFFD), lowers to
+// non-ASCII bytes.  Neither C4 nor E2 is a UTF-8 continuation byte, so those byte
+// sequences always decode as the runes.  A keyword then occurs in the lowered text iff
+// its letters occur contiguously in s, each as itself, its upper case, or for 'i' / 'k'
+// as the rune's bytes -- without lowering (and copying) the file.
+bool contains_fold_runes(const uint8_t* s, size_t n, const std::string& kw) {
+  const size_t m = kw.size();
+  if (m == 0) return true;
+  auto at = [&](size_t i, size_t j, size_t* w) -> bool {  // kw[j] at s[i..]: width in *w
+    const uint8_t c = (uint8_t)kw[j];
+    if (i >= n) return false;
+    uint8_t x = s[i];
+    if (x >= 'A' && x <= 'Z') x |= 0x20;
+    if (x == c) {
+      *w = 1;
+      return true;
+    }
+    if (c == 'i' && s[i] == 0xC4 && i + 1 < n && s[i + 1] == 0xB0) {
+      *w = 2;
+      return true;
+    }
+    if (c == 'k' && s[i] == 0xE2 && i + 2 < n && s[i + 1] == 0x84 && s[i + 2] == 0xAA) {
+      *w = 3;
+      return true;
+    }
+    return false;
+  };
+  const uint8_t c0 = (uint8_t)kw[0];
+  const uint8_t u0 = (c0 >= 'a' && c0 <= 'z') ? (uint8_t)(c0 - 32) : c0;
+  const uint8_t r0 = c0 == 'i' ? 0xC4 : c0 == 'k' ? 0xE2 : c0;  // the rune's lead byte
+  const __m128i v0 = _mm_set1_epi8((char)c0), v1 = _mm_set1_epi8((char)u0), v2 = _mm_set1_epi8((char)r0);
+  auto try_at = [&](size_t i) {
+    size_t p = i;
+    for (size_t j = 0; j < m; j++) {
+      size_t w;
+      if (!at(p, j, &w)) return false;
+      p += w;
+    }
+    return true;
+  };
+  size_t i = 0;
+  for (; i + 16 <= n; i += 16) {
+    const __m128i b = _mm_loadu_si128((const __m128i*)(s + i));
+    uint32_t bits = (uint32_t)_mm_movemask_epi8(
+        _mm_or_si128(_mm_or_si128(_mm_cmpeq_epi8(b, v0), _mm_cmpeq_epi8(b, v1)), _mm_cmpeq_epi8(b, v2)));
+    while (bits) {
+      const size_t k = i + (size_t)__builtin_ctz(bits);
+      bits &= bits - 1;
+      if (try_at(k)) return true;
+    }
+  }
+  for (; i < n; i++)
+    if ((s[i] == c0 || s[i] == u0 || s[i] == r0) && try_at(i)) return true;
+  return false;
+}
+
 // ------------------------------------------------------------------ Go sort.Slice
 // pdqsort_func from Go 1.19 sort/zsortfunc.go, restated over a vector with `less`.
 namespace gosort {
@@ -568,13 +626,14 @@ void scan_file(const Ruleset& rs, const std::string& path, const uint8_t* conten
     if (r.path && !r.path->Match((const uint8_t*)path.data(), path.size())) continue;
     if (allow_path(r.allow, path)) continue;
     ph.lap(1);
-    if (gate && gate->kw_state[ri] == 2 && gate->ascii_fold_exact && r.kw_ascii) {
+    if (gate && gate->kw_state[ri] == 2 && r.kw_ascii) {
       // exact keyword gate without lowering the file (per-keyword results cached)
       bool hit = r.kw_lower.empty();
       for (size_t k = 0; k < r.kw_lower.size() && !hit; k++) {
         const std::string& kw = r.kw_lower[k];
         int8_t& c = kwcache[kw];
-        if (c == 0) c = contains_fold_ascii(content, n, kw) ? 1 : -1;
+        if (c == 0)
+          c = (gate->ascii_fold_exact ? contains_fold_ascii(content, n, kw) : contains_fold_runes(content, n, kw)) ? 1 : -1;
         hit = c > 0;
       }
       ph.lap(2);

@@ -98,6 +98,8 @@ struct FileGate {
 };
 
 bool contains_fold_ascii(const uint8_t* s, size_t n, const std::string& kw);
+// the same for any content: U+0130 / U+212A count as 'i' / 'k' (bytes.ToLower)
+bool contains_fold_runes(const uint8_t* s, size_t n, const std::string& kw);
 
 // Exact Scan of one file (scanner.go:341-416).
 void scan_file(const Ruleset& rs, const std::string& path, const uint8_t* content, size_t n,
