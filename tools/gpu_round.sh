@@ -1,0 +1,19 @@
+#!/bin/bash
+# Round evidence on one MI355X: GPU parity suite, smoke, headline bench + rocprofv3 kernel
+# stats / FETCH_SIZE / SQ passes, configs[3] and configs[4] benches, configs[0] end to end.
+# usage: tools/gpu_round.sh TAG     (every GPU step under its own limit; stops at a failure)
+set -o pipefail
+tag=${1:-r2}
+out=gpurun_out/$tag
+mkdir -p $out
+cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
+echo "== tests" && timeout -k 10 400 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
+  > $out/gpu_tests.log 2>&1 || { tail -20 $out/gpu_tests.log; exit 1; }
+tail -1 $out/gpu_tests.log
+echo "== smoke" && timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke()" > $out/smoke.log 2>&1 || { tail $out/smoke.log; exit 2; }
+cat $out/smoke.log
+tools/gpu_bench_prof.sh $tag || exit 3
+echo "== configs[3]" && timeout -k 10 400 python -u bench.py --rules user1000 --steps 2 --warmup 1 --cpu-mib 16 > $out/bench_user1000.json 2> $out/bench_user1000.err || { tail $out/bench_user1000.err; exit 4; }
+echo "== configs[4]" && timeout -k 10 400 python -u bench.py --rules allow-exclude --steps 2 --warmup 1 --cpu-mib 256 > $out/bench_allow.json 2> $out/bench_allow.err || { tail $out/bench_allow.err; exit 5; }
+echo "== configs[0]" && timeout -k 10 400 python -u tools/fs_bench.py > $out/fs_bench.json 2> $out/fs_bench.err || { tail $out/fs_bench.err; exit 6; }
+echo done

@@ -8,6 +8,9 @@
 //        Outputs per-file keyword bits and per-chunk event bits (plan.hpp kEv*).  The
 //        automaton runs over the batch as one byte stream; each chain first replays `warm`
 //        bytes before its segment, so every literal / run ending inside it is seen.
+//   K1X  (large rule sets only) the literals of >= 4 bytes that do not fit K1's LDS
+//        automaton: a hashed 4-gram prefilter over every byte (LDS bitmap) and an exact
+//        verification of the hit positions; ORs keyword and event bits into K1's output.
 //   gates per file: which K2 groups the keyword bits switch on; per chunk: which of those
 //        groups have an event within `back` chunks after it -> (file, chunk) items,
 //        counted; a one-block layout kernel turns the counts into item regions and K2's
@@ -1052,10 +1055,11 @@ __device__ __forceinline__ void emit_cand(const K2Args& A, uint32_t file, uint32
   if (lane == leader) base = atomicAdd(A.cand_count, (uint32_t)__popcll(m));
   base = __shfl(base, (int)leader);
   const uint32_t idx = base + (uint32_t)__popcll(m & ((1ull << lane) - 1));
-  if (idx < A.cand_cap) {
+  if (idx < A.cand_cap && end <= 0xFFFFFFFFull) {
     A.cand[idx] = DevCand{file, rule, (uint32_t)end};
   } else {
-    A.ovf[file] = 1;
+    A.ovf[file] = 1;  // (also a file of 4 GiB or more: its 32-bit end offsets would wrap)
+    if (idx < A.cand_cap) A.cand[idx] = DevCand{file, rule, 0};
   }
 }
 
