@@ -48,8 +48,15 @@ enum : uint8_t { kGroupNone = 0, kGroupList = 1, kGroupDense = 2, kGroupSkip = 3
       return fail(TSG_ERR_GPU, std::string(#x) + ": " + hipGetErrorString(e_));       \
   } while (0)
 
+// K1 registers: one 64-B block per chain in flight and the byte loop unrolled 8 ways keep a
+// lane at 128 VGPRs, so 4 waves per SIMD hide the dependent LDS chain (2.1 -> 2.5 TB/s
+// against two blocks in flight, 16-way unroll and 206 VGPRs at 2 waves per SIMD;
+// profiles/r02/k1_experiments/occupancy_sweep.txt).  K1_TWOBUF restores the old layout.
 #ifndef K1_UNROLL
-#define K1_UNROLL 16
+#define K1_UNROLL 8
+#endif
+#ifndef K1_TWOBUF
+#define K1_ONEBUF
 #endif
 #ifdef K1_EXP_COAL  // timing experiment only (wrong results): wave-coalesced loads
 #define K1_ADDR(a, i, off) \
@@ -67,10 +74,10 @@ constexpr int kBlock = 256;
 // K1 block and occupancy target: two blocks of K1_BLOCK threads share a CU's LDS (one
 // 80 KiB automaton image each); K1_WAVES waves per SIMD bounds the registers per lane
 #ifndef K1_BLOCK
-#define K1_BLOCK 256
+#define K1_BLOCK 512
 #endif
 #ifndef K1_WAVES
-#define K1_WAVES 2
+#define K1_WAVES 4
 #endif
 constexpr int kK1Block = K1_BLOCK;
 constexpr int kPad = 256;     // zero bytes before and after the batch in HBM (>= K1 warm-up)
@@ -507,6 +514,19 @@ struct K1Lane {
 #pragma unroll
         for (int t = 0; t < 4; t++) r[i][t] = *(const uint4*)(src[t] + ((uint64_t)i * L + j));
     };
+#ifdef K1_ONEBUF  // one 64-B block per chain in registers (fewer VGPRs, more waves)
+    uint4 r0[NS][4];
+    load(r0, 0);
+    for (uint64_t j = 0; j < L; j += 64) {
+      uint4 cur[NS][4];
+#pragma unroll
+      for (int i = 0; i < NS; i++)
+#pragma unroll
+        for (int t = 0; t < 4; t++) cur[i][t] = r0[i][t];
+      load(r0, j + 64);
+      block(j, cur);
+    }
+#else
     uint4 r0[NS][4], r1[NS][4];
     load(r0, 0);
     load(r1, 64);
@@ -516,6 +536,7 @@ struct K1Lane {
       block(j + 64, r1);
       load(r1, j + 192);
     }
+#endif
   }
 };
 
