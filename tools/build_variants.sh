@@ -14,10 +14,9 @@ build() {
 }
 for v in "$@"; do
   case $v in
-    ob4w4) build $v -DK1_ONEBUF -DK1_UNROLL=4 -DK1_BLOCK=512 -DK1_WAVES=4 ;;
-    ob8w4) build $v -DK1_ONEBUF -DK1_UNROLL=8 -DK1_BLOCK=512 -DK1_WAVES=3 ;;
-    db8w3) build $v -DK1_UNROLL=8 -DK1_BLOCK=512 -DK1_WAVES=3 ;;
-    db16b512) build $v -DK1_BLOCK=512 ;;
+    ob4w4) build $v -DK1_UNROLL=4 ;;
+    db8w3) build $v -DK1_TWOBUF -DK1_UNROLL=8 -DK1_BLOCK=512 -DK1_WAVES=3 ;;
+    db16) build $v -DK1_TWOBUF -DK1_UNROLL=16 -DK1_BLOCK=256 -DK1_WAVES=2 ;;
     nolds) build $v -DK1_EXP_NO_CLS -DK1_EXP_NO_TAB ;;
     noruns) build $v -DK1_EXP_NO_RUNS ;;
     nocls) build $v -DK1_EXP_NO_CLS ;;
