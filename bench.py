@@ -237,7 +237,10 @@ def main():
                                      extra_plants=extra, extra_per_mib=2.0 if extra else 0.0,
                                      binary_frac=binary_frac)
     gen_s = time.perf_counter() - t0
-    dev = local if world > 1 else 0
+    dev = 0
+    if world > 1:  # one rank per GPU; more ranks than GPUs share them round-robin (rehearsals)
+        import torch
+        dev = local % max(1, torch.cuda.device_count())
     batch_bytes = args.batch_mib << 20
     nslots = -(-nbytes // batch_bytes) + 2
     ctx = S.GpuContext(sc, dev, chunk_bytes=args.chunk, host_threads=args.host_threads,
