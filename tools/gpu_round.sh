@@ -16,4 +16,5 @@ tools/gpu_bench_prof.sh $tag || exit 3
 echo "== configs[3]" && timeout -k 10 400 python -u bench.py --rules user1000 --steps 2 --warmup 1 --cpu-mib 16 > $out/bench_user1000.json 2> $out/bench_user1000.err || { tail $out/bench_user1000.err; exit 4; }
 echo "== configs[4]" && timeout -k 10 400 python -u bench.py --rules allow-exclude --steps 2 --warmup 1 --cpu-mib 256 > $out/bench_allow.json 2> $out/bench_allow.err || { tail $out/bench_allow.err; exit 5; }
 echo "== configs[0]" && timeout -k 10 400 python -u tools/fs_bench.py > $out/fs_bench.json 2> $out/fs_bench.err || { tail $out/fs_bench.err; exit 6; }
+echo "== configs[2] shape" && timeout -k 10 400 python -u tools/layer_bench.py 2 3 > $out/layer_bench.json 2> $out/layer_bench.err || { tail $out/layer_bench.err; exit 7; }
 echo done

@@ -43,6 +43,17 @@ def main():
         res = an.scanner.ScanBatch(b, ctx=ctx)
         times.append(time.perf_counter() - t)
     nfind = sum(len(r["Findings"] or []) for r in res)
+    # configs[2] over W GPUs: each rank packs only its byte run (tsg_layer_pack_shard);
+    # the slowest rank's pack time, measured here rank by rank
+    shard = {}
+    for world in (2, 4, 8):
+        worst = 0.0
+        for rank in range(world):
+            t = time.perf_counter()
+            W.NativeLayer(an.scanner, tar, rank=rank, world=world)
+            worst = max(worst, time.perf_counter() - t)
+        shard[str(world)] = {"slowest_rank_pack_s": round(worst, 4),
+                             "per_rank_ingest_GBps_of_tar": round(len(tar) / worst / 1e9, 2)}
     pack_s = min(packs)
     scan_s = min(times)
     print(json.dumps({
@@ -52,7 +63,8 @@ def main():
         "ingest_GBps_of_tar": len(tar) / pack_s / 1e9, "ingest_s": pack_s,
         "scan_s_incl_h2d_and_resolve": scan_s, "scan_GBps": scanned / scan_s / 1e9,
         "upload_s": up_s, "gen_s": gen_s,
-        "layer_e2e_GBps_of_tar": len(tar) / (pack_s + scan_s) / 1e9}))
+        "layer_e2e_GBps_of_tar": len(tar) / (pack_s + scan_s) / 1e9,
+        "sharded_pack": shard}))
 
 
 if __name__ == "__main__":
