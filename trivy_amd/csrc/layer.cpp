@@ -551,9 +551,17 @@ extern "C" int tsg_layer_pack_shard(const tsg_ruleset* rs, const uint8_t* tar, u
         L->path_offsets.push_back(L->paths.size());
       }
     L->data.reset(new uint8_t[total ? total : 1]);
-    par([&](size_t i) {
-      if (keep[i] && walked[i].size) std::memcpy(L->data.get() + dst[i], tar + walked[i].dpos, walked[i].size);
-    });
+    // the copies in pieces of at most 4 MiB, so one large file does not serialize the pack
+    constexpr uint64_t kPiece = 4ull << 20;
+    std::vector<std::pair<size_t, uint64_t>> pieces;  // (file, offset in it)
+    for (size_t i = 0; i < n; i++)
+      if (keep[i])
+        for (uint64_t o = 0; o < walked[i].size; o += kPiece) pieces.push_back({i, o});
+    pool_for(pieces.size(), T, [&](size_t k) {
+      const size_t i = pieces[k].first;
+      const uint64_t o = pieces[k].second, len = std::min(kPiece, walked[i].size - o);
+      std::memcpy(L->data.get() + dst[i] + o, tar + walked[i].dpos + o, len);
+    }, 16);
     if (prof)
       fprintf(stderr, "layer: walk %.1f ms, gates %.1f ms, pack %.1f ms (%d threads)\n",
               std::chrono::duration<double, std::milli>(t1 - t0).count(),
