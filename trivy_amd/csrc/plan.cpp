@@ -883,6 +883,30 @@ void resolve_batch(const Ruleset& rs, const Plan& plan, const BatchView& b,
     std::vector<const RuleWindows*> wptr(R, nullptr);
     std::vector<uint8_t> kws(R);
     for (size_t r = 0; r < R; r++) kws[r] = kw_state(r);
+    if (fbbits & 3) {
+      // U+0130 / U+212A present: a keyword K1 did not see (its bit is clear; bits are exact
+      // for ASCII) can only occur through one of those runes, i.e. inside a window of 3 bytes
+      // per keyword letter around a rune.  Check the uncertain rules' keywords there instead
+      // of over the whole file: not found -> the gate fails (0), found -> exact scan (2).
+      std::vector<int64_t> runes;
+      for (int64_t q = 0; q + 1 < n; q++)
+        if ((content[q] == 0xC4 && content[q + 1] == 0xB0) ||
+            (content[q] == 0xE2 && q + 2 < n && content[q + 1] == 0x84 && content[q + 2] == 0xAA))
+          runes.push_back(q);
+      for (size_t r = 0; r < R; r++) {
+        if (kws[r] != 3 || !rs.rules[r].kw_ascii) continue;
+        bool hit = false;
+        for (const auto& kw : rs.rules[r].kw_lower) {
+          const int64_t span = 3 * (int64_t)kw.size();
+          for (size_t i = 0; i < runes.size() && !hit; i++) {
+            const int64_t a = std::max<int64_t>(0, runes[i] - span), e = std::min<int64_t>(n, runes[i] + span);
+            hit = contains_fold_runes(content + a, (size_t)(e - a), kw);
+          }
+          if (hit) break;
+        }
+        kws[r] = hit ? 3 : 0;  // 3 -> whole-file exact resolution below
+      }
+    }
     if (ovf) {
       for (size_t r = 0; r < R; r++) {
         wins[r].whole = true;
