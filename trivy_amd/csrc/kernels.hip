@@ -97,6 +97,7 @@ struct DevDFA {  // K2 rule group
   const uint8_t* cls;         // [256]
   const uint32_t* rules;      // group-local id -> global rule
   uint32_t nc, ns, mw, nmasks, state_acc;
+  uint32_t nrules;            // rules in the group
   uint32_t inv_nc;            // ceil(2^32 / nc): state_of(row) = umulhi(row, inv_nc), exact below 2^16
   uint32_t start[4];          // start rows per previous-byte context
   uint32_t o_cls, o_accs, o_masks, lds_bytes;
@@ -1068,6 +1069,8 @@ struct K2Args {
 // Candidate emission, wave-aggregated: the lanes that reach an accept together reserve
 // their records with ONE atomic (ballot, popcount prefix, broadcast of the base).  A record
 // past the capacity flags its file for whole-file host resolution instead.
+// end == kCandWhole: "resolve this rule over the whole file" (a follow-on tail past
+// ext_cap), which the host reads instead of an end offset (plan.hpp kCandWhole)
 __device__ __forceinline__ void emit_cand(const K2Args& A, uint32_t file, uint32_t rule, uint64_t end) {
   const unsigned long long m = __ballot(1);
   const uint32_t lane = threadIdx.x & 63;
@@ -1076,7 +1079,7 @@ __device__ __forceinline__ void emit_cand(const K2Args& A, uint32_t file, uint32
   if (lane == leader) base = atomicAdd(A.cand_count, (uint32_t)__popcll(m));
   base = __shfl(base, (int)leader);
   const uint32_t idx = base + (uint32_t)__popcll(m & ((1ull << lane) - 1));
-  if (idx < A.cand_cap && end <= 0xFFFFFFFFull) {
+  if (idx < A.cand_cap && (end < kCandWhole || end == (uint64_t)kCandWhole)) {
     A.cand[idx] = DevCand{file, rule, (uint32_t)end};
   } else {
     A.ovf[file] = 1;  // (also a file of 4 GiB or more: its 32-bit end offsets would wrap)
@@ -1149,8 +1152,8 @@ struct Lane {
     uint64_t w = q & ~15ull;
     uint4 cur = *(const uint4*)(data + w);
     while (q < fe && !d.dead[state_of(s)]) {
-      if (q - b >= A.ext_cap) {
-        A.ovf[file] = 1;
+      if (q - b >= A.ext_cap) {  // the group's rules over the whole file, on the host
+        for (uint32_t k = 0; k < d.nrules; k++) emit_cand(A, file, d.rules[k], kCandWhole);
         return;
       }
       const uint4 nxt = *(const uint4*)(data + w + 16);
@@ -1484,6 +1487,7 @@ static uint32_t align16(uint32_t x) { return (x + 15) & ~15u; }
 static int make_device_dfa(const DFA& dd, const std::vector<uint32_t>& rules, DevDFA* out,
                            std::vector<void*>* allocs) {
   if (dd.nstates >= 0x8000) return fail(TSG_ERR_INTERNAL, "DFA too large for u16 tables");
+  out->nrules = (uint32_t)rules.size();
   // rows of at least 2 entries (state_of's reciprocal needs nc >= 2): a one-class DFA gets a
   // duplicate column no byte maps to
   DFA padded;

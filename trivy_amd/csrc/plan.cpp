@@ -951,7 +951,14 @@ void resolve_batch(const Ruleset& rs, const Plan& plan, const BatchView& b,
       RuleWindows& w = wins[r];
       wptr[r] = &w;
       if (!w.whole) {
-        for (uint32_t j = k; j < e; j++) add_end(w, r, cand[j].end);
+        for (uint32_t j = k; j < e && !w.whole; j++) {
+          if (cand[j].end == kCandWhole) {
+            w.whole = true;
+            w.iv.clear();
+          } else {
+            add_end(w, r, cand[j].end);
+          }
+        }
         normalize(w);
       }
       k = e;
@@ -1135,7 +1142,8 @@ void emulate_kernels(const Plan& plan, const BatchView& bv, uint32_t chunk, uint
           for (size_t k = 0; k < g.rules.size(); k++)
             if ((m[k / 64] >> (k % 64)) & 1) ko->cand.push_back({f, g.rules[k], (uint32_t)pos});
         });
-        if (o) ko->overflow[f] = 1;
+        if (o)  // a tail past ext_cap: the group's rules over the whole file (kCandWhole)
+          for (uint32_t r : g.rules) ko->cand.push_back({f, r, kCandWhole});
       }
     }
   }

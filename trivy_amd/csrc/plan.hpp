@@ -96,7 +96,10 @@ struct PlanOptions {
 
 std::unique_ptr<Plan> build_plan(const Ruleset& rs, const PlanOptions& opt, std::string* err);
 
-// One GPU candidate: rule `rule` has a match ending at byte `end` of file `file`.
+// One GPU candidate: rule `rule` has a match ending at byte `end` of file `file`, or, with
+// end == kCandWhole, the rule's K2 thread ran past ext_cap: resolve the rule over the whole
+// file (only that rule: the other rules of the file keep their windows).
+constexpr uint32_t kCandWhole = 0xFFFFFFFFu;
 struct Candidate {
   uint32_t file;
   uint32_t rule;
