@@ -743,8 +743,10 @@ class Compiler {
  public:
   // relax >= 0: GPU superset program -- every counted repetition x{n,m} whose bounds
   // exceed `relax` becomes x{min(n,relax),} (see Regexp::RelaxedProg)
-  Compiler(const std::vector<Node>& nodes, Prog* p, int relax = -1)
-      : n_(nodes), p_(p), relax_(relax) {
+  // fold_high: U+017F / U+212A count as non-ASCII members too (a superset that also
+  // accepts the runes (?i) folds into s / k; the host's folding-rune path)
+  Compiler(const std::vector<Node>& nodes, Prog* p, int relax = -1, bool fold_high = false)
+      : n_(nodes), p_(p), relax_(relax), fold_high_(fold_high) {
     p_->inst.push_back(Inst{Op::Fail, 0, 0});
   }
 
@@ -820,6 +822,7 @@ class Compiler {
   const std::vector<Node>& n_;
   Prog* p_;
   int relax_;
+  bool fold_high_;
 
   uint32_t inst(Op op) {
     p_->inst.push_back(Inst{op, 0, 0});
@@ -878,7 +881,7 @@ class Compiler {
         // U+017F / U+212A only enter a set through (?i) folding of s / k; files that
         // contain them are resolved whole on the host (K1 fallback keywords), so the
         // GPU program may ignore them
-        if (lo != 0x17F && lo != 0x212A) {
+        if (fold_high_ || (lo != 0x17F && lo != 0x212A)) {
           other_high = true;
           break;
         }
@@ -1084,10 +1087,10 @@ int Regexp::NumAtoms() const {
   return (int)atoms.size();
 }
 
-Prog Regexp::RelaxedProg(int k, int natoms, int first_atom) const {
+Prog Regexp::RelaxedProg(int k, int natoms, int first_atom, bool fold_high) const {
   Prog p;
   p.nslots = 2 * (ast_->ncap + 1);
-  Compiler c(ast_->nodes, &p, k);
+  Compiler c(ast_->nodes, &p, k, fold_high);
   if (natoms < 0 && first_atom <= 0) {
     c.finish(ast_->root);
   } else {

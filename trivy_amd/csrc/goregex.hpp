@@ -99,7 +99,7 @@ class Regexp {
   // Non-ASCII members of rune sets become "one or more bytes >= 0x80" (kHighByteRune).
   // first_atom > 0 drops that many leading elements instead (a suffix program: every
   // match of the regex ends where a match of the suffix ends).
-  Prog RelaxedProg(int k, int natoms = -1, int first_atom = 0) const;
+  Prog RelaxedProg(int k, int natoms = -1, int first_atom = 0, bool fold_high = false) const;
   int NumAtoms() const;
   std::vector<AtomInfo> Atoms() const;
 

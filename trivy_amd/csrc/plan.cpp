@@ -514,6 +514,23 @@ std::unique_ptr<Plan> build_plan(const Ruleset& rs, const PlanOptions& opt, std:
 
   if (tprof) fprintf(stderr, "plan: K1 %.1f ms\n", tms(tp));
   tp = tnow();
+  // ---- host resolver: fold-rune DFAs of the unbounded relaxed rules
+  p->rule_fold_dfa.resize(R);
+  pool_for(R, plan_threads, [&](size_t r) {
+    const RuleC& rule = rs.rules[r];
+    if (!rule.regex || p->rule_relax[r] < 0 || p->rule_maxlen[r] >= 0 || p->rule_group[r] < 0) return;
+    DFAOptions o;
+    o.max_states = 4096;
+    for (int k : {p->rule_relax[r], 8, 2, 0}) {
+      Prog pr = rule.regex->RelaxedProg(k, -1, 0, true);
+      std::string e;
+      auto d = build_dfa({&pr}, o, &e);
+      if (d) {
+        p->rule_fold_dfa[r] = std::move(d);
+        break;
+      }
+    }
+  }, 1);
   // ---- host resolver: reverse DFAs of the exact programs
   p->rule_rev.resize(R);
   // (only where the forward bound is loose: unbounded or long windows; the subset
@@ -981,6 +998,13 @@ void resolve_batch(const Ruleset& rs, const Plan& plan, const BatchView& b,
         const int64_t ml = plan.rule_maxlen[r];
         if (ml >= 0) {
           for (int64_t q : fold) w.iv.push_back({align_rune(content, n, std::max<int64_t>(0, q - ml)), q});
+        } else if (const DFA* fd = plan.rule_fold_dfa[r].get()) {
+          // relaxed rule: its fold-rune DFA (a superset that accepts the runes) gives the
+          // candidate ends over the file
+          w.iv.clear();
+          run_segment(*fd, content, 0, (uint64_t)n, 0, (uint64_t)n, ~0u, [&](uint32_t mi, uint64_t pos) {
+            if (fd->masks[mi][0] & 1) add_end(w, (uint32_t)r, (int64_t)pos);
+          });
         } else if (plan.rule_group[r] >= 0 && plan.rule_relax[r] < 0) {
           // only an unrelaxed GPU program keeps U+017F / U+212A in its (?i) sets (relaxed
           // ones drop them, goregex.cpp Compiler::rune): a relaxed rule is resolved whole

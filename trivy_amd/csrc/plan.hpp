@@ -83,6 +83,11 @@ struct Plan {
   std::vector<Prog> rule_prog;       // the program the rule's GPU DFA was built from
   // reverse DFA of the exact program (null: state cap): bounds and filters the windows
   std::vector<std::unique_ptr<DFA>> rule_rev;
+  // unbounded rules with a relaxed GPU program: a relaxed forward DFA that also accepts
+  // U+017F / U+212A where (?i) folds s / k (null: state cap or not needed).  Run on the
+  // host over a file holding those runes, it gives candidate ends instead of a whole-file
+  // FindAll.
+  std::vector<std::unique_ptr<DFA>> rule_fold_dfa;
   std::unique_ptr<DFA> allow_path_dfa;  // Global.AllowPath on ASCII paths
 };
 
