@@ -155,6 +155,9 @@ struct BatchView {
   const uint64_t* path_offsets;  // [nfiles + 1]
 };
 
+// Start offsets of the folding runes in s: which = 1 U+0130, 2 U+212A, 4 U+017F (ORed).
+void fold_rune_positions(const uint8_t* s, int64_t n, uint32_t which, std::vector<int64_t>* out);
+
 // Host resolution: exact findings for every file of the batch.
 void resolve_batch(const Ruleset& rs, const Plan& plan, const BatchView& b,
                    const KernelOutputView& ko, int nthreads, BatchResult* out);
