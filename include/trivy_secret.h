@@ -330,6 +330,35 @@ int tsg_layer_pack_shard(const tsg_ruleset* rs, const uint8_t* tar, uint64_t tar
                          const char* const* skip_dirs, uint32_t n_skip_dirs, const char* config_path,
                          uint32_t rank, uint32_t world, tsg_layer** out);
 int tsg_layer_get(const tsg_layer* layer, tsg_layer_view* out);
+/* The header index itself split over the ranks (configs[2] at N GPUs; replaces the whole-chain
+ * walk of tar.go:33-84 that tsg_layer_pack_shard repeats on every rank).  Rank r owns the
+ * entries whose header group starts in its 512-aligned byte range [lo, hi) of the tar.
+ *   1. tsg_layer_range_walk: speculative walk of the range from its first block that
+ *      checksums as a ustar header; info = {lo, hi, start, end} (start/end ~0: no header /
+ *      malformed on the speculative chain).
+ *   2. The ranks exchange info and fix the true chain in rank order: pos(0) = 0,
+ *      pos(r+1) = the true end of range r, which is info.end when info.start == pos(r) (a
+ *      walk from a group position is deterministic); otherwise rank r calls
+ *      tsg_layer_range_sync(pos(r)) and publishes its end (trivy_amd/shard.py:layer_chain).
+ *      Every rank calls tsg_layer_range_sync with its pos before steps 3-4.
+ *   3. tsg_layer_range_dirs: the dirs this range adds to the walker's skipDirs (tar.go:62-66),
+ *      NUL-terminated, in walk order; they are handed to the later ranks.
+ *   4. tsg_layer_range_pack: tar.go:45-84 over the range's entries with the earlier ranks'
+ *      skip dirs first, then Required / IsBinary and the pack.  opq / wh are the range's own.
+ * The union over ranks equals tsg_layer_pack's batch; an archive error on the true chain is
+ * returned by the sync of the range holding it, as one sequential walk would report it. */
+typedef struct tsg_layer_range tsg_layer_range;
+int tsg_layer_range_walk(const uint8_t* tar, uint64_t tar_len, uint32_t rank, uint32_t world,
+                         tsg_layer_range** out, uint64_t info[4]);
+int tsg_layer_range_sync(tsg_layer_range* range, uint64_t pos, uint64_t* end);
+int tsg_layer_range_dirs(tsg_layer_range* range, const char* const* skip_dirs, uint32_t n_skip_dirs,
+                         const char** out, uint64_t* out_len);
+int tsg_layer_range_pack(const tsg_ruleset* rs, const tsg_layer_range* range,
+                         const char* const* skip_files, uint32_t n_skip_files,
+                         const char* const* skip_dirs, uint32_t n_skip_dirs,
+                         const char* const* prior_dirs, uint32_t n_prior_dirs,
+                         const char* config_path, tsg_layer** out);
+void tsg_layer_range_free(tsg_layer_range* range);
 /* Filesystem ingest (configs[0], trivy fs): replaces walker.FS.Walk (pkg/fanal/walker/fs.go:25-63)
  * + the fs artifact's relative paths (pkg/fanal/artifact/local/fs.go:83-100) + Required +
  * IsBinary; files are read in parallel and packed in path order (paths relative to root, no

@@ -311,3 +311,123 @@ def test_native_layer_shards_partition_the_layer(analyzer, world):
     assert max(sizes) < 2 * (sum(sizes) / world) + (1 << 20)
     with pytest.raises(Exception):
         W.NativeLayer(analyzer.scanner, tar, rank=world, world=world)
+
+
+def _union(layers):
+    paths, blobs, walked, opq, wh = [], [], 0, [], []
+    for lay in layers:
+        b = lay.batch
+        walked += lay.walked
+        opq += lay.opq
+        wh += lay.wh
+        for i in range(b.nfiles):
+            paths.append(b.path(i))
+            blobs.append(bytes(b.data[int(b.offsets[i]):int(b.offsets[i + 1])]))
+    return paths, blobs, walked, opq, wh
+
+
+def _nested_tar():
+    inner = layer_bytes(tarfile.USTAR_FORMAT)
+    buf = io.BytesIO()
+    with tarfile.open(fileobj=buf, mode="w", format=tarfile.PAX_FORMAT) as tf:
+        _special(tf, "sys/", tarfile.DIRTYPE)  # a skip dir early: later ranks must apply it
+        for i in range(60):
+            _reg(tf, "d%d/" % i + "x" * (90 + i) + "/f.env",
+                 ("k=%d\nexport GITHUB_TOKEN=%s\n" % (i, GHP)).encode() * (1 + i % 7))
+            if i % 9 == 0:
+                _reg(tf, "nested/layer%d.tar.txt" % i, inner)  # headers inside file data
+            if i % 20 == 10:
+                _reg(tf, "sys/x%d/late.env" % i, b"export GITHUB_TOKEN=%s\n" % GHP.encode())
+                _special(tf, "z%d/.git/" % i, tarfile.DIRTYPE)
+                _reg(tf, "z%d/.git/k.env" % i, b"export GITHUB_TOKEN=%s\n" % GHP.encode())
+                _reg(tf, "w%d/.wh.gone" % i, b"")
+    return buf.getvalue()
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 5, 8, 64])
+@pytest.mark.parametrize("which", ["nested", "seeded", "golden"])
+def test_layer_ranges_partition_the_layer(analyzer, world, which):
+    """The distributed header index (tsg_layer_range_*, configs[2]): each rank walks only its
+    byte range, the ranks fix the true chain and hand their skip dirs on, and the union of
+    the ranges' batches in rank order is tsg_layer_pack's batch file for file, with its
+    whiteouts and opaque dirs -- also when ranges start inside a member's data that holds tar
+    headers (nested tars), which sends a speculative walk off the chain."""
+    tar = {"nested": _nested_tar, "seeded": lambda: configs.layer_tar(2 << 20, seed=23),
+           "golden": layer_bytes}[which]()
+    whole = W.NativeLayer(analyzer.scanner, tar)
+    wb = whole.batch
+    paths, blobs, walked, opq, wh = _union(W.pack_layer_ranges(analyzer.scanner, tar, world))
+    assert paths == [wb.path(i) for i in range(wb.nfiles)]
+    assert blobs == [bytes(wb.data[int(wb.offsets[i]):int(wb.offsets[i + 1])]) for i in range(wb.nfiles)]
+    assert (walked, opq, wh) == (whole.walked, whole.opq, whole.wh)
+
+
+def test_layer_chain_resyncs_a_misspeculated_range(analyzer):
+    """A range whose first plausible header lies inside a member's data (a tar stored in the
+    layer) is not on the chain: layer_chain_step asks that rank to sync, and the rest of the
+    chain follows from its published end."""
+    tar = _nested_tar()
+    world = 16
+    rngs = [W.LayerRange(tar, r, world) for r in range(world)]
+    seq = W.LayerRange(tar, 0, 1)
+    seq.sync(0)
+    infos = [g.info for g in rngs]
+    confirmed, asked = {}, []
+    while True:
+        st = W.layer_chain_step(infos, confirmed)
+        if st[0] == "done":
+            break
+        asked.append(st[1])
+        confirmed[st[1]] = rngs[st[1]].sync(st[2])
+    assert asked  # this layer does send some range off the chain
+    assert st[1][0] == 0 and sorted(st[1]) == st[1]
+
+
+def test_layer_ranges_errors(analyzer):
+    """An archive error on the true chain fails the sync of the range holding it (every
+    rank raises in layer_chain), as one sequential walk fails; errors on a speculative
+    walk that the chain never takes do not count."""
+    from trivy_amd import _native as N
+    tar = _nested_tar()
+    for cut in (len(tar) // 2 + 100, len(tar) - 700):
+        try:
+            W.NativeLayer(analyzer.scanner, tar[:cut])
+            want = "ok"
+        except N.NativeError:
+            want = "error"
+        for world in (2, 5):
+            try:
+                W.pack_layer_ranges(analyzer.scanner, tar[:cut], world)
+                got = "ok"
+            except N.NativeError:
+                got = "error"
+            assert got == want, (cut, world)
+
+
+@pytest.mark.parametrize("range_kib", [1, 7])
+@pytest.mark.parametrize("world", [2, 3])
+def test_layer_ranges_with_parallel_subranges(analyzer, monkeypatch, range_kib, world):
+    """Each rank's range is itself walked in speculative parallel sub-ranges (walk_par)."""
+    tar = _nested_tar()
+    monkeypatch.delenv("TSG_TAR_RANGE_KIB", raising=False)
+    whole = W.NativeLayer(analyzer.scanner, tar)
+    wb = whole.batch
+    monkeypatch.setenv("TSG_TAR_RANGE_KIB", str(range_kib))
+    paths, blobs, walked, opq, wh = _union(W.pack_layer_ranges(analyzer.scanner, tar, world))
+    assert paths == [wb.path(i) for i in range(wb.nfiles)]
+    assert blobs == [bytes(wb.data[int(wb.offsets[i]):int(wb.offsets[i + 1])]) for i in range(wb.nfiles)]
+    assert (walked, opq, wh) == (whole.walked, whole.opq, whole.wh)
+    for cut in (len(tar) // 2 + 100, len(tar) - 700):
+        monkeypatch.delenv("TSG_TAR_RANGE_KIB")
+        try:
+            W.NativeLayer(analyzer.scanner, tar[:cut])
+            want = "ok"
+        except Exception:
+            want = "error"
+        monkeypatch.setenv("TSG_TAR_RANGE_KIB", str(range_kib))
+        try:
+            W.pack_layer_ranges(analyzer.scanner, tar[:cut], world)
+            got = "ok"
+        except Exception:
+            got = "error"
+        assert got == want

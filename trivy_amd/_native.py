@@ -142,6 +142,15 @@ SIGNATURES = [
                                        C.POINTER(C.c_char_p), C.c_uint32, C.c_char_p, C.c_uint32,
                                        C.c_uint32, C.POINTER(_P)]),
     ("tsg_layer_get", C.c_int, [_P, C.POINTER(LayerView)]),
+    ("tsg_layer_range_walk", C.c_int, [_P, C.c_uint64, C.c_uint32, C.c_uint32, C.POINTER(_P),
+                                       _U64P]),
+    ("tsg_layer_range_sync", C.c_int, [_P, C.c_uint64, _U64P]),
+    ("tsg_layer_range_dirs", C.c_int, [_P, C.POINTER(C.c_char_p), C.c_uint32,
+                                       C.POINTER(C.c_void_p), _U64P]),
+    ("tsg_layer_range_pack", C.c_int, [_P, _P, C.POINTER(C.c_char_p), C.c_uint32,
+                                       C.POINTER(C.c_char_p), C.c_uint32, C.POINTER(C.c_char_p),
+                                       C.c_uint32, C.c_char_p, C.POINTER(_P)]),
+    ("tsg_layer_range_free", None, [_P]),
     ("tsg_fs_pack", C.c_int, [_P, C.c_char_p, C.POINTER(C.c_char_p), C.c_uint32,
                               C.POINTER(C.c_char_p), C.c_uint32, C.c_char_p, C.POINTER(_P)]),
     ("tsg_layer_free", None, [_P]),

@@ -344,13 +344,17 @@ uint64_t walk_tar(const uint8_t* tar, uint64_t tar_len, uint64_t pos, uint64_t s
 // given group position is deterministic); otherwise range k is walked again from the true
 // position.  Errors count only on the true chain, so the result (entries or the first
 // error) is that of one sequential walk.
-bool index_tar(const uint8_t* tar, uint64_t tar_len, std::vector<TarEntry>* out, std::string* err) {
+// walk_tar(pos, stop) with the speculative parallel walk above, same contract (entries,
+// groups, return value); index_tar is walk_par(0, tar_len).
+uint64_t walk_par(const uint8_t* tar, uint64_t tar_len, uint64_t pos0, uint64_t stop, std::vector<TarEntry>* out,
+                  std::vector<uint64_t>* groups, std::string* err) {
   // ranges of at least 64 MiB (TSG_TAR_RANGE_KIB lowers it: tests of the stitching)
   const uint64_t kMinRange =
       getenv("TSG_TAR_RANGE_KIB") ? std::max(1ull, strtoull(getenv("TSG_TAR_RANGE_KIB"), nullptr, 10)) << 10
                                   : 64ull << 20;
-  const int T = (int)std::min<uint64_t>(16, std::max<uint64_t>(1, tar_len / kMinRange));
-  if (T == 1) return walk_tar(tar, tar_len, 0, tar_len, out, nullptr, err) != ~0ull;
+  const uint64_t span = stop > pos0 ? stop - pos0 : 0;
+  const int T = (int)std::min<uint64_t>(16, std::max<uint64_t>(1, span / kMinRange));
+  if (T == 1) return walk_tar(tar, tar_len, pos0, stop, out, groups, err);
   struct Part {
     uint64_t lo = 0, hi = 0, start = 0, end = 0;
     std::vector<TarEntry> e;
@@ -359,8 +363,8 @@ bool index_tar(const uint8_t* tar, uint64_t tar_len, std::vector<TarEntry>* out,
   };
   std::vector<Part> parts(T);
   for (int k = 0; k < T; k++) {
-    parts[k].lo = (tar_len * k / T) & ~511ull;
-    parts[k].hi = k + 1 == T ? tar_len : ((tar_len * (k + 1) / T) & ~511ull);
+    parts[k].lo = k == 0 ? pos0 : ((pos0 + span * k / T) & ~511ull);
+    parts[k].hi = k + 1 == T ? stop : ((pos0 + span * (k + 1) / T) & ~511ull);
   }
   pool_for((size_t)T, T, [&](size_t k) {
     Part& P = parts[k];
@@ -377,7 +381,7 @@ bool index_tar(const uint8_t* tar, uint64_t tar_len, std::vector<TarEntry>* out,
     P.start = c;
     P.end = walk_tar(tar, tar_len, c, P.hi, &P.e, &P.groups, &P.err);
   }, 1);
-  uint64_t pos = 0;
+  uint64_t pos = pos0;
   for (int k = 0; k < T; k++) {
     Part& P = parts[k];
     if (pos >= P.hi && k + 1 < T) continue;  // the previous member spans this range
@@ -402,19 +406,22 @@ bool index_tar(const uint8_t* tar, uint64_t tar_len, std::vector<TarEntry>* out,
       P.end = walk_tar(tar, tar_len, pos, P.hi, &P.e, &P.groups, &P.err);
       first = 0;
     }
-    for (size_t i = first; i < P.e.size(); i++) out->push_back(std::move(P.e[i]));
+    for (size_t i = first; i < P.e.size(); i++) {
+      out->push_back(std::move(P.e[i]));
+      if (groups) groups->push_back(P.groups[i]);
+    }
     if (P.end == ~0ull) {
       *err = P.err;
-      return false;
+      return ~0ull;
     }
-    if (P.end == tar_len && (k + 1 == T || P.end >= P.hi)) {
-      // the archive ended (or its last member reaches the end): done once the chain has
-      // consumed the rest
-      if (P.end == tar_len) return true;
-    }
+    if (P.end == tar_len) return tar_len;  // the archive ended
     pos = P.end;
   }
-  return true;
+  return pos;
+}
+
+bool index_tar(const uint8_t* tar, uint64_t tar_len, std::vector<TarEntry>* out, std::string* err) {
+  return walk_par(tar, tar_len, 0, tar_len, out, nullptr, err) != ~0ull;
 }
 
 }  // namespace
@@ -430,10 +437,131 @@ extern "C" int tsg_layer_pack(const tsg_ruleset* rs, const uint8_t* tar, uint64_
                               config_path, 0, 1, out);
 }
 
+namespace tsg {
+namespace {
+
+struct Walked {
+  uint64_t dpos, size;
+  std::string fp;
+};
+
+Gate make_gate(const tsg_ruleset* rs, const char* const* skip_files, uint32_t n_skip_files,
+               const char* const* skip_dirs, uint32_t n_skip_dirs, const char* config_path) {
+  Gate g{rs->rs, rs->plan.get(), base(config_path ? config_path : ""), {}, {}};
+  for (uint32_t i = 0; i < n_skip_files; i++)  // walk.go:25-33
+    g.skip_files.push_back(trim_left_slash(clean(skip_files[i])));
+  std::vector<std::string> sd;
+  for (uint32_t i = 0; i < n_skip_dirs; i++) sd.push_back(skip_dirs[i]);
+  for (const char* s : {"proc", "sys", "dev"}) sd.push_back(s);  // walk.go:15
+  for (const auto& s : sd) g.skip_dirs.push_back(trim_left_slash(clean(s)));
+  return g;
+}
+
+// LayerTar.Walk's per-entry logic (tar.go:45-84) over entries [first, end) in walk order.
+// `skipped` is tar.go:35's skipDirs: it enters with the directories earlier entries added
+// (another rank's, for a range of the layer) and leaves with this run's appended.
+void classify(const std::vector<TarEntry>& entries, size_t first, const Gate& g,
+              std::vector<std::string>* skipped, tsg_layer* L, std::vector<Walked>* walked) {
+  for (size_t i = first; i < entries.size(); i++) {
+    const TarEntry& te = entries[i];
+    char type = te.type;
+    const std::string& name = te.name;
+    if (type == 0) type = (!name.empty() && name.back() == '/') ? '5' : '0';
+    const std::string fp = trim_left_slash(clean(name));
+    const size_t k = fp.rfind('/');
+    const std::string fdir = k == std::string::npos ? "" : fp.substr(0, k + 1);
+    const std::string fname = k == std::string::npos ? fp : fp.substr(k + 1);
+    if (fname == ".wh..wh..opq") {
+      L->opq += fdir;
+      L->opq += '\0';
+      continue;
+    }
+    if (starts_with(fname, ".wh.")) {
+      std::string j = fdir + fname.substr(4);
+      L->wh += j.empty() ? j : clean(j);
+      L->wh += '\0';
+      continue;
+    }
+    if (type == '5') {
+      const std::string d = trim_left_slash(fp);
+      if (base(d) == ".git" || contains(g.skip_dirs, d)) {  // walk.go:56-71
+        skipped->push_back(fp);
+        continue;
+      }
+    } else if (type == '0') {
+      if (contains(g.skip_files, trim_left_slash(fp))) continue;
+    } else {
+      continue;  // links, devices, fifos, sparse, contiguous: no content
+    }
+    bool under = false;  // tar.go:100-111
+    for (const auto& s : *skipped) {
+      std::string r;
+      if (!rel(s, fp, &r)) break;
+      if (!starts_with(r, "../")) {
+        under = true;
+        break;
+      }
+    }
+    if (under || type == '5') continue;
+    L->walked++;
+    walked->push_back({te.dpos, te.size, fp});
+  }
+}
+
+// AnalyzerGroup.AnalyzeFile (analyzer.go:399-409) + SecretAnalyzer.Analyze: the gates of the
+// walked files in parallel (Required's AllowPath is the costly part), then the kept files
+// copied into the batch in parallel
+void gate_and_pack(const uint8_t* tar, const Gate& g, const std::vector<Walked>& walked, tsg_layer* L,
+                   std::chrono::steady_clock::time_point t0) {
+  auto now = [] { return std::chrono::steady_clock::now(); };
+  const bool prof = getenv("TSG_LAYER_PROF") != nullptr;
+  auto t1 = now();
+  const size_t n = walked.size();
+  const int T = 16;  // the process-wide host pool (plan.cpp)
+  std::vector<uint8_t> keep(n);
+  pool_for(n, T, [&](size_t i) {
+    const Walked& w = walked[i];
+    keep[i] = g.required(w.fp, (int64_t)w.size) && !is_binary(tar + w.dpos, (int64_t)w.size);
+  }, 64);
+  auto t2 = now();
+  std::vector<uint64_t> dst(n);
+  uint64_t total = 0;
+  for (size_t i = 0; i < n; i++)
+    if (keep[i]) {
+      dst[i] = total;
+      total += walked[i].size;
+      L->offsets.push_back(total);
+      L->paths += '/';
+      L->paths += walked[i].fp;
+      L->path_offsets.push_back(L->paths.size());
+    }
+  L->data.reset(new uint8_t[total ? total : 1]);
+  // the copies in pieces of at most 4 MiB, so one large file does not serialize the pack
+  constexpr uint64_t kPiece = 4ull << 20;
+  std::vector<std::pair<size_t, uint64_t>> pieces;  // (file, offset in it)
+  for (size_t i = 0; i < n; i++)
+    if (keep[i])
+      for (uint64_t o = 0; o < walked[i].size; o += kPiece) pieces.push_back({i, o});
+  pool_for(pieces.size(), T, [&](size_t k) {
+    const size_t i = pieces[k].first;
+    const uint64_t o = pieces[k].second, len = std::min(kPiece, walked[i].size - o);
+    std::memcpy(L->data.get() + dst[i] + o, tar + walked[i].dpos + o, len);
+  }, 16);
+  if (prof)
+    fprintf(stderr, "layer: walk %.1f ms, gates %.1f ms, pack %.1f ms (%d threads)\n",
+            std::chrono::duration<double, std::milli>(t1 - t0).count(),
+            std::chrono::duration<double, std::milli>(t2 - t1).count(),
+            std::chrono::duration<double, std::milli>(now() - t2).count(), T);
+}
+
+}  // namespace
+}  // namespace tsg
+
 // One rank's share of a layer (SURVEY.md §8e, configs[2]): every rank indexes the header
 // chain (headers only, parallel), and applies the walker's whiteout / skip-dir logic, which
 // needs the whole chain; the walked files are then cut into `world` contiguous runs of
 // about equal bytes, and only this rank's run is gated (Required, IsBinary) and packed.
+// (tsg_layer_range_* below splits the index itself over the ranks.)
 extern "C" int tsg_layer_pack_shard(const tsg_ruleset* rs, const uint8_t* tar, uint64_t tar_len,
                                     const char* const* skip_files, uint32_t n_skip_files,
                                     const char* const* skip_dirs, uint32_t n_skip_dirs,
@@ -443,20 +571,9 @@ extern "C" int tsg_layer_pack_shard(const tsg_ruleset* rs, const uint8_t* tar, u
     return fail(TSG_ERR_ARG, "bad argument");
   *out = nullptr;
   try {
-    Gate g{rs->rs, rs->plan.get(), base(config_path ? config_path : ""), {}, {}};
-    for (uint32_t i = 0; i < n_skip_files; i++)  // walk.go:25-33
-      g.skip_files.push_back(trim_left_slash(clean(skip_files[i])));
-    std::vector<std::string> sd;
-    for (uint32_t i = 0; i < n_skip_dirs; i++) sd.push_back(skip_dirs[i]);
-    for (const char* s : {"proc", "sys", "dev"}) sd.push_back(s);  // walk.go:15
-    for (const auto& s : sd) g.skip_dirs.push_back(trim_left_slash(clean(s)));
-
+    const Gate g = make_gate(rs, skip_files, n_skip_files, skip_dirs, n_skip_dirs, config_path);
     const auto t0 = std::chrono::steady_clock::now();
     auto L = std::make_unique<tsg_layer>();
-    struct Walked {
-      uint64_t dpos, size;
-      std::string fp;
-    };
     std::vector<Walked> walked;
     std::vector<std::string> skipped;  // tar.go:35 skipDirs
     std::vector<TarEntry> entries;
@@ -465,52 +582,7 @@ extern "C" int tsg_layer_pack_shard(const tsg_ruleset* rs, const uint8_t* tar, u
       if (!index_tar(tar, tar_len, &entries, &err))
         return fail(TSG_ERR_ARG, std::string("failed to extract the archive: ") + err);
     }
-    for (const TarEntry& te : entries) {
-      char type = te.type;
-      const std::string& name = te.name;
-      if (type == 0) type = (!name.empty() && name.back() == '/') ? '5' : '0';
-      const uint64_t dpos = te.dpos;
-      const int64_t size = (int64_t)te.size;
-      // tar.go:45-84
-      const std::string fp = trim_left_slash(clean(name));
-      const size_t k = fp.rfind('/');
-      const std::string fdir = k == std::string::npos ? "" : fp.substr(0, k + 1);
-      const std::string fname = k == std::string::npos ? fp : fp.substr(k + 1);
-      if (fname == ".wh..wh..opq") {
-        L->opq += fdir;
-        L->opq += '\0';
-        continue;
-      }
-      if (starts_with(fname, ".wh.")) {
-        std::string j = fdir + fname.substr(4);
-        L->wh += j.empty() ? j : clean(j);
-        L->wh += '\0';
-        continue;
-      }
-      if (type == '5') {
-        const std::string d = trim_left_slash(fp);
-        if (base(d) == ".git" || contains(g.skip_dirs, d)) {  // walk.go:56-71
-          skipped.push_back(fp);
-          continue;
-        }
-      } else if (type == '0') {
-        if (contains(g.skip_files, trim_left_slash(fp))) continue;
-      } else {
-        continue;  // links, devices, fifos, sparse, contiguous: no content
-      }
-      bool under = false;  // tar.go:100-111
-      for (const auto& s : skipped) {
-        std::string r;
-        if (!rel(s, fp, &r)) break;
-        if (!starts_with(r, "../")) {
-          under = true;
-          break;
-        }
-      }
-      if (under || type == '5') continue;
-      L->walked++;
-      walked.push_back({dpos, (uint64_t)size, fp});
-    }
+    classify(entries, 0, g, &skipped, L.get(), &walked);
     if (world > 1) {  // this rank's contiguous run of the walked files, by bytes
       uint64_t all = 0;
       for (const Walked& w : walked) all += w.size;
@@ -524,49 +596,7 @@ extern "C" int tsg_layer_pack_shard(const tsg_ruleset* rs, const uint8_t* tar, u
       }
       walked.swap(mine);
     }
-    // AnalyzerGroup.AnalyzeFile (analyzer.go:399-409) + SecretAnalyzer.Analyze: the gates of
-    // the walked files in parallel (Required's AllowPath is the costly part), then the
-    // kept files copied into the batch in parallel
-    auto now = [] { return std::chrono::steady_clock::now(); };
-    const bool prof = getenv("TSG_LAYER_PROF") != nullptr;
-    auto t1 = now();
-    const size_t n = walked.size();
-    const int T = 16;  // the process-wide host pool (plan.cpp)
-    std::vector<uint8_t> keep(n);
-    auto par = [&](const std::function<void(size_t)>& fn) { pool_for(n, T, fn, 64); };
-    par([&](size_t i) {
-      const Walked& w = walked[i];
-      keep[i] = g.required(w.fp, (int64_t)w.size) && !is_binary(tar + w.dpos, (int64_t)w.size);
-    });
-    auto t2 = now();
-    std::vector<uint64_t> dst(n);
-    uint64_t total = 0;
-    for (size_t i = 0; i < n; i++)
-      if (keep[i]) {
-        dst[i] = total;
-        total += walked[i].size;
-        L->offsets.push_back(total);
-        L->paths += '/';
-        L->paths += walked[i].fp;
-        L->path_offsets.push_back(L->paths.size());
-      }
-    L->data.reset(new uint8_t[total ? total : 1]);
-    // the copies in pieces of at most 4 MiB, so one large file does not serialize the pack
-    constexpr uint64_t kPiece = 4ull << 20;
-    std::vector<std::pair<size_t, uint64_t>> pieces;  // (file, offset in it)
-    for (size_t i = 0; i < n; i++)
-      if (keep[i])
-        for (uint64_t o = 0; o < walked[i].size; o += kPiece) pieces.push_back({i, o});
-    pool_for(pieces.size(), T, [&](size_t k) {
-      const size_t i = pieces[k].first;
-      const uint64_t o = pieces[k].second, len = std::min(kPiece, walked[i].size - o);
-      std::memcpy(L->data.get() + dst[i] + o, tar + walked[i].dpos + o, len);
-    }, 16);
-    if (prof)
-      fprintf(stderr, "layer: walk %.1f ms, gates %.1f ms, pack %.1f ms (%d threads)\n",
-              std::chrono::duration<double, std::milli>(t1 - t0).count(),
-              std::chrono::duration<double, std::milli>(t2 - t1).count(),
-              std::chrono::duration<double, std::milli>(now() - t2).count(), T);
+    gate_and_pack(tar, g, walked, L.get(), t0);
     *out = L.release();
     return TSG_OK;
   } catch (const std::bad_alloc&) {
@@ -575,6 +605,166 @@ extern "C" int tsg_layer_pack_shard(const tsg_ruleset* rs, const uint8_t* tar, u
     return fail(TSG_ERR_INTERNAL, e.what());
   }
 }
+
+// ---------------------------------------------------------------- distributed index
+// The header index split over the ranks (configs[2] at N GPUs): rank r owns the entry groups
+// that start in its byte range [lo, hi) of the tar.  The speculative walk of index_tar runs
+// per rank (tsg_layer_range_walk); the ranks exchange {lo, hi, start, end} and fix the true
+// chain in rank order (trivy_amd/shard.py:layer_chain); a rank whose speculative start was
+// not on the chain is re-synced with tsg_layer_range_sync.  The skip dirs each range adds
+// (tsg_layer_range_dirs) go to the later ranks, which apply them before their own (tar.go:35
+// accumulates them in walk order); then every rank classifies, gates and packs its range.
+struct tsg_layer_range {
+  const uint8_t* tar;
+  uint64_t tar_len, lo, hi, start, end;
+  std::vector<tsg::TarEntry> e;
+  std::vector<uint64_t> groups;
+  std::string err;
+  size_t first = 0;      // first entry on the true chain (after a sync)
+  bool synced = false;
+  bool empty = false;    // no group starts in the range
+};
+
+extern "C" int tsg_layer_range_walk(const uint8_t* tar, uint64_t tar_len, uint32_t rank, uint32_t world,
+                                    tsg_layer_range** out, uint64_t info[4]) {
+  if (!out || !info || (!tar && tar_len) || world == 0 || rank >= world) return fail(TSG_ERR_ARG, "bad argument");
+  *out = nullptr;
+  try {
+    auto R = std::make_unique<tsg_layer_range>();
+    R->tar = tar;
+    R->tar_len = tar_len;
+    R->lo = (uint64_t)((unsigned __int128)tar_len * rank / world) & ~511ull;
+    R->hi = rank + 1 == world ? tar_len : ((uint64_t)((unsigned __int128)tar_len * (rank + 1) / world) & ~511ull);
+    uint64_t c = R->lo;
+    if (rank > 0) {  // first plausible header of the range
+      while (c + 512 <= R->hi && !(std::memcmp(tar + c + 257, "ustar", 5) == 0 && tsg::checksum_ok(tar + c)))
+        c += 512;
+    }
+    if (rank > 0 && c + 512 > R->hi) {
+      R->start = R->end = ~0ull;  // none: the chain crosses the range inside one member
+    } else {
+      R->start = c;
+      R->end = tsg::walk_par(tar, tar_len, c, R->hi, &R->e, &R->groups, &R->err);
+    }
+    info[0] = R->lo;
+    info[1] = R->hi;
+    info[2] = R->start;
+    info[3] = R->end;
+    *out = R.release();
+    return TSG_OK;
+  } catch (const std::bad_alloc&) {
+    return fail(TSG_ERR_NOMEM, "out of memory");
+  } catch (const std::exception& e) {
+    return fail(TSG_ERR_INTERNAL, e.what());
+  }
+}
+
+// The true chain enters the range at `pos` (the previous range's true end; 0 for rank 0).
+// Keeps the walk's entries from there, or walks the range again from pos.  *end = the true
+// end of this range (the next range's pos).  A malformed archive on the true chain fails
+// with the walker's error, as one sequential walk would.
+extern "C" int tsg_layer_range_sync(tsg_layer_range* R, uint64_t pos, uint64_t* end) {
+  if (!R || !end) return fail(TSG_ERR_ARG, "bad argument");
+  try {
+    R->synced = true;
+    if (pos >= R->hi) {  // the previous member spans this range, or the archive ended
+      R->empty = true;
+      R->first = R->e.size();
+      *end = pos;
+      return TSG_OK;
+    }
+    bool ok = false;
+    if (R->start == pos) {
+      ok = true;
+      R->first = 0;
+    } else if (R->start != ~0ull) {
+      auto it = std::lower_bound(R->groups.begin(), R->groups.end(), pos);
+      if (it != R->groups.end() && *it == pos) {
+        ok = true;
+        R->first = (size_t)(it - R->groups.begin());
+      } else if (R->end == pos) {
+        ok = true;  // the walk reached the true position exactly at its stop
+        R->first = R->e.size();
+      }
+    }
+    if (!ok) {
+      R->e.clear();
+      R->groups.clear();
+      R->err.clear();
+      R->first = 0;
+      R->start = pos;
+      R->end = tsg::walk_par(R->tar, R->tar_len, pos, R->hi, &R->e, &R->groups, &R->err);
+    }
+    if (R->end == ~0ull) return fail(TSG_ERR_ARG, std::string("failed to extract the archive: ") + R->err);
+    *end = R->end;
+    return TSG_OK;
+  } catch (const std::bad_alloc&) {
+    return fail(TSG_ERR_NOMEM, "out of memory");
+  } catch (const std::exception& e) {
+    return fail(TSG_ERR_INTERNAL, e.what());
+  }
+}
+
+// The directories this range's entries add to the walker's skipDirs (tar.go:62-66), as
+// NUL-terminated strings in walk order (*out valid until the range is freed).
+extern "C" int tsg_layer_range_dirs(tsg_layer_range* R, const char* const* skip_dirs, uint32_t n_skip_dirs,
+                                    const char** out, uint64_t* out_len) {
+  if (!R || !out || !out_len || !R->synced) return fail(TSG_ERR_ARG, "bad argument");
+  try {
+    std::vector<std::string> sd;
+    for (uint32_t i = 0; i < n_skip_dirs; i++) sd.push_back(skip_dirs[i]);
+    for (const char* s : {"proc", "sys", "dev"}) sd.push_back(s);
+    for (auto& s : sd) s = tsg::trim_left_slash(tsg::clean(s));
+    R->err.clear();
+    for (size_t i = R->first; i < R->e.size(); i++) {
+      const tsg::TarEntry& te = R->e[i];
+      const bool dir = te.type == '5' || (te.type == 0 && !te.name.empty() && te.name.back() == '/');
+      if (!dir) continue;
+      const std::string fp = tsg::trim_left_slash(tsg::clean(te.name));
+      const size_t k = fp.rfind('/');
+      const std::string fname = k == std::string::npos ? fp : fp.substr(k + 1);
+      if (fname == ".wh..wh..opq" || tsg::starts_with(fname, ".wh.")) continue;
+      if (tsg::base(fp) == ".git" || tsg::contains(sd, fp)) {
+        R->err += fp;
+        R->err += '\0';
+      }
+    }
+    *out = R->err.data();
+    *out_len = R->err.size();
+    return TSG_OK;
+  } catch (const std::exception& e) {
+    return fail(TSG_ERR_INTERNAL, e.what());
+  }
+}
+
+// Classify, gate and pack the range's entries (tsg_layer_pack's batch for them); `prior`
+// holds the skip dirs of the ranks before this one, in rank order.
+extern "C" int tsg_layer_range_pack(const tsg_ruleset* rs, const tsg_layer_range* R,
+                                    const char* const* skip_files, uint32_t n_skip_files,
+                                    const char* const* skip_dirs, uint32_t n_skip_dirs,
+                                    const char* const* prior, uint32_t n_prior,
+                                    const char* config_path, tsg_layer** out) {
+  if (!rs || !R || !out || !R->synced) return fail(TSG_ERR_ARG, "bad argument");
+  *out = nullptr;
+  try {
+    const auto t0 = std::chrono::steady_clock::now();
+    const tsg::Gate g = tsg::make_gate(rs, skip_files, n_skip_files, skip_dirs, n_skip_dirs, config_path);
+    auto L = std::make_unique<tsg_layer>();
+    std::vector<std::string> skipped;
+    for (uint32_t i = 0; i < n_prior; i++) skipped.push_back(prior[i]);
+    std::vector<tsg::Walked> walked;
+    tsg::classify(R->e, R->first, g, &skipped, L.get(), &walked);
+    tsg::gate_and_pack(R->tar, g, walked, L.get(), t0);
+    *out = L.release();
+    return TSG_OK;
+  } catch (const std::bad_alloc&) {
+    return fail(TSG_ERR_NOMEM, "out of memory");
+  } catch (const std::exception& e) {
+    return fail(TSG_ERR_INTERNAL, e.what());
+  }
+}
+
+extern "C" void tsg_layer_range_free(tsg_layer_range* R) { delete R; }
 
 extern "C" int tsg_layer_get(const tsg_layer* L, tsg_layer_view* v) {
   if (!L || !v) return fail(TSG_ERR_ARG, "bad argument");

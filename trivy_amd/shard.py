@@ -48,16 +48,30 @@ def scan_sharded(scanner, args, rank, world, dist=None, device=None, emulate_chu
 
 
 def scan_layer_sharded(analyzer, tar, rank, world, dist=None, device=None, emulate_chunk=0,
-                       skip_files=(), skip_dirs=()):
+                       skip_files=(), skip_dirs=(), index="range"):
     """BASELINE configs[2]: one image layer's files sharded over `world` ranks.
 
-    Each rank indexes the layer's header chain and packs only its own contiguous byte run
-    of the walked files (tsg_layer_pack_shard: `Required`, `IsBinary` and the copy for that
-    run only), scans it, and the findings are gathered on rank 0; rank 0 returns (sorted
-    AnalysisResult.Secrets, opq_dirs, wh_files), the others None."""
-    from .walker import NativeLayer
-    lay = NativeLayer(analyzer.scanner, tar, skip_files, skip_dirs, analyzer.configPath,
-                      rank=rank, world=world)
+    index="range" (default): the header index itself is split; each rank walks its own byte
+    range of the tar and the ranks fix the true chain and the walker's skip dirs with two
+    tiny all-gathers (walker.layer_chain, tsg_layer_range_*), then each packs and scans the
+    files of its range.  index="whole": every rank indexes the whole chain and packs its
+    contiguous byte run of the walked files (tsg_layer_pack_shard).  The findings are
+    gathered on rank 0; rank 0 returns (sorted AnalysisResult.Secrets, opq_dirs, wh_files),
+    the others None."""
+    from .walker import NativeLayer, LayerRange, layer_chain
+    if index == "range" and world > 1 and dist is not None:
+        def allgather(obj):
+            out = [None] * world
+            dist.all_gather_object(out, obj)
+            return out
+        rng = LayerRange(tar, rank, world)
+        layer_chain(rng, rank, world, allgather)
+        dirs = allgather(rng.dirs(skip_dirs))
+        prior = [d for r in range(rank) for d in dirs[r]]
+        lay = rng.pack(analyzer.scanner, skip_files, skip_dirs, prior, analyzer.configPath)
+    else:
+        lay = NativeLayer(analyzer.scanner, tar, skip_files, skip_dirs, analyzer.configPath,
+                          rank=rank, world=world)
     b = lay.batch
     if b.nfiles == 0:
         local = []
@@ -68,11 +82,16 @@ def scan_layer_sharded(analyzer, tar, rank, world, dist=None, device=None, emula
     mine = [r for r in local if r and r["Findings"]]
     if world == 1 or dist is None:
         return findings_sorted(mine), lay.opq, lay.wh
+    per_rank = index == "range"  # opq / wh of the range only: concatenated in rank order
     gathered = [None] * world if rank == 0 else None
-    dist.gather_object(mine, gathered, dst=0)
+    dist.gather_object((mine, lay.opq, lay.wh), gathered, dst=0)
     if rank != 0:
         return None
-    return findings_sorted([r for part in gathered for r in part]), lay.opq, lay.wh
+    secrets = findings_sorted([r for part in gathered for r in part[0]])
+    if per_rank:
+        return (secrets, [d for part in gathered for d in part[1]],
+                [w for part in gathered for w in part[2]])
+    return secrets, lay.opq, lay.wh
 
 
 def findings_sorted(results):

@@ -231,6 +231,11 @@ class NativeLayer:
                                        sf, len(skip_files), sd, len(skip_dirs),
                                        config_path.encode("utf-8", "surrogateescape"), rank, world,
                                        C.byref(h)))
+        self._adopt(h)
+
+    def _adopt(self, h):
+        """Take ownership of a tsg_layer handle and view its batch, opq, wh and walked."""
+        L = N.lib()
         self._h = h
         v = N.LayerView()
         N.check(L.tsg_layer_get(h, C.byref(v)))
@@ -242,16 +247,138 @@ class NativeLayer:
         self.batch = S.Batch(as_u8(v.data, int(offs[-1])), offs, as_u8(v.paths, int(poffs[-1])),
                              poffs)
         self.batch._owner = self
-        lst = lambda p, k: [x.decode("utf-8", "surrogateescape")
-                            for x in C.string_at(p, k).split(b"\0")[:-1]] if k else []
-        self.opq = lst(v.opq, v.opq_len)
-        self.wh = lst(v.wh, v.wh_len)
+        self.opq = _nul_list(v.opq, v.opq_len)
+        self.wh = _nul_list(v.wh, v.wh_len)
         self.walked = v.walked
 
     def __del__(self):
         if getattr(self, "_h", None):
             N.lib().tsg_layer_free(self._h)
             self._h = None
+
+
+def _nul_list(p, k):
+    return [x.decode("utf-8", "surrogateescape") for x in C.string_at(p, k).split(b"\0")[:-1]] if k else []
+
+
+def _cstrs(xs):
+    return (C.c_char_p * max(1, len(xs)))(*[x.encode("utf-8", "surrogateescape") for x in xs])
+
+
+_NO_POS = (1 << 64) - 1
+
+
+class LayerRange:
+    """One rank's byte range of a layer's header chain (tsg_layer_range_*, trivy_secret.h):
+    the speculative walk on construction (`.info` = lo, hi, start, end), then `sync(pos)`
+    once the true chain's entry position is known, `dirs()` for the skip dirs it hands to
+    later ranks, and `pack()` for its batch."""
+
+    def __init__(self, tar, rank, world):
+        L = N.lib()
+        self._h = None
+        self._tar = np.frombuffer(tar, dtype=np.uint8) if len(tar) else np.zeros(1, np.uint8)
+        h, info = C.c_void_p(), (C.c_uint64 * 4)()
+        N.check(L.tsg_layer_range_walk(C.c_void_p(self._tar.ctypes.data), len(tar), rank, world,
+                                       C.byref(h), info))
+        self._h = h
+        self.info = tuple(int(x) for x in info)
+
+    def sync(self, pos):
+        end = C.c_uint64()
+        N.check(N.lib().tsg_layer_range_sync(self._h, pos, C.byref(end)))
+        return int(end.value)
+
+    def dirs(self, skip_dirs=()):
+        p, k = C.c_void_p(), C.c_uint64()
+        N.check(N.lib().tsg_layer_range_dirs(self._h, _cstrs(list(skip_dirs)), len(skip_dirs),
+                                             C.byref(p), C.byref(k)))
+        return _nul_list(p.value, k.value)
+
+    def pack(self, scanner, skip_files=(), skip_dirs=(), prior_dirs=(), config_path=""):
+        h = C.c_void_p()
+        N.check(N.lib().tsg_layer_range_pack(
+            scanner.handle, self._h, _cstrs(list(skip_files)), len(skip_files),
+            _cstrs(list(skip_dirs)), len(skip_dirs), _cstrs(list(prior_dirs)), len(prior_dirs),
+            config_path.encode("utf-8", "surrogateescape"), C.byref(h)))
+        lay = NativeLayer.__new__(NativeLayer)
+        lay._tar = self._tar
+        lay._range = self  # the entries' names live in the range; the batch copies the bytes
+        lay._adopt(h)
+        return lay
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            N.lib().tsg_layer_range_free(self._h)
+            self._h = None
+
+
+def layer_chain_step(infos, confirmed):
+    """The true header chain over ranks' ranges, as far as the exchanged data fixes it.
+
+    infos[r] = LayerRange.info of rank r; confirmed[r] = the end rank r reported after
+    tsg_layer_range_sync.  Returns ("done", pos) with every rank's entry position, or
+    ("need", r, pos): rank r must sync at pos and publish its end (its speculative start
+    was not on the chain, or the chain errs in its range)."""
+    pos, out = 0, []
+    for r, (lo, hi, start, end) in enumerate(infos):
+        out.append(pos)
+        if r in confirmed:
+            pos = confirmed[r]
+        elif pos >= hi:
+            pass  # a member spans the range, or the archive ended before it
+        elif start == pos and end != _NO_POS:
+            pos = end  # a walk from a group position is deterministic
+        else:
+            return ("need", r, pos)
+    return ("done", out)
+
+
+def layer_chain(rng, rank, world, allgather):
+    """Fix the true chain across ranks (allgather(obj) -> list over ranks) and sync `rng` to
+    it; returns this rank's entry position.  Raises the archive error of the chain on every
+    rank, as one sequential walk fails."""
+    infos = allgather(rng.info)
+    confirmed = {}
+    while True:
+        st = layer_chain_step(infos, confirmed)
+        if st[0] == "done":
+            pos = st[1][rank]
+            rng.sync(pos)
+            return pos
+        _, r, pos = st
+        msg = None
+        if r == rank:
+            try:
+                msg = ("ok", rng.sync(pos))
+            except Exception as e:  # noqa: BLE001 - forwarded to every rank
+                msg = ("err", str(e))
+        got = allgather(msg)[r]
+        if got[0] == "err":
+            raise RuntimeError(got[1])
+        confirmed[r] = got[1]
+
+
+def pack_layer_ranges(scanner, tar, world, skip_files=(), skip_dirs=(), config_path=""):
+    """All `world` ranges of one layer in this process (the single-host form of the
+    distributed index, and its test): returns the per-rank NativeLayer list."""
+    rngs = [LayerRange(tar, r, world) for r in range(world)]
+    infos = [g.info for g in rngs]
+    confirmed = {}
+    while True:
+        st = layer_chain_step(infos, confirmed)
+        if st[0] == "done":
+            break
+        _, r, pos = st
+        confirmed[r] = rngs[r].sync(pos)
+    for g, pos in zip(rngs, st[1]):
+        g.sync(pos)
+    dirs = [g.dirs(skip_dirs) for g in rngs]
+    out, prior = [], []
+    for r, g in enumerate(rngs):
+        out.append(g.pack(scanner, skip_files, skip_dirs, prior, config_path))
+        prior = prior + dirs[r]
+    return out
 
 
 class NativeFS(NativeLayer):
