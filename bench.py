@@ -19,9 +19,11 @@ ranks wall time of the timed steps.
 Rank 0 prints ONE JSON line with, besides the contract fields:
   roofline       K1 (the dominant kernel): algorithmic bytes per launch / mean HIP-event
                  duration of its launches (events on the lane stream around each launch)
-                 vs 8 TB/s; traffic = HBM bytes per launch from the committed FETCH_SIZE
-                 pass of the same command (profiles/r02/), converted with the factor
-                 calibrated for K1's access pattern (tools/fetch_calib.hip)
+                 vs 8 TB/s; traffic = HBM bytes per launch from the FETCH_SIZE pass of the
+                 same command recorded in profiles/pmc/<rules>.json, used only when that
+                 pass ran the same device code (sha256 of the HIP sources) and batch size,
+                 else null; converted with the factor calibrated for K1's access pattern
+                 (tools/fetch_calib.hip)
   kernels        K1, K2 (on the bytes it reads) and K1+gates+K2 GB/s (HIP events)
   pipeline       H2D GB/s, per-batch stage times, resolution time
   cpu_baseline   the library's exact C++ CPU path (the reference algorithm restated:
@@ -29,6 +31,9 @@ Rank 0 prints ONE JSON line with, besides the contract fields:
                  files) on this host's cores, on a bounded sample of the same corpus
   cpu_optimised  the GPU algorithm (K1 automaton + K2 DFAs + the same exact resolution)
                  emulated on the same cores and sample
+  checks         every step's findings (files with findings, findings) must equal the
+                 warmup step's, and a device scan of the cpu_baseline sample must be
+                 byte-identical to the exact CPU path's result; the bench fails otherwise
 """
 import argparse
 import json
@@ -40,8 +45,9 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
-# FETCH_SIZE of the same command (rocprofv3 --pmc FETCH_SIZE), committed under profiles/
-PMC_FETCH_CSV = os.path.join(ROOT, "profiles", "r02", "bench_pmc_fetch.csv")
+# FETCH_SIZE passes of this command per rule set (rocprofv3 --pmc FETCH_SIZE, recorded by
+# tools/pmc_traffic.py --record), committed under profiles/
+PMC_DIR = os.path.join(ROOT, "profiles", "pmc")
 
 
 def _dist():
@@ -98,16 +104,18 @@ def _sub_batch(batch, max_bytes):
 
 def cpu_baselines(sc, batch, max_bytes, nthreads):
     """The exact CPU path (the reference algorithm, restated in C++) and the optimised CPU
-    path (the GPU algorithm emulated), both on `nthreads` threads over the same prefix."""
+    path (the GPU algorithm emulated), both on `nthreads` threads over the same prefix.
+    Returns them with the sample and the exact path's raw result bytes."""
     from trivy_amd import _native as N
     import ctypes as C
+    L = N.lib()
     sub, nf = _sub_batch(batch, max_bytes)
     nb = int(sub.offsets[-1])
     out = C.c_void_p()
     t0 = time.perf_counter()
-    N.check(N.lib().tsg_scan_cpu_batch(sc.handle, *sub.ptrs(), nthreads, C.byref(out)))
+    N.check(L.tsg_scan_cpu_batch(sc.handle, *sub.ptrs(), nthreads, C.byref(out)))
     dt = time.perf_counter() - t0
-    N.lib().tsg_result_free(out)
+    exact_bytes = _raw(out)
     model = cpu_model()
     exact = {"value": round(nb / dt / 1e9, 4), "unit": "GB/s", "cores": nthreads, "kind": "port",
              "cpu": model,
@@ -117,34 +125,61 @@ def cpu_baselines(sc, batch, max_bytes, nthreads):
                        % (nf, nb / 1e6, dt)}
     from trivy_amd.secret import GpuContext
     ctx = GpuContext(sc, 0, emulate=True, host_threads=nthreads)
+    out = C.c_void_p()
     t0 = time.perf_counter()
-    ctx.upload(sub)
-    ctx.submit()
-    N.lib().tsg_result_free(ctx.collect_raw())
+    N.check(L.tsg_scan_batch(ctx.handle, *sub.ptrs(), C.byref(out)))
     dt2 = time.perf_counter() - t0
+    L.tsg_result_free(out)
     ctx.close()
     opt = {"value": round(nb / dt2 / 1e9, 4), "unit": "GB/s", "cores": nthreads, "kind": "port",
            "cpu": model,
            "sample": "same %.0f MB; the GPU algorithm (K1 automaton, gates, K2 DFAs) emulated "
                      "on the CPU + the same exact resolution (TSG_CTX_EMULATE), %.1f s"
                      % (nb / 1e6, dt2)}
-    return exact, opt
+    return exact, opt, sub, exact_bytes
 
 
-def _traffic_per_launch(batch_bytes):
-    """K1 HBM bytes per launch from the committed FETCH_SIZE pass (None when absent or for
-    another batch size)."""
-    if not os.path.exists(PMC_FETCH_CSV):
+def _raw(out):
+    """The bytes of a tsg_result (freed)."""
+    from trivy_amd import _native as N
+    import ctypes as C
+    n = C.c_size_t()
+    p = N.lib().tsg_result_data(out, C.byref(n))
+    b = C.string_at(p, n.value)
+    N.lib().tsg_result_free(out)
+    return b
+
+
+def _summary(out):
+    """(files with findings, findings) of a tsg_result."""
+    from trivy_amd import _native as N
+    import ctypes as C
+    ff, nf = C.c_uint64(), C.c_uint64()
+    N.check(N.lib().tsg_result_summary(out, None, C.byref(ff), C.byref(nf)))
+    return ff.value, nf.value
+
+
+def kernel_source_sha():
+    """sha256 of the device code (HIP sources and the headers they include)."""
+    import glob
+    import hashlib
+    h = hashlib.sha256()
+    csrc = os.path.join(ROOT, "trivy_amd", "csrc")
+    for f in sorted(glob.glob(os.path.join(csrc, "*.hip")) + [os.path.join(csrc, "device.hpp")]):
+        h.update(open(f, "rb").read())
+    return h.hexdigest()
+
+
+def _traffic_record(rules, batch_bytes):
+    """The FETCH_SIZE record of this rule set when it was measured on the same device code
+    and batch size (else None)."""
+    path = os.path.join(PMC_DIR, "%s.json" % rules)
+    if not os.path.exists(path):
         return None
-    meta = PMC_FETCH_CSV.replace(".csv", ".json")
-    if os.path.exists(meta):
-        m = json.load(open(meta))
-        if int(m.get("batch_bytes", -1)) != int(batch_bytes):
-            return None
-    sys.path.insert(0, os.path.join(ROOT, "tools"))
-    from pmc_traffic import traffic
-    t = traffic(PMC_FETCH_CSV, "k1_kernel")
-    return None if t is None else int(t)
+    m = json.load(open(path))
+    if m.get("kernels_sha256") != kernel_source_sha() or int(m.get("batch_bytes", -1)) != int(batch_bytes):
+        return None
+    return m
 
 
 def rule_set(name):
@@ -255,15 +290,35 @@ def main():
     log("corpus %.2f GiB (%d files) in %.1fs, rules compiled in %.1fs, packed in %.1fs"
         % (info["bytes"] / (1 << 30), info["files"], gen_s, compile_s, pack_s))
 
+    import collections
+    import ctypes as C
+    step_findings = []  # (files with findings, findings) of every step, warmup included
+
+    def collect(q, per_step):
+        t, k = q.popleft()
+        out = C.c_void_p()
+        N.check(L.tsg_batch_collect(ctx.handle, t, C.byref(out)))
+        ff, nf = _summary(out)
+        L.tsg_result_free(out)
+        per_step[k][0] += ff
+        per_step[k][1] += nf
+
     def run(steps):
+        """`steps` scans of the corpus, pipelined across step boundaries (batches of step
+        k+1 are submitted while step k's last ones resolve); every result is collected."""
+        q = collections.deque()
+        per_step = [[0, 0] for _ in range(steps)]
         for k in range(steps):
             log("step %d/%d" % (k + 1, steps))
             for sid, nf, _ in slots:
-                ctx.submit_slot(sid, nf)
-                while ctx.pending() >= args.depth:
-                    L.tsg_result_free(ctx.collect_raw())
-        while ctx.pending():
-            L.tsg_result_free(ctx.collect_raw())
+                t = C.c_uint64()
+                N.check(L.tsg_slot_submit(ctx.handle, sid, nf, C.byref(t)))
+                q.append((t.value, k))
+                while len(q) >= args.depth:
+                    collect(q, per_step)
+        while q:
+            collect(q, per_step)
+        step_findings.extend(tuple(x) for x in per_step)
 
     run(args.warmup)
     st0 = ctx.stats()
@@ -282,6 +337,7 @@ def main():
     dev_ms = d["sum_k1_ms"] + d["sum_gate_ms"] + d["sum_k2_ms"]
     launch_bytes = d["sum_bytes"] / nbat
     k2_read = st["k2_bytes"]  # last batch: chunk bytes K2 read
+    pmc = _traffic_record(args.rules, int(launch_bytes))
     line = {
         "metric": "secret-scan GB/s (builtin rules) at 1/2/4/8 MI355X; % of HBM peak",
         "value": round(total_bytes / dt / 1e9, 3),
@@ -306,11 +362,14 @@ def main():
         "roofline": {"bound": "hbm", "kernel": "K1 keyword automaton (k1_kernel)",
                      "achieved": round(k1_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(k1_gbs / HBM_PEAK_GBS, 4),
-                     "traffic": _traffic_per_launch(launch_bytes),
+                     "traffic": pmc["k1_bytes_per_launch"] if pmc else None,
                      "algorithmic_bytes_per_launch": int(launch_bytes),
-                     "traffic_source": os.path.relpath(PMC_FETCH_CSV, ROOT),
+                     "traffic_source": pmc["csv"] if pmc else
+                     "none: no FETCH_SIZE pass of this device code, rule set and batch size "
+                     "in profiles/pmc/",
                      "traffic_calibration": "FETCH_SIZE KiB x 1024 / 0.922 (K1's quad-transposed "
-                                            "64-B loads; profiles/r02/fetch_calib.json)"},
+                                            "64-B loads; profiles/r02/fetch_calib.json)",
+                     "k1_gates_k2_frac": round(d["sum_bytes"] / (dev_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4)},
         "kernels": {"k1_GBps": round(k1_gbs, 1),
                     "k2_GBps_on_item_bytes": round(k2_read / (st["k2_ms"] / 1e3) / 1e9, 1)
                     if st["k2_ms"] else None,
@@ -332,9 +391,23 @@ def main():
                      "rule_compile_s": round(compile_s, 2)},
     }
     log("timed %d steps: %.3f s" % (args.steps, dt))
+    # every step must have produced the same findings (the timed loop reads every result)
+    if len(set(step_findings)) != 1:
+        raise SystemExit("bench: findings differ between steps: %s" % step_findings)
+    line["checks"] = {"findings_per_step": step_findings[0][1],
+                      "files_with_findings_per_step": step_findings[0][0],
+                      "steps_checked": len(step_findings)}
     if rank == 0 and not args.no_cpu_baseline:
         nt = args.host_threads or 16
-        line["cpu_baseline"], line["cpu_optimised"] = cpu_baselines(sc, batch, args.cpu_mib << 20, nt)
+        exact, opt, sub, exact_bytes = cpu_baselines(sc, batch, args.cpu_mib << 20, nt)
+        line["cpu_baseline"], line["cpu_optimised"] = exact, opt
+        out = C.c_void_p()
+        N.check(L.tsg_scan_batch(ctx.handle, *sub.ptrs(), C.byref(out)))
+        if _raw(out) != exact_bytes:
+            raise SystemExit("bench: the device result of the cpu_baseline sample differs from "
+                             "the exact CPU path")
+        line["checks"]["sample_device_eq_exact_cpu"] = True
+        line["checks"]["sample_files"] = sub.nfiles
     for sid, _, _ in slots:
         ctx.release_slot(sid)
     ctx.close()

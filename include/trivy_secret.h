@@ -17,11 +17,14 @@
  *   SecretAnalyzer.Analyze per-file goroutines        tsg_queue_scan (concurrent callers
  *       analyzer/secret/secret.go:78-110,               coalesced into pinned batches),
  *       analyzer.go:419-443                             tsg_slot_* / tsg_scan_batch (batches)
+ *   per-layer goroutines over a node's GPUs           tsg_multi_* (one process, N devices)
+ *       artifact/image/image.go:210-234
  *
  * Error convention: every call returns TSG_OK (0) or a negative TSG_ERR_*; the
  * message of the last failing call on this thread is tsg_last_error().  No C++
- * exception crosses the ABI.  Every entry point is thread-safe; a tsg_ruleset is
- * immutable and may be shared by any number of threads and contexts.  The library never
+ * exception crosses the ABI.  Every entry point is thread-safe (the GPU calls name the
+ * caller's own slot and submission ticket; none acts on "the last" batch); a tsg_ruleset
+ * is immutable and may be shared by any number of threads and contexts.  The library never
  * retains a caller pointer past a call.
  *
  * Result format (tsg_result_data), little endian:
@@ -125,14 +128,22 @@ const uint8_t* tsg_result_data(const tsg_result* r, size_t* len);
 int tsg_go_sort_perm(const uint8_t* keys, const uint64_t* key_offsets, const int64_t* secondary,
                      uint32_t n, uint32_t* perm);
 void tsg_result_free(tsg_result* r);
+/* Counts of a result (bench and test checks): files, files with findings, findings. */
+int tsg_result_summary(const tsg_result* r, uint64_t* nfiles, uint64_t* files_with_findings,
+                       uint64_t* findings);
 
-/* ---- GPU (one context per device; one process per GPU) ----
+/* ---- GPU (one context per device) ----
  *
  * A context owns the rule tables on one device, two lanes (HIP stream + HBM buffers: the
  * H2D of one batch overlaps the kernels of the other), a pool of pinned host slots that
- * batches are staged in, and the host resolvers of batches in flight.  Every entry point
- * is thread-safe; the library never retains a caller pointer past a call (batch bytes are
- * copied into, or written directly by the caller into, library-owned pinned slots). */
+ * batches are staged in, and the host resolvers of batches in flight.  The library never
+ * retains a caller pointer past a call (batch bytes are copied into, or written directly
+ * by the caller into, library-owned pinned slots).
+ *
+ * Threading: every entry point below is thread-safe on a shared context.  No call acts on
+ * "the last" anything: a caller names its own slot (slot id) and its own submission
+ * (ticket), so concurrent per-layer / per-file callers (image.go:210-234,
+ * analyzer.go:419-443) never see each other's batches. */
 typedef struct tsg_ctx_options {
   uint32_t chunk_bytes;      /* bytes per lane (multiple of 16); 0 = default */
   uint32_t ext_cap;          /* max bytes a lane follows a match past its chunk; 0 = default */
@@ -143,7 +154,8 @@ typedef struct tsg_ctx_options {
                                 keyword gates are then checked on the host); 0 = 64,
                                 0xFFFFFFFF = never */
   uint32_t flags;            /* TSG_CTX_* */
-  uint32_t slot_mib;         /* default capacity of a pinned slot (tsg_queue batches); 0 = 256 */
+  uint32_t slot_mib;         /* default capacity of a pinned slot (tsg_queue batches,
+                                tsg_multi pieces); 0 = 256 */
   uint32_t max_slots;        /* pinned slots a context may hold; 0 = 16 */
 } tsg_ctx_options;
 
@@ -159,8 +171,9 @@ void tsg_ctx_destroy(tsg_ctx* ctx);
 
 /* -- Zero-copy staging: the caller packs files straight into a pinned slot -------------
  * Replaces the per-file io.ReadAll copy of SecretAnalyzer.Analyze
- * (pkg/fanal/analyzer/secret/secret.go:85): ingest writes file bytes into the slot,
- * offsets[i] / path_offsets[i] describe file i exactly as for tsg_batch_upload. */
+ * (pkg/fanal/analyzer/secret/secret.go:85): ingest writes file bytes into the slot;
+ * offsets[0] = path_offsets[0] = 0 and file i = data[offsets[i] .. offsets[i+1]),
+ * path i = paths[path_offsets[i] .. path_offsets[i+1]). */
 typedef struct tsg_slot_view {
   uint32_t id;
   uint8_t* data;            /* data_cap bytes */
@@ -171,34 +184,36 @@ typedef struct tsg_slot_view {
   uint64_t paths_cap;
   uint64_t* path_offsets;   /* files_cap + 1 */
 } tsg_slot_view;
-/* A free slot with at least these capacities (allocated or grown if needed). */
+/* A free slot with at least these capacities (allocated or grown if needed), owned by the
+ * caller until tsg_slot_release.  Waits while every slot is busy with submissions. */
 int tsg_slot_acquire(tsg_ctx* ctx, uint64_t data_bytes, uint32_t nfiles, uint64_t path_bytes,
                      tsg_slot_view* out);
-/* Submit the slot's first nfiles files (the device part runs asynchronously, the host
- * resolution follows it on the resolver pool); collect with tsg_batch_collect.  The slot
- * stays the caller's: it may be submitted again (same bytes) once earlier submissions are
- * collected or immediately (they only read it), and must not be written until they are. */
-int tsg_slot_submit(tsg_ctx* ctx, uint32_t slot_id, uint32_t nfiles);
-/* Give the slot back to the context (it becomes free when its submissions are collected). */
+/* Submit the slot's first nfiles files: the device part runs asynchronously, the host
+ * resolution follows it on the resolver pool.  *ticket names this submission for
+ * tsg_batch_collect.  The slot may be submitted again (same bytes) at once (submissions
+ * only read it) and must not be written until its submissions are collected. */
+int tsg_slot_submit(tsg_ctx* ctx, uint32_t slot_id, uint32_t nfiles, uint64_t* ticket);
+/* Give the slot back to the context (it is reused once its submissions are done). */
 int tsg_slot_release(tsg_ctx* ctx, uint32_t slot_id);
 
-/* -- Copying staging (compatibility): the batch is copied into a context-owned slot ----- */
+/* -- Copying staging: the batch is copied into a free slot, which is then the caller's
+ * (submit it with tsg_slot_submit, give it back with tsg_slot_release). */
 int tsg_batch_upload(tsg_ctx* ctx, const uint8_t* data, const uint64_t* offsets,
-                     uint32_t nfiles, const char* paths, const uint64_t* path_offsets);
-/* The device part of a scan of the last uploaded batch, synchronously, no resolution
- * (test hook: tsg_batch_k1_output then reads its keyword bits / chunk events). */
-int tsg_batch_kernels(tsg_ctx* ctx);
-/* Submit the last uploaded batch (it may be submitted again). */
-int tsg_batch_submit(tsg_ctx* ctx);
-/* Results of the oldest submitted batch (slot or upload), waiting for its resolution. */
-int tsg_batch_collect(tsg_ctx* ctx, tsg_result** out);
-/* number of submitted, uncollected batches */
+                     uint32_t nfiles, const char* paths, const uint64_t* path_offsets,
+                     uint32_t* slot_id);
+/* Results of one submission (waits for its resolution); each ticket is collected once. */
+int tsg_batch_collect(tsg_ctx* ctx, uint64_t ticket, tsg_result** out);
+/* number of submitted, uncollected tickets of the context (all callers) */
 int tsg_batch_pending(const tsg_ctx* ctx);
-/* submit + collect of the last uploaded batch */
-int tsg_batch_scan(tsg_ctx* ctx, tsg_result** out);
-/* upload + scan */
+/* One batch, synchronously: copied into a slot of its own, scanned, resolved, slot freed
+ * (the Scan of many files; thread-safe, any number of concurrent callers). */
 int tsg_scan_batch(tsg_ctx* ctx, const uint8_t* data, const uint64_t* offsets, uint32_t nfiles,
                    const char* paths, const uint64_t* path_offsets, tsg_result** out);
+/* Test hook: the device part of a scan of an acquired slot's first nfiles files,
+ * synchronously, without resolution; writes K1's keyword bits [nfiles * kw_words] and chunk
+ * event bits [ceil(bytes / chunk_bytes)] (either pointer may be NULL). */
+int tsg_batch_kernels(tsg_ctx* ctx, uint32_t slot_id, uint32_t nfiles, uint32_t* kw,
+                      size_t kw_len, uint32_t* ev, size_t ev_len);
 
 typedef struct tsg_stats {
   double k1_ms;          /* K1 literal automaton + run counters, last collected batch (HIP events) */
@@ -243,9 +258,25 @@ int tsg_queue_flush(tsg_queue* q);
 /* waits for every call in flight */
 void tsg_queue_destroy(tsg_queue* q);
 
-/* K1 output of the last tsg_batch_kernels: keyword bits [nfiles * kw_words] and chunk
- * event bits [ceil(bytes / chunk_bytes)] (test hook; either pointer may be NULL). */
-int tsg_batch_k1_output(tsg_ctx* ctx, uint32_t* kw, size_t kw_len, uint32_t* ev, size_t ev_len);
+/* -- One process, several GPUs (multi.cpp) ------------------------------------------
+ * trivy is one process: per-layer goroutines (pkg/fanal/artifact/image/image.go:210-234)
+ * and per-file goroutines (pkg/fanal/analyzer/analyzer.go:419-443) drive every GPU of the
+ * node from one address space.  tsg_multi holds one context per device (same options);
+ * tsg_multi_scan_batch shards a batch's files over them, largest first onto the least
+ * loaded device (LPT by bytes), copies each share straight into that device's pinned
+ * slots (pieces of slot_mib), and returns the results in input order (tsg_result format),
+ * identical to tsg_scan_batch on one context.  Thread-safe; no collective. */
+typedef struct tsg_multi tsg_multi;
+int tsg_multi_create(const int* devices, uint32_t n, const tsg_ruleset* rs,
+                     const tsg_ctx_options* opt, tsg_multi** out);
+int tsg_multi_size(const tsg_multi* m);
+/* the i-th device's context (owned by m; e.g. for a tsg_queue per device) */
+int tsg_multi_ctx(tsg_multi* m, uint32_t i, tsg_ctx** out);
+int tsg_multi_scan_batch(tsg_multi* m, const uint8_t* data, const uint64_t* offsets,
+                         uint32_t nfiles, const char* paths, const uint64_t* path_offsets,
+                         tsg_result** out);
+int tsg_multi_get_stats(const tsg_multi* m, uint32_t i, tsg_stats* out);
+void tsg_multi_destroy(tsg_multi* m);
 
 const char* tsg_last_error(void);
 

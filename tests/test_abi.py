@@ -23,8 +23,9 @@ def declared():
 def test_header_declares_the_boundary():
     names = declared()
     for n in ["tsg_ruleset_compile", "tsg_ruleset_allow_path", "tsg_scan_cpu", "tsg_scan_batch",
-              "tsg_ctx_create", "tsg_batch_upload", "tsg_batch_scan", "tsg_batch_submit",
-              "tsg_batch_collect", "tsg_result_data", "tsg_result_free", "tsg_last_error"]:
+              "tsg_ctx_create", "tsg_batch_upload", "tsg_slot_submit", "tsg_batch_collect",
+              "tsg_multi_create", "tsg_multi_scan_batch", "tsg_result_data", "tsg_result_free",
+              "tsg_last_error"]:
         assert n in names
 
 
@@ -61,9 +62,12 @@ def test_ctx_create_without_gpu_fails_loudly():
 
 def test_bad_arguments():
     L = N.lib()
-    assert L.tsg_batch_scan(None, None) == N.TSG_ERR_ARG
-    assert L.tsg_batch_collect(None, None) == N.TSG_ERR_ARG
+    assert L.tsg_scan_batch(None, None, None, 0, None, None, None) == N.TSG_ERR_ARG
+    assert L.tsg_batch_collect(None, 1, None) == N.TSG_ERR_ARG
+    assert L.tsg_slot_submit(None, 0, 0, None) == N.TSG_ERR_ARG
     assert L.tsg_batch_pending(None) == N.TSG_ERR_ARG
+    assert L.tsg_multi_scan_batch(None, None, None, 0, None, None, None) == N.TSG_ERR_ARG
+    assert L.tsg_result_summary(None, None, None, None) == N.TSG_ERR_ARG
 
 
 def test_go_sort_perm_matches_oracle_with_ties():

@@ -354,3 +354,64 @@ def test_source_tree_config0_gpu(tmp_path):
         n += len(want["Findings"] or [])
     assert n > 5
     assert W.analyze_fs(an, root, device=0) == W.analyze_fs(an, root)
+
+
+def test_batch_api_concurrent_callers_gpu(builtin):
+    """16 threads share one device context: tsg_scan_batch and upload + ticketed
+    submit/collect, each thread getting exactly its own batches' results (per-layer
+    goroutines, pkg/fanal/artifact/image/image.go:210-234)."""
+    import ctypes as C
+    import threading
+    from trivy_amd import _native as N
+    batches = [corpus.make_corpus((256 + 64 * (k % 7)) << 10, seed=500 + k, plants_per_mib=200)[0]
+               for k in range(48)]
+    want = [builtin.ScanBatch(b, nthreads=4) for b in batches]
+    ctx = S.GpuContext(builtin, 0, max_slots=8)
+    L = N.lib()
+    got = [None] * len(batches)
+    errors = []
+
+    def worker(k):
+        try:
+            for i in range(k, len(batches), 16):
+                b = batches[i]
+                if i % 2:
+                    got[i] = ctx.scan_batch(b)
+                    continue
+                sid, t = C.c_uint32(), C.c_uint64()
+                N.check(L.tsg_batch_upload(ctx.handle, *b.ptrs(), C.byref(sid)))
+                N.check(L.tsg_slot_submit(ctx.handle, sid.value, b.nfiles, C.byref(t)))
+                N.check(L.tsg_slot_release(ctx.handle, sid.value))
+                out = C.c_void_p()
+                N.check(L.tsg_batch_collect(ctx.handle, t.value, C.byref(out)))
+                got[i] = builtin.decode(out, [b.path(j) for j in range(b.nfiles)])
+        except Exception as e:  # pragma: no cover
+            errors.append(e)
+
+    ts = [threading.Thread(target=worker, args=(k,)) for k in range(16)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    ctx.close()
+    assert not errors, errors
+    for i in range(len(batches)):
+        assert got[i] == want[i], "batch %d" % i
+
+
+def test_multi_two_contexts_one_device_gpu(builtin):
+    """tsg_multi with two contexts on device 0 in one process (the one-GPU rehearsal of
+    the node-wide dispatcher): LPT shards, results in input order == exact CPU path, and
+    the oracle on a sample."""
+    from oracle import secret as O
+    b, _ = corpus.make_corpus(24 << 20, seed=77, plants_per_mib=40)
+    m = S.MultiGpu(builtin, [0, 0], slot_mib=4)
+    got = m.scan_batch(b)
+    per = [m.stats(i)["sum_bytes"] for i in range(2)]
+    m.close()
+    assert got == builtin.ScanBatch(b, nthreads=16)
+    assert min(per) > 0 and sum(per) == int(b.offsets[-1])
+    osc = O.NewScanner(None)
+    for i in range(0, b.nfiles, 97):
+        c = bytes(b.data[int(b.offsets[i]):int(b.offsets[i + 1])])
+        assert canon_secret(got[i]) == canon_secret(osc.Scan(b.path(i), c)), b.path(i)

@@ -7,6 +7,8 @@ import subprocess
 import sys
 import textwrap
 
+import pytest
+
 from tests.conftest import ROOT
 from trivy_amd.shard import lpt_shards
 
@@ -72,16 +74,36 @@ LAYER_WORKER = textwrap.dedent("""
     from tests.helpers import canon_secret
     from trivy_amd import analyzer as A, configs, secret as S, walker as W
     from trivy_amd.shard import scan_layer_sharded
+    rank = int(sys.argv[1])
+    device = %(device)r
+    if rank == %(fail_rank)d:  # an ingest failure on this rank alone
+        def bad(self, *a, **k):
+            raise RuntimeError("injected failure")
+        W.LayerRange.dirs = bad
     dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%(port)d",
-                            rank=int(sys.argv[1]), world_size=2)
-    tar = configs.layer_tar(1 << 20, seed=21)
+                            rank=rank, world_size=2)
+    tar = configs.layer_tar(%(nbytes)d, seed=21)
     an = A.SecretAnalyzer(S.NewScanner(None), "")
-    out = scan_layer_sharded(an, tar, dist.get_rank(), 2, dist=dist, emulate_chunk=64)
-    if dist.get_rank() == 0:
+    try:
+        out = scan_layer_sharded(an, tar, rank, 2, dist=dist, device=device,
+                                 emulate_chunk=0 if device is not None else 64)
+    except RuntimeError as e:
+        print("RAISED", e)
+        sys.exit(3)
+    if rank == 0:
         got, opq, wh = out
         want, opq2, wh2 = W.analyze_layer(an, io.BytesIO(tar))
         assert [canon_secret(s) for s in got] == [canon_secret(s) for s in want]
         assert (opq, wh) == (opq2, wh2) and len(got) > 10
+        if device is not None:  # the device union against the oracle on a sample
+            from oracle import secret as O
+            osc = O.NewScanner(None)
+            lay = W.NativeLayer(an.scanner, tar)
+            b = lay.batch
+            content = {b.path(i): bytes(b.data[int(b.offsets[i]):int(b.offsets[i + 1])])
+                       for i in range(b.nfiles)}
+            for s in got[::4]:
+                assert canon_secret(s) == canon_secret(osc.Scan(s["FilePath"], content[s["FilePath"]]))
         print("OK", len(got))
     else:
         assert out is None
@@ -89,15 +111,44 @@ LAYER_WORKER = textwrap.dedent("""
 """)
 
 
-def test_two_ranks_layer_gloo(tmp_path):
-    """configs[2]: one layer's files sharded over 2 ranks == the single-process layer scan."""
+def _run_layer_ranks(tmp_path, device=None, fail_rank=-1, nbytes=1 << 20):
     port = _free_port()
     script = tmp_path / "wl.py"
-    script.write_text(LAYER_WORKER % {"root": ROOT, "port": port})
+    script.write_text(LAYER_WORKER % {"root": ROOT, "port": port, "device": device,
+                                      "fail_rank": fail_rank, "nbytes": nbytes})
     env = dict(os.environ, MASTER_ADDR="127.0.0.1")
     procs = [subprocess.Popen([sys.executable, str(script), str(r)], cwd=ROOT, env=env,
                               stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
              for r in range(2)]
-    outs = [p.communicate(timeout=300)[0] for p in procs]
+    try:
+        outs = [p.communicate(timeout=240)[0] for p in procs]
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    return procs, outs
+
+
+def test_two_ranks_layer_gloo(tmp_path):
+    """configs[2]: one layer's files sharded over 2 ranks == the single-process layer scan."""
+    procs, outs = _run_layer_ranks(tmp_path)
+    assert all(p.returncode == 0 for p in procs), outs
+    assert "OK" in outs[0]
+
+
+def test_two_ranks_layer_error_on_one_rank(tmp_path):
+    """An ingest failure on one rank of the distributed index raises on every rank instead
+    of leaving the others waiting in a collective."""
+    procs, outs = _run_layer_ranks(tmp_path, fail_rank=1)
+    assert [p.returncode for p in procs] == [3, 3], outs
+    assert all("rank 1: injected failure" in o for o in outs), outs
+
+
+@pytest.mark.gpu
+def test_two_ranks_layer_gpu(tmp_path):
+    """configs[2] on the device: the distributed index (index="range") at world size 2 over
+    gloo, both ranks sharing the one GPU; rank 0's union == the single-process layer scan,
+    and a sample of it == the oracle."""
+    procs, outs = _run_layer_ranks(tmp_path, device=0, nbytes=6 << 20)
     assert all(p.returncode == 0 for p in procs), outs
     assert "OK" in outs[0]

@@ -120,6 +120,18 @@ def test_apply_layers_keeps_lower_layer_rules():
         ("r2", 9, "b"), ("r1", 1, "a")]
 
 
+def test_apply_layers_duplicate_lower_rule_ids():
+    """secretFindingsContains looks at the growing newSecret.Findings
+    (applier/docker.go:280-284): of a lower layer's findings [r1@1, r1@5] the upper layer
+    [r2@9] keeps only r1@1."""
+    f = lambda rule, line: {"RuleID": rule, "StartLine": line, "Code": {"Lines": None}}
+    got = R.apply_layers([
+        {"Digest": "a", "Secrets": [{"FilePath": "x", "Findings": [f("r1", 1), f("r1", 5)]}]},
+        {"Digest": "b", "Secrets": [{"FilePath": "x", "Findings": [f("r2", 9)]}]},
+    ])
+    assert [(g["RuleID"], g["StartLine"]) for g in got[0]["Findings"]] == [("r2", 9), ("r1", 1)]
+
+
 def test_go_json_string_rules():
     assert R._go_string(b"<a & b>") == '"\\u003ca \\u0026 b\\u003e"'
     assert R._go_string(b"bad \xff byte") == '"bad � byte"'

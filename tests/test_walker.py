@@ -208,6 +208,42 @@ def test_native_layer_errors(analyzer):
 
 
 @pytest.mark.gpu
+def test_native_layer_gpu_vs_oracle(analyzer):
+    """configs[2] on the device against the oracle (not the product's own CPU path): the
+    native layer ingest of a seeded layer with whiteouts, an opaque dir, system / .git /
+    node_modules trees and a --skip-dirs entry (walker/tar.go:33-86), the "/" prefix of image
+    files (analyzer/secret/secret.go:94-96), then the device scan; every 16th scanned file
+    and every file with findings == oracle Scan of the same path and content."""
+    from oracle import secret as O
+    from trivy_amd import configs
+    tar = configs.layer_tar(12 << 20, seed=36)
+    lay = W.NativeLayer(analyzer.scanner, tar, skip_dirs=["/deep"])
+    b = lay.batch
+    paths = [b.path(i) for i in range(b.nfiles)]
+    assert all(p.startswith("/") for p in paths)
+    assert not any(p.startswith(("/deep/", "/proc/", "/srv/.git/", "/app/node_modules/"))
+                   for p in paths)
+    assert lay.wh and lay.opq
+    got = analyzer.scanner.ScanBatch(b, device=0)
+    osc = O.NewScanner(None)
+    checked = nfind = 0
+    for i in range(b.nfiles):
+        if i % 16 and not got[i]["Findings"]:
+            continue
+        c = bytes(b.data[int(b.offsets[i]):int(b.offsets[i + 1])])
+        want = canon_secret(osc.Scan(paths[i], c))
+        assert canon_secret(got[i]) == want, paths[i]
+        checked += 1
+        nfind += len(want["Findings"] or [])
+    assert checked > 200 and nfind > 100
+    # the walker's view of the same layer (whiteouts, opaque dirs, kept files) is the oracle's
+    want_files = []
+    opq, wh = W.LayerTar(skip_dirs=["/deep"]).Walk(io.BytesIO(tar), lambda p, n, rd: (
+        analyzer.Required(p, n) and not A.IsBinary(c := rd(), n) and want_files.append("/" + p)))
+    assert paths == want_files and (lay.opq, lay.wh) == (opq, wh)
+
+
+@pytest.mark.gpu
 def test_native_layer_gpu(analyzer):
     from trivy_amd import configs
     tar = configs.layer_tar(16 << 20, seed=34)

@@ -99,24 +99,31 @@ SIGNATURES = [
                                      C.POINTER(_P)]),
     ("tsg_result_data", _P, [_P, C.POINTER(C.c_size_t)]),
     ("tsg_result_free", None, [_P]),
+    ("tsg_result_summary", C.c_int, [_P, _U64P, _U64P, _U64P]),
     ("tsg_ctx_create", C.c_int, [C.c_int, _P, C.POINTER(CtxOptions), C.POINTER(_P)]),
     ("tsg_ctx_destroy", None, [_P]),
-    ("tsg_batch_upload", C.c_int, [_P, _P, _U64P, C.c_uint32, _P, _U64P]),
-    ("tsg_batch_scan", C.c_int, [_P, C.POINTER(_P)]),
-    ("tsg_batch_kernels", C.c_int, [_P]),
-    ("tsg_batch_submit", C.c_int, [_P]),
-    ("tsg_batch_collect", C.c_int, [_P, C.POINTER(_P)]),
+    ("tsg_batch_upload", C.c_int, [_P, _P, _U64P, C.c_uint32, _P, _U64P, C.POINTER(C.c_uint32)]),
+    ("tsg_batch_kernels", C.c_int, [_P, C.c_uint32, C.c_uint32, C.POINTER(C.c_uint32), C.c_size_t,
+                                    C.POINTER(C.c_uint32), C.c_size_t]),
+    ("tsg_batch_collect", C.c_int, [_P, C.c_uint64, C.POINTER(_P)]),
     ("tsg_batch_pending", C.c_int, [_P]),
     ("tsg_scan_batch", C.c_int, [_P, _P, _U64P, C.c_uint32, _P, _U64P, C.POINTER(_P)]),
     ("tsg_ctx_get_stats", C.c_int, [_P, C.POINTER(Stats)]),
     ("tsg_slot_acquire", C.c_int, [_P, C.c_uint64, C.c_uint32, C.c_uint64, C.POINTER(SlotView)]),
-    ("tsg_slot_submit", C.c_int, [_P, C.c_uint32, C.c_uint32]),
+    ("tsg_slot_submit", C.c_int, [_P, C.c_uint32, C.c_uint32, _U64P]),
     ("tsg_slot_release", C.c_int, [_P, C.c_uint32]),
     ("tsg_queue_create", C.c_int, [_P, C.c_uint32, C.POINTER(_P)]),
     ("tsg_queue_scan", C.c_int, [_P, C.c_char_p, C.c_size_t, C.c_char_p, C.c_size_t,
                                  C.POINTER(_P)]),
     ("tsg_queue_flush", C.c_int, [_P]),
     ("tsg_queue_destroy", None, [_P]),
+    ("tsg_multi_create", C.c_int, [C.POINTER(C.c_int), C.c_uint32, _P, C.POINTER(CtxOptions),
+                                   C.POINTER(_P)]),
+    ("tsg_multi_size", C.c_int, [_P]),
+    ("tsg_multi_ctx", C.c_int, [_P, C.c_uint32, C.POINTER(_P)]),
+    ("tsg_multi_scan_batch", C.c_int, [_P, _P, _U64P, C.c_uint32, _P, _U64P, C.POINTER(_P)]),
+    ("tsg_multi_get_stats", C.c_int, [_P, C.c_uint32, C.POINTER(Stats)]),
+    ("tsg_multi_destroy", None, [_P]),
     ("tsg_last_error", C.c_char_p, []),
     ("tsg_regex_compile", C.c_int, [C.c_char_p, C.POINTER(_P), C.c_char_p, C.c_size_t]),
     ("tsg_regex_free", None, [_P]),
@@ -132,8 +139,6 @@ SIGNATURES = [
                                               _U64P]),
     ("tsg_ruleset_rule_plan", C.c_int, [_P, C.c_uint32, C.POINTER(C.c_int32),
                                         C.POINTER(C.c_int32), C.POINTER(C.c_int64)]),
-    ("tsg_batch_k1_output", C.c_int, [_P, C.POINTER(C.c_uint32), C.c_size_t,
-                                      C.POINTER(C.c_uint32), C.c_size_t]),
     ("tsg_emulate_k1", C.c_int, [_P, _P, _U64P, C.c_uint32, C.c_uint32, C.POINTER(C.c_uint32),
                                  C.c_size_t, C.POINTER(C.c_uint32), C.c_size_t]),
     ("tsg_layer_pack", C.c_int, [_P, _P, C.c_uint64, C.POINTER(C.c_char_p), C.c_uint32,

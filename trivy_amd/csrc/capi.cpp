@@ -331,6 +331,28 @@ const uint8_t* tsg_result_data(const tsg_result* r, size_t* len) {
 
 void tsg_result_free(tsg_result* r) { delete r; }
 
+int tsg_result_summary(const tsg_result* r, uint64_t* nfiles, uint64_t* files_with_findings,
+                       uint64_t* findings) {
+  if (!r) return fail(TSG_ERR_ARG, "bad argument");
+  try {
+    std::vector<size_t> rec;
+    result_record_spans(r->buf, &rec);
+    uint64_t ff = 0, nf = 0;
+    for (size_t i = 0; i + 1 < rec.size(); i++) {
+      uint32_t k;
+      std::memcpy(&k, r->buf.data() + rec[i] + 1, 4);
+      ff += k > 0;
+      nf += k;
+    }
+    if (nfiles) *nfiles = rec.size() - 1;
+    if (files_with_findings) *files_with_findings = ff;
+    if (findings) *findings = nf;
+    return TSG_OK;
+  } catch (const std::exception& ex) {
+    return fail(TSG_ERR_ARG, ex.what());
+  }
+}
+
 // ---- test hooks
 struct tsg_regex {
   std::shared_ptr<Regexp> re;

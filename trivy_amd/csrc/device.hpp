@@ -83,5 +83,8 @@ int enqueue_scan(DeviceRules* d, LaneState* l, const ScanInput& in, HostOut* out
 int batch_times(const HostOut* out, ScanTimes* t);
 // K1 output of the lane's last batch (test hook): chunk events [nchunks]
 int lane_events(LaneState* l, uint32_t* ev, size_t n);
+// K2 per-entry trace of the lane's last batch (TSG_K2_TRACE; empty otherwise): per entry
+// {start, end, group << 32 | items, XCC_ID << 32 | HW_ID}
+int lane_k2_trace(LaneState* l, std::vector<unsigned long long>* out);
 
 }  // namespace tsg

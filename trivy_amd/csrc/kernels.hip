@@ -1064,6 +1064,9 @@ struct K2Args {
   uint8_t* ovf;
   uint32_t* diag;  // null, or [4]: tail bytes, longest tail, tails over 4 KiB, word replays
   uint32_t* claim;  // [2] next list / dense entry (zeroed per batch)
+  // null, or per entry {start, end (wall clock, 100 MHz), group << 32 | items,
+  // XCC_ID << 32 | HW_ID} written by the block that ran it (TSG_K2_TRACE)
+  unsigned long long* etrace;
 };
 
 // Candidate emission, wave-aggregated: the lanes that reach an accept together reserve
@@ -1432,11 +1435,24 @@ __device__ __forceinline__ void k2_run(const DevDFA* __restrict__ dfas, const K2
                                        uint32_t E, uint32_t* claim, uint8_t* smem) {
   __shared__ uint32_t s_e;
   uint32_t staged = 0xFFFFFFFFu;
+  uint32_t prev = 0xFFFFFFFFu;  // the entry this block ran last (trace)
   for (;;) {
     if (threadIdx.x == 0) s_e = atomicAdd(claim, 1u);
     __syncthreads();
     const uint32_t e = s_e;
     __syncthreads();  // every lane has read s_e (and is done with the previous entry)
+    if (!DENSE && A.etrace && threadIdx.x == 0) {  // trace: the previous entry ends, this one starts
+      const unsigned long long now = wall_clock64();
+      if (prev != 0xFFFFFFFFu) A.etrace[(size_t)prev * 4 + 1] = now;
+      if (e < E) {
+        const uint4 en = entries[e];
+        A.etrace[(size_t)e * 4 + 0] = now;
+        A.etrace[(size_t)e * 4 + 2] = ((unsigned long long)en.x << 32) | en.z;
+        A.etrace[(size_t)e * 4 + 3] = ((unsigned long long)__builtin_amdgcn_s_getreg(20 | (15 << 11)) << 32) |
+                                      (uint32_t)__builtin_amdgcn_s_getreg(4 | (31 << 11));
+      }
+    }
+    prev = e;
     if (e >= E) break;
     const uint4 en = entries[e];
     const uint32_t g = __builtin_amdgcn_readfirstlane(en.x);
@@ -1819,13 +1835,15 @@ struct LaneState {
   uint64_t* base = nullptr;     // [G]
   uint8_t* kind = nullptr;      // [G]
   uint8_t* gskip = nullptr;     // [G]
+  unsigned long long* etrace = nullptr;  // [entries_cap * 4] K2 entry trace (TSG_K2_TRACE)
+  size_t etrace_cap = 0;
   uint64_t nchunks = 0;         // last batch
   ~LaneState() {
     if (!d) return;
     (void)hipSetDevice(d->device);
     if (st) (void)hipStreamSynchronize(st);
     void* bufs[] = {data_alloc, off, chunk_file, ev_bits, xlist, xcount, evlist, kw, ggate, ovf, paths, poff, pathok,
-                    items, entries, dentries, cand, counts, gcount, cursor, base, kind, gskip};
+                    items, entries, dentries, cand, counts, gcount, cursor, base, kind, gskip, etrace};
     for (void* b : bufs) (void)hipFree(b);
     if (st) (void)hipStreamDestroy(st);
   }
@@ -2301,6 +2319,10 @@ int enqueue_scan(DeviceRules* r, LaneState* l, const ScanInput& in, HostOut* out
     static const bool diag = getenv("TSG_K2_DIAG") != nullptr;
     A.diag = diag ? l->counts + 8 : nullptr;
     A.claim = l->counts + 12;
+    static const bool trace = getenv("TSG_K2_TRACE") != nullptr;
+    if (trace && (rc = ensure(&l->etrace, &l->etrace_cap, (size_t)entries_cap * 4))) return rc;
+    if (trace) HIP_TRY(hipMemsetAsync(l->etrace, 0, sizeof(unsigned long long) * entries_cap * 4, st));
+    A.etrace = trace ? l->etrace : nullptr;
     // one block per resident slot (the grids are persistent)
     hipLaunchKernelGGL(k2_kernel, dim3(r->k2_grid), dim3(kBlock), r->max_lds, st, (const DevDFA*)r->d_groups, A);
     HIP_TRY(hipGetLastError());
@@ -2335,6 +2357,19 @@ int batch_times(const HostOut* o, ScanTimes* t) {
   t->gates = x[3];
   t->k2 = x[4];
   t->d2h = x[5];
+  return TSG_OK;
+}
+
+int lane_k2_trace(LaneState* l, std::vector<unsigned long long>* out) {
+  HIP_TRY(hipSetDevice(l->d->device));
+  HIP_TRY(hipStreamSynchronize(l->st));
+  out->clear();
+  if (!l->etrace) return TSG_OK;
+  uint32_t counts[16];
+  HIP_TRY(hipMemcpy(counts, l->counts, sizeof(counts), hipMemcpyDeviceToHost));
+  const size_t n = std::min<size_t>((size_t)counts[2] * 4, l->etrace_cap);
+  out->resize(n);
+  if (n) HIP_TRY(hipMemcpy(out->data(), l->etrace, n * sizeof(unsigned long long), hipMemcpyDeviceToHost));
   return TSG_OK;
 }
 

@@ -18,10 +18,12 @@
 #include <algorithm>
 #include <chrono>
 #include <condition_variable>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <deque>
-#include <future>
+#include <functional>
+#include <map>
 #include <memory>
 #include <mutex>
 #include <thread>
@@ -56,6 +58,7 @@ struct Slot {
   bool pinned = false;
   int inflight = 0;  // submissions whose host job has not finished
   int owner = kFree;
+  std::thread::id holder;  // thread that took it (kCaller / kUpload)
   uint32_t nfiles = 0;
 };
 
@@ -66,7 +69,12 @@ struct Batch {
   uint64_t bytes = 0;
   int out = -1;          // HostOut index (device mode)
   bool keep_result = false;  // queue: keep the BatchResult instead of serializing
-  std::future<void> fut;
+  uint64_t ticket = 0;
+  // completion: set by the batch's job thread once its results (or error) are final
+  std::mutex dm;
+  std::condition_variable dcv;
+  bool done = false;
+  std::function<void(const std::shared_ptr<Batch>&)> on_done;  // called after `done`
   int rc = TSG_OK;
   std::string err;
   std::unique_ptr<tsg_result> res;
@@ -98,15 +106,9 @@ struct tsg_ctx {
   std::vector<std::unique_ptr<Slot>> slots;
   std::vector<HostOut> outs;
   std::vector<char> out_busy;
-  std::deque<std::shared_ptr<Batch>> pending;  // tsg_batch_collect order
-  int jobs = 0;                                // host jobs running (any API)
-  int uploaded = -1;
-  // tsg_batch_kernels (test hook) output
-  int kernels_out = -1;
-  LaneState* kernels_lane = nullptr;
-  uint32_t kernels_nfiles = 0;
-  KernelOutput kernels_emu;
-  std::vector<uint32_t> kernels_emu_ev;
+  std::map<uint64_t, std::shared_ptr<Batch>> pending;  // submitted, uncollected, by ticket
+  uint64_t next_ticket = 1;
+  int jobs = 0;                                // host job threads running (any API)
   tsg_stats stats{};
 
   ~tsg_ctx() {
@@ -198,14 +200,17 @@ int slot_take(tsg_ctx* c, std::unique_lock<std::mutex>& lk, int owner, uint64_t 
       int rc = slot_reserve(c, c->slots[pick].get(), bytes, files, pbytes);
       if (rc) return rc;
       c->slots[pick]->owner = owner;
+      c->slots[pick]->holder = std::this_thread::get_id();
       *id = (uint32_t)pick;
       return TSG_OK;
     }
-    // nothing will free a slot if no job is running and no queue batch is being filled
-    // (a queue batch's slot is submitted as soon as its last writer is done)
-    bool queue_held = false;
-    for (const auto& sl : c->slots) queue_held |= sl->owner == kQueue;
-    if (c->jobs == 0 && !queue_held) return fail(TSG_ERR_ARG, "every pinned slot is held by the caller");
+    // nothing will free a slot if no job is running and every slot is held by this very
+    // thread (a queue batch's slot is submitted as soon as its last writer is done; other
+    // threads release theirs)
+    bool others = false;
+    const auto me = std::this_thread::get_id();
+    for (const auto& sl : c->slots) others |= sl->owner == kQueue || (sl->owner != kFree && sl->holder != me);
+    if (c->jobs == 0 && !others) return fail(TSG_ERR_ARG, "every pinned slot is held by the caller");
     c->cv.wait(lk);
   }
 }
@@ -323,16 +328,34 @@ void run_job(tsg_ctx* c, std::shared_ptr<Batch> b, BatchView view, HostOut ho,
     b->rc = c->emulate ? TSG_ERR_INTERNAL : TSG_ERR_GPU;
     b->err = ex.what();
   }
+  {  // the slot may be reused and the pinned outputs retaken from here on
+    std::lock_guard<std::mutex> g(c->m);
+    c->slots[b->slot]->inflight--;
+    if (b->out >= 0) c->out_busy[b->out] = 0;
+    if (b->rc == TSG_OK) update_stats(c, *b);
+    c->cv.notify_all();
+  }
+  {
+    std::lock_guard<std::mutex> g(b->dm);
+    b->done = true;
+  }
+  b->dcv.notify_all();
+  if (b->on_done) {  // moved out first: a callback holding the batch's owner is no cycle
+    auto cb = std::move(b->on_done);
+    b->on_done = nullptr;
+    cb(b);
+  }
+  b.reset();  // (the last reference may be this thread's)
   std::lock_guard<std::mutex> g(c->m);
-  c->slots[b->slot]->inflight--;
-  if (b->out >= 0) c->out_busy[b->out] = 0;
-  if (b->rc == TSG_OK) update_stats(c, *b);
-  c->jobs--;
+  c->jobs--;  // after this the context may be destroyed: nothing below touches it
   c->cv.notify_all();
 }
 
-// submit nfiles files of slot `sid` (lock held)
-int submit_locked(tsg_ctx* c, uint32_t sid, uint32_t nfiles, bool keep_result, std::shared_ptr<Batch>* out) {
+// submit nfiles files of slot `sid` (lock held); the job runs on a thread of its own,
+// which mostly waits for the lane's completion event (the resolution itself fans out on
+// the process-wide pool)
+int submit_locked(tsg_ctx* c, uint32_t sid, uint32_t nfiles, bool keep_result,
+                  std::function<void(const std::shared_ptr<Batch>&)> on_done, std::shared_ptr<Batch>* out) {
   Slot& s = *c->slots[sid];
   int rc = check_layout(s, nfiles);
   if (rc) return rc;
@@ -341,6 +364,7 @@ int submit_locked(tsg_ctx* c, uint32_t sid, uint32_t nfiles, bool keep_result, s
   b->nfiles = nfiles;
   b->bytes = s.off[nfiles];
   b->keep_result = keep_result;
+  b->on_done = std::move(on_done);
   BatchView view{s.data, s.off, nfiles, s.paths, s.poff};
   HostOut ho;
   std::shared_ptr<const std::vector<uint8_t>> kwu;
@@ -358,20 +382,25 @@ int submit_locked(tsg_ctx* c, uint32_t sid, uint32_t nfiles, bool keep_result, s
   s.inflight++;
   c->jobs++;
   try {
-    b->fut = std::async(std::launch::async, run_job, c, b, view, ho, kwu);
-  } catch (const std::exception& ex) {
+    std::thread(run_job, c, b, view, ho, kwu).detach();
+  } catch (const std::exception& ex) {  // no thread: the enqueued device work is waited for here
     s.inflight--;
     c->jobs--;
-    if (b->out >= 0) c->out_busy[b->out] = 0;
-    return fail(TSG_ERR_INTERNAL, ex.what());
+    if (b->out >= 0) {
+      (void)hipEventSynchronize(ho.ev[kEvDone]);
+      c->out_busy[b->out] = 0;
+    }
+    return fail(TSG_ERR_INTERNAL, std::string("cannot start a batch job: ") + ex.what());
   }
+  b->ticket = c->next_ticket++;
   *out = b;
   return TSG_OK;
 }
 
 // wait for a submission's job; its result
-int finish(std::shared_ptr<Batch> b) {
-  b->fut.wait();
+int finish(const std::shared_ptr<Batch>& b) {
+  std::unique_lock<std::mutex> lk(b->dm);
+  b->dcv.wait(lk, [&] { return b->done; });
   if (b->rc) return fail(b->rc, b->err);
   return TSG_OK;
 }
@@ -435,20 +464,28 @@ struct tsg_queue {
   std::thread flusher;
   bool stop = false;
   int calls = 0;                       // tsg_queue_scan calls in progress
-  std::vector<std::thread> waiters;    // one per submitted batch (joined at destroy)
 };
 
 namespace tsg {
 namespace {
 
-// submit a sealed batch whose writers are done (q->m held)
+// submit a sealed batch whose writers are done (q->m held); its job marks the QBatch
+// ready, which wakes the batch's callers
 void q_submit(tsg_queue* q, std::shared_ptr<OpenBatch> ob) {
   auto qb = ob->qb;
   std::shared_ptr<Batch> b;
   int rc;
+  auto ready = [qb](const std::shared_ptr<Batch>& done) {
+    std::lock_guard<std::mutex> g(qb->m);
+    qb->b = done;
+    qb->rc = done->rc;
+    qb->err = done->err;
+    qb->ready = true;
+    qb->cv.notify_all();
+  };
   {
     std::lock_guard<std::mutex> g(q->c->m);
-    rc = submit_locked(q->c, ob->slot, ob->nfiles, true, &b);
+    rc = submit_locked(q->c, ob->slot, ob->nfiles, true, ready, &b);
     q->c->slots[ob->slot]->owner = kFree;  // free once its job is done
     q->c->cv.notify_all();
   }
@@ -458,17 +495,7 @@ void q_submit(tsg_queue* q, std::shared_ptr<OpenBatch> ob) {
     qb->err = tsg_last_error();
     qb->ready = true;
     qb->cv.notify_all();
-    return;
   }
-  q->waiters.emplace_back([qb, b]() {
-    b->fut.wait();
-    std::lock_guard<std::mutex> g(qb->m);
-    qb->b = b;
-    qb->rc = b->rc;
-    qb->err = b->err;
-    qb->ready = true;
-    qb->cv.notify_all();
-  });
 }
 
 // no more files for this batch; submitted as soon as its last writer is done (q->m held)
@@ -551,15 +578,16 @@ int tsg_slot_acquire(tsg_ctx* c, uint64_t data_bytes, uint32_t nfiles, uint64_t 
   });
 }
 
-int tsg_slot_submit(tsg_ctx* c, uint32_t slot_id, uint32_t nfiles) {
-  if (!c) return fail(TSG_ERR_ARG, "bad argument");
+int tsg_slot_submit(tsg_ctx* c, uint32_t slot_id, uint32_t nfiles, uint64_t* ticket) {
+  if (!c || !ticket) return fail(TSG_ERR_ARG, "bad argument");
   return guard([&]() -> int {
     std::lock_guard<std::mutex> g(c->m);
     if (slot_id >= c->slots.size() || c->slots[slot_id]->owner != kCaller) return fail(TSG_ERR_ARG, "not an acquired slot");
     std::shared_ptr<Batch> b;
-    int rc = submit_locked(c, slot_id, nfiles, false, &b);
+    int rc = submit_locked(c, slot_id, nfiles, false, nullptr, &b);
     if (rc) return rc;
-    c->pending.push_back(b);
+    c->pending.emplace(b->ticket, b);
+    *ticket = b->ticket;
     return TSG_OK;
   });
 }
@@ -573,63 +601,52 @@ int tsg_slot_release(tsg_ctx* c, uint32_t slot_id) {
   return TSG_OK;
 }
 
-int tsg_batch_upload(tsg_ctx* c, const uint8_t* data, const uint64_t* offsets, uint32_t nfiles, const char* paths,
-                     const uint64_t* path_offsets) {
-  if (!c || !offsets || !path_offsets) return fail(TSG_ERR_ARG, "bad argument");
+namespace tsg {
+namespace {
+// a free slot owned by `owner` holding a copy of the caller's batch
+int upload_into_slot(tsg_ctx* c, int owner, const uint8_t* data, const uint64_t* offsets, uint32_t nfiles,
+                     const char* paths, const uint64_t* path_offsets, uint32_t* id) {
+  if (!offsets || !path_offsets) return fail(TSG_ERR_ARG, "bad argument");
   if (offsets[0] != 0 || path_offsets[0] != 0) return fail(TSG_ERR_ARG, "offsets[0] must be 0");
   for (uint32_t i = 0; i < nfiles; i++)
     if (offsets[i + 1] < offsets[i] || path_offsets[i + 1] < path_offsets[i])
       return fail(TSG_ERR_ARG, "offsets must be non-decreasing");
   const uint64_t total = offsets[nfiles], pbytes = path_offsets[nfiles];
   if ((total && !data) || (pbytes && !paths)) return fail(TSG_ERR_ARG, "bad argument");
-  return guard([&]() -> int {
-    uint32_t id;
-    Slot* sp;
-    {
-      std::unique_lock<std::mutex> lk(c->m);
-      if (c->uploaded >= 0) {  // the previous upload's slot is free once its submissions finish
-        c->slots[c->uploaded]->owner = kFree;
-        c->uploaded = -1;
-        c->cv.notify_all();
-      }
-      int rc = slot_take(c, lk, kUpload, total, nfiles, pbytes, &id);
-      if (rc) return rc;
-      sp = c->slots[id].get();
-    }
-    Slot& s = *sp;
-    parallel_copy(s.data, data, total, c->nt);
-    std::memcpy(s.off, offsets, sizeof(uint64_t) * ((size_t)nfiles + 1));
-    std::memcpy(s.paths, paths ? paths : "", pbytes);
-    std::memcpy(s.poff, path_offsets, sizeof(uint64_t) * ((size_t)nfiles + 1));
-    s.nfiles = nfiles;
-    std::lock_guard<std::mutex> g(c->m);
-    c->uploaded = (int)id;
-    return TSG_OK;
-  });
-}
-
-int tsg_batch_submit(tsg_ctx* c) {
-  if (!c) return fail(TSG_ERR_ARG, "bad argument");
-  return guard([&]() -> int {
-    std::lock_guard<std::mutex> g(c->m);
-    if (c->uploaded < 0) return fail(TSG_ERR_ARG, "no batch uploaded");
-    std::shared_ptr<Batch> b;
-    int rc = submit_locked(c, (uint32_t)c->uploaded, c->slots[c->uploaded]->nfiles, false, &b);
+  Slot* sp;
+  {
+    std::unique_lock<std::mutex> lk(c->m);
+    int rc = slot_take(c, lk, owner, total, nfiles, pbytes, id);
     if (rc) return rc;
-    c->pending.push_back(b);
-    return TSG_OK;
-  });
+    sp = c->slots[*id].get();
+  }
+  Slot& s = *sp;  // ours alone until it is submitted
+  parallel_copy(s.data, data, total, c->nt);
+  std::memcpy(s.off, offsets, sizeof(uint64_t) * ((size_t)nfiles + 1));
+  if (pbytes) std::memcpy(s.paths, paths, pbytes);
+  std::memcpy(s.poff, path_offsets, sizeof(uint64_t) * ((size_t)nfiles + 1));
+  s.nfiles = nfiles;
+  return TSG_OK;
+}
+}  // namespace
+}  // namespace tsg
+
+int tsg_batch_upload(tsg_ctx* c, const uint8_t* data, const uint64_t* offsets, uint32_t nfiles, const char* paths,
+                     const uint64_t* path_offsets, uint32_t* slot_id) {
+  if (!c || !slot_id) return fail(TSG_ERR_ARG, "bad argument");
+  return guard([&]() -> int { return upload_into_slot(c, kCaller, data, offsets, nfiles, paths, path_offsets, slot_id); });
 }
 
-int tsg_batch_collect(tsg_ctx* c, tsg_result** out) {
+int tsg_batch_collect(tsg_ctx* c, uint64_t ticket, tsg_result** out) {
   if (!c || !out) return fail(TSG_ERR_ARG, "bad argument");
   return guard([&]() -> int {
     std::shared_ptr<Batch> b;
     {
       std::lock_guard<std::mutex> g(c->m);
-      if (c->pending.empty()) return fail(TSG_ERR_ARG, "no submitted batch");
-      b = c->pending.front();
-      c->pending.pop_front();
+      auto it = c->pending.find(ticket);
+      if (it == c->pending.end()) return fail(TSG_ERR_ARG, "no such submitted batch (unknown or already collected ticket)");
+      b = it->second;
+      c->pending.erase(it);
     }
     int rc = finish(b);
     if (rc) return rc;
@@ -644,77 +661,78 @@ int tsg_batch_pending(const tsg_ctx* c) {
   return (int)c->pending.size();
 }
 
-int tsg_batch_scan(tsg_ctx* c, tsg_result** out) {
-  if (!c || !out) return fail(TSG_ERR_ARG, "bad argument");
-  {
-    std::lock_guard<std::mutex> g(c->m);
-    if (!c->pending.empty()) return fail(TSG_ERR_ARG, "collect the submitted batches first");
-  }
-  int rc = tsg_batch_submit(c);
-  if (rc) return rc;
-  return tsg_batch_collect(c, out);
-}
-
 int tsg_scan_batch(tsg_ctx* c, const uint8_t* data, const uint64_t* offsets, uint32_t nfiles, const char* paths,
                    const uint64_t* path_offsets, tsg_result** out) {
-  int rc = tsg_batch_upload(c, data, offsets, nfiles, paths, path_offsets);
-  if (rc) return rc;
-  return tsg_batch_scan(c, out);
-}
-
-int tsg_batch_kernels(tsg_ctx* c) {
-  if (!c) return fail(TSG_ERR_ARG, "bad argument");
+  if (!c || !out) return fail(TSG_ERR_ARG, "bad argument");
   return guard([&]() -> int {
-    std::unique_lock<std::mutex> lk(c->m);
-    if (c->uploaded < 0) return fail(TSG_ERR_ARG, "no batch uploaded");
-    Slot& s = *c->slots[c->uploaded];
-    const uint32_t F = s.nfiles;
-    BatchView view{s.data, s.off, F, s.paths, s.poff};
-    if (c->emulate) {
-      emulate_kernels(*c->rs->plan, view, c->opt.chunk_bytes, c->opt.ext_cap, &c->kernels_emu);
-      k1_reference(*c->rs->plan, view, c->opt.chunk_bytes, &c->kernels_emu.kw, &c->kernels_emu_ev);
-      c->kernels_nfiles = F;
-      return TSG_OK;
+    uint32_t id;
+    int rc = upload_into_slot(c, kUpload, data, offsets, nfiles, paths, path_offsets, &id);
+    if (rc) return rc;
+    std::shared_ptr<Batch> b;
+    {
+      std::lock_guard<std::mutex> g(c->m);
+      rc = submit_locked(c, id, nfiles, false, nullptr, &b);
+      c->slots[id]->owner = kFree;  // reusable once its submission is done
+      c->cv.notify_all();
     }
-    if (c->kernels_out >= 0) c->out_busy[c->kernels_out] = 0;
-    c->kernels_out = -1;
-    int oi, rc;
-    if ((rc = out_take(c, F, &oi))) return rc;
-    LaneState* l = c->lanes[c->seq++ % c->lanes.size()];
-    ScanInput in{s.data, s.off, F, s.off[F], s.paths, s.poff};
-    if ((rc = enqueue_scan(c->dr, l, in, &c->outs[oi]))) {
-      c->out_busy[oi] = 0;
-      return rc;
-    }
-    c->kernels_out = oi;
-    c->kernels_lane = l;
-    c->kernels_nfiles = F;
-    HostOut ho = c->outs[oi];
-    lk.unlock();
-    HIP_TRY(hipEventSynchronize(ho.ev[kEvDone]));
-    Batch b;
-    (void)batch_times(&ho, &b.t);
-    std::memcpy(b.counts, ho.counts, sizeof(b.counts));
-    b.bytes = s.off[F];
-    lk.lock();
-    update_stats(c, b);
+    if (rc) return rc;
+    if ((rc = finish(b))) return rc;
+    *out = b->res.release();
     return TSG_OK;
   });
 }
 
-int tsg_batch_k1_output(tsg_ctx* c, uint32_t* kw, size_t kw_len, uint32_t* ev, size_t ev_len) {
+int tsg_batch_kernels(tsg_ctx* c, uint32_t slot_id, uint32_t nfiles, uint32_t* kw, size_t kw_len, uint32_t* ev,
+                      size_t ev_len) {
   if (!c) return fail(TSG_ERR_ARG, "bad argument");
-  std::lock_guard<std::mutex> g(c->m);
-  const size_t W = (size_t)c->rs->plan->kw_words;
-  if (c->emulate) {
-    if (kw) std::memcpy(kw, c->kernels_emu.kw.data(), sizeof(uint32_t) * std::min(kw_len, c->kernels_emu.kw.size()));
-    if (ev) std::memcpy(ev, c->kernels_emu_ev.data(), sizeof(uint32_t) * std::min(ev_len, c->kernels_emu_ev.size()));
-    return TSG_OK;
-  }
-  if (c->kernels_out < 0) return fail(TSG_ERR_ARG, "no tsg_batch_kernels output");
-  if (kw) std::memcpy(kw, c->outs[c->kernels_out].kw, sizeof(uint32_t) * std::min(kw_len, W * c->kernels_nfiles));
-  if (ev) return lane_events(c->kernels_lane, ev, ev_len);
-  return TSG_OK;
+  return guard([&]() -> int {
+    // the whole call holds the context lock: no other batch can be enqueued on the lane
+    // before its event buffer is read back
+    std::lock_guard<std::mutex> g(c->m);
+    if (slot_id >= c->slots.size() || c->slots[slot_id]->owner != kCaller) return fail(TSG_ERR_ARG, "not an acquired slot");
+    Slot& s = *c->slots[slot_id];
+    int rc = check_layout(s, nfiles);
+    if (rc) return rc;
+    const size_t W = (size_t)c->rs->plan->kw_words;
+    BatchView view{s.data, s.off, nfiles, s.paths, s.poff};
+    if (c->emulate) {
+      std::vector<uint32_t> kwv, evv;
+      k1_reference(*c->rs->plan, view, c->opt.chunk_bytes, &kwv, &evv);
+      if (kw) std::memcpy(kw, kwv.data(), sizeof(uint32_t) * std::min(kw_len, kwv.size()));
+      if (ev) std::memcpy(ev, evv.data(), sizeof(uint32_t) * std::min(ev_len, evv.size()));
+      return TSG_OK;
+    }
+    int oi;
+    if ((rc = out_take(c, nfiles, &oi))) return rc;
+    LaneState* l = c->lanes[c->seq++ % c->lanes.size()];
+    ScanInput in{s.data, s.off, nfiles, s.off[nfiles], s.paths, s.poff};
+    if ((rc = enqueue_scan(c->dr, l, in, &c->outs[oi]))) {
+      c->out_busy[oi] = 0;
+      return rc;
+    }
+    HostOut ho = c->outs[oi];
+    hipError_t e = hipEventSynchronize(ho.ev[kEvDone]);
+    if (e == hipSuccess) {
+      Batch b;
+      (void)batch_times(&ho, &b.t);
+      std::memcpy(b.counts, ho.counts, sizeof(b.counts));
+      b.bytes = s.off[nfiles];
+      update_stats(c, b);
+      if (kw) std::memcpy(kw, ho.kw, sizeof(uint32_t) * std::min(kw_len, W * nfiles));
+      if (ev) rc = lane_events(l, ev, ev_len);
+      if (const char* tp = getenv("TSG_K2_TRACE")) {  // append the K2 entry trace (measurements)
+        std::vector<unsigned long long> tr;
+        if (!rc) rc = lane_k2_trace(l, &tr);
+        if (FILE* f = tr.empty() ? nullptr : fopen(tp, "ab")) {
+          fwrite(tr.data(), sizeof(unsigned long long), tr.size(), f);
+          fclose(f);
+        }
+      }
+    }
+    c->out_busy[oi] = 0;
+    if (e != hipSuccess) return fail(TSG_ERR_GPU, std::string("tsg_batch_kernels: ") + hipGetErrorString(e));
+    return rc;
+  });
 }
 
 int tsg_ctx_get_stats(const tsg_ctx* c, tsg_stats* out) {
@@ -850,7 +868,6 @@ void tsg_queue_destroy(tsg_queue* q) {
     q->cv.notify_all();
   }
   q->flusher.join();
-  for (auto& t : q->waiters) t.join();
   if (q->open) {  // opened, never filled
     std::lock_guard<std::mutex> g(q->c->m);
     q->c->slots[q->open->slot]->owner = kFree;

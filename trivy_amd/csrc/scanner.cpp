@@ -825,4 +825,36 @@ void serialize_results(const std::vector<FileResult>& res, std::string* out) {
   }
 }
 
+static uint32_t rd_u32(const std::string& b, size_t& p) {
+  if (p + 4 > b.size()) throw std::runtime_error("truncated result");
+  uint32_t v;
+  std::memcpy(&v, b.data() + p, 4);
+  p += 4;
+  return v;
+}
+
+void result_record_spans(const std::string& b, std::vector<size_t>* rec) {
+  size_t p = 0;
+  if (rd_u32(b, p) != 0x31475354u) throw std::runtime_error("bad result magic");
+  const uint32_t n = rd_u32(b, p);
+  rec->resize((size_t)n + 1);
+  for (uint32_t i = 0; i < n; i++) {
+    (*rec)[i] = p;
+    p += 1;  // status
+    const uint32_t nf = rd_u32(b, p);
+    for (uint32_t f = 0; f < nf; f++) {
+      p += 12;              // rule, start line, end line
+      p += rd_u32(b, p);    // match
+      const uint32_t nl = rd_u32(b, p);
+      for (uint32_t l = 0; l < nl; l++) {
+        p += 5;             // number, flags
+        p += rd_u32(b, p);  // content
+      }
+    }
+    if (p > b.size()) throw std::runtime_error("truncated result");
+  }
+  if (p != b.size()) throw std::runtime_error("trailing bytes after the last file record");
+  (*rec)[n] = p;
+}
+
 }  // namespace tsg

@@ -110,6 +110,9 @@ bool match_keywords(const RuleC& r, const std::string& lowered);
 
 // Serialization of results (format documented in include/trivy_secret.h).
 void serialize_batch(const BatchResult& br, std::string* out, int nthreads = 1);
+// byte offset of each per-file record of a serialized result, and its end: file i is
+// [rec[i], rec[i+1]) (throws on a malformed buffer)
+void result_record_spans(const std::string& b, std::vector<size_t>* rec);
 
 // f(i) for i in [0, n) on the process-wide worker pool (plan.cpp), `grain` indices a claim
 void pool_for(size_t n, int nthreads, const std::function<void(size_t)>& f, size_t grain);

@@ -47,10 +47,14 @@ def apply_layers(blobs):
                 f["Layer"] = dict(lay)
             old = merged.get(new["FilePath"])
             if old is not None:
+                # secretFindingsContains checks the growing newSecret.Findings
+                # (applier/docker.go:280-284, :290-297): of several lower-layer findings with
+                # a RuleID the upper layer lacks, only the first is kept
                 have = {f["RuleID"] for f in new["Findings"] or []}
                 for f in old["Findings"] or []:
                     if f["RuleID"] not in have:
                         new["Findings"] = (new["Findings"] or []) + [f]
+                        have.add(f["RuleID"])
             merged[new["FilePath"]] = new
     return [merged[k] for k in sorted(merged)]
 

@@ -384,60 +384,89 @@ def decode_results(buf, paths, rules):
 class GpuContext:
     """One device context (tsg_ctx): rule tables replicated in HBM, two lanes, pinned slots.
 
-    upload() copies a batch into a context-owned pinned slot (the library keeps no pointer
-    to the caller's buffers); submit()/collect() pipeline scans, each collected result is
-    decoded with the paths of the batch it was submitted for (FIFO).  emulate=True runs
-    the kernels' algorithm on the CPU over the same pipeline (tests without a GPU)."""
+    upload() copies a batch into a pinned slot that this object then holds (the library
+    keeps no pointer to the caller's buffers); submit() / submit_slot() return the native
+    ticket of the submission and collect(ticket) decodes its results with the paths it was
+    submitted with (collect() with no ticket takes this object's oldest submission).
+    scan_batch() is the one-call, thread-safe Scan of a batch.  emulate=True runs the
+    kernels' algorithm on the CPU over the same pipeline (tests without a GPU)."""
 
     def __init__(self, scanner, device=0, chunk_bytes=0, ext_cap=0, cand_capacity=0,
                  host_threads=0, adapt_mib=0, emulate=False, slot_mib=0, max_slots=0):
+        import threading
         self._h = None
         self.scanner = scanner
+        self.chunk = chunk_bytes or 256
         opt = N.CtxOptions(chunk_bytes, ext_cap, cand_capacity, host_threads, adapt_mib,
                            N.TSG_CTX_EMULATE if emulate else 0, slot_mib, max_slots)
         h = C.c_void_p()
         N.check(N.lib().tsg_ctx_create(int(device), scanner.handle, C.byref(opt), C.byref(h)))
         self._h = h
-        self._paths = None      # paths of the last uploaded batch
-        self._nfiles = 0
-        self._fifo = []         # paths of each submitted, uncollected batch
+        self._upload = None     # (slot id, Batch) of the last upload
+        self._k1 = None
+        self._lock = threading.Lock()
+        self._fifo = []         # (ticket, paths) of this object's uncollected submissions
+        self._paths = {}        # ticket -> paths
 
     @property
     def handle(self):
         return self._h
 
     def upload(self, batch):
-        N.check(N.lib().tsg_batch_upload(self._h, *batch.ptrs()))
-        self._paths = batch
-        self._nfiles = batch.nfiles
+        """Copy the batch into a pinned slot held by this object (the previous upload's slot
+        is given back)."""
+        sid = C.c_uint32()
+        N.check(N.lib().tsg_batch_upload(self._h, *batch.ptrs(), C.byref(sid)))
+        with self._lock:
+            prev, self._upload = self._upload, (sid.value, batch)
+        if prev is not None:
+            N.check(N.lib().tsg_slot_release(self._h, prev[0]))
 
     def kernels(self):
-        N.check(N.lib().tsg_batch_kernels(self._h))
+        """The device part of a scan of the uploaded batch, synchronously (test hook);
+        k1_output() then returns its keyword bits and chunk events."""
+        sid, b = self._upload
+        W = (self.scanner.info()["n_keywords"] + 31) // 32
+        kw = np.zeros(b.nfiles * W, dtype=np.uint32)
+        ev = np.zeros((int(b.offsets[-1]) + self.chunk - 1) // self.chunk, dtype=np.uint32)
+        u32p = C.POINTER(C.c_uint32)
+        N.check(N.lib().tsg_batch_kernels(self._h, sid, b.nfiles, kw.ctypes.data_as(u32p), kw.size,
+                                          ev.ctypes.data_as(u32p), ev.size))
+        self._k1 = (kw.reshape(b.nfiles, W), ev)
 
     def k1_output(self, chunk):
         """(keyword bits [nfiles, kw_words], chunk event bits) of the last kernels() call."""
-        b = self._paths
-        W = (self.scanner.info()["n_keywords"] + 31) // 32
-        kw = np.zeros(b.nfiles * W, dtype=np.uint32)
-        ev = np.zeros((int(b.offsets[-1]) + chunk - 1) // chunk, dtype=np.uint32)
-        u32p = C.POINTER(C.c_uint32)
-        N.check(N.lib().tsg_batch_k1_output(self._h, kw.ctypes.data_as(u32p), kw.size,
-                                            ev.ctypes.data_as(u32p), ev.size))
-        return kw.reshape(b.nfiles, W), ev
+        assert chunk == self.chunk, "the context's chunk is %d" % self.chunk
+        return self._k1
 
-    def _paths_of(self, batch):
-        return [batch.path(i) for i in range(batch.nfiles)]
+    @staticmethod
+    def _paths_of(batch):
+        if isinstance(batch, Batch):
+            return [batch.path(i) for i in range(batch.nfiles)]
+        return list(batch)
+
+    def _track(self, ticket, paths_of):
+        with self._lock:
+            self._fifo.append(ticket)
+            self._paths[ticket] = paths_of
+        return ticket
 
     def submit(self):
         """Device part of a scan of the uploaded batch, asynchronously; its host resolution
-        follows it in the background."""
-        N.check(N.lib().tsg_batch_submit(self._h))
-        self._fifo.append(self._paths)
+        follows it in the background.  Returns the ticket."""
+        sid, b = self._upload
+        t = C.c_uint64()
+        N.check(N.lib().tsg_slot_submit(self._h, sid, b.nfiles, C.byref(t)))
+        return self._track(t.value, b)
 
-    def submit_slot(self, slot_id, nfiles, paths_of=None):
-        """Submit the first nfiles files of an acquired slot (see acquire_slot)."""
-        N.check(N.lib().tsg_slot_submit(self._h, int(slot_id), int(nfiles)))
-        self._fifo.append(paths_of)
+    def submit_slot(self, slot_id, nfiles, paths_of):
+        """Submit the first nfiles files of an acquired slot (see acquire_slot); paths_of is
+        the Batch or the list of paths they were packed from.  Returns the ticket."""
+        if paths_of is None:
+            raise ValueError("submit_slot needs the submitted files' paths (a Batch or a list)")
+        t = C.c_uint64()
+        N.check(N.lib().tsg_slot_submit(self._h, int(slot_id), int(nfiles), C.byref(t)))
+        return self._track(t.value, paths_of)
 
     def acquire_slot(self, data_bytes, nfiles, path_bytes):
         """A pinned slot to fill directly: (id, data, offsets, paths, path_offsets) as
@@ -454,27 +483,43 @@ class GpuContext:
     def release_slot(self, slot_id):
         N.check(N.lib().tsg_slot_release(self._h, int(slot_id)))
 
-    def collect_raw(self):
-        """Results of the oldest submitted scan (raw tsg_result handle)."""
+    def _take(self, ticket):
+        with self._lock:
+            if ticket is None:
+                if not self._fifo:
+                    raise N.NativeError(N.TSG_ERR_ARG, "no submitted batch")
+                ticket = self._fifo.pop(0)
+            elif ticket in self._paths:
+                self._fifo.remove(ticket)
+            return ticket, self._paths.pop(ticket, None)
+
+    def collect_raw(self, ticket=None):
+        """Results of one submission (default: this object's oldest) as a raw tsg_result
+        handle; the caller frees it."""
+        ticket, _ = self._take(ticket)
         out = C.c_void_p()
-        try:
-            N.check(N.lib().tsg_batch_collect(self._h, C.byref(out)))
-        finally:
-            if self._fifo:
-                self._last_collected = self._fifo.pop(0)
+        N.check(N.lib().tsg_batch_collect(self._h, ticket, C.byref(out)))
         return out
 
-    def collect(self):
-        out = self.collect_raw()
-        b = self._last_collected
-        return self.scanner.decode(out, self._paths_of(b))
+    def collect(self, ticket=None):
+        ticket, paths = self._take(ticket)
+        out = C.c_void_p()
+        N.check(N.lib().tsg_batch_collect(self._h, ticket, C.byref(out)))
+        return self.scanner.decode(out, self._paths_of(paths))
 
     def pending(self):
+        """Uncollected submissions of the context (every caller)."""
         return N.lib().tsg_batch_pending(self._h)
 
     def scan(self):
-        self.submit()
-        return self.collect()
+        return self.collect(self.submit())
+
+    def scan_batch(self, batch):
+        """tsg_scan_batch: copy, scan and resolve one batch in a slot of its own
+        (thread-safe: any number of threads may call it on one context)."""
+        out = C.c_void_p()
+        N.check(N.lib().tsg_scan_batch(self._h, *batch.ptrs(), C.byref(out)))
+        return self.scanner.decode(out, self._paths_of(batch))
 
     def stats(self):
         s = N.Stats()
@@ -483,7 +528,46 @@ class GpuContext:
 
     def close(self):
         if self._h:
+            if self._upload is not None:
+                N.lib().tsg_slot_release(self._h, self._upload[0])
+                self._upload = None
             N.lib().tsg_ctx_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        self.close()
+
+
+class MultiGpu:
+    """tsg_multi: one process driving several devices (trivy's per-layer goroutines over a
+    node's GPUs, pkg/fanal/artifact/image/image.go:210-234).  scan_batch() shards a batch's
+    files LPT by bytes over the devices and returns the results in input order."""
+
+    def __init__(self, scanner, devices, slot_mib=0, host_threads=0, emulate=False, max_slots=0):
+        self._h = None
+        self.scanner = scanner
+        opt = N.CtxOptions(0, 0, 0, host_threads, 0, N.TSG_CTX_EMULATE if emulate else 0,
+                           slot_mib, max_slots)
+        devs = (C.c_int * len(devices))(*[int(d) for d in devices])
+        h = C.c_void_p()
+        N.check(N.lib().tsg_multi_create(devs, len(devices), scanner.handle, C.byref(opt),
+                                         C.byref(h)))
+        self._h = h
+        self.n = len(devices)
+
+    def scan_batch(self, batch):
+        out = C.c_void_p()
+        N.check(N.lib().tsg_multi_scan_batch(self._h, *batch.ptrs(), C.byref(out)))
+        return self.scanner.decode(out, GpuContext._paths_of(batch))
+
+    def stats(self, i):
+        s = N.Stats()
+        N.check(N.lib().tsg_multi_get_stats(self._h, int(i), C.byref(s)))
+        return {k: getattr(s, k) for k, _ in N.Stats._fields_}
+
+    def close(self):
+        if self._h:
+            N.lib().tsg_multi_destroy(self._h)
             self._h = None
 
     def __del__(self):

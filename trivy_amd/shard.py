@@ -59,26 +59,51 @@ def scan_layer_sharded(analyzer, tar, rank, world, dist=None, device=None, emula
     gathered on rank 0; rank 0 returns (sorted AnalysisResult.Secrets, opq_dirs, wh_files),
     the others None."""
     from .walker import NativeLayer, LayerRange, layer_chain
+
+    def scan(lay):
+        b = lay.batch
+        if b.nfiles == 0:
+            return []
+        if device is not None or emulate_chunk:
+            return analyzer.scanner.ScanBatch(b, device=device, emulate_chunk=emulate_chunk)
+        return analyzer.scanner.ScanBatch(b, nthreads=16)
+
     if index == "range" and world > 1 and dist is not None:
         def allgather(obj):
             out = [None] * world
             dist.all_gather_object(out, obj)
             return out
-        rng = LayerRange(tar, rank, world)
-        layer_chain(rng, rank, world, allgather)
-        dirs = allgather(rng.dirs(skip_dirs))
+
+        def guarded(fn):
+            """fn() on this rank, then one all-gather of (ok, value) / (err, message): every
+            rank raises if any rank failed, so no rank is left waiting in a collective."""
+            try:
+                mine = ("ok", fn())
+            except Exception as e:  # noqa: BLE001 - forwarded to every rank
+                mine = ("err", "rank %d: %s" % (rank, e))
+            out = allgather(mine)
+            bad = [m for k, m in out if k == "err"]
+            if bad:
+                raise RuntimeError("; ".join(bad))
+            return [v for _, v in out]
+
+        holder = {}
+        guarded(lambda: holder.setdefault("rng", LayerRange(tar, rank, world)) and None)
+        rng = holder["rng"]
+        guarded(lambda: layer_chain(rng, rank, world, allgather) and None)
+        dirs = guarded(lambda: rng.dirs(skip_dirs))
         prior = [d for r in range(rank) for d in dirs[r]]
-        lay = rng.pack(analyzer.scanner, skip_files, skip_dirs, prior, analyzer.configPath)
+
+        def pack_scan():
+            holder["lay"] = rng.pack(analyzer.scanner, skip_files, skip_dirs, prior,
+                                     analyzer.configPath)
+            holder["local"] = scan(holder["lay"])
+        guarded(pack_scan)
+        lay, local = holder["lay"], holder["local"]
     else:
         lay = NativeLayer(analyzer.scanner, tar, skip_files, skip_dirs, analyzer.configPath,
                           rank=rank, world=world)
-    b = lay.batch
-    if b.nfiles == 0:
-        local = []
-    elif device is not None or emulate_chunk:
-        local = analyzer.scanner.ScanBatch(b, device=device, emulate_chunk=emulate_chunk)
-    else:
-        local = analyzer.scanner.ScanBatch(b, nthreads=16)
+        local = scan(lay)
     mine = [r for r in local if r and r["Findings"]]
     if world == 1 or dist is None:
         return findings_sorted(mine), lay.opq, lay.wh
