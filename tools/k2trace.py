@@ -31,10 +31,11 @@ def run(out, mib=1024, rules="builtin"):
     sc, extra, binary_frac, _, _ = rule_set(rules)
     b, info = corpus.make_corpus(mib << 20, seed=2, plants_per_mib=1.0, extra_plants=extra,
                                  extra_per_mib=2.0 if extra else 0.0, binary_frac=binary_frac)
+    os.environ["TSG_K2_TRACE"] = path  # (read once, at the first batch)
     ctx = S.GpuContext(sc, 0)
     ctx.upload(b)
     ctx.kernels()  # (adaptation)
-    os.environ["TSG_K2_TRACE"] = path
+    os.remove(path)
     ctx.kernels()
     st = ctx.stats()
     ctx.close()
