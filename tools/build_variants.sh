@@ -20,5 +20,7 @@ for v in "$@"; do
     nolds) build $v -DK1_EXP_NO_CLS -DK1_EXP_NO_TAB ;;
     noruns) build $v -DK1_EXP_NO_RUNS ;;
     nocls) build $v -DK1_EXP_NO_CLS ;;
+    notab) build $v -DK1_EXP_NO_TAB ;;
+    k2ctr) build $v -DK2_TRACE_CTR ;;
   esac
 done

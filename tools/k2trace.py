@@ -48,7 +48,7 @@ def run(out, mib=1024, rules="builtin"):
 
 def report(out):
     meta = json.load(open(os.path.join(out, "k2trace_meta.json")))
-    t = np.fromfile(os.path.join(out, "k2trace.bin"), dtype=np.uint64).reshape(-1, 4)
+    t = np.fromfile(os.path.join(out, "k2trace.bin"), dtype=np.uint64).reshape(-1, 8)
     t = t[t[:, 0] > 0]
     st, en = t[:, 0].astype(np.int64), t[:, 1].astype(np.int64)
     en = np.where(en > 0, en, st)
@@ -69,8 +69,13 @@ def report(out):
            "end_us": {k: round(float(np.percentile(us(en - t0), p)), 2) for k, p in
                       (("p50", 50), ("p90", 90), ("p99", 99), ("max", 100))},
            "slowest": [{"group": int(g[i]), "items": int(n[i]), "dur_us": round(float(dur[i]), 1),
-                        "start_us": round(float(us(st[i] - t0)), 1), "xcc": int(xcc[i])}
-                       for i in order[:15]]}
+                        "start_us": round(float(us(st[i] - t0)), 1), "xcc": int(xcc[i]),
+                        "replays": int(t[i, 4]), "cands": int(t[i, 5]), "tail_bytes": int(t[i, 6]),
+                        "tail_max": int(t[i, 7])}
+                       for i in order[:15]],
+           # per-entry counters (K2_TRACE_CTR builds; zero otherwise)
+           "counters_total": {"replays": int(t[:, 4].sum()), "cands": int(t[:, 5].sum()),
+                              "tail_bytes": int(t[:, 6].sum()), "tail_max": int(t[:, 7].max())}}
     per_g = {}
     for i in range(len(t)):
         d = per_g.setdefault(int(g[i]), [0, 0.0, 0.0])

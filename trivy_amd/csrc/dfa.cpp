@@ -226,6 +226,7 @@ class Builder {
     }
     d->nstates = (int)keys_.size();
     d->max_len = longest_match(nfa_);
+    mark_immortal(d.get());
     return d;
   }
 
@@ -379,6 +380,34 @@ class Builder {
 };
 
 }  // namespace
+
+// immortal = noinject and unable to reach a dead state (backward search from the dead
+// states over the transitions; noinject states only lead to noinject states)
+void mark_immortal(DFA* d) {
+  const size_t ns = (size_t)d->nstates, nc = (size_t)d->nclasses;
+  std::vector<std::vector<uint32_t>> pred(ns);
+  for (size_t s = 0; s < ns; s++)
+    if (d->noinject[s])
+      for (size_t c = 0; c < nc; c++) pred[d->next[s * nc + c]].push_back((uint32_t)s);
+  std::vector<uint8_t> mortal(ns, 0);
+  std::vector<uint32_t> st;
+  for (size_t s = 0; s < ns; s++)
+    if (d->dead[s]) {
+      mortal[s] = 1;
+      st.push_back((uint32_t)s);
+    }
+  while (!st.empty()) {
+    const uint32_t t = st.back();
+    st.pop_back();
+    for (uint32_t s : pred[t])
+      if (!mortal[s]) {
+        mortal[s] = 1;
+        st.push_back(s);
+      }
+  }
+  d->immortal.assign(ns, 0);
+  for (size_t s = 0; s < ns; s++) d->immortal[s] = d->noinject[s] && !mortal[s];
+}
 
 Ctx DFA::ctx_of(uint8_t c, const DFA& d) {
   Ctx x = kCtxOther;

@@ -45,6 +45,9 @@ struct DFA {
   uint32_t start[4] = {0, 0, 0, 0};  // inject-mode start state per previous-byte context
   std::vector<uint32_t> to_noinject;  // [nstates] same threads, noinject mode
   std::vector<uint8_t> dead;         // [nstates] noinject and no live thread
+  // [nstates] noinject states from which no dead state is reachable: their threads never all
+  // die, so a tail entering one runs to the end of the file (e.g. after begin(?s).*end)
+  std::vector<uint8_t> immortal;
   std::vector<uint8_t> noinject;     // [nstates] mode bit
   int64_t max_len = -1;              // longest match in bytes (-1 = unbounded)
   uint32_t anchored = 0;             // DFAOptions::anchored: noinject state of the start node
@@ -58,6 +61,9 @@ struct DFA {
   static Ctx ctx_of(uint8_t c, const DFA& d);
   bool need_word = false, need_nl = false, need_bot = false;
 };
+
+// fills DFA::immortal (build_dfa does; for DFAs assembled by hand)
+void mark_immortal(DFA* d);
 
 struct DFAOptions {
   int max_states = 8192;

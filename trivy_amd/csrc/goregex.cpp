@@ -1039,6 +1039,33 @@ struct Regexp::Ast {
   int ncap = 0;
 };
 
+// Prog.Prefix (regexp/syntax/prog.go) over ASCII runes: an ASCII byte never lies inside a
+// multi-byte rune, so each occurrence found by memmem is a position the matchers visit.
+static std::string literal_prefix(const Prog& p) {
+  std::string s;
+  uint32_t pc = p.start;
+  for (size_t guard = 0; guard < p.inst.size() && pc != 0; guard++) {
+    const Inst& i = p.inst[pc];
+    if (i.op == Op::Nop || i.op == Op::Cap) {
+      pc = i.out;
+      continue;
+    }
+    if (i.op != Op::Rune) break;
+    const Ranges& r = p.runes[i.arg];
+    if (r.size() != 1 || r[0].first != r[0].second || r[0].first < 0 || r[0].first >= 0x80) break;
+    s.push_back((char)r[0].first);
+    pc = i.out;
+  }
+  return s;
+}
+
+// first occurrence of the program's prefix at or after pos (-1: none)
+static int64_t next_prefix(const Prog& p, const uint8_t* b, size_t n, int64_t pos) {
+  if ((size_t)pos >= n) return -1;
+  const void* q = memmem(b + pos, n - (size_t)pos, p.prefix.data(), p.prefix.size());
+  return q ? (int64_t)((const uint8_t*)q - b) : -1;
+}
+
 Regexp::Regexp() = default;
 Regexp::~Regexp() = default;
 
@@ -1058,6 +1085,7 @@ std::shared_ptr<Regexp> Regexp::Compile(const std::string& src, std::string* err
       for (const auto& rg : re->prog_.runes[k])
         for (int32_t c = std::max<int32_t>(rg.first, 0); c <= std::min<int32_t>(rg.second, 127); c++)
           re->prog_.ascii[k * 2 + c / 64] |= 1ull << (c % 64);
+    re->prog_.prefix = literal_prefix(re->prog_);
     re->ast_ = std::make_shared<Ast>();
     re->ast_->nodes = std::move(p.nodes);
     re->ast_->root = root;
@@ -1263,6 +1291,18 @@ class Machine {
       if (runq->dense.empty()) {
         if (matched_) break;
         if (pos > start_hi) break;
+        if (!p_.prefix.empty()) {  // no thread alive: the next match starts at a prefix
+          const int64_t q = next_prefix(p_, b, n, pos);
+          if (q < 0 || q > start_hi) break;
+          if (q > pos) {
+            pos = q;
+            r = decode_rune(b, n, (size_t)pos, &w);
+            r1 = kEOT;
+            if (r != kEOT) r1 = decode_rune(b, n, (size_t)pos + w, &w1);
+            fr1 = b[pos - 1];
+            fr2 = r;
+          }
+        }
       }
       if (!matched_ && pos <= start_hi) {
         if (ns_ > 0) matchcap_[0] = pos;
@@ -1435,6 +1475,19 @@ class Backtracker {
     bool found = false;
     std::fill(matchcap_.begin(), matchcap_.end(), -1);
     for (int64_t s = pos; s <= n_ && s <= start_hi;) {
+      if (!p_.prefix.empty()) {  // a match starts at a prefix occurrence
+        const int64_t q = next_prefix(p_, b, n, s);
+        if (q < 0 || q > start_hi) break;
+        if (q > s && q - base_ > 4096) {  // far jump: restart the visited rows at q
+          if (maxrow_ >= 0) {
+            const uint64_t hi = ((uint64_t)(maxrow_ + 1) * np_ + 63) / 64;
+            std::fill(visited_.begin(), visited_.begin() + std::min<uint64_t>(hi, visited_.size()), 0);
+          }
+          base_ = q;
+          maxrow_ = -1;
+        }
+        s = q;
+      }
       std::fill(cap_.begin(), cap_.end(), -1);
       if (ns_ > 0) cap_[0] = s;
       if (try_at(s)) {

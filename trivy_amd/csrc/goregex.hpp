@@ -80,6 +80,11 @@ struct Prog {
   // [runes.size() * 2]: ASCII members of each rune set as a 128-bit map (matcher fast
   // path; filled by Regexp::Compile, empty for derived programs)
   std::vector<uint64_t> ascii;
+  // regexp/syntax Prog.Prefix restricted to ASCII: the literal every match starts with (the
+  // leading single-rune, case-sensitive instructions after Nop / Cap), or empty.  The
+  // matchers jump between its occurrences while no thread is alive (regexp/exec.go
+  // machine.match, backtrack.go), so a whole-file search costs a memmem where it can.
+  std::string prefix;
 };
 
 class Regexp {

@@ -92,7 +92,7 @@ struct DevDFA {  // K2 rule group
   const uint16_t* acc_state;  // [ns] accept-mask index per state (state_acc DFAs)
   const uint16_t* eot;        // [ns] accept-mask index at end of text
   const uint16_t* to_ni;      // [ns] row of the noinject twin
-  const uint8_t* dead;        // [ns]
+  const uint8_t* dead;        // [ns] bit 0 dead, bit 1 immortal (DFA::immortal)
   const uint64_t* masks;      // [nmasks * mw]
   const uint8_t* cls;         // [256]
   const uint32_t* rules;      // group-local id -> global rule
@@ -1064,10 +1064,18 @@ struct K2Args {
   uint8_t* ovf;
   uint32_t* diag;  // null, or [4]: tail bytes, longest tail, tails over 4 KiB, word replays
   uint32_t* claim;  // [2] next list / dense entry (zeroed per batch)
-  // null, or per entry {start, end (wall clock, 100 MHz), group << 32 | items,
-  // XCC_ID << 32 | HW_ID} written by the block that ran it (TSG_K2_TRACE)
+  // null, or per entry kTraceW words {start, end (wall clock, 100 MHz), group << 32 | items,
+  // XCC_ID << 32 | HW_ID, then (K2_TRACE_CTR builds only) replayed words, candidates,
+  // tail bytes, longest tail} written by the block that ran it (TSG_K2_TRACE)
   unsigned long long* etrace;
 };
+constexpr int kTraceW = 8;
+#ifdef K2_TRACE_CTR  // measurement builds: per-entry counters of the running entry
+__shared__ unsigned long long* s_ectr;
+#define K2_CTR(k, op, v) (s_ectr ? (void)op(&s_ectr[k], (unsigned long long)(v)) : (void)0)
+#else
+#define K2_CTR(k, op, v) ((void)0)
+#endif
 
 // Candidate emission, wave-aggregated: the lanes that reach an accept together reserve
 // their records with ONE atomic (ballot, popcount prefix, broadcast of the base).  A record
@@ -1079,7 +1087,10 @@ __device__ __forceinline__ void emit_cand(const K2Args& A, uint32_t file, uint32
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t leader = (uint32_t)__builtin_ctzll(m);
   uint32_t base = 0;
-  if (lane == leader) base = atomicAdd(A.cand_count, (uint32_t)__popcll(m));
+  if (lane == leader) {
+    base = atomicAdd(A.cand_count, (uint32_t)__popcll(m));
+    K2_CTR(1, atomicAdd, __popcll(m));
+  }
   base = __shfl(base, (int)leader);
   const uint32_t idx = base + (uint32_t)__popcll(m & ((1ull << lane) - 1));
   if (idx < A.cand_cap && (end < kCandWhole || end == (uint64_t)kCandWhole)) {
@@ -1110,6 +1121,61 @@ struct Lane {
   }
 
   __device__ __forceinline__ uint32_t state_of(uint32_t row) const { return __umulhi(row, d.inv_nc); }
+
+  // accept-mask index of the transition at table index ix out of row s, and its rule count
+  __device__ __forceinline__ uint32_t acc_index(uint32_t s, uint32_t ix) const {
+    return d.state_acc ? s_accs[state_of(s)] : d.acc[ix];
+  }
+  __device__ __forceinline__ const uint64_t* mask_of(uint32_t mi) const {
+    return (d.state_acc && mi < d.nmasks) ? s_masks + (size_t)mi * d.mw : d.masks + (size_t)mi * d.mw;
+  }
+  __device__ __forceinline__ uint32_t mask_rules(uint32_t mi) const {
+    const uint64_t* m = mask_of(mi);
+    uint32_t n = 0;
+    for (uint32_t w = 0; w < d.mw; w++) n += (uint32_t)__popcll(m[w]);
+    return n;
+  }
+  // one candidate record at idx (see emit_cand)
+  __device__ __forceinline__ void put(uint32_t idx, uint32_t rule, uint64_t end) const {
+    if (idx < A.cand_cap && end < kCandWhole) {
+      A.cand[idx] = DevCand{file, rule, (uint32_t)end};
+    } else {
+      A.ovf[file] = 1;
+      if (idx < A.cand_cap) A.cand[idx] = DevCand{file, rule, 0};
+    }
+  }
+  // A word with an accept, again from registers (bytes lo..hi-1 of v, batch position wb):
+  // its candidates are counted, reserved with one atomic and written.  A relaxed unbounded
+  // rule accepts at every byte of a long token run, and emitting those one by one (an
+  // atomic round trip each, after byte loads from memory) made a few entries of a few
+  // dozen items the kernel's long pole (profiles/r03/d2).
+  __device__ void replay_emit(uint32_t s0, const uint4 v, int lo, int hi, uint64_t wb) {
+    uint32_t n = 0, r = s0;
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+      const uint32_t ix = r + s_cls[byte_of(v, k)];
+      const uint32_t e = s_tab[ix];
+      const bool in = k >= lo && k < hi;
+      if (in && (e & 0x8000u)) n += mask_rules(acc_index(r, ix));
+      r = in ? (e & 0x7FFFu) : r;
+    }
+    if (!n) return;
+    uint32_t at = atomicAdd(A.cand_count, n);
+    K2_CTR(1, atomicAdd, n);
+    r = s0;
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+      const uint32_t ix = r + s_cls[byte_of(v, k)];
+      const uint32_t e = s_tab[ix];
+      const bool in = k >= lo && k < hi;
+      if (in && (e & 0x8000u)) {
+        const uint64_t* m = mask_of(acc_index(r, ix));
+        for (uint32_t w = 0; w < d.mw; w++)
+          for (uint64_t bits = m[w]; bits; bits &= bits - 1) put(at++, d.rules[w * 64 + __builtin_ctzll(bits)], wb + k - fs);
+      }
+      r = in ? (e & 0x7FFFu) : r;
+    }
+  }
 
   // s is a row throughout
   __device__ __forceinline__ uint32_t step(uint32_t s, uint32_t byte, uint64_t pos) {
@@ -1154,8 +1220,10 @@ struct Lane {
     uint64_t q = b;
     uint64_t w = q & ~15ull;
     uint4 cur = *(const uint4*)(data + w);
-    while (q < fe && !d.dead[state_of(s)]) {
-      if (q - b >= A.ext_cap) {  // the group's rules over the whole file, on the host
+    while (q < fe && !(d.dead[state_of(s)] & 1)) {
+      // past ext_cap, or in a state whose threads never die (the tail would run to the end
+      // of the file): the group's rules over the whole file, on the host
+      if (q - b >= A.ext_cap || (d.dead[state_of(s)] & 2)) {
         for (uint32_t k = 0; k < d.nrules; k++) emit_cand(A, file, d.rules[k], kCandWhole);
         return;
       }
@@ -1165,13 +1233,15 @@ struct Lane {
       cur = nxt;
       w += 16;
     }
+    K2_CTR(2, atomicAdd, q - b);
+    K2_CTR(3, atomicMax, q - b);
     if (A.diag) {
       const uint32_t n = (uint32_t)min<uint64_t>(q - b, 0xFFFFFFFFull);
       atomicAdd(&A.diag[0], n);
       atomicMax(&A.diag[1], n);
       if (n > 4096) atomicAdd(&A.diag[2], 1u);
     }
-    if (q >= fe && !d.dead[state_of(s)]) {
+    if (q >= fe && !(d.dead[state_of(s)] & 1)) {
       const uint32_t m = d.eot[state_of(s)];
       if (m) emit(m, fe);
     }
@@ -1343,10 +1413,10 @@ __device__ __forceinline__ void k2_list_pair(const DevDFA& d, const K2Args& A, c
     }
     if (__builtin_expect(any & 0x8000u, 0)) {  // an accept: replay the word, emitting
       if (A.diag) atomicAdd(&A.diag[3], 1u);
+      K2_CTR(0, atomicAdd, 1);
       L.file = c.file;
       L.fs = c.fs;
-      uint32_t r = s0;  // (bytes re-read from memory: no dynamic index into registers)
-      for (int k = lo; k < hi; k++) r = L.step(r, A.data[wb + k], wb + k);
+      L.replay_emit(s0, v, lo, hi, wb);
     }
     c.s = s;
   };
@@ -1436,6 +1506,9 @@ __device__ __forceinline__ void k2_run(const DevDFA* __restrict__ dfas, const K2
   __shared__ uint32_t s_e;
   uint32_t staged = 0xFFFFFFFFu;
   uint32_t prev = 0xFFFFFFFFu;  // the entry this block ran last (trace)
+#ifdef K2_TRACE_CTR
+  if (threadIdx.x == 0) s_ectr = nullptr;
+#endif
   for (;;) {
     if (threadIdx.x == 0) s_e = atomicAdd(claim, 1u);
     __syncthreads();
@@ -1443,15 +1516,21 @@ __device__ __forceinline__ void k2_run(const DevDFA* __restrict__ dfas, const K2
     __syncthreads();  // every lane has read s_e (and is done with the previous entry)
     if (!DENSE && A.etrace && threadIdx.x == 0) {  // trace: the previous entry ends, this one starts
       const unsigned long long now = wall_clock64();
-      if (prev != 0xFFFFFFFFu) A.etrace[(size_t)prev * 4 + 1] = now;
+      if (prev != 0xFFFFFFFFu) A.etrace[(size_t)prev * kTraceW + 1] = now;
       if (e < E) {
         const uint4 en = entries[e];
-        A.etrace[(size_t)e * 4 + 0] = now;
-        A.etrace[(size_t)e * 4 + 2] = ((unsigned long long)en.x << 32) | en.z;
-        A.etrace[(size_t)e * 4 + 3] = ((unsigned long long)__builtin_amdgcn_s_getreg(20 | (15 << 11)) << 32) |
-                                      (uint32_t)__builtin_amdgcn_s_getreg(4 | (31 << 11));
+        A.etrace[(size_t)e * kTraceW + 0] = now;
+        A.etrace[(size_t)e * kTraceW + 2] = ((unsigned long long)en.x << 32) | en.z;
+        A.etrace[(size_t)e * kTraceW + 3] = ((unsigned long long)__builtin_amdgcn_s_getreg(20 | (15 << 11)) << 32) |
+                                            (uint32_t)__builtin_amdgcn_s_getreg(4 | (31 << 11));
+#ifdef K2_TRACE_CTR
+        s_ectr = A.etrace + (size_t)e * kTraceW + 4;
+#endif
       }
     }
+#ifdef K2_TRACE_CTR
+    __syncthreads();
+#endif
     prev = e;
     if (e >= E) break;
     const uint4 en = entries[e];
@@ -1541,7 +1620,9 @@ static int make_device_dfa(const DFA& dd, const std::vector<uint32_t>& rules, De
     eot[s] = (uint16_t)d.eot_acc[s];
     ni[s] = (uint16_t)(d.to_noinject[s] * nc);
   }
-  std::vector<uint8_t> dead(d.dead.begin(), d.dead.end());
+  std::vector<uint8_t> dead(d.nstates);
+  for (int s = 0; s < d.nstates; s++)
+    dead[s] = (d.dead[s] ? 1 : 0) | ((size_t)s < d.immortal.size() && d.immortal[s] ? 2 : 0);
   std::vector<uint64_t> masks;
   for (const auto& m : d.masks) masks.insert(masks.end(), m.begin(), m.end());
   std::vector<uint8_t> cls(d.cls, d.cls + 256);
@@ -1835,7 +1916,7 @@ struct LaneState {
   uint64_t* base = nullptr;     // [G]
   uint8_t* kind = nullptr;      // [G]
   uint8_t* gskip = nullptr;     // [G]
-  unsigned long long* etrace = nullptr;  // [entries_cap * 4] K2 entry trace (TSG_K2_TRACE)
+  unsigned long long* etrace = nullptr;  // [entries_cap * kTraceW] K2 entry trace (TSG_K2_TRACE)
   size_t etrace_cap = 0;
   uint64_t nchunks = 0;         // last batch
   ~LaneState() {
@@ -2320,8 +2401,8 @@ int enqueue_scan(DeviceRules* r, LaneState* l, const ScanInput& in, HostOut* out
     A.diag = diag ? l->counts + 8 : nullptr;
     A.claim = l->counts + 12;
     static const bool trace = getenv("TSG_K2_TRACE") != nullptr;
-    if (trace && (rc = ensure(&l->etrace, &l->etrace_cap, (size_t)entries_cap * 4))) return rc;
-    if (trace) HIP_TRY(hipMemsetAsync(l->etrace, 0, sizeof(unsigned long long) * entries_cap * 4, st));
+    if (trace && (rc = ensure(&l->etrace, &l->etrace_cap, (size_t)entries_cap * kTraceW))) return rc;
+    if (trace) HIP_TRY(hipMemsetAsync(l->etrace, 0, sizeof(unsigned long long) * entries_cap * kTraceW, st));
     A.etrace = trace ? l->etrace : nullptr;
     // one block per resident slot (the grids are persistent)
     hipLaunchKernelGGL(k2_kernel, dim3(r->k2_grid), dim3(kBlock), r->max_lds, st, (const DevDFA*)r->d_groups, A);
@@ -2367,7 +2448,7 @@ int lane_k2_trace(LaneState* l, std::vector<unsigned long long>* out) {
   if (!l->etrace) return TSG_OK;
   uint32_t counts[16];
   HIP_TRY(hipMemcpy(counts, l->counts, sizeof(counts), hipMemcpyDeviceToHost));
-  const size_t n = std::min<size_t>((size_t)counts[2] * 4, l->etrace_cap);
+  const size_t n = std::min<size_t>((size_t)counts[2] * kTraceW, l->etrace_cap);
   out->resize(n);
   if (n) HIP_TRY(hipMemcpy(out->data(), l->etrace, n * sizeof(unsigned long long), hipMemcpyDeviceToHost));
   return TSG_OK;

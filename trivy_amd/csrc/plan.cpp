@@ -733,7 +733,10 @@ bool run_segment(const DFA& d, const uint8_t* data, uint64_t fs, uint64_t fe, ui
   s = d.to_noinject[s];
   uint64_t p = b;
   while (p < fe && !d.dead[s]) {
-    if (p - b >= ext_cap) return true;  // overflow: host resolves the file whole
+    // at the kernels' 16-byte word boundaries: past ext_cap, or in a state whose threads
+    // never die (the tail would run to the end of the file) -> the host resolves the
+    // file whole
+    if ((p == b || (p & 15) == 0) && (p - b >= ext_cap || d.immortal[s])) return true;
     size_t e = (size_t)s * nc + d.cls[data[p]];
     if (d.acc[e]) on_acc(d.acc[e], p - fs);
     s = d.next[e];
