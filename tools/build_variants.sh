@@ -15,12 +15,15 @@ build() {
 for v in "$@"; do
   case $v in
     ob4w4) build $v -DK1_UNROLL=4 ;;
-    db8w3) build $v -DK1_TWOBUF -DK1_UNROLL=8 -DK1_BLOCK=512 -DK1_WAVES=3 ;;
-    db16) build $v -DK1_TWOBUF -DK1_UNROLL=16 -DK1_BLOCK=256 -DK1_WAVES=2 ;;
     nolds) build $v -DK1_EXP_NO_CLS -DK1_EXP_NO_TAB ;;
     noruns) build $v -DK1_EXP_NO_RUNS ;;
     nocls) build $v -DK1_EXP_NO_CLS ;;
     notab) build $v -DK1_EXP_NO_TAB ;;
     k2ctr) build $v -DK2_TRACE_CTR ;;
+    coal) build $v -DK1_EXP_COAL ;;
+    nostep) build $v -DK1_EXP_NOSTEP ;;
+    noload) build $v -DK1_EXP_NOLOAD ;;
+    noload_nolds) build $v -DK1_EXP_NOLOAD -DK1_EXP_NO_CLS -DK1_EXP_NO_TAB ;;
+    nolds_coal) build $v -DK1_EXP_NO_CLS -DK1_EXP_NO_TAB -DK1_EXP_COAL ;;
   esac
 done

@@ -17,4 +17,7 @@ for r in builtin user1000; do
   timeout -k 10 300 python -u tools/kab.py 1024 5 --rules $r > $out/kab_$r.json 2> $out/kab_$r.err || exit 3
   cat $out/kab_$r.json
 done
+echo "== SQ builtin"
+timeout -k 10 -s KILL 240 rocprofv3 --pmc SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_WAIT_INST_LDS \
+  --output-format csv -d $out/sq -o run -- python tools/kab.py 1024 3 > $out/kab_sq.log 2>&1 || exit 4
 echo done

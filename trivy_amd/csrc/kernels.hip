@@ -67,19 +67,20 @@ enum : uint8_t { kGroupNone = 0, kGroupList = 1, kGroupDense = 2, kGroupSkip = 3
 constexpr int kStreams = 4;       // K2 dense: chunks per lane
 constexpr int kK1MaxStreams = 8;  // K1: chains per lane, the largest variant
 constexpr int kK1Seg = 8;         // K1: consecutive chunks per chain
-// static LDS size classes of the K1 kernel (KiB): 3, 2 or 1 blocks per CU
+// static LDS size classes of the K1 kernel (KiB): 3, 2 or 1 blocks per CU, of 512, 512 and
+// 1024 threads (16 waves per CU at K1_WAVES = 4 per SIMD, whose registers bound a lane)
 constexpr int kK1Lds[3] = {52, 80, 156};
-constexpr uint32_t kK1Tab = 1024;  // K1 LDS: 256 class words, then the transition table   // independent DFA chains per lane (dense passes)
+constexpr int kK1BlocksPerCU[3] = {3, 2, 1};
+constexpr __host__ __device__ int k1_threads(int ldsk) { return ldsk == 156 ? 1024 : 512; }
+// K1 LDS image: the byte -> class table, then the transition table.  The class table is
+// replicated per lane of a 32-lane half (K1_REP layout, [byte][lane & 31] words: every lane
+// reads its own bank, so the class read never conflicts) when the automaton leaves room for
+// it; otherwise 256 words (K1 tables of more than 124 KiB).
+constexpr uint32_t kK1RepBytes = 256 * 32 * 4;
 constexpr int kBlock = 256;
-// K1 block and occupancy target: two blocks of K1_BLOCK threads share a CU's LDS (one
-// 80 KiB automaton image each); K1_WAVES waves per SIMD bounds the registers per lane
-#ifndef K1_BLOCK
-#define K1_BLOCK 512
-#endif
 #ifndef K1_WAVES
 #define K1_WAVES 4
 #endif
-constexpr int kK1Block = K1_BLOCK;
 constexpr int kPad = 256;     // zero bytes before and after the batch in HBM (>= K1 warm-up)
 constexpr int kMaxBack = 16;  // event windows up to this many chunks; larger -> whole file
 
@@ -114,6 +115,7 @@ struct DevK1 {
   uint32_t nc, ns, nmasks, mw, kw_words, start, warm, kU, kD;  // start: row; kD = threshold << 8
   uint32_t acc_row;
   uint32_t lds_class;  // index into kK1Lds
+  uint32_t rep;        // class table replicated per lane (K1_REP layout)
   const uint16_t* kw_len;  // [kw_words * 32] byte length of each keyword (rare path)
   uint32_t kw_maxlen;      // longest keyword: an occurrence ending this far into a file fits
 };
@@ -189,19 +191,10 @@ __global__ void path_allow_kernel(DevPathDFA d, const uint8_t* __restrict__ path
 typedef unsigned short us2 __attribute__((ext_vector_type(2)));
 
 // K1 class table in LDS.  The class word of a byte is class * 2 (low byte) | 0xFF00 if the
-// byte is in run class D | 0xFFFF0000 if in U.  The table holds it as u16 (class * 2 |
-// D << 14 | U << 15): 512 bytes, so the bytes of text hit twice fewer LDS banks per
-// dword than with a 1 KiB u32 table, and one v_perm (sign bits of bytes 1 of e and
-// e << 1) rebuilds the word.  Built with K1_CLS16; the default u32 table measured faster.
-#ifndef K1_CLS16
-typedef uint32_t k1cls_t;
-__device__ __forceinline__ uint32_t k1_class_word(uint32_t e) { return e; }
-#else
-typedef uint16_t k1cls_t;
-__device__ __forceinline__ uint32_t k1_class_word(uint32_t e) {
-  return __builtin_amdgcn_perm(e << 1, e, 0x08080A00u);
-}
-#endif
+// byte is in run class D | 0xFFFF0000 if in U.  Text bytes of 32 lanes fall on 32 banks by
+// their value (byte mod 32), which cost 2.3 extra LDS cycles per class read
+// (profiles/r03/d1: SQ of a build without transition reads; tools/k1_banksim.py agrees), so
+// the table is replicated per lane where it fits (K1_REP).
 
 // run counters: high half = U run length, low half = D run length << 8 (both saturating);
 // m (the byte's class word) keeps the halves of the classes the byte belongs to
@@ -274,17 +267,17 @@ struct K1Chain {
   uint32_t s, cnt, mx, evl;
 };
 
-template <int KWW>
+template <int KWW, bool REP>
 struct K1Lane {
   const DevK1& d;
   const K1Args& A;
   const uint16_t* s_tab;
-  const k1cls_t* s_cls;
+  const uint32_t* s_cls;  // REP: this lane's column of the replicated table
   const uint16_t* s_accs;
   const uint32_t* s_masks;
 
-  // the class word of byte b (see k1cls_t)
-  __device__ __forceinline__ uint32_t cls(uint32_t b) const { return k1_class_word(s_cls[b]); }
+  // the class word of byte b
+  __device__ __forceinline__ uint32_t cls(uint32_t b) const { return REP ? s_cls[b << 5] : s_cls[b]; }
   // m's low byte is the byte's class * 2: the entry's byte offset is 2 * row + m[7:0]
   __device__ __forceinline__ uint32_t next(uint32_t s, uint32_t m) const {
     return *(const uint16_t*)((const uint8_t*)s_tab + (s + s + (m & 0xFFu)));
@@ -476,7 +469,12 @@ struct K1Lane {
       uint64_t pos[NS];
 #pragma unroll
       for (int i = 0; i < NS; i++) pos[i] = ghost ? A.total : a + (uint64_t)i * L + jw;
+      #ifdef K1_EXP_NOSTEP  // timing experiment only (wrong results): no byte steps, the words folded
+#pragma unroll
+      for (int ii = 0; ii < NS; ii++) c[ii].s ^= v[ii].x ^ v[ii].y ^ v[ii].z ^ v[ii].w;
+#else
       fast16<NS>(c, v, pos);
+#endif
       jc += 16;
       if (jc == C) {
         if (!ghost)
@@ -509,12 +507,28 @@ struct K1Lane {
       word(j + 32, v2);
       word(j + 48, v3);
     };
+#ifdef K1_EXP_COAL  // timing experiment only (wrong results): the wave's bytes, each load instruction 1 KiB contiguous
+    const uint64_t wbase = (it0 + q - (threadIdx.x & 63)) * ib + (threadIdx.x & 63) * 16, wlim = A.nitems * ib - 16;
     auto load = [&](uint4 (&r)[NS][4], uint64_t j) __attribute__((always_inline)) {
 #pragma unroll
       for (int i = 0; i < NS; i++)
 #pragma unroll
-        for (int t = 0; t < 4; t++) r[i][t] = *(const uint4*)(src[t] + ((uint64_t)i * L + j));
+        for (int t = 0; t < 4; t++)
+          r[i][t] = *(const uint4*)(data + min(wlim, wbase + (((uint64_t)i * (L / 64) + j / 64) * 4 + t) * 1024));
     };
+#else
+    auto load = [&](uint4 (&r)[NS][4], uint64_t j) __attribute__((always_inline)) {
+#pragma unroll
+      for (int i = 0; i < NS; i++)
+#pragma unroll
+        for (int t = 0; t < 4; t++)
+#ifdef K1_EXP_NOLOAD  // timing experiment only (wrong results): register data instead of loads
+          r[i][t] = make_uint4((uint32_t)j * 0x9E3779B1u + t, (uint32_t)j + i * 77u, (uint32_t)(j >> 3) ^ 0x5bd1e995u, (uint32_t)j * 31u + q);
+#else
+          r[i][t] = *(const uint4*)(src[t] + ((uint64_t)i * L + j));
+#endif
+    };
+#endif
 #ifdef K1_ONEBUF  // one 64-B block per chain in registers (fewer VGPRs, more waves)
     uint4 r0[NS][4];
     load(r0, 0);
@@ -541,29 +555,24 @@ struct K1Lane {
   }
 };
 
-// K1 LDS image (static, so every table address is a constant): the 256 class words at 0
-// (a byte's word is at byte * 4), the transitions from 1 KiB.  Accept masks stay in
-// global memory (rare path).
-template <int KWW, int LDSK, int NS>
-__global__ void __launch_bounds__(kK1Block) __attribute__((amdgpu_waves_per_eu(K1_WAVES, 8))) k1_kernel(DevK1 d, K1Args A) {
+// K1 LDS image (static, so every table address is a constant): the class words at 0 (REP:
+// byte b's word for lane l at (b * 32 + l % 32) * 4; else at b * 4), the transitions after
+// them.  Accept masks stay in global memory (rare path).
+template <int KWW, int LDSK, int NS, bool REP>
+__global__ void __launch_bounds__(k1_threads(LDSK)) __attribute__((amdgpu_waves_per_eu(K1_WAVES, 8))) k1_kernel(DevK1 d, K1Args A) {
   __shared__ __attribute__((aligned(16))) uint8_t smem[LDSK * 1024];
-  k1cls_t* s_cls = (k1cls_t*)smem;
-  uint16_t* s_tab = (uint16_t*)(smem + 1024);
+  constexpr uint32_t kTabOff = REP ? kK1RepBytes : 1024;
+  static_assert(!REP || LDSK * 1024 > (int)kK1RepBytes, "K1_REP needs room for the automaton");
+  uint32_t* s_cls = (uint32_t*)smem;
+  uint16_t* s_tab = (uint16_t*)(smem + kTabOff);
   {
     const uint32_t* src = (const uint32_t*)d.tab;
     uint32_t* dst = (uint32_t*)s_tab;
     for (uint32_t i = threadIdx.x; i < (d.ns * d.nc + 1) / 2; i += blockDim.x) dst[i] = src[i];
-    for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) {
-      const uint32_t w = d.cls[i];
-#ifndef K1_CLS16
-      s_cls[i] = w;
-#else
-      s_cls[i] = (k1cls_t)((w & 0xFFu) | ((w >> 31) << 15) | (((w >> 15) & 1u) << 14));
-#endif
-    }
+    for (uint32_t i = threadIdx.x; i < (REP ? 256u * 32u : 256u); i += blockDim.x) s_cls[i] = d.cls[REP ? i >> 5 : i];
   }
   __syncthreads();
-  K1Lane<KWW> L{d, A, s_tab, s_cls, d.accs, d.masks};
+  K1Lane<KWW, REP> L{d, A, s_tab, s_cls + (REP ? (threadIdx.x & 31) : 0), d.accs, d.masks};
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
 #ifdef K1_NO_QUAD
   for (uint64_t it = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; it < A.nitems; it += stride)
@@ -1110,9 +1119,9 @@ struct Lane {
   const uint64_t* s_masks;
   uint32_t file;
   uint64_t fs;
+  uint32_t group;
 
-  // rare path (an accept); the unrolled loops below never call it directly: they only OR
-  // the accept bits of 16 transitions and replay the word through step() when one is set
+  // accept at end of text (rare): one record per rule of the state's end-of-text mask
   __device__ __forceinline__ void emit(uint32_t mi, uint64_t pos) {
     const uint64_t* m = (d.state_acc && mi < d.nmasks) ? s_masks + (size_t)mi * d.mw : d.masks + (size_t)mi * d.mw;
     for (uint32_t w = 0; w < d.mw; w++)
@@ -1122,19 +1131,8 @@ struct Lane {
 
   __device__ __forceinline__ uint32_t state_of(uint32_t row) const { return __umulhi(row, d.inv_nc); }
 
-  // accept-mask index of the transition at table index ix out of row s, and its rule count
-  __device__ __forceinline__ uint32_t acc_index(uint32_t s, uint32_t ix) const {
-    return d.state_acc ? s_accs[state_of(s)] : d.acc[ix];
-  }
-  __device__ __forceinline__ const uint64_t* mask_of(uint32_t mi) const {
-    return (d.state_acc && mi < d.nmasks) ? s_masks + (size_t)mi * d.mw : d.masks + (size_t)mi * d.mw;
-  }
-  __device__ __forceinline__ uint32_t mask_rules(uint32_t mi) const {
-    const uint64_t* m = mask_of(mi);
-    uint32_t n = 0;
-    for (uint32_t w = 0; w < d.mw; w++) n += (uint32_t)__popcll(m[w]);
-    return n;
-  }
+  // the record of an accepting transition (kCandTrans: the host expands its accept mask)
+  __device__ __forceinline__ uint32_t trans(uint32_t ix) const { return kCandTrans | (group << 16) | ix; }
   // one candidate record at idx (see emit_cand)
   __device__ __forceinline__ void put(uint32_t idx, uint32_t rule, uint64_t end) const {
     if (idx < A.cand_cap && end < kCandWhole) {
@@ -1145,18 +1143,18 @@ struct Lane {
     }
   }
   // A word with an accept, again from registers (bytes lo..hi-1 of v, batch position wb):
-  // its candidates are counted, reserved with one atomic and written.  A relaxed unbounded
-  // rule accepts at every byte of a long token run, and emitting those one by one (an
-  // atomic round trip each, after byte loads from memory) made a few entries of a few
-  // dozen items the kernel's long pole (profiles/r03/d2).
+  // its accepting transitions are counted, reserved with one atomic and written as
+  // transition records.  A relaxed unbounded rule accepts at every byte of a long token
+  // run; emitting those one by one, each after a dependent global lookup of the accept
+  // mask and the rules, made entries of a few dozen items the kernel's long pole
+  // (profiles/r03/d2, r03/k2a: 30-80 items, ~600 candidates, 0.4-0.5 ms).
   __device__ void replay_emit(uint32_t s0, const uint4 v, int lo, int hi, uint64_t wb) {
     uint32_t n = 0, r = s0;
 #pragma unroll
     for (int k = 0; k < 16; k++) {
-      const uint32_t ix = r + s_cls[byte_of(v, k)];
-      const uint32_t e = s_tab[ix];
+      const uint32_t e = s_tab[r + s_cls[byte_of(v, k)]];
       const bool in = k >= lo && k < hi;
-      if (in && (e & 0x8000u)) n += mask_rules(acc_index(r, ix));
+      n += (in && (e & 0x8000u)) ? 1u : 0u;
       r = in ? (e & 0x7FFFu) : r;
     }
     if (!n) return;
@@ -1168,11 +1166,7 @@ struct Lane {
       const uint32_t ix = r + s_cls[byte_of(v, k)];
       const uint32_t e = s_tab[ix];
       const bool in = k >= lo && k < hi;
-      if (in && (e & 0x8000u)) {
-        const uint64_t* m = mask_of(acc_index(r, ix));
-        for (uint32_t w = 0; w < d.mw; w++)
-          for (uint64_t bits = m[w]; bits; bits &= bits - 1) put(at++, d.rules[w * 64 + __builtin_ctzll(bits)], wb + k - fs);
-      }
+      if (in && (e & 0x8000u)) put(at++, trans(ix), wb + k - fs);
       r = in ? (e & 0x7FFFu) : r;
     }
   }
@@ -1181,7 +1175,7 @@ struct Lane {
   __device__ __forceinline__ uint32_t step(uint32_t s, uint32_t byte, uint64_t pos) {
     const uint32_t ix = s + s_cls[byte];
     const uint32_t e = s_tab[ix];
-    if (__builtin_expect(e & 0x8000u, 0)) emit(d.state_acc ? s_accs[state_of(s)] : d.acc[ix], pos);
+    if (__builtin_expect(e & 0x8000u, 0)) emit_cand(A, file, trans(ix), pos - fs);
     return e & 0x7FFFu;
   }
 
@@ -1384,7 +1378,7 @@ __device__ __forceinline__ void k2_list_pair(const DevDFA& d, const K2Args& A, c
       const uint64_t bt = __shfl((unsigned long long)it[i].base, (int)((lane & ~3u) + t));
       src[i][t] = A.data + bt + 16u * q;
     }
-  Lane L{d, A, s_tab, s_cls, s_accs, s_masks, 0, 0};
+  Lane L{d, A, s_tab, s_cls, s_accs, s_masks, 0, 0, g};
   if (C & 127) {  // chunk sizes that are not whole 128-byte lines (tests): lane by lane
 #pragma unroll
     for (int i = 0; i < 2; i++)
@@ -1461,7 +1455,7 @@ __device__ __forceinline__ void k2_list_pair(const DevDFA& d, const K2Args& A, c
 __device__ __forceinline__ void k2_dense_entry(const DevDFA& d, const K2Args& A, uint32_t g, const uint16_t* s_tab,
                                                const uint8_t* s_cls, const uint16_t* s_accs,
                                                const uint64_t* s_masks, uint4 en) {
-  Lane L{d, A, s_tab, s_cls, s_accs, s_masks, 0, 0};
+  Lane L{d, A, s_tab, s_cls, s_accs, s_masks, 0, 0, g};
   const uint32_t* gm = A.gmask + (size_t)g * A.kw_words;
   const uint32_t always = A.galways[g];
   const uint64_t c0 = en.y + (uint64_t)threadIdx.x * kStreams;
@@ -1682,17 +1676,21 @@ struct K1Host {  // host copies of the K1 tables (adaptation rebuilds the device
 // an odd number of dwords and equal classes of different rows fall in different LDS banks
 // (ds_read_u16 banks are dword mod 32).  Padding is skipped when it would need a larger LDS
 // image or overflow the 16-bit rows.  TSG_K1_STRIDE=0 turns it off (measurements).
+// K1 LDS class of a transition table of tab_bytes (2 * the class count for the REP layout,
+// preferred; 3 = too large)
+static int k1_lds_class(size_t tab_bytes) {
+  for (int k = 0; k < 3; k++)
+    if (tab_bytes + kK1RepBytes <= (size_t)kK1Lds[k] * 1024) return 2 * k + 1;
+  return tab_bytes + 1024 <= (size_t)kK1Lds[2] * 1024 ? 2 * 2 : 2 * 3;
+}
+
 static size_t k1_stride(size_t nc, size_t ns) {
   const char* e = getenv("TSG_K1_STRIDE");
   if (e && atoi(e) == 0) return nc;
   size_t rs = nc;
   while (rs % 4 != 2) rs++;
-  auto lds_class = [&](size_t r) {
-    for (int k = 0; k < 3; k++)
-      if (ns * r * 2 + 2 + 1024 <= (size_t)kK1Lds[k] * 1024) return k;
-    return 3;
-  };
-  if ((ns - 1) * rs > 0xFFFF || lds_class(rs) != lds_class(nc)) return nc;
+  auto tab = [&](size_t r) { return (ns * r + (ns * r & 1)) * 2; };
+  if ((ns - 1) * rs > 0xFFFF || k1_lds_class(tab(rs)) != k1_lds_class(tab(nc))) return nc;
   return rs;
 }
 
@@ -1819,13 +1817,11 @@ static int make_device_k1(const Plan& p, DevK1* out, std::vector<void*>* allocs,
   }
   if ((rc = upload_vec(kwlen, &v.kw_len, allocs))) return rc;
   host->masks = masks;
-  const uint32_t need = (uint32_t)(host->tab.size() * 2) + 1024;
-  v.lds_class = 3;
-  for (uint32_t k = 0; k < 3; k++)
-    if (need <= (uint32_t)kK1Lds[k] * 1024) {
-      v.lds_class = k;
-      break;
-    }
+  const int lc = k1_lds_class(host->tab.size() * 2);
+  v.lds_class = (uint32_t)(lc >> 1);
+  v.rep = (uint32_t)(lc & 1);
+  if (getenv("TSG_K1_NOREP") && v.rep && host->tab.size() * 2 + 1024 <= (size_t)kK1Lds[v.lds_class] * 1024)
+    v.rep = 0;  // (measurements: the 256-word class table in the same LDS class)
   if (v.lds_class > 2) return fail(TSG_ERR_INTERNAL, "keyword automaton exceeds LDS");
   return TSG_OK;
 }
@@ -1941,20 +1937,21 @@ static int ensure(T** p, size_t* cap, size_t n) {
   return TSG_OK;
 }
 
-template <int LDSK, int NS>
+template <int LDSK, int NS, bool REP>
 static const void* k1_fn_w(uint32_t kw_words) {
-  if (kw_words <= 1) return (const void*)k1_kernel<1, LDSK, NS>;
-  if (kw_words <= 2) return (const void*)k1_kernel<2, LDSK, NS>;
-  if (kw_words <= 4) return (const void*)k1_kernel<4, LDSK, NS>;
-  return (const void*)k1_kernel<8, LDSK, NS>;
+  if (kw_words <= 1) return (const void*)k1_kernel<1, LDSK, NS, REP>;
+  if (kw_words <= 2) return (const void*)k1_kernel<2, LDSK, NS, REP>;
+  if (kw_words <= 4) return (const void*)k1_kernel<4, LDSK, NS, REP>;
+  return (const void*)k1_kernel<8, LDSK, NS, REP>;
 }
 
+// (the 256-word class table only in the largest class: smaller automata always fit REP)
 template <int NS>
-static const void* k1_fn_ns(uint32_t kw_words, uint32_t lds_class) {
+static const void* k1_fn_ns(uint32_t kw_words, uint32_t lds_class, uint32_t rep) {
   switch (lds_class) {
-    case 0: return k1_fn_w<kK1Lds[0], NS>(kw_words);
-    case 1: return k1_fn_w<kK1Lds[1], NS>(kw_words);
-    default: return k1_fn_w<kK1Lds[2], NS>(kw_words);
+    case 0: return k1_fn_w<kK1Lds[0], NS, true>(kw_words);
+    case 1: return k1_fn_w<kK1Lds[1], NS, true>(kw_words);
+    default: return rep ? k1_fn_w<kK1Lds[2], NS, true>(kw_words) : k1_fn_w<kK1Lds[2], NS, false>(kw_words);
   }
 }
 
@@ -1965,20 +1962,22 @@ static uint32_t k1_streams() {
   return ns;
 }
 
-static const void* k1_fn(uint32_t kw_words, uint32_t lds_class, uint32_t ns) {
-  return ns == 2 ? k1_fn_ns<2>(kw_words, lds_class) : k1_fn_ns<4>(kw_words, lds_class);
+static const void* k1_fn(uint32_t kw_words, uint32_t lds_class, uint32_t rep, uint32_t ns) {
+  return ns == 2 ? k1_fn_ns<2>(kw_words, lds_class, rep) : k1_fn_ns<4>(kw_words, lds_class, rep);
 }
 
 static int launch_k1(DeviceRules* r, const K1Args& A, hipStream_t st) {
-  // blocks per CU: 2 = the resident blocks of the 80 KiB LDS class (a persistent grid, each
-  // block stages the automaton once); TSG_K1_GRID overrides (measurements)
+  // a persistent grid of the resident blocks of the LDS class (each block stages the
+  // automaton once); TSG_K1_GRID overrides the blocks per CU (measurements)
   static const int gmul = getenv("TSG_K1_GRID") ? atoi(getenv("TSG_K1_GRID")) : 0;
-  const uint64_t cap = (uint64_t)r->grid / 8 * (gmul > 0 ? gmul : 2);
-  const int grid = (int)std::min<uint64_t>((A.nitems + kK1Block - 1) / kK1Block, cap);
+  const uint32_t lc = std::min<uint32_t>(r->k1.lds_class, 2);
+  const int threads = k1_threads(kK1Lds[lc]);
+  const uint64_t cap = (uint64_t)r->grid / 8 * (gmul > 0 ? gmul : kK1BlocksPerCU[lc]);
+  const int grid = (int)std::min<uint64_t>((A.nitems + threads - 1) / threads, cap);
   DevK1 d = r->k1;
   K1Args a = A;
   void* args[] = {&d, &a};
-  HIP_TRY(hipLaunchKernel(k1_fn(r->k1.kw_words, r->k1.lds_class, A.streams), dim3(grid), dim3(kK1Block), args, 0, st));
+  HIP_TRY(hipLaunchKernel(k1_fn(r->k1.kw_words, r->k1.lds_class, r->k1.rep, A.streams), dim3(grid), dim3(threads), args, 0, st));
   HIP_TRY(hipGetLastError());
   return TSG_OK;
 }
@@ -2101,6 +2100,7 @@ int device_rules_create(int device, const Plan& p, uint32_t chunk, uint32_t ext_
     r->has_pathdfa = true;
   }
   const uint32_t G = (uint32_t)p.groups.size();
+  if (G > 0x7FFF) return fail(TSG_ERR_INTERNAL, "more K2 groups than transition records can name");
   r->GW = std::max<uint32_t>(1, (G + 63) / 64);
   std::vector<uint32_t> gmask, galways, gevents;
   std::vector<unsigned long long> gofbit(32 * r->GW, 0);

@@ -753,14 +753,44 @@ void resolve_batch(const Ruleset& rs, const Plan& plan, const BatchView& b,
   const uint32_t F = b.nfiles;
   const size_t R = rs.rules.size();
   const uint64_t t_ser0 = __rdtsc();
+  // K2 transition records (kCandTrans) -> one candidate per rule of their accept mask
+  std::vector<Candidate> expanded;
+  const Candidate* kc = ko.cand;
+  size_t nkc = ko.ncand;
+  {
+    size_t ntrans = 0;
+    for (size_t i = 0; i < nkc; i++) ntrans += (kc[i].rule & kCandTrans) && kc[i].end != kCandWhole;
+    if (ntrans) {
+      expanded.reserve(nkc + ntrans);
+      for (size_t i = 0; i < nkc; i++) {
+        const Candidate& c = kc[i];
+        if (!(c.rule & kCandTrans) || c.end == kCandWhole) {
+          expanded.push_back(c);
+          continue;
+        }
+        const uint32_t g = (c.rule >> 16) & 0x7FFFu, ix = c.rule & 0xFFFFu;
+        if (g >= plan.groups.size()) continue;
+        const GroupPlan& gp = plan.groups[g];
+        const DFA& d = *gp.dfa;
+        const uint32_t ncd = (uint32_t)std::max(2, d.nclasses);  // the device's row width
+        const size_t st = ix / ncd, cl = std::min<size_t>(ix % ncd, (size_t)d.nclasses - 1);
+        if (st >= (size_t)d.nstates) continue;
+        const auto& m = d.masks[d.acc[st * d.nclasses + cl]];
+        for (size_t k = 0; k < gp.rules.size(); k++)
+          if ((m[k / 64] >> (k % 64)) & 1) expanded.push_back({c.file, gp.rules[k], c.end});
+      }
+      kc = expanded.data();
+      nkc = expanded.size();
+    }
+  }
   // bucket candidates by file (counting sort), then sort each file's few by (rule, end)
   std::vector<uint32_t> first(F + 1, 0);
-  for (size_t i = 0; i < ko.ncand; i++) first[ko.cand[i].file + 1]++;
+  for (size_t i = 0; i < nkc; i++) first[kc[i].file + 1]++;
   for (uint32_t f = 0; f < F; f++) first[f + 1] += first[f];
-  std::vector<Candidate> cand(ko.ncand);
+  std::vector<Candidate> cand(nkc);
   {
     std::vector<uint32_t> fill(first.begin(), first.end() - 1);
-    for (size_t i = 0; i < ko.ncand; i++) cand[fill[ko.cand[i].file]++] = ko.cand[i];
+    for (size_t i = 0; i < nkc; i++) cand[fill[kc[i].file]++] = kc[i];
   }
   auto by_rule_end = [](const Candidate& x, const Candidate& y) {
     return x.rule != y.rule ? x.rule < y.rule : x.end < y.end;

@@ -105,6 +105,11 @@ std::unique_ptr<Plan> build_plan(const Ruleset& rs, const PlanOptions& opt, std:
 // end == kCandWhole, the rule's K2 thread ran past ext_cap: resolve the rule over the whole
 // file (only that rule: the other rules of the file keep their windows).
 constexpr uint32_t kCandWhole = 0xFFFFFFFFu;
+// Candidate.rule with this bit: a K2 transition record {group g = bits 16-30, table index ix
+// = bits 0-15 (state * max(2, nclasses) + class of the group's DFA)}: the transition at
+// `end` accepts, and its accept mask names the rules (expanded on the host, so the kernel
+// looks up no mask per accepting byte)
+constexpr uint32_t kCandTrans = 0x80000000u;
 struct Candidate {
   uint32_t file;
   uint32_t rule;
