@@ -254,7 +254,15 @@ def main():
                     help="rule set: builtin (configs[1]), builtin + 1,000 user rules "
                          "(configs[3]), allow rules + exclude blocks over text and binary "
                          "blobs (configs[4])")
+    ap.add_argument("--e2e", choices=["fs", "layer"], default=None,
+                    help="end-to-end ingest + scan instead of the configs[1] line: 'fs' = a "
+                         "seeded source tree on disk (configs[0] shape, --e2e-mib), 'layer' = a "
+                         "seeded layer tar in memory (configs[2] shape); each step walks, gates "
+                         "(Required, IsBinary), packs straight into a pinned slot and scans")
+    ap.add_argument("--e2e-mib", type=int, default=0, help="e2e input size (default fs 200, layer 2048)")
     args = ap.parse_args()
+    if args.e2e:
+        return main_e2e(args)
 
     T0 = time.perf_counter()
     dist, rank, world, local = _dist()
@@ -415,6 +423,87 @@ def main():
         print(json.dumps(line), flush=True)
     if dist is not None:
         dist.destroy_process_group()
+
+
+def main_e2e(args):
+    """ingest -> findings on one GPU, every stage inside the timed step.
+    One step = tsg_fs_pack_slot / tsg_layer_pack_slot (walk, Required, IsBinary, files
+    written straight into a pinned slot) + the device scan of that slot + host resolution of
+    every finding + release.  The first step's results are checked against the exact CPU
+    path over the pageable pack of the same input; every step must find the same."""
+    import shutil
+    import tempfile
+    from trivy_amd import analyzer as A
+    from trivy_amd import configs
+    from trivy_amd import secret as S
+    from trivy_amd import walker as W
+    an = A.SecretAnalyzer()
+    an.Init("")
+    sc = an.scanner
+    mib = args.e2e_mib or (200 if args.e2e == "fs" else 2048)
+    tmp = None
+    t0 = time.perf_counter()
+    if args.e2e == "fs":
+        tmp = tempfile.mkdtemp(prefix="tsg_e2e_")
+        root = os.path.join(tmp, "tree")
+        configs.source_tree(root, mib << 20, seed=args.seed)
+        in_bytes = sum(os.path.getsize(os.path.join(d, f)) for d, _, fs in os.walk(root) for f in fs)
+        ingest = lambda ctx: W.SlotIngest.fs(ctx, root, config_path=an.configPath)  # noqa: E731
+        ref = W.NativeFS(sc, root)
+        what = "seeded source tree on local disk (page cache warm), %d MiB, configs[0] shape" % mib
+    else:
+        tar = configs.layer_tar(mib << 20, seed=args.seed)
+        in_bytes = len(tar)
+        ingest = lambda ctx: W.SlotIngest.layer(ctx, tar, config_path=an.configPath)  # noqa: E731
+        ref = W.NativeLayer(sc, tar)
+        what = "seeded uncompressed layer tar in host memory, %d MiB, configs[2] shape" % mib
+    gen_s = time.perf_counter() - t0
+    ctx = S.GpuContext(sc, 0, host_threads=args.host_threads)
+
+    def step():
+        a = time.perf_counter()
+        g = ingest(ctx)
+        b = time.perf_counter()
+        res = g.scan()
+        c = time.perf_counter()
+        nb = int(g.batch.offsets[-1])
+        g.release()
+        return res, nb, b - a, c - b
+
+    for _ in range(max(1, args.warmup)):
+        res0, scanned, _, _ = step()
+    want = sc.ScanBatch(ref.batch, nthreads=args.host_threads or 16)
+    if res0 != want:
+        raise SystemExit("bench --e2e: device results differ from the exact CPU path")
+    nfind = sum(len(r["Findings"] or []) for r in res0)
+    t_ing = t_scan = 0.0
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        res, nb, a, b = step()
+        t_ing += a
+        t_scan += b
+        if sum(len(r["Findings"] or []) for r in res) != nfind:
+            raise SystemExit("bench --e2e: findings differ between steps")
+    dt = time.perf_counter() - t0
+    ctx.close()
+    if tmp:
+        shutil.rmtree(tmp, ignore_errors=True)
+    line = {"metric": "end-to-end secret scan (ingest + scan) GB/s of input, 1 MI355X",
+            "value": round(in_bytes * args.steps / dt / 1e9, 3), "unit": "GB/s", "n_gpus": 1,
+            "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(dt / args.steps * 1e3, 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+            "data": "synthetic: " + what,
+            "config": {"workload": "e2e-" + args.e2e, "input_bytes": in_bytes,
+                       "scanned_bytes": scanned, "files_scanned": ref.batch.nfiles,
+                       "findings": nfind, "rules": len(sc.Rules)},
+            "stages": {"ingest_GBps_of_input": round(in_bytes * args.steps / t_ing / 1e9, 3),
+                       "ingest_ms_per_step": round(t_ing / args.steps * 1e3, 2),
+                       "scan_ms_per_step": round(t_scan / args.steps * 1e3, 2),
+                       "scan_GBps_of_scanned": round(scanned * args.steps / t_scan / 1e9, 3),
+                       "gen_s": round(gen_s, 2)},
+            "checks": {"step1_eq_exact_cpu": True, "findings_per_step": nfind}}
+    print(json.dumps(line), flush=True)
 
 
 if __name__ == "__main__":

@@ -397,6 +397,26 @@ void tsg_layer_range_free(tsg_layer_range* range);
 int tsg_fs_pack(const tsg_ruleset* rs, const char* root, const char* const* skip_files,
                 uint32_t n_skip_files, const char* const* skip_dirs, uint32_t n_skip_dirs,
                 const char* config_path, tsg_layer** out);
+/* Ingest straight into a pinned slot: tsg_layer_pack / tsg_layer_range_pack /
+ * tsg_fs_pack whose kept files are written into a slot acquired from ctx instead of pageable
+ * memory, so no second copy precedes the upload: a layer's files are copied once, tar ->
+ * slot, and a tree's files are read straight into it (pread).  The rule set is ctx's.  On
+ * success *slot_id is the caller's, as after tsg_slot_acquire: the slot's offsets and paths
+ * are filled in, so tsg_slot_submit(ctx, *slot_id, view.nfiles) scans it, and
+ * tsg_slot_release gives it back; the tsg_layer's view (tsg_layer_get) points into the slot
+ * and is valid until then.  Waits, like tsg_slot_acquire, while every slot is busy. */
+int tsg_layer_pack_slot(tsg_ctx* ctx, const uint8_t* tar, uint64_t tar_len,
+                        const char* const* skip_files, uint32_t n_skip_files,
+                        const char* const* skip_dirs, uint32_t n_skip_dirs, const char* config_path,
+                        uint32_t* slot_id, tsg_layer** out);
+int tsg_layer_range_pack_slot(tsg_ctx* ctx, const tsg_layer_range* range,
+                              const char* const* skip_files, uint32_t n_skip_files,
+                              const char* const* skip_dirs, uint32_t n_skip_dirs,
+                              const char* const* prior_dirs, uint32_t n_prior_dirs,
+                              const char* config_path, uint32_t* slot_id, tsg_layer** out);
+int tsg_fs_pack_slot(tsg_ctx* ctx, const char* root, const char* const* skip_files,
+                     uint32_t n_skip_files, const char* const* skip_dirs, uint32_t n_skip_dirs,
+                     const char* config_path, uint32_t* slot_id, tsg_layer** out);
 void tsg_layer_free(tsg_layer* layer);
 
 #ifdef __cplusplus

@@ -415,3 +415,34 @@ def test_multi_two_contexts_one_device_gpu(builtin):
     for i in range(0, b.nfiles, 97):
         c = bytes(b.data[int(b.offsets[i]):int(b.offsets[i + 1])])
         assert canon_secret(got[i]) == canon_secret(osc.Scan(b.path(i), c)), b.path(i)
+
+
+def test_slot_ingest_gpu(tmp_path):
+    """Ingest straight into pinned slots on the device (tsg_fs_pack_slot /
+    tsg_layer_pack_slot): the slot holds exactly the pageable pack's batch,
+    its device scan equals the exact CPU path on every file and the oracle on a sample."""
+    import numpy as np
+    from oracle import secret as O
+    from trivy_amd import analyzer as A
+    from trivy_amd import configs
+    from trivy_amd import walker as W
+    an = A.SecretAnalyzer()
+    an.Init("")
+    sc = an.scanner
+    ctx = S.GpuContext(sc, 0)
+    root = str(tmp_path / "tree")
+    configs.source_tree(root, 6 << 20, seed=3)
+    tar = configs.layer_tar(6 << 20, seed=5, binary_frac=0.1)
+    osc = O.NewScanner(None)
+    for got, ref in [(W.SlotIngest.fs(ctx, root), W.NativeFS(sc, root)),
+                     (W.SlotIngest.layer(ctx, tar), W.NativeLayer(sc, tar))]:
+        assert np.array_equal(got.batch.offsets, ref.batch.offsets)
+        n = int(ref.batch.offsets[-1])
+        assert bytes(got.batch.data[:n]) == bytes(ref.batch.data[:n])
+        res = got.scan()
+        assert res == sc.ScanBatch(ref.batch, nthreads=16)
+        for i in range(0, ref.batch.nfiles, 41):
+            c = bytes(ref.batch.data[int(ref.batch.offsets[i]):int(ref.batch.offsets[i + 1])])
+            assert canon_secret(res[i]) == canon_secret(osc.Scan(ref.batch.path(i), c)), ref.batch.path(i)
+        got.release()
+    ctx.close()

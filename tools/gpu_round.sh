@@ -17,4 +17,6 @@ echo "== configs[3]" && timeout -k 10 400 python -u bench.py --rules user1000 --
 echo "== configs[4]" && timeout -k 10 400 python -u bench.py --rules allow-exclude --steps 2 --warmup 1 --cpu-mib 256 > $out/bench_allow.json 2> $out/bench_allow.err || { tail $out/bench_allow.err; exit 5; }
 echo "== configs[0]" && timeout -k 10 400 python -u tools/fs_bench.py > $out/fs_bench.json 2> $out/fs_bench.err || { tail $out/fs_bench.err; exit 6; }
 echo "== configs[2] shape" && timeout -k 10 400 python -u tools/layer_bench.py 2 3 > $out/layer_bench.json 2> $out/layer_bench.err || { tail $out/layer_bench.err; exit 7; }
+echo "== e2e fs" && timeout -k 10 300 python -u bench.py --e2e fs --steps 3 > $out/e2e_fs.json 2> $out/e2e_fs.err || { tail $out/e2e_fs.err; exit 8; }
+echo "== e2e layer" && timeout -k 10 300 python -u bench.py --e2e layer --steps 3 > $out/e2e_layer.json 2> $out/e2e_layer.err || { tail $out/e2e_layer.err; exit 9; }
 echo done

@@ -19,4 +19,6 @@ struct tsg_result {
 namespace tsg {
 void set_error(const std::string& msg);
 int fail(int code, const std::string& msg);
+// the rule set a context was created with (pipeline.cpp)
+const tsg_ruleset* ctx_ruleset(const tsg_ctx* c);
 }  // namespace tsg

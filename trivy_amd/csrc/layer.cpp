@@ -31,6 +31,7 @@
 
 struct tsg_layer {
   std::unique_ptr<uint8_t[]> data;  // not zero-filled: every byte is copied in
+  const uint8_t* ext = nullptr;     // the kept files in a context's pinned slot (*_pack_slot)
   std::vector<uint64_t> offsets{0};
   std::string paths;
   std::vector<uint64_t> path_offsets{0};
@@ -508,11 +509,58 @@ void classify(const std::vector<TarEntry>& entries, size_t first, const Gate& g,
   }
 }
 
+}  // namespace
+}  // namespace tsg
+
+namespace tsg {
+
+struct SinkError {
+  int rc;
+  std::string msg;
+};
+
+// Where a pack's kept files go: the layer's own pageable buffer (tsg_layer_pack /
+// tsg_fs_pack), or a pinned slot of a context (the *_pack_slot entry points: the bytes are
+// written once, straight into the memory the device uploads from).
+struct Sink {
+  tsg_ctx* ctx = nullptr;
+  tsg_slot_view v{};
+  bool held = false;
+  // room for `total` bytes of nfiles files and pbytes of paths; the data pointer
+  uint8_t* reserve(tsg_layer* L, uint64_t total, uint32_t nfiles, uint64_t pbytes) {
+    if (!ctx) {
+      L->data.reset(new uint8_t[total ? total : 1]);
+      return L->data.get();
+    }
+    const int rc = tsg_slot_acquire(ctx, total, nfiles, pbytes, &v);
+    if (rc != TSG_OK) throw SinkError{rc, tsg_last_error()};
+    held = true;
+    L->ext = v.data;
+    return v.data;
+  }
+  // the batch's offsets and paths into the slot
+  void finish(const tsg_layer* L) {
+    if (!ctx) return;
+    std::memcpy(v.offsets, L->offsets.data(), L->offsets.size() * sizeof(uint64_t));
+    if (!L->paths.empty()) std::memcpy(v.paths, L->paths.data(), L->paths.size());
+    std::memcpy(v.path_offsets, L->path_offsets.data(), L->path_offsets.size() * sizeof(uint64_t));
+  }
+  uint32_t take() {
+    held = false;
+    return v.id;
+  }
+  ~Sink() {
+    if (held) (void)tsg_slot_release(ctx, v.id);
+  }
+};
+
+namespace {
+
 // AnalyzerGroup.AnalyzeFile (analyzer.go:399-409) + SecretAnalyzer.Analyze: the gates of the
 // walked files in parallel (Required's AllowPath is the costly part), then the kept files
-// copied into the batch in parallel
+// copied into the batch (the sink) in parallel
 void gate_and_pack(const uint8_t* tar, const Gate& g, const std::vector<Walked>& walked, tsg_layer* L,
-                   std::chrono::steady_clock::time_point t0) {
+                   std::chrono::steady_clock::time_point t0, Sink& sink) {
   auto now = [] { return std::chrono::steady_clock::now(); };
   const bool prof = getenv("TSG_LAYER_PROF") != nullptr;
   auto t1 = now();
@@ -535,7 +583,7 @@ void gate_and_pack(const uint8_t* tar, const Gate& g, const std::vector<Walked>&
       L->paths += walked[i].fp;
       L->path_offsets.push_back(L->paths.size());
     }
-  L->data.reset(new uint8_t[total ? total : 1]);
+  uint8_t* const out = sink.reserve(L, total, (uint32_t)(L->offsets.size() - 1), L->paths.size());
   // the copies in pieces of at most 4 MiB, so one large file does not serialize the pack
   constexpr uint64_t kPiece = 4ull << 20;
   std::vector<std::pair<size_t, uint64_t>> pieces;  // (file, offset in it)
@@ -545,8 +593,9 @@ void gate_and_pack(const uint8_t* tar, const Gate& g, const std::vector<Walked>&
   pool_for(pieces.size(), T, [&](size_t k) {
     const size_t i = pieces[k].first;
     const uint64_t o = pieces[k].second, len = std::min(kPiece, walked[i].size - o);
-    std::memcpy(L->data.get() + dst[i] + o, tar + walked[i].dpos + o, len);
+    std::memcpy(out + dst[i] + o, tar + walked[i].dpos + o, len);
   }, 16);
+  sink.finish(L);
   if (prof)
     fprintf(stderr, "layer: walk %.1f ms, gates %.1f ms, pack %.1f ms (%d threads)\n",
             std::chrono::duration<double, std::milli>(t1 - t0).count(),
@@ -562,11 +611,11 @@ void gate_and_pack(const uint8_t* tar, const Gate& g, const std::vector<Walked>&
 // needs the whole chain; the walked files are then cut into `world` contiguous runs of
 // about equal bytes, and only this rank's run is gated (Required, IsBinary) and packed.
 // (tsg_layer_range_* below splits the index itself over the ranks.)
-extern "C" int tsg_layer_pack_shard(const tsg_ruleset* rs, const uint8_t* tar, uint64_t tar_len,
-                                    const char* const* skip_files, uint32_t n_skip_files,
-                                    const char* const* skip_dirs, uint32_t n_skip_dirs,
-                                    const char* config_path, uint32_t rank, uint32_t world,
-                                    tsg_layer** out) {
+static int layer_pack(const tsg_ruleset* rs, const uint8_t* tar, uint64_t tar_len,
+                      const char* const* skip_files, uint32_t n_skip_files,
+                      const char* const* skip_dirs, uint32_t n_skip_dirs,
+                      const char* config_path, uint32_t rank, uint32_t world, Sink& sink,
+                      tsg_layer** out) {
   if (!rs || !out || (!tar && tar_len) || world == 0 || rank >= world)
     return fail(TSG_ERR_ARG, "bad argument");
   *out = nullptr;
@@ -596,14 +645,40 @@ extern "C" int tsg_layer_pack_shard(const tsg_ruleset* rs, const uint8_t* tar, u
       }
       walked.swap(mine);
     }
-    gate_and_pack(tar, g, walked, L.get(), t0);
+    gate_and_pack(tar, g, walked, L.get(), t0, sink);
     *out = L.release();
     return TSG_OK;
+  } catch (const SinkError& e) {
+    return fail(e.rc, e.msg);
   } catch (const std::bad_alloc&) {
     return fail(TSG_ERR_NOMEM, "out of memory");
   } catch (const std::exception& e) {
     return fail(TSG_ERR_INTERNAL, e.what());
   }
+}
+
+extern "C" int tsg_layer_pack_shard(const tsg_ruleset* rs, const uint8_t* tar, uint64_t tar_len,
+                                    const char* const* skip_files, uint32_t n_skip_files,
+                                    const char* const* skip_dirs, uint32_t n_skip_dirs,
+                                    const char* config_path, uint32_t rank, uint32_t world,
+                                    tsg_layer** out) {
+  Sink sink;
+  return layer_pack(rs, tar, tar_len, skip_files, n_skip_files, skip_dirs, n_skip_dirs, config_path, rank,
+                    world, sink, out);
+}
+
+// tsg_layer_pack with the kept files copied once, tar -> a pinned slot of ctx
+extern "C" int tsg_layer_pack_slot(tsg_ctx* ctx, const uint8_t* tar, uint64_t tar_len,
+                                   const char* const* skip_files, uint32_t n_skip_files,
+                                   const char* const* skip_dirs, uint32_t n_skip_dirs,
+                                   const char* config_path, uint32_t* slot_id, tsg_layer** out) {
+  if (!ctx || !slot_id) return fail(TSG_ERR_ARG, "bad argument");
+  Sink sink;
+  sink.ctx = ctx;
+  const int rc = layer_pack(ctx_ruleset(ctx), tar, tar_len, skip_files, n_skip_files, skip_dirs, n_skip_dirs,
+                            config_path, 0, 1, sink, out);
+  if (rc == TSG_OK) *slot_id = sink.take();
+  return rc;
 }
 
 // ---------------------------------------------------------------- distributed index
@@ -739,11 +814,10 @@ extern "C" int tsg_layer_range_dirs(tsg_layer_range* R, const char* const* skip_
 
 // Classify, gate and pack the range's entries (tsg_layer_pack's batch for them); `prior`
 // holds the skip dirs of the ranks before this one, in rank order.
-extern "C" int tsg_layer_range_pack(const tsg_ruleset* rs, const tsg_layer_range* R,
-                                    const char* const* skip_files, uint32_t n_skip_files,
-                                    const char* const* skip_dirs, uint32_t n_skip_dirs,
-                                    const char* const* prior, uint32_t n_prior,
-                                    const char* config_path, tsg_layer** out) {
+static int range_pack(const tsg_ruleset* rs, const tsg_layer_range* R, const char* const* skip_files,
+                      uint32_t n_skip_files, const char* const* skip_dirs, uint32_t n_skip_dirs,
+                      const char* const* prior, uint32_t n_prior, const char* config_path, tsg::Sink& sink,
+                      tsg_layer** out) {
   if (!rs || !R || !out || !R->synced) return fail(TSG_ERR_ARG, "bad argument");
   *out = nullptr;
   try {
@@ -754,9 +828,11 @@ extern "C" int tsg_layer_range_pack(const tsg_ruleset* rs, const tsg_layer_range
     for (uint32_t i = 0; i < n_prior; i++) skipped.push_back(prior[i]);
     std::vector<tsg::Walked> walked;
     tsg::classify(R->e, R->first, g, &skipped, L.get(), &walked);
-    tsg::gate_and_pack(R->tar, g, walked, L.get(), t0);
+    tsg::gate_and_pack(R->tar, g, walked, L.get(), t0, sink);
     *out = L.release();
     return TSG_OK;
+  } catch (const tsg::SinkError& e) {
+    return fail(e.rc, e.msg);
   } catch (const std::bad_alloc&) {
     return fail(TSG_ERR_NOMEM, "out of memory");
   } catch (const std::exception& e) {
@@ -764,11 +840,36 @@ extern "C" int tsg_layer_range_pack(const tsg_ruleset* rs, const tsg_layer_range
   }
 }
 
+extern "C" int tsg_layer_range_pack(const tsg_ruleset* rs, const tsg_layer_range* R,
+                                    const char* const* skip_files, uint32_t n_skip_files,
+                                    const char* const* skip_dirs, uint32_t n_skip_dirs,
+                                    const char* const* prior, uint32_t n_prior,
+                                    const char* config_path, tsg_layer** out) {
+  tsg::Sink sink;
+  return range_pack(rs, R, skip_files, n_skip_files, skip_dirs, n_skip_dirs, prior, n_prior, config_path, sink,
+                    out);
+}
+
+// tsg_layer_range_pack with the range's kept files copied once, tar -> a pinned slot of ctx
+extern "C" int tsg_layer_range_pack_slot(tsg_ctx* ctx, const tsg_layer_range* R,
+                                         const char* const* skip_files, uint32_t n_skip_files,
+                                         const char* const* skip_dirs, uint32_t n_skip_dirs,
+                                         const char* const* prior, uint32_t n_prior,
+                                         const char* config_path, uint32_t* slot_id, tsg_layer** out) {
+  if (!ctx || !slot_id) return fail(TSG_ERR_ARG, "bad argument");
+  tsg::Sink sink;
+  sink.ctx = ctx;
+  const int rc = range_pack(tsg::ctx_ruleset(ctx), R, skip_files, n_skip_files, skip_dirs, n_skip_dirs, prior,
+                            n_prior, config_path, sink, out);
+  if (rc == TSG_OK) *slot_id = sink.take();
+  return rc;
+}
+
 extern "C" void tsg_layer_range_free(tsg_layer_range* R) { delete R; }
 
 extern "C" int tsg_layer_get(const tsg_layer* L, tsg_layer_view* v) {
   if (!L || !v) return fail(TSG_ERR_ARG, "bad argument");
-  v->data = L->offsets.back() ? L->data.get() : nullptr;
+  v->data = L->ext ? L->ext : L->offsets.back() ? L->data.get() : nullptr;
   v->offsets = L->offsets.data();
   v->nfiles = (uint32_t)(L->offsets.size() - 1);
   v->paths = (const uint8_t*)L->paths.data();
@@ -788,11 +889,43 @@ extern "C" void tsg_layer_free(tsg_layer* L) { delete L; }
 // (pkg/fanal/artifact/local/fs.go:83-100) + AnalyzerGroup.AnalyzeFile's Required gate
 // (analyzer.go:399-409) + SecretAnalyzer.Analyze's IsBinary (secret.go:78-84): walks a
 // directory tree and packs every file the secret analyzer would scan into one batch.
-// Files are read in parallel on the host pool.  The reference walks with concurrent
-// goroutines (order unspecified); here files are packed in path order.
-extern "C" int tsg_fs_pack(const tsg_ruleset* rs, const char* root, const char* const* skip_files,
-                           uint32_t n_skip_files, const char* const* skip_dirs, uint32_t n_skip_dirs,
-                           const char* config_path, tsg_layer** out) {
+// The reference walks with concurrent goroutines (order unspecified); here the tree is
+// walked level by level on the host pool and files are packed in path order.
+//   1. walk: each level's directories listed in parallel; lstat per entry (regular files
+//      only, fs.go:37-38), skip dirs / files, Required on the walk-time size;
+//   2. heads: every kept file opened once in parallel; a file up to kSmall bytes is read
+//      whole, a larger one only for IsBinary's 300 bytes (utils.go:74-77);
+//   3. pack: the non-binary files in path order into the sink (a pinned slot for
+//      tsg_fs_pack_slot): small files copied from their head, large files read straight
+//      into place with pread.
+namespace tsg {
+namespace {
+
+constexpr uint64_t kSmall = 64 << 10;
+
+struct FsFile {
+  std::string full, fp;
+  uint64_t size = 0;                // at the walk
+  std::vector<uint8_t> head;        // whole content (size <= kSmall) or the first 300 bytes
+  uint64_t got = 0;                 // bytes of the file as read
+  bool keep = false;
+};
+
+// up to n bytes of the file at fd from offset 0 into p; the bytes read (a file that shrank
+// since the walk is read as it is now)
+uint64_t read_upto(int fd, uint8_t* p, uint64_t n) {
+  uint64_t r = 0;
+  while (r < n) {
+    const ssize_t k = pread(fd, p + r, n - r, (off_t)r);
+    if (k <= 0) break;
+    r += (uint64_t)k;
+  }
+  return r;
+}
+
+int fs_pack(const tsg_ruleset* rs, const char* root, const char* const* skip_files, uint32_t n_skip_files,
+            const char* const* skip_dirs, uint32_t n_skip_dirs, const char* config_path, Sink& sink,
+            tsg_layer** out) {
   if (!rs || !root || !out) return fail(TSG_ERR_ARG, "bad argument");
   *out = nullptr;
   try {
@@ -816,82 +949,148 @@ extern "C" int tsg_fs_pack(const tsg_ruleset* rs, const char* root, const char* 
       const size_t k = r0.rfind('/');
       directory = k == std::string::npos ? "." : (k == 0 ? "/" : r0.substr(0, k));
     }
-    struct Found {
-      std::string full, fp;
-      uint64_t size;
+    const int T = 16;  // the process-wide host pool (plan.cpp)
+    // 1. the walk, one level of directories at a time
+    struct Visit {
+      std::vector<std::string> children;  // a directory's entries
+      std::unique_ptr<FsFile> file;       // a kept regular file
+      bool walked = false;                // a regular file handed to the analyzer
+      int err = 0;                        // opendir errno (not EACCES)
     };
-    std::vector<Found> found;
+    std::vector<std::unique_ptr<FsFile>> files;
     uint32_t walked = 0;
-    std::vector<std::string> stack{r0};
-    while (!stack.empty()) {
-      const std::string path = stack.back();
-      stack.pop_back();
-      struct stat s2;
-      if (lstat(path.c_str(), &s2) != 0) continue;
-      if (S_ISDIR(s2.st_mode)) {
-        if (skip_dir(path)) continue;
-        DIR* d = opendir(path.c_str());
-        if (!d) {
-          if (errno == EACCES) continue;  // fs.go:48-55: permission errors are ignored
-          return fail(TSG_ERR_ARG, "walk error: cannot read " + path);
+    std::vector<std::string> level{r0};
+    while (!level.empty()) {
+      std::vector<Visit> vis(level.size());
+      pool_for(level.size(), T, [&](size_t i) {
+        const std::string& path = level[i];
+        Visit& v = vis[i];
+        struct stat s2;
+        if (lstat(path.c_str(), &s2) != 0) return;
+        if (S_ISDIR(s2.st_mode)) {
+          if (skip_dir(path)) return;
+          DIR* d = opendir(path.c_str());
+          if (!d) {
+            if (errno != EACCES) v.err = errno ? errno : EIO;  // fs.go:48-55: permission errors are ignored
+            return;
+          }
+          while (dirent* e = readdir(d)) {
+            const char* nm = e->d_name;
+            if (!strcmp(nm, ".") || !strcmp(nm, "..")) continue;
+            v.children.push_back(clean(path + "/" + nm));
+          }
+          closedir(d);
+          return;
         }
-        while (dirent* e = readdir(d)) {
-          const std::string name = e->d_name;
-          if (name == "." || name == "..") continue;
-          stack.push_back(clean(path + "/" + name));
-        }
-        closedir(d);
-        continue;
+        if (!S_ISREG(s2.st_mode)) return;  // fs.go:37-38
+        if (contains(g.skip_files, trim_left_slash(path))) return;
+        std::string fp;
+        if (!rel(directory, path, &fp)) fp = path;
+        v.walked = true;
+        if (!g.required(trim_left_slash(fp), (int64_t)s2.st_size)) return;
+        v.file.reset(new FsFile);
+        v.file->full = path;
+        v.file->fp = fp;
+        v.file->size = (uint64_t)s2.st_size;
+      }, 8);
+      std::vector<std::string> next;
+      for (size_t i = 0; i < vis.size(); i++) {
+        if (vis[i].err) return fail(TSG_ERR_ARG, "walk error: cannot read " + level[i]);
+        walked += vis[i].walked;
+        if (vis[i].file) files.push_back(std::move(vis[i].file));
+        for (auto& c : vis[i].children) next.push_back(std::move(c));
       }
-      if (!S_ISREG(s2.st_mode)) continue;  // fs.go:37-38
-      if (contains(g.skip_files, trim_left_slash(path))) continue;
-      std::string fp;
-      if (!rel(directory, path, &fp)) fp = path;
-      walked++;
-      const std::string clean_fp = trim_left_slash(fp);
-      if (!g.required(clean_fp, (int64_t)s2.st_size)) continue;
-      found.push_back({path, fp, (uint64_t)s2.st_size});
+      level.swap(next);
     }
-    std::sort(found.begin(), found.end(), [](const Found& a, const Found& b) { return a.fp < b.fp; });
-    const size_t n = found.size();
-    std::vector<uint64_t> at(n + 1, 0);
-    for (size_t i = 0; i < n; i++) at[i + 1] = at[i] + found[i].size;
+    std::sort(files.begin(), files.end(), [](const std::unique_ptr<FsFile>& a, const std::unique_ptr<FsFile>& b) {
+      return a->fp < b->fp;
+    });
+    const size_t n = files.size();
+    // 2. heads: io.ReadAll (secret.go:85) of the small files, IsBinary's head of the others
+    pool_for(n, T, [&](size_t i) {
+      FsFile& f = *files[i];
+      const int fd = open(f.full.c_str(), O_RDONLY);
+      if (fd < 0) return;  // analyzer.go:411-413: a permission error skips the file
+      const uint64_t want = f.size <= kSmall ? f.size : 300;
+      f.head.resize(want);
+      const uint64_t r = read_upto(fd, f.head.data(), want);
+      close(fd);
+      f.head.resize(r);
+      f.got = f.size <= kSmall ? r : f.size;
+      f.keep = !is_binary(f.head.data(), (int64_t)(f.size <= kSmall ? r : std::min<uint64_t>(r, f.size)));
+    }, 8);
     auto L = std::make_unique<tsg_layer>();
     L->walked = walked;
-    std::unique_ptr<uint8_t[]> buf(new uint8_t[at[n] ? at[n] : 1]);
-    std::vector<uint8_t> keep(n, 0);
-    std::vector<uint64_t> got(n, 0);
-    pool_for(n, 16, [&](size_t i) {  // io.ReadAll (secret.go:85), then utils.IsBinary
-      const int fd = open(found[i].full.c_str(), O_RDONLY);
-      if (fd < 0) return;  // analyzer.go:411-413: a permission error skips the file
-      uint64_t r = 0;
-      while (r < found[i].size) {
-        const ssize_t k = pread(fd, buf.get() + at[i] + r, found[i].size - r, (off_t)r);
-        if (k <= 0) break;
-        r += (uint64_t)k;
-      }
-      close(fd);
-      got[i] = r;  // a file that shrank since the walk is read as it is now
-      keep[i] = !is_binary(buf.get() + at[i], (int64_t)r);
-    }, 8);
+    // 3. the pack, in path order (fs scans keep the relative path: secret.go:94-96, no "/")
+    std::vector<uint64_t> at;
     uint64_t total = 0;
-    for (size_t i = 0; i < n; i++)
-      if (keep[i]) total += got[i];
-    L->data.reset(new uint8_t[total ? total : 1]);
-    uint64_t o = 0;
     for (size_t i = 0; i < n; i++) {
-      if (!keep[i]) continue;
-      std::memcpy(L->data.get() + o, buf.get() + at[i], got[i]);
-      o += got[i];
-      L->offsets.push_back(o);
-      L->paths += found[i].fp;  // fs scans keep the relative path (secret.go:94-96: no "/")
+      const FsFile& f = *files[i];
+      if (!f.keep) continue;
+      at.push_back(total);
+      total += f.got;
+      L->offsets.push_back(total);
+      L->paths += f.fp;
       L->path_offsets.push_back(L->paths.size());
     }
+    uint8_t* const dst = sink.reserve(L.get(), total, (uint32_t)at.size(), L->paths.size());
+    std::vector<size_t> kept;
+    for (size_t i = 0; i < n; i++)
+      if (files[i]->keep) kept.push_back(i);
+    std::vector<uint64_t> got(kept.size());
+    pool_for(kept.size(), T, [&](size_t k) {
+      FsFile& f = *files[kept[k]];
+      if (f.size <= kSmall) {
+        if (f.got) std::memcpy(dst + at[k], f.head.data(), f.got);
+        got[k] = f.got;
+        return;
+      }
+      const int fd = open(f.full.c_str(), O_RDONLY);
+      got[k] = fd < 0 ? 0 : read_upto(fd, dst + at[k], f.got);
+      if (fd >= 0) close(fd);
+    }, 4);
+    // a large file that shrank between the walk and its read: close the gaps (rare)
+    bool short_read = false;
+    for (size_t k = 0; k < kept.size(); k++) short_read |= got[k] != files[kept[k]]->got;
+    if (short_read) {
+      uint64_t o = 0;
+      for (size_t k = 0; k < kept.size(); k++) {
+        if (o != at[k]) std::memmove(dst + o, dst + at[k], got[k]);
+        o += got[k];
+        L->offsets[k + 1] = o;
+      }
+    }
+    sink.finish(L.get());
     *out = L.release();
     return TSG_OK;
+  } catch (const SinkError& e) {
+    return fail(e.rc, e.msg);
   } catch (const std::bad_alloc&) {
     return fail(TSG_ERR_NOMEM, "out of memory");
   } catch (const std::exception& e) {
     return fail(TSG_ERR_INTERNAL, e.what());
   }
+}
+
+}  // namespace
+}  // namespace tsg
+
+extern "C" int tsg_fs_pack(const tsg_ruleset* rs, const char* root, const char* const* skip_files,
+                           uint32_t n_skip_files, const char* const* skip_dirs, uint32_t n_skip_dirs,
+                           const char* config_path, tsg_layer** out) {
+  tsg::Sink sink;
+  return tsg::fs_pack(rs, root, skip_files, n_skip_files, skip_dirs, n_skip_dirs, config_path, sink, out);
+}
+
+// tsg_fs_pack with the kept files read straight into a pinned slot of ctx
+extern "C" int tsg_fs_pack_slot(tsg_ctx* ctx, const char* root, const char* const* skip_files,
+                                uint32_t n_skip_files, const char* const* skip_dirs, uint32_t n_skip_dirs,
+                                const char* config_path, uint32_t* slot_id, tsg_layer** out) {
+  if (!ctx || !slot_id) return fail(TSG_ERR_ARG, "bad argument");
+  tsg::Sink sink;
+  sink.ctx = ctx;
+  const int rc = tsg::fs_pack(tsg::ctx_ruleset(ctx), root, skip_files, n_skip_files, skip_dirs, n_skip_dirs,
+                              config_path, sink, out);
+  if (rc == TSG_OK) *slot_id = sink.take();
+  return rc;
 }

@@ -524,6 +524,8 @@ void q_flusher(tsg_queue* q) {
 }
 
 }  // namespace
+
+const tsg_ruleset* ctx_ruleset(const tsg_ctx* c) { return c ? c->rs : nullptr; }
 }  // namespace tsg
 
 extern "C" {

@@ -410,6 +410,81 @@ class NativeFS(NativeLayer):
         self.walked = v.walked
 
 
+class SlotIngest(NativeLayer):
+    """Ingest straight into a pinned slot of a GpuContext (tsg_layer_pack_slot /
+    tsg_fs_pack_slot / tsg_layer_range_pack_slot): the kept files are written once into the
+    memory the device uploads from.  `.batch` views the slot; `scan()` submits it and returns
+    the per-file results; `release()` (or garbage collection) gives the slot back."""
+
+    @classmethod
+    def layer(cls, ctx, tar, skip_files=(), skip_dirs=(), config_path=""):
+        self = cls.__new__(cls)
+        self._init(ctx, tar)
+        h, sid = C.c_void_p(), C.c_uint32()
+        N.check(N.lib().tsg_layer_pack_slot(ctx.handle, C.c_void_p(self._tar.ctypes.data), len(tar),
+                                            _cstrs(list(skip_files)), len(skip_files),
+                                            _cstrs(list(skip_dirs)), len(skip_dirs),
+                                            config_path.encode("utf-8", "surrogateescape"),
+                                            C.byref(sid), C.byref(h)))
+        self._adopt_slot(h, sid.value)
+        return self
+
+    @classmethod
+    def fs(cls, ctx, root, skip_files=(), skip_dirs=(), config_path=""):
+        self = cls.__new__(cls)
+        self._init(ctx, b"")
+        h, sid = C.c_void_p(), C.c_uint32()
+        N.check(N.lib().tsg_fs_pack_slot(ctx.handle, root.encode("utf-8", "surrogateescape"),
+                                         _cstrs(list(skip_files)), len(skip_files),
+                                         _cstrs(list(skip_dirs)), len(skip_dirs),
+                                         config_path.encode("utf-8", "surrogateescape"),
+                                         C.byref(sid), C.byref(h)))
+        self._adopt_slot(h, sid.value)
+        return self
+
+    @classmethod
+    def layer_range(cls, ctx, rng, skip_files=(), skip_dirs=(), prior_dirs=(), config_path=""):
+        self = cls.__new__(cls)
+        self._init(ctx, b"")
+        self._tar, self._range = rng._tar, rng
+        h, sid = C.c_void_p(), C.c_uint32()
+        N.check(N.lib().tsg_layer_range_pack_slot(
+            ctx.handle, rng._h, _cstrs(list(skip_files)), len(skip_files),
+            _cstrs(list(skip_dirs)), len(skip_dirs), _cstrs(list(prior_dirs)), len(prior_dirs),
+            config_path.encode("utf-8", "surrogateescape"), C.byref(sid), C.byref(h)))
+        self._adopt_slot(h, sid.value)
+        return self
+
+    def _init(self, ctx, tar):
+        self._h = None
+        self._slot = None
+        self._ctx = ctx
+        self._tar = np.frombuffer(tar, dtype=np.uint8) if len(tar) else np.zeros(1, np.uint8)
+
+    def _adopt_slot(self, h, sid):
+        self._slot = sid
+        self._adopt(h)
+
+    def submit(self):
+        """tsg_slot_submit of the packed files; the ticket (GpuContext.collect)."""
+        return self._ctx.submit_slot(self._slot, self.batch.nfiles, self.batch)
+
+    def scan(self):
+        """Scan.Scan of every packed file, in batch order."""
+        if not self.batch.nfiles:
+            return []
+        return self._ctx.collect(self.submit())
+
+    def release(self):
+        if self._slot is not None and self._ctx is not None and self._ctx.handle:
+            self._ctx.release_slot(self._slot)
+        self._slot = None
+
+    def __del__(self):
+        self.release()
+        NativeLayer.__del__(self)
+
+
 def analyze_fs(analyzer, root, device=None, ctx=None, emulate_chunk=0, skip_files=(), skip_dirs=()):
     """`trivy fs --security-checks secret <root>`'s secret analysis (BASELINE configs[0]):
     the native fs ingest, one batch, the sorted AnalysisResult.Secrets."""
