@@ -86,3 +86,32 @@ def test_k1_keyword_bits_exact_across_file_boundaries(builtin):
         one, _ = builtin.k1_reference(S.Batch.from_args([a]), 64)
         assert np.array_equal(kw[i], one[0]), i
     assert kw.any()
+
+
+@pytest.mark.parametrize("chunk", [64, 256])
+def test_fold_runes_unbounded_rules_emulated_vs_exact(builtin, chunk):
+    """Matches of the unbounded rules (aws-secret-access-key, aws-account-id, private-key)
+    with U+017F / U+212A inside them, before the first and after the last rune of a file:
+    the resolver's one combined fold-DFA pass (injected up to the last rune, ends from the
+    first rune on) plus the kernels' candidates must find exactly what the exact path finds."""
+    rng = np.random.default_rng(5)
+    fold = lambda s: "".join(  # noqa: E731
+        ("ſ" if c in "sS" else "K" if c in "kK" else c) if rng.random() < 0.5 else c for c in s)
+    key = "".join(rng.choice(list("ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789/+"), 40))
+    lines = ["aws_secret_access_key = '%s'" % key,
+             "AWS_SECRET_ACCESS_KEY=%s" % key,
+             "aws_account_id = 123456789012",
+             "-----BEGIN RSA PRIVATE KEY-----\nMIIEpAIBAAKCAQEA0Z3VS5JJcds3xfn\n-----END RSA PRIVATE KEY-----"]
+    args = []
+    for i in range(120):
+        parts = []
+        for _ in range(int(rng.integers(2, 8))):
+            filler = "".join(rng.choice(list("abc skx KS\n=:'\"_-"), int(rng.integers(20, 400))))
+            parts.append(fold(filler) if rng.random() < 0.5 else filler)
+            ln = lines[int(rng.integers(0, len(lines)))]
+            parts.append(fold(ln) if rng.random() < 0.7 else ln)
+        args.append(S.ScanArgs("u/%d.txt" % i, "\n".join(parts).encode()))
+    batch = S.Batch.from_args(args)
+    want = builtin.ScanBatch(batch, nthreads=8)
+    assert builtin.ScanBatch(batch, emulate_chunk=chunk) == want
+    assert sum(len(w["Findings"] or []) for w in want) > 50

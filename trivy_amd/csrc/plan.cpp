@@ -516,6 +516,7 @@ std::unique_ptr<Plan> build_plan(const Ruleset& rs, const PlanOptions& opt, std:
   tp = tnow();
   // ---- host resolver: fold-rune DFAs of the unbounded relaxed rules
   p->rule_fold_dfa.resize(R);
+  std::vector<Prog> fold_prog(R);
   pool_for(R, plan_threads, [&](size_t r) {
     const RuleC& rule = rs.rules[r];
     if (!rule.regex || p->rule_relax[r] < 0 || p->rule_maxlen[r] >= 0 || p->rule_group[r] < 0) return;
@@ -527,10 +528,32 @@ std::unique_ptr<Plan> build_plan(const Ruleset& rs, const PlanOptions& opt, std:
       auto d = build_dfa({&pr}, o, &e);
       if (d) {
         p->rule_fold_dfa[r] = std::move(d);
+        fold_prog[r] = std::move(pr);
         break;
       }
     }
   }, 1);
+  {  // all unbounded rules' fold programs in one DFA (resolve_batch: one pass per file)
+    std::vector<const Prog*> progs;
+    for (size_t r = 0; r < R; r++) {
+      if (!rs.rules[r].regex || p->rule_maxlen[r] >= 0) continue;
+      if (p->rule_fold_dfa[r]) {
+        progs.push_back(&fold_prog[r]);
+      } else if (p->rule_group[r] >= 0 && p->rule_relax[r] < 0) {
+        progs.push_back(&p->rule_prog[r]);
+      } else {
+        continue;
+      }
+      p->fold_rules.push_back((uint32_t)r);
+    }
+    if (progs.size() > 1) {
+      DFAOptions o;
+      o.max_states = 16384;
+      std::string e;
+      p->fold_all_dfa = build_dfa(progs, o, &e);
+      if (p->fold_all_dfa) p->fold_all_dfa->pack();
+    }
+  }
   // ---- host resolver: reverse DFAs of the exact programs
   p->rule_rev.resize(R);
   // (only where the forward bound is loose: unbounded or long windows; the subset
@@ -721,7 +744,17 @@ bool run_segment(const DFA& d, const uint8_t* data, uint64_t fs, uint64_t fe, ui
                  uint64_t b, uint32_t ext_cap, OnAcc on_acc) {
   const int nc = d.nclasses;
   uint32_t s = (a == fs) ? d.start[kCtxBOT] : d.start[DFA::ctx_of(data[a - 1], d)];
-  for (uint64_t p = a; p < b; p++) {
+  if (!d.packed.empty()) {  // one load per byte: next row | accept | next dead (DFA::pack)
+    uint32_t row = s * (uint32_t)nc;
+    for (uint64_t p = a; p < b; p++) {
+      const uint32_t e = row + d.cls[data[p]];
+      const uint32_t x = d.packed[e];
+      if (x >> 31) on_acc(d.acc[e], p - fs);
+      row = x & 0x3FFFFFFFu;
+    }
+    s = row / (uint32_t)nc;
+  }
+  for (uint64_t p = d.packed.empty() ? a : b; p < b; p++) {
     size_t e = (size_t)s * nc + d.cls[data[p]];
     if (d.acc[e]) on_acc(d.acc[e], p - fs);
     s = d.next[e];
@@ -861,7 +894,9 @@ void resolve_batch(const Ruleset& rs, const Plan& plan, const BatchView& b,
             (t_ser1 - t_ser0) / 1e6, nslots);
   // TSG_PROF: per-thread cycle counters (no shared atomics in the loop)
   struct alignas(64) Slot {
-    uint64_t cyc[5] = {0, 0, 0, 0, 0};  // fast files, candidate files, other files, count cand, scan_file
+    // fast files, candidate files, other files, count cand, scan_file, fold-rune keyword
+    // windows, fold windows of bounded rules, fold DFA / group DFA whole-file runs
+    uint64_t cyc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   };
   static std::atomic<int> next_tid{0};
   std::vector<Slot> slots(prof ? 256 : 0);
@@ -933,6 +968,7 @@ void resolve_batch(const Ruleset& rs, const Plan& plan, const BatchView& b,
     std::vector<const RuleWindows*> wptr(R, nullptr);
     std::vector<uint8_t> kws(R);
     for (size_t r = 0; r < R; r++) kws[r] = kw_state(r);
+    const uint64_t tk0 = prof ? __rdtsc() : 0;
     if (fbbits & 3) {
       // U+0130 / U+212A present: a keyword K1 did not see (its bit is clear; bits are exact
       // for ASCII) can only occur through one of those runes, i.e. inside a window of 3 bytes
@@ -954,6 +990,7 @@ void resolve_batch(const Ruleset& rs, const Plan& plan, const BatchView& b,
         kws[r] = hit ? 3 : 0;  // 3 -> whole-file exact resolution below
       }
     }
+    if (prof) slots[tid].cyc[5] += __rdtsc() - tk0;
     if (ovf) {
       for (size_t r = 0; r < R; r++) {
         wins[r].whole = true;
@@ -1010,7 +1047,26 @@ void resolve_batch(const Ruleset& rs, const Plan& plan, const BatchView& b,
       }
       k = e;
     }
+    const uint64_t tf0 = prof ? __rdtsc() : 0;
+    uint64_t tdfa = 0;
     if (fbbits & 6) {
+      // The windows and whole-file runs below are only needed for rules whose keyword gate
+      // passes.  A gate K1 left to the host (kws 2: an adapted hot keyword such as "key")
+      // is settled exactly first, as scan_file would (scanner.go:164-176): random binary
+      // blobs hold folding-rune byte pairs but rarely the keyword.
+      std::map<std::string, bool> kwhit;
+      for (size_t r = 0; r < R; r++) {
+        if (kws[r] != 2 || !rs.rules[r].kw_ascii || rs.rules[r].kw_lower.empty()) continue;
+        bool hit = false;
+        for (const auto& kw : rs.rules[r].kw_lower) {
+          auto it = kwhit.find(kw);
+          if (it == kwhit.end())
+            it = kwhit.emplace(kw, (fbbits & 3) ? contains_fold_runes(content, (size_t)n, kw)
+                                                : contains_fold_ascii(content, (size_t)n, kw)).first;
+          if ((hit = it->second)) break;
+        }
+        if (!hit) kws[r] = 0;
+      }
       // U+212A / U+017F join ASCII letters under (?i), which the K1 anchors (literal
       // automaton, token-run counters) do not see: a match the kernels may have missed
       // contains one of them, so its start lies within rule_maxlen bytes before it.  A
@@ -1018,8 +1074,43 @@ void resolve_batch(const Ruleset& rs, const Plan& plan, const BatchView& b,
       // exact (relaxed programs leave these runes out of their sets), else the whole file.
       std::vector<int64_t> fold;
       fold_rune_positions(content, n, 2 | 4, &fold);
+      // the unbounded rules in one pass of their combined fold DFA: threads injected up to
+      // the last rune and followed until they die; an end before the first rune belongs to
+      // a match without one (the kernels' candidates cover those)
+      std::vector<uint8_t> done(R, 0);
+      if (plan.fold_all_dfa && !fold.empty()) {
+        const DFA& fd = *plan.fold_all_dfa;
+        const size_t nf = plan.fold_rules.size();
+        std::vector<uint8_t> want(nf, 0);
+        bool any = false;
+        for (size_t k = 0; k < nf; k++) {
+          const uint32_t r = plan.fold_rules[k];
+          want[k] = !(kws[r] == 0 || kws[r] == 3 || wins[r].whole);
+          any |= want[k] != 0;
+        }
+        if (any) {
+          const uint64_t td = prof ? __rdtsc() : 0;
+          const int64_t q0 = fold.front(), q1 = fold.back();
+          run_segment(fd, content, 0, (uint64_t)n, 0, (uint64_t)std::min<int64_t>(n, q1 + 1), ~0u,
+                      [&](uint32_t mi, uint64_t pos) {
+                        if ((int64_t)pos < q0) return;
+                        const auto& m = fd.masks[mi];
+                        for (size_t k = 0; k < nf; k++)
+                          if (want[k] && ((m[k / 64] >> (k % 64)) & 1))
+                            add_end(wins[plan.fold_rules[k]], plan.fold_rules[k], (int64_t)pos);
+                      });
+          if (prof) tdfa += __rdtsc() - td;
+          for (size_t k = 0; k < nf; k++)
+            if (want[k]) {
+              const uint32_t r = plan.fold_rules[k];
+              done[r] = 1;
+              wptr[r] = &wins[r];
+              normalize(wins[r]);
+            }
+        }
+      }
       for (size_t r = 0; r < R; r++) {
-        if (kws[r] == 0 || kws[r] == 3 || !rs.rules[r].regex || wins[r].whole || fold.empty()) continue;
+        if (done[r] || kws[r] == 0 || kws[r] == 3 || !rs.rules[r].regex || wins[r].whole || fold.empty()) continue;
         RuleWindows& w = wins[r];
         wptr[r] = &w;
         const int64_t ml = plan.rule_maxlen[r];
@@ -1029,9 +1120,11 @@ void resolve_batch(const Ruleset& rs, const Plan& plan, const BatchView& b,
           // relaxed rule: its fold-rune DFA (a superset that accepts the runes) gives the
           // candidate ends over the file
           w.iv.clear();
+          const uint64_t td = prof ? __rdtsc() : 0;
           run_segment(*fd, content, 0, (uint64_t)n, 0, (uint64_t)n, ~0u, [&](uint32_t mi, uint64_t pos) {
             if (fd->masks[mi][0] & 1) add_end(w, (uint32_t)r, (int64_t)pos);
           });
+          if (prof) tdfa += __rdtsc() - td;
         } else if (plan.rule_group[r] >= 0 && plan.rule_relax[r] < 0) {
           // only an unrelaxed GPU program keeps U+017F / U+212A in its (?i) sets (relaxed
           // ones drop them, goregex.cpp Compiler::rune): a relaxed rule is resolved whole
@@ -1040,9 +1133,11 @@ void resolve_batch(const Ruleset& rs, const Plan& plan, const BatchView& b,
           while (g.rules[local] != r) local++;
           const DFA& d = *g.dfa;
           w.iv.clear();
+          const uint64_t td = prof ? __rdtsc() : 0;
           run_segment(d, content, 0, (uint64_t)n, 0, (uint64_t)n, ~0u, [&](uint32_t mi, uint64_t pos) {
             if ((d.masks[mi][local / 64] >> (local % 64)) & 1) add_end(w, (uint32_t)r, (int64_t)pos);
           });
+          if (prof) tdfa += __rdtsc() - td;
         } else {
           w.whole = true;
           w.iv.clear();
@@ -1050,6 +1145,10 @@ void resolve_batch(const Ruleset& rs, const Plan& plan, const BatchView& b,
         }
         normalize(w);
       }
+    }
+    if (prof) {
+      slots[tid].cyc[6] += __rdtsc() - tf0 - tdfa;
+      slots[tid].cyc[7] += tdfa;
     }
     // a rule whose keyword gate is uncertain and that the kernels did not scan (its
     // keyword bits were clear) is resolved over the whole file when the exact gate passes
@@ -1085,13 +1184,15 @@ void resolve_batch(const Ruleset& rs, const Plan& plan, const BatchView& b,
     if (prof) slots[tid].cyc[4] += __rdtsc() - ts0;
   });
   if (prof) {
-    uint64_t t[5] = {0, 0, 0, 0, 0};
+    uint64_t t[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     for (const auto& sl : slots)
-      for (int k = 0; k < 5; k++) t[k] += sl.cyc[k];
+      for (int k = 0; k < 8; k++) t[k] += sl.cyc[k];
     fprintf(stderr, "resolve: parallel part %.1f Mcyc wall; thread Mcyc: no-candidate files %.1f, candidate files %.1f "
             "(%lu files, %ld whole-prefix rule scans; scan_file %.1f), other %.1f\n",
             (__rdtsc() - t_par0) / 1e6, t[0] / 1e6, t[1] / 1e6, (unsigned long)t[3], (long)n_whole, t[4] / 1e6,
             t[2] / 1e6);
+    fprintf(stderr, "resolve: fold runes: keyword windows %.1f, bounded-rule windows %.1f, whole-file DFAs %.1f Mcyc\n",
+            t[5] / 1e6, t[6] / 1e6, t[7] / 1e6);
   }
 }
 

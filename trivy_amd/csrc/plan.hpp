@@ -88,6 +88,12 @@ struct Plan {
   // host over a file holding those runes, it gives candidate ends instead of a whole-file
   // FindAll.
   std::vector<std::unique_ptr<DFA>> rule_fold_dfa;
+  // The unbounded rules' fold programs (rule_fold_dfa's, or the GPU program of an unrelaxed
+  // rule, which keeps U+017F / U+212A) in ONE forward DFA, accept id k = fold_rules[k]: one
+  // pass over a file with folding runes gives every such rule's candidate ends (null: state
+  // cap; the per-rule DFAs are used)
+  std::unique_ptr<DFA> fold_all_dfa;
+  std::vector<uint32_t> fold_rules;
   std::unique_ptr<DFA> allow_path_dfa;  // Global.AllowPath on ASCII paths
 };
 
