@@ -260,6 +260,7 @@ def main():
                          "seeded layer tar in memory (configs[2] shape); each step walks, gates "
                          "(Required, IsBinary), packs straight into a pinned slot and scans")
     ap.add_argument("--e2e-mib", type=int, default=0, help="e2e input size (default fs 200, layer 2048)")
+    ap.add_argument("--e2e-slot-mib", type=int, default=0, help="e2e piece / slot size (0: 256)")
     args = ap.parse_args()
     if args.e2e:
         return main_e2e(args)
@@ -427,76 +428,93 @@ def main():
 
 def main_e2e(args):
     """ingest -> findings on one GPU, every stage inside the timed step.
-    One step = tsg_fs_pack_slot / tsg_layer_pack_slot (walk, Required, IsBinary, files
-    written straight into a pinned slot) + the device scan of that slot + host resolution of
-    every finding + release.  The first step's results are checked against the exact CPU
-    path over the pageable pack of the same input; every step must find the same."""
+    One step = one tsg_fs_scan / tsg_layer_scan call: walk, Required, IsBinary, the kept
+    files written straight into pinned slots in pieces of the context's slot size, each piece
+    uploaded, scanned and resolved while the next is written; the step ends with the
+    serialized per-file results of every kept file in the library's result buffer.  The
+    first step's result bytes must equal the exact CPU path's over the pageable pack of the
+    same input, and every step must find the same.  An unpipelined step (the pack into one
+    slot, then its scan) is timed once beside it for the stage breakdown."""
+    import ctypes as C
     import shutil
     import tempfile
+    from trivy_amd import _native as N
     from trivy_amd import analyzer as A
     from trivy_amd import configs
     from trivy_amd import secret as S
     from trivy_amd import walker as W
+    L = N.lib()
     an = A.SecretAnalyzer()
     an.Init("")
     sc = an.scanner
     mib = args.e2e_mib or (200 if args.e2e == "fs" else 2048)
     tmp = None
+    cfg = an.configPath.encode()
+    none = (C.c_char_p * 1)()
     t0 = time.perf_counter()
     if args.e2e == "fs":
         tmp = tempfile.mkdtemp(prefix="tsg_e2e_")
         root = os.path.join(tmp, "tree")
         configs.source_tree(root, mib << 20, seed=args.seed)
         in_bytes = sum(os.path.getsize(os.path.join(d, f)) for d, _, fs in os.walk(root) for f in fs)
-        ingest = lambda ctx: W.SlotIngest.fs(ctx, root, config_path=an.configPath)  # noqa: E731
+
+        def one_call(ctx, out):
+            h = C.c_void_p()
+            N.check(L.tsg_fs_scan(ctx.handle, root.encode(), none, 0, none, 0, cfg, C.byref(h), C.byref(out)))
+            L.tsg_layer_free(h)
+        unpiped = lambda ctx: W.SlotIngest.fs(ctx, root, config_path=an.configPath)  # noqa: E731
         ref = W.NativeFS(sc, root)
         what = "seeded source tree on local disk (page cache warm), %d MiB, configs[0] shape" % mib
     else:
         tar = configs.layer_tar(mib << 20, seed=args.seed)
         in_bytes = len(tar)
-        ingest = lambda ctx: W.SlotIngest.layer(ctx, tar, config_path=an.configPath)  # noqa: E731
+        import numpy as np
+        tarr = np.frombuffer(tar, dtype=np.uint8)
+
+        def one_call(ctx, out):
+            h = C.c_void_p()
+            N.check(L.tsg_layer_scan(ctx.handle, C.c_void_p(tarr.ctypes.data), len(tar), none, 0, none, 0, cfg,
+                                     C.byref(h), C.byref(out)))
+            L.tsg_layer_free(h)
+        unpiped = lambda ctx: W.SlotIngest.layer(ctx, tar, config_path=an.configPath)  # noqa: E731
         ref = W.NativeLayer(sc, tar)
         what = "seeded uncompressed layer tar in host memory, %d MiB, configs[2] shape" % mib
     gen_s = time.perf_counter() - t0
-    ctx = S.GpuContext(sc, 0, host_threads=args.host_threads)
-    import ctypes as C
-    from trivy_amd import _native as N
-    L = N.lib()
+    ctx = S.GpuContext(sc, 0, host_threads=args.host_threads, slot_mib=args.e2e_slot_mib)
+    scanned = int(ref.batch.offsets[-1])
 
     def step(check=False):
-        """ingest -> slot -> device scan -> resolved, serialized per-file results (the
-        library's result buffer: findings materialised, nothing left to the caller)"""
-        a = time.perf_counter()
-        g = ingest(ctx)
-        b = time.perf_counter()
-        t, out = C.c_uint64(), C.c_void_p()
-        N.check(L.tsg_slot_submit(ctx.handle, g._slot, g.batch.nfiles, C.byref(t)))
-        N.check(L.tsg_batch_collect(ctx.handle, t.value, C.byref(out)))
-        c = time.perf_counter()
+        out = C.c_void_p()
+        one_call(ctx, out)
         summ = _summary(out)
-        raw = _raw(out) if check else L.tsg_result_free(out)
-        nb = int(g.batch.offsets[-1])
-        g.release()
-        return summ, raw, nb, b - a, c - b
+        return summ, (_raw(out) if check else L.tsg_result_free(out))
 
     for _ in range(max(1, args.warmup)):
-        summ0, raw0, scanned, _, _ = step(check=True)
+        summ0, raw0 = step(check=True)
     out = C.c_void_p()
     t0 = time.perf_counter()
     N.check(L.tsg_scan_cpu_batch(sc.handle, *ref.batch.ptrs(), args.host_threads or 16, C.byref(out)))
     cpu_s = time.perf_counter() - t0
     if raw0 != _raw(out):
         raise SystemExit("bench --e2e: device results differ from the exact CPU path")
-    t_ing = t_scan = 0.0
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        summ, _, nb, a, b = step()
-        t_ing += a
-        t_scan += b
+        summ, _ = step()
         if summ != summ0:
             raise SystemExit("bench --e2e: findings differ between steps")
     dt = time.perf_counter() - t0
-    nfind = summ0[1]
+    # stage breakdown, unpipelined: the whole input packed into one slot, then scanned
+    a = time.perf_counter()
+    g = unpiped(ctx)
+    b = time.perf_counter()
+    tk, out = C.c_uint64(), C.c_void_p()
+    N.check(L.tsg_slot_submit(ctx.handle, g._slot, g.batch.nfiles, C.byref(tk)))
+    N.check(L.tsg_batch_collect(ctx.handle, tk.value, C.byref(out)))
+    c = time.perf_counter()
+    if _summary(out) != summ0:
+        raise SystemExit("bench --e2e: the unpipelined scan finds something else")
+    L.tsg_result_free(out)
+    g.release()
     ctx.close()
     if tmp:
         shutil.rmtree(tmp, ignore_errors=True)
@@ -506,18 +524,19 @@ def main_e2e(args):
             "ms_per_step": round(dt / args.steps * 1e3, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "u8",
             "data": "synthetic: " + what,
-            "config": {"workload": "e2e-" + args.e2e, "input_bytes": in_bytes,
-                       "scanned_bytes": scanned, "files_scanned": ref.batch.nfiles,
-                       "findings": nfind, "rules": len(sc.Rules)},
-            "stages": {"ingest_GBps_of_input": round(in_bytes * args.steps / t_ing / 1e9, 3),
-                       "ingest_ms_per_step": round(t_ing / args.steps * 1e3, 2),
-                       "scan_ms_per_step": round(t_scan / args.steps * 1e3, 2),
-                       "scan_GBps_of_scanned": round(scanned * args.steps / t_scan / 1e9, 3),
-                       "gen_s": round(gen_s, 2)},
+            "config": {"workload": "e2e-" + args.e2e, "input_bytes": in_bytes, "scanned_bytes": scanned,
+                       "files_scanned": ref.batch.nfiles, "findings": summ0[1], "rules": len(sc.Rules),
+                       "piece_mib": args.e2e_slot_mib or 256,
+                       "api": "tsg_fs_scan" if args.e2e == "fs" else "tsg_layer_scan"},
+            "unpipelined": {"ingest_ms": round((b - a) * 1e3, 2),
+                            "ingest_GBps_of_input": round(in_bytes / (b - a) / 1e9, 3),
+                            "scan_ms": round((c - b) * 1e3, 2),
+                            "scan_GBps_of_scanned": round(scanned / (c - b) / 1e9, 3)},
             "cpu_baseline": {"value": round(scanned / cpu_s / 1e9, 4), "unit": "GB/s of scanned bytes",
                              "cores": args.host_threads or 16, "kind": "port",
                              "sample": "the whole packed input; exact CPU path (tsg_scan_cpu_batch)"},
-            "checks": {"step1_eq_exact_cpu": True, "findings_per_step": nfind,
+            "gen_s": round(gen_s, 2),
+            "checks": {"step1_eq_exact_cpu": True, "findings_per_step": summ0[1],
                        "files_with_findings_per_step": summ0[0]}}
     print(json.dumps(line), flush=True)
 

@@ -417,6 +417,20 @@ int tsg_layer_range_pack_slot(tsg_ctx* ctx, const tsg_layer_range* range,
 int tsg_fs_pack_slot(tsg_ctx* ctx, const char* root, const char* const* skip_files,
                      uint32_t n_skip_files, const char* const* skip_dirs, uint32_t n_skip_dirs,
                      const char* config_path, uint32_t* slot_id, tsg_layer** out);
+/* One call per layer / tree, pipelined (what a per-layer goroutine binds,
+ * pkg/fanal/artifact/image/image.go:210-234): the walk and gates of tsg_layer_pack /
+ * tsg_fs_pack, then the kept files cut in walk order into pieces of about the context's slot
+ * size; each piece is written straight into a pinned slot and submitted while the next one
+ * is written, so ingest, upload, kernels and host resolution overlap.  *out holds one record
+ * per kept file in the order of *layer's paths (tsg_result format); *layer carries the paths,
+ * offsets, opq, wh and walked count (its data view is NULL: the bytes lived in the slots). */
+int tsg_layer_scan(tsg_ctx* ctx, const uint8_t* tar, uint64_t tar_len,
+                   const char* const* skip_files, uint32_t n_skip_files,
+                   const char* const* skip_dirs, uint32_t n_skip_dirs, const char* config_path,
+                   tsg_layer** layer, tsg_result** out);
+int tsg_fs_scan(tsg_ctx* ctx, const char* root, const char* const* skip_files, uint32_t n_skip_files,
+                const char* const* skip_dirs, uint32_t n_skip_dirs, const char* config_path,
+                tsg_layer** layer, tsg_result** out);
 void tsg_layer_free(tsg_layer* layer);
 
 #ifdef __cplusplus

@@ -446,3 +446,28 @@ def test_slot_ingest_gpu(tmp_path):
             assert canon_secret(res[i]) == canon_secret(osc.Scan(ref.batch.path(i), c)), ref.batch.path(i)
         got.release()
     ctx.close()
+
+
+def test_pipelined_layer_and_fs_scan_gpu(tmp_path):
+    """tsg_layer_scan / tsg_fs_scan on the device with 2 MiB pieces (many slots in flight):
+    results in walk order == the exact CPU path over the pageable pack."""
+    from trivy_amd import analyzer as A
+    from trivy_amd import configs
+    from trivy_amd import walker as W
+    an = A.SecretAnalyzer()
+    an.Init("")
+    sc = an.scanner
+    ctx = S.GpuContext(sc, 0, slot_mib=2)
+    tar = configs.layer_tar(12 << 20, seed=8, binary_frac=0.05)
+    ref = W.NativeLayer(sc, tar)
+    paths, res, opq, wh, walked = W.scan_layer_pipelined(ctx, tar)
+    assert paths == [ref.batch.path(i) for i in range(ref.batch.nfiles)]
+    assert res == sc.ScanBatch(ref.batch, nthreads=16)
+    assert (opq, wh, walked) == (ref.opq, ref.wh, ref.walked)
+    root = str(tmp_path / "tree")
+    configs.source_tree(root, 10 << 20, seed=4)
+    ref = W.NativeFS(sc, root)
+    paths, res, _, _, _ = W.scan_fs_pipelined(ctx, root)
+    assert paths == [ref.batch.path(i) for i in range(ref.batch.nfiles)]
+    assert res == sc.ScanBatch(ref.batch, nthreads=16)
+    ctx.close()

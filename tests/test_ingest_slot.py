@@ -167,3 +167,44 @@ def test_slot_ingest_errors(scanner, tmp_path):
     assert ok.batch.nfiles > 0
     ok.release()
     ctx.close()
+
+
+@pytest.mark.parametrize("slot_mib", [1, 256])
+def test_layer_scan_pipelined_matches_pack(scanner, slot_mib):
+    """tsg_layer_scan (pieces of slot_mib, overlapped) == scanning tsg_layer_pack's batch:
+    the same files, paths, order, results, opq / wh / walked."""
+    tar = configs.layer_tar(6 << 20, seed=11, binary_frac=0.1)
+    ctx = S.GpuContext(scanner, 0, emulate=True, slot_mib=slot_mib)
+    ref = W.NativeLayer(scanner, tar)
+    paths, res, opq, wh, walked = W.scan_layer_pipelined(ctx, tar)
+    assert paths == [ref.batch.path(i) for i in range(ref.batch.nfiles)]
+    assert res == scanner.ScanBatch(ref.batch)
+    assert (opq, wh, walked) == (ref.opq, ref.wh, ref.walked)
+    assert sum(len(r["Findings"] or []) for r in res) > 10
+    ctx.close()
+
+
+@pytest.mark.parametrize("slot_mib", [1, 256])
+def test_fs_scan_pipelined_matches_pack(tmp_path, scanner, slot_mib):
+    root = str(tmp_path / "t")
+    _tree(root)
+    configs.source_tree(os.path.join(root, "src"), 4 << 20, seed=2)
+    ctx = S.GpuContext(scanner, 0, emulate=True, slot_mib=slot_mib)
+    ref = W.NativeFS(scanner, root)
+    paths, res, _, _, walked = W.scan_fs_pipelined(ctx, root)
+    assert paths == [ref.batch.path(i) for i in range(ref.batch.nfiles)]
+    assert res == scanner.ScanBatch(ref.batch)
+    assert walked == ref.walked
+    ctx.close()
+
+
+def test_pipelined_scan_errors_leave_no_pending(scanner, tmp_path):
+    ctx = S.GpuContext(scanner, 0, emulate=True, slot_mib=1)
+    with pytest.raises(Exception):
+        W.scan_layer_pipelined(ctx, b"\x01" * 1024)
+    with pytest.raises(Exception):
+        W.scan_fs_pipelined(ctx, str(tmp_path / "missing"))
+    assert ctx.pending() == 0
+    paths, res, _, _, _ = W.scan_layer_pipelined(ctx, layer_bytes())
+    assert len(paths) == len(res) > 0
+    ctx.close()

@@ -168,6 +168,12 @@ SIGNATURES = [
     ("tsg_fs_pack_slot", C.c_int, [_P, C.c_char_p, C.POINTER(C.c_char_p), C.c_uint32,
                                    C.POINTER(C.c_char_p), C.c_uint32, C.c_char_p,
                                    C.POINTER(C.c_uint32), C.POINTER(_P)]),
+    ("tsg_layer_scan", C.c_int, [_P, _P, C.c_uint64, C.POINTER(C.c_char_p), C.c_uint32,
+                                 C.POINTER(C.c_char_p), C.c_uint32, C.c_char_p, C.POINTER(_P),
+                                 C.POINTER(_P)]),
+    ("tsg_fs_scan", C.c_int, [_P, C.c_char_p, C.POINTER(C.c_char_p), C.c_uint32,
+                              C.POINTER(C.c_char_p), C.c_uint32, C.c_char_p, C.POINTER(_P),
+                              C.POINTER(_P)]),
     ("tsg_layer_free", None, [_P]),
     ("tsg_go_sort_perm", C.c_int, [_P, _U64P, _I64P, C.c_uint32, C.POINTER(C.c_uint32)]),
     ("tsg_ruleset_rule_anchor", C.c_int, [_P, C.c_uint32, C.POINTER(C.c_uint32),

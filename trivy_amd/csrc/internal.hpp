@@ -21,4 +21,6 @@ void set_error(const std::string& msg);
 int fail(int code, const std::string& msg);
 // the rule set a context was created with (pipeline.cpp)
 const tsg_ruleset* ctx_ruleset(const tsg_ctx* c);
+// bytes of a default pinned slot (tsg_ctx_options.slot_mib)
+uint64_t ctx_slot_bytes(const tsg_ctx* c);
 }  // namespace tsg

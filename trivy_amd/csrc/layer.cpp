@@ -554,11 +554,99 @@ struct Sink {
   }
 };
 
+// The kept files of L (offsets / paths already laid out) scanned in pieces of about the
+// context's slot size, in order: each piece is written straight into a pinned slot by
+// fill(i, dst) (file i's bytes; returns how many it wrote, <= its size: a file that shrank
+// since the walk), submitted, and released (free again once its job is done), while the
+// next piece is being written, so ingest, upload, kernels and host resolution of successive
+// pieces overlap.  The pieces' results are joined in file order into *out; L's offsets
+// become the files' actual sizes.
+int scan_in_pieces(tsg_ctx* ctx, tsg_layer* L, const std::function<uint64_t(size_t, uint8_t*)>& fill,
+                   tsg_result** out) {
+  const size_t n = L->offsets.size() - 1;
+  const uint64_t piece_bytes = ctx_slot_bytes(ctx);
+  std::vector<uint64_t> tickets, got(n, 0);
+  int rc = TSG_OK;
+  size_t i = 0;
+  while (i < n && rc == TSG_OK) {
+    const size_t a = i;
+    while (i < n && (i == a || L->offsets[i + 1] - L->offsets[a] <= piece_bytes)) i++;
+    const uint64_t bytes = L->offsets[i] - L->offsets[a];
+    const uint64_t pbytes = L->path_offsets[i] - L->path_offsets[a];
+    tsg_slot_view v;
+    if ((rc = tsg_slot_acquire(ctx, bytes, (uint32_t)(i - a), pbytes, &v))) break;
+    pool_for(i - a, 16, [&](size_t k) {
+      got[a + k] = fill(a + k, v.data + (L->offsets[a + k] - L->offsets[a]));
+    }, 1);
+    uint64_t o = 0;
+    v.offsets[0] = 0;
+    v.path_offsets[0] = 0;
+    for (size_t k = 0; k < i - a; k++) {  // (a short file moves the rest of the piece down)
+      const uint64_t at = L->offsets[a + k] - L->offsets[a];
+      if (o != at && got[a + k]) std::memmove(v.data + o, v.data + at, got[a + k]);
+      o += got[a + k];
+      v.offsets[k + 1] = o;
+      v.path_offsets[k + 1] = L->path_offsets[a + k + 1] - L->path_offsets[a];
+    }
+    if (pbytes) std::memcpy(v.paths, L->paths.data() + L->path_offsets[a], pbytes);
+    uint64_t t = 0;
+    rc = tsg_slot_submit(ctx, v.id, (uint32_t)(i - a), &t);
+    const int rr = tsg_slot_release(ctx, v.id);
+    if (!rc) {
+      tickets.push_back(t);
+      rc = rr;
+    }
+  }
+  // every submitted piece is collected, also after a failure (nothing stays pending)
+  auto res = std::make_unique<tsg_result>();
+  res->buf.assign(8, '\0');
+  int crc = TSG_OK;
+  for (uint64_t t : tickets) {
+    tsg_result* r = nullptr;
+    const int e = tsg_batch_collect(ctx, t, &r);
+    if (e) {
+      if (!crc) crc = e;
+      continue;
+    }
+    res->buf.append(r->buf, 8, std::string::npos);  // the piece's records (after its header)
+    tsg_result_free(r);
+  }
+  if (rc || crc) return rc ? rc : crc;
+  const uint32_t hdr[2] = {0x31475354u, (uint32_t)n};
+  std::memcpy(&res->buf[0], hdr, 8);
+  for (size_t k = 0; k < n; k++) L->offsets[k + 1] = L->offsets[k] + got[k];
+  *out = res.release();
+  return TSG_OK;
+}
+
 namespace {
 
 // AnalyzerGroup.AnalyzeFile (analyzer.go:399-409) + SecretAnalyzer.Analyze: the gates of the
 // walked files in parallel (Required's AllowPath is the costly part), then the kept files
 // copied into the batch (the sink) in parallel
+// the gates of the walked files in parallel; the kept ones (in walk order) get their
+// offsets and "/"-prefixed paths in L; returns their indices into walked
+std::vector<size_t> gate_kept(const uint8_t* tar, const Gate& g, const std::vector<Walked>& walked, tsg_layer* L) {
+  const size_t n = walked.size();
+  std::vector<uint8_t> keep(n);
+  pool_for(n, 16, [&](size_t i) {
+    const Walked& w = walked[i];
+    keep[i] = g.required(w.fp, (int64_t)w.size) && !is_binary(tar + w.dpos, (int64_t)w.size);
+  }, 64);
+  std::vector<size_t> kept;
+  uint64_t total = 0;
+  for (size_t i = 0; i < n; i++)
+    if (keep[i]) {
+      kept.push_back(i);
+      total += walked[i].size;
+      L->offsets.push_back(total);
+      L->paths += '/';
+      L->paths += walked[i].fp;
+      L->path_offsets.push_back(L->paths.size());
+    }
+  return kept;
+}
+
 void gate_and_pack(const uint8_t* tar, const Gate& g, const std::vector<Walked>& walked, tsg_layer* L,
                    std::chrono::steady_clock::time_point t0, Sink& sink) {
   auto now = [] { return std::chrono::steady_clock::now(); };
@@ -566,23 +654,15 @@ void gate_and_pack(const uint8_t* tar, const Gate& g, const std::vector<Walked>&
   auto t1 = now();
   const size_t n = walked.size();
   const int T = 16;  // the process-wide host pool (plan.cpp)
-  std::vector<uint8_t> keep(n);
-  pool_for(n, T, [&](size_t i) {
-    const Walked& w = walked[i];
-    keep[i] = g.required(w.fp, (int64_t)w.size) && !is_binary(tar + w.dpos, (int64_t)w.size);
-  }, 64);
+  const std::vector<size_t> kept = gate_kept(tar, g, walked, L);
   auto t2 = now();
   std::vector<uint64_t> dst(n);
-  uint64_t total = 0;
-  for (size_t i = 0; i < n; i++)
-    if (keep[i]) {
-      dst[i] = total;
-      total += walked[i].size;
-      L->offsets.push_back(total);
-      L->paths += '/';
-      L->paths += walked[i].fp;
-      L->path_offsets.push_back(L->paths.size());
-    }
+  std::vector<uint8_t> keep(n, 0);
+  for (size_t k = 0; k < kept.size(); k++) {
+    dst[kept[k]] = L->offsets[k];
+    keep[kept[k]] = 1;
+  }
+  const uint64_t total = L->offsets.back();
   uint8_t* const out = sink.reserve(L, total, (uint32_t)(L->offsets.size() - 1), L->paths.size());
   // the copies in pieces of at most 4 MiB, so one large file does not serialize the pack
   constexpr uint64_t kPiece = 4ull << 20;
@@ -679,6 +759,49 @@ extern "C" int tsg_layer_pack_slot(tsg_ctx* ctx, const uint8_t* tar, uint64_t ta
                             config_path, 0, 1, sink, out);
   if (rc == TSG_OK) *slot_id = sink.take();
   return rc;
+}
+
+// One call: walk, gate and scan a layer, pipelined in pieces (scan_in_pieces)
+extern "C" int tsg_layer_scan(tsg_ctx* ctx, const uint8_t* tar, uint64_t tar_len,
+                              const char* const* skip_files, uint32_t n_skip_files,
+                              const char* const* skip_dirs, uint32_t n_skip_dirs, const char* config_path,
+                              tsg_layer** layer, tsg_result** out) {
+  if (!ctx || !layer || !out || (!tar && tar_len)) return fail(TSG_ERR_ARG, "bad argument");
+  *layer = nullptr;
+  *out = nullptr;
+  try {
+    const Gate g = make_gate(ctx_ruleset(ctx), skip_files, n_skip_files, skip_dirs, n_skip_dirs, config_path);
+    auto L = std::make_unique<tsg_layer>();
+    std::vector<TarEntry> entries;
+    {
+      std::string err;
+      if (!index_tar(tar, tar_len, &entries, &err))
+        return fail(TSG_ERR_ARG, std::string("failed to extract the archive: ") + err);
+    }
+    std::vector<std::string> skipped;
+    std::vector<Walked> walked;
+    classify(entries, 0, g, &skipped, L.get(), &walked);
+    const std::vector<size_t> kept = gate_kept(tar, g, walked, L.get());
+    constexpr uint64_t kPart = 4ull << 20;  // (a large file is copied by several threads)
+    const int rc = scan_in_pieces(ctx, L.get(), [&](size_t k, uint8_t* dst) {
+      const Walked& w = walked[kept[k]];
+      if (w.size <= kPart) {
+        std::memcpy(dst, tar + w.dpos, w.size);
+      } else {
+        pool_for((w.size + kPart - 1) / kPart, 16, [&](size_t j) {
+          std::memcpy(dst + j * kPart, tar + w.dpos + j * kPart, std::min(kPart, w.size - j * kPart));
+        }, 1);
+      }
+      return w.size;
+    }, out);
+    if (rc) return rc;
+    *layer = L.release();
+    return TSG_OK;
+  } catch (const std::bad_alloc&) {
+    return fail(TSG_ERR_NOMEM, "out of memory");
+  } catch (const std::exception& e) {
+    return fail(TSG_ERR_INTERNAL, e.what());
+  }
 }
 
 // ---------------------------------------------------------------- distributed index
@@ -869,7 +992,7 @@ extern "C" void tsg_layer_range_free(tsg_layer_range* R) { delete R; }
 
 extern "C" int tsg_layer_get(const tsg_layer* L, tsg_layer_view* v) {
   if (!L || !v) return fail(TSG_ERR_ARG, "bad argument");
-  v->data = L->ext ? L->ext : L->offsets.back() ? L->data.get() : nullptr;
+  v->data = L->ext ? L->ext : (L->offsets.back() && L->data) ? L->data.get() : nullptr;
   v->offsets = L->offsets.data();
   v->nfiles = (uint32_t)(L->offsets.size() - 1);
   v->paths = (const uint8_t*)L->paths.data();
@@ -923,12 +1046,11 @@ uint64_t read_upto(int fd, uint8_t* p, uint64_t n) {
   return r;
 }
 
-int fs_pack(const tsg_ruleset* rs, const char* root, const char* const* skip_files, uint32_t n_skip_files,
-            const char* const* skip_dirs, uint32_t n_skip_dirs, const char* config_path, Sink& sink,
-            tsg_layer** out) {
-  if (!rs || !root || !out) return fail(TSG_ERR_ARG, "bad argument");
-  *out = nullptr;
-  try {
+// steps 1-2 (walk, heads) into *files (path order, keep flags) and L's walked count
+int fs_collect(const tsg_ruleset* rs, const char* root, const char* const* skip_files, uint32_t n_skip_files,
+               const char* const* skip_dirs, uint32_t n_skip_dirs, const char* config_path,
+               std::vector<std::unique_ptr<FsFile>>* out_files, uint32_t* out_walked) {
+  {
     Gate g{rs->rs, rs->plan.get(), base(config_path ? config_path : ""), {}, {}};
     for (uint32_t i = 0; i < n_skip_files; i++)  // walk.go:25-33
       g.skip_files.push_back(trim_left_slash(clean(skip_files[i])));
@@ -1019,46 +1141,68 @@ int fs_pack(const tsg_ruleset* rs, const char* root, const char* const* skip_fil
       f.got = f.size <= kSmall ? r : f.size;
       f.keep = !is_binary(f.head.data(), (int64_t)(f.size <= kSmall ? r : std::min<uint64_t>(r, f.size)));
     }, 8);
+    *out_files = std::move(files);
+    *out_walked = walked;
+    return TSG_OK;
+  }
+}
+
+// the kept files' offsets and paths in L (fs scans keep the relative path: secret.go:94-96,
+// no "/"); returns their indices
+std::vector<size_t> fs_layout(const std::vector<std::unique_ptr<FsFile>>& files, tsg_layer* L) {
+  std::vector<size_t> kept;
+  uint64_t total = 0;
+  for (size_t i = 0; i < files.size(); i++) {
+    const FsFile& f = *files[i];
+    if (!f.keep) continue;
+    kept.push_back(i);
+    total += f.got;
+    L->offsets.push_back(total);
+    L->paths += f.fp;
+    L->path_offsets.push_back(L->paths.size());
+  }
+  return kept;
+}
+
+// file f's bytes at dst: a small file from its head, a large one read in place
+uint64_t fs_fill(FsFile& f, uint8_t* dst) {
+  if (f.size <= kSmall) {
+    if (f.got) std::memcpy(dst, f.head.data(), f.got);
+    return f.got;
+  }
+  const int fd = open(f.full.c_str(), O_RDONLY);
+  const uint64_t r = fd < 0 ? 0 : read_upto(fd, dst, f.got);
+  if (fd >= 0) close(fd);
+  return r;
+}
+
+int fs_pack(const tsg_ruleset* rs, const char* root, const char* const* skip_files, uint32_t n_skip_files,
+            const char* const* skip_dirs, uint32_t n_skip_dirs, const char* config_path, Sink& sink,
+            tsg_layer** out) {
+  if (!rs || !root || !out) return fail(TSG_ERR_ARG, "bad argument");
+  *out = nullptr;
+  try {
+    std::vector<std::unique_ptr<FsFile>> files;
+    uint32_t walked = 0;
+    int rc = fs_collect(rs, root, skip_files, n_skip_files, skip_dirs, n_skip_dirs, config_path, &files, &walked);
+    if (rc) return rc;
     auto L = std::make_unique<tsg_layer>();
     L->walked = walked;
-    // 3. the pack, in path order (fs scans keep the relative path: secret.go:94-96, no "/")
-    std::vector<uint64_t> at;
-    uint64_t total = 0;
-    for (size_t i = 0; i < n; i++) {
-      const FsFile& f = *files[i];
-      if (!f.keep) continue;
-      at.push_back(total);
-      total += f.got;
-      L->offsets.push_back(total);
-      L->paths += f.fp;
-      L->path_offsets.push_back(L->paths.size());
-    }
-    uint8_t* const dst = sink.reserve(L.get(), total, (uint32_t)at.size(), L->paths.size());
-    std::vector<size_t> kept;
-    for (size_t i = 0; i < n; i++)
-      if (files[i]->keep) kept.push_back(i);
+    // 3. the pack, in path order
+    const std::vector<size_t> kept = fs_layout(files, L.get());
+    uint8_t* const dst = sink.reserve(L.get(), L->offsets.back(), (uint32_t)kept.size(), L->paths.size());
     std::vector<uint64_t> got(kept.size());
-    pool_for(kept.size(), T, [&](size_t k) {
-      FsFile& f = *files[kept[k]];
-      if (f.size <= kSmall) {
-        if (f.got) std::memcpy(dst + at[k], f.head.data(), f.got);
-        got[k] = f.got;
-        return;
-      }
-      const int fd = open(f.full.c_str(), O_RDONLY);
-      got[k] = fd < 0 ? 0 : read_upto(fd, dst + at[k], f.got);
-      if (fd >= 0) close(fd);
-    }, 4);
+    pool_for(kept.size(), 16, [&](size_t k) { got[k] = fs_fill(*files[kept[k]], dst + L->offsets[k]); }, 4);
     // a large file that shrank between the walk and its read: close the gaps (rare)
     bool short_read = false;
-    for (size_t k = 0; k < kept.size(); k++) short_read |= got[k] != files[kept[k]]->got;
+    for (size_t k = 0; k < kept.size(); k++) short_read |= got[k] != L->offsets[k + 1] - L->offsets[k];
     if (short_read) {
       uint64_t o = 0;
       for (size_t k = 0; k < kept.size(); k++) {
-        if (o != at[k]) std::memmove(dst + o, dst + at[k], got[k]);
+        if (o != L->offsets[k]) std::memmove(dst + o, dst + L->offsets[k], got[k]);
         o += got[k];
-        L->offsets[k + 1] = o;
       }
+      for (size_t k = 0; k < kept.size(); k++) L->offsets[k + 1] = L->offsets[k] + got[k];
     }
     sink.finish(L.get());
     *out = L.release();
@@ -1080,6 +1224,34 @@ extern "C" int tsg_fs_pack(const tsg_ruleset* rs, const char* root, const char* 
                            const char* config_path, tsg_layer** out) {
   tsg::Sink sink;
   return tsg::fs_pack(rs, root, skip_files, n_skip_files, skip_dirs, n_skip_dirs, config_path, sink, out);
+}
+
+// One call: walk, gate and scan a tree, pipelined in pieces (scan_in_pieces)
+extern "C" int tsg_fs_scan(tsg_ctx* ctx, const char* root, const char* const* skip_files, uint32_t n_skip_files,
+                           const char* const* skip_dirs, uint32_t n_skip_dirs, const char* config_path,
+                           tsg_layer** layer, tsg_result** out) {
+  if (!ctx || !root || !layer || !out) return fail(TSG_ERR_ARG, "bad argument");
+  *layer = nullptr;
+  *out = nullptr;
+  try {
+    std::vector<std::unique_ptr<tsg::FsFile>> files;
+    uint32_t walked = 0;
+    int rc = tsg::fs_collect(tsg::ctx_ruleset(ctx), root, skip_files, n_skip_files, skip_dirs, n_skip_dirs,
+                             config_path, &files, &walked);
+    if (rc) return rc;
+    auto L = std::make_unique<tsg_layer>();
+    L->walked = walked;
+    const std::vector<size_t> kept = tsg::fs_layout(files, L.get());
+    rc = tsg::scan_in_pieces(ctx, L.get(), [&](size_t k, uint8_t* dst) { return tsg::fs_fill(*files[kept[k]], dst); },
+                             out);
+    if (rc) return rc;
+    *layer = L.release();
+    return TSG_OK;
+  } catch (const std::bad_alloc&) {
+    return fail(TSG_ERR_NOMEM, "out of memory");
+  } catch (const std::exception& e) {
+    return fail(TSG_ERR_INTERNAL, e.what());
+  }
 }
 
 // tsg_fs_pack with the kept files read straight into a pinned slot of ctx

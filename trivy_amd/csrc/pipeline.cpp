@@ -526,6 +526,7 @@ void q_flusher(tsg_queue* q) {
 }  // namespace
 
 const tsg_ruleset* ctx_ruleset(const tsg_ctx* c) { return c ? c->rs : nullptr; }
+uint64_t ctx_slot_bytes(const tsg_ctx* c) { return (uint64_t)(c && c->opt.slot_mib ? c->opt.slot_mib : 256) << 20; }
 }  // namespace tsg
 
 extern "C" {

@@ -485,6 +485,45 @@ class SlotIngest(NativeLayer):
         NativeLayer.__del__(self)
 
 
+def scan_layer_pipelined(ctx, tar, skip_files=(), skip_dirs=(), config_path=""):
+    """tsg_layer_scan: walk, gate and scan a layer in one pipelined call.  Returns
+    (paths, per-file Scan results in that order, opq, wh, walked)."""
+    t = np.frombuffer(tar, dtype=np.uint8) if len(tar) else np.zeros(1, np.uint8)
+    h, out = C.c_void_p(), C.c_void_p()
+    N.check(N.lib().tsg_layer_scan(ctx.handle, C.c_void_p(t.ctypes.data), len(tar),
+                                   _cstrs(list(skip_files)), len(skip_files),
+                                   _cstrs(list(skip_dirs)), len(skip_dirs),
+                                   config_path.encode("utf-8", "surrogateescape"),
+                                   C.byref(h), C.byref(out)))
+    return _pipelined_result(ctx, h, out)
+
+
+def scan_fs_pipelined(ctx, root, skip_files=(), skip_dirs=(), config_path=""):
+    """tsg_fs_scan: walk, gate and scan a tree in one pipelined call."""
+    h, out = C.c_void_p(), C.c_void_p()
+    N.check(N.lib().tsg_fs_scan(ctx.handle, root.encode("utf-8", "surrogateescape"),
+                                _cstrs(list(skip_files)), len(skip_files),
+                                _cstrs(list(skip_dirs)), len(skip_dirs),
+                                config_path.encode("utf-8", "surrogateescape"),
+                                C.byref(h), C.byref(out)))
+    return _pipelined_result(ctx, h, out)
+
+
+def _pipelined_result(ctx, h, out):
+    L = N.lib()
+    try:
+        v = N.LayerView()
+        N.check(L.tsg_layer_get(h, C.byref(v)))
+        n = v.nfiles
+        poffs = np.ctypeslib.as_array(v.path_offsets, shape=(n + 1,))
+        raw = C.string_at(v.paths, int(poffs[-1])) if n and poffs[-1] else b""
+        paths = [raw[int(poffs[i]):int(poffs[i + 1])].decode("utf-8", "surrogateescape") for i in range(n)]
+        opq, wh, walked = _nul_list(v.opq, v.opq_len), _nul_list(v.wh, v.wh_len), v.walked
+    finally:
+        L.tsg_layer_free(h)
+    return paths, ctx.scanner.decode(out, paths), opq, wh, walked
+
+
 def analyze_fs(analyzer, root, device=None, ctx=None, emulate_chunk=0, skip_files=(), skip_dirs=()):
     """`trivy fs --security-checks secret <root>`'s secret analysis (BASELINE configs[0]):
     the native fs ingest, one batch, the sorted AnalysisResult.Secrets."""
