@@ -238,6 +238,46 @@ int main(int argc, char** argv) {
   });
   tsg_multi_destroy(m);
   std::printf("multi done\n");
+  // 5. pipelined one-call layer / tree scans (1 MiB pieces) from 8 threads on one context,
+  // each == the exact CPU path over the pageable pack of the same input
+  {
+    const std::string tar = slurp(dir + "/layer.tar");
+    const std::string tree = dir + "/tree";
+    std::string want_layer, want_tree;
+    for (int which = 0; which < 2; which++) {
+      tsg_layer* L = nullptr;
+      const int rc = which == 0 ? tsg_layer_pack(rs, (const uint8_t*)tar.data(), tar.size(), nullptr, 0, nullptr, 0, "", &L)
+                                : tsg_fs_pack(rs, tree.c_str(), nullptr, 0, nullptr, 0, "", &L);
+      if (rc) return 2;
+      tsg_layer_view v;
+      tsg_layer_get(L, &v);
+      tsg_result* r = nullptr;
+      check(!tsg_scan_cpu_batch(rs, v.data, v.offsets, v.nfiles, (const char*)v.paths, v.path_offsets, 2, &r),
+            "pack cpu", which);
+      (which == 0 ? want_layer : want_tree) = take(r);
+      tsg_layer_free(L);
+    }
+    tsg_ctx* c2 = nullptr;
+    if (tsg_ctx_create(0, rs, &o, &c2)) return 2;
+    threads(8, [&](int t) {
+      for (int k = 0; k < 3; k++) {
+        tsg_layer* L = nullptr;
+        tsg_result* r = nullptr;
+        const bool lay = (t + k) % 2 == 0;
+        const int rc = lay ? tsg_layer_scan(c2, (const uint8_t*)tar.data(), tar.size(), nullptr, 0, nullptr, 0, "", &L, &r)
+                           : tsg_fs_scan(c2, tree.c_str(), nullptr, 0, nullptr, 0, "", &L, &r);
+        if (rc) {
+          check(false, "pipelined scan", t);
+          continue;
+        }
+        check(take(r) == (lay ? want_layer : want_tree), "pipelined scan result", t);
+        tsg_layer_free(L);
+      }
+    });
+    check(tsg_batch_pending(c2) == 0, "nothing pending after pipelined scans", 0);
+    tsg_ctx_destroy(c2);
+  }
+  std::printf("pipelined scans done\n");
   tsg_ruleset_destroy(rs);
   std::printf(g_fail ? "FAILED %d\n" : "OK\n", g_fail.load());
   return g_fail ? 1 : 0;

@@ -69,6 +69,11 @@ def write_inputs(d, nbytes=3 << 20, seed=9):
                                  "\x1e".join(r.Keywords), r.SecretGroupName]) + "\n")
         for a in allow:
             f.write("\x1f".join(["ALLOW", a.ID, a.Description, na(a.Regex), na(a.Path)]) + "\n")
+    from trivy_amd import configs
+    with open(os.path.join(d, "layer.tar"), "wb") as f:  # pipelined layer / tree scans
+        f.write(configs.layer_tar(nbytes // 2, seed=seed, binary_frac=0.05))
+    if not os.path.isdir(os.path.join(d, "tree")):
+        configs.source_tree(os.path.join(d, "tree"), nbytes // 2, seed=seed)
     b = corpus.fold_runes_batch(seed, nbytes=nbytes, plants=200, frac=0.05)
     b.data.tofile(os.path.join(d, "data.bin"))
     np.asarray(b.offsets, dtype=np.uint64).tofile(os.path.join(d, "offsets.bin"))
