@@ -21,6 +21,11 @@ for v in "$@"; do
     notab) build $v -DK1_EXP_NO_TAB ;;
     k2ctr) build $v -DK2_TRACE_CTR ;;
     coal) build $v -DK1_EXP_COAL ;;
+    clspf8) build $v -DK1_CLSPF=8 ;;
+    clspf8_ip) build $v -DK1_CLSPF=8 -DK1_INPLACE ;;
+    clspf4) build $v -DK1_CLSPF=4 ;;
+    clspf4_ip) build $v -DK1_CLSPF=4 -DK1_INPLACE ;;
+    inplace) build $v -DK1_INPLACE ;;
     nostep) build $v -DK1_EXP_NOSTEP ;;
     noload) build $v -DK1_EXP_NOLOAD ;;
     noload_nolds) build $v -DK1_EXP_NOLOAD -DK1_EXP_NO_CLS -DK1_EXP_NO_TAB ;;

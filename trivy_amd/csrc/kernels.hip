@@ -48,15 +48,17 @@ enum : uint8_t { kGroupNone = 0, kGroupList = 1, kGroupDense = 2, kGroupSkip = 3
       return fail(TSG_ERR_GPU, std::string(#x) + ": " + hipGetErrorString(e_));       \
   } while (0)
 
-// K1 registers: one 64-B block per chain in flight and the byte loop unrolled 8 ways keep a
-// lane at 128 VGPRs, so 4 waves per SIMD hide the dependent LDS chain (2.1 -> 2.5 TB/s
-// against two blocks in flight, 16-way unroll and 206 VGPRs at 2 waves per SIMD;
-// profiles/r02/k1_experiments/occupancy_sweep.txt).  K1_TWOBUF restores the old layout.
+// K1 registers: one 64-B block per chain, stepped in place and then reloaded, with the byte
+// loop unrolled 8 ways keeps a lane at 100 VGPRs: 4 waves per SIMD hide the dependent LDS
+// chain (2.1 -> 2.5 TB/s against two blocks in flight, 16-way unroll and 206 VGPRs at 2
+// waves per SIMD, profiles/r02/k1_experiments/occupancy_sweep.txt; in place instead of a
+// copy of the block: 0.400 -> 0.385 ms per GiB, profiles/r03/k1).  K1_ONEBUF / K1_TWOBUF
+// restore the older layouts.
 #ifndef K1_UNROLL
 #define K1_UNROLL 8
 #endif
-#ifndef K1_TWOBUF
-#define K1_ONEBUF
+#if !defined(K1_TWOBUF) && !defined(K1_ONEBUF)
+#define K1_INPLACE  // one 64-B block per chain, stepped in place then reloaded (100 VGPRs)
 #endif
 #ifdef K1_EXP_COAL  // timing experiment only (wrong results): wave-coalesced loads
 #define K1_ADDR(a, i, off) \
@@ -328,6 +330,30 @@ struct K1Lane {
       s0[i] = c[i].s;
       top[i] = 0;
     }
+#ifdef K1_CLSPF
+    // the word's class words first (they do not depend on the state): their LDS reads are
+    // all in flight together instead of each one in front of its transition
+    constexpr int G = K1_CLSPF;  // bytes per prefetch group
+#pragma unroll 1
+    for (int k0 = 0; k0 < 16; k0 += G) {
+      uint32_t mw[NS][G];
+#pragma unroll
+      for (int k = 0; k < G; k++)
+#pragma unroll
+        for (int i = 0; i < NS; i++) mw[i][k] = cls(byte_of(v[i], k0 + k));
+#pragma unroll
+      for (int k = 0; k < G; k++)
+#pragma unroll
+        for (int i = 0; i < NS; i++) {
+          const uint32_t m = mw[i][k];
+          c[i].s = next(c[i].s, m);
+          top[i] = max(top[i], c[i].s);
+          c[i].cnt = run_step(c[i].cnt, m);
+          c[i].mx = run_max(c[i].mx, c[i].cnt);
+        }
+      __builtin_amdgcn_sched_barrier(0);  // (the next group's reads stay behind this one)
+    }
+#else
 #pragma unroll(NS > 4 ? K1_UNROLL / 4 : K1_UNROLL)
     for (int k = 0; k < 16; k++)
 #pragma unroll
@@ -348,6 +374,7 @@ struct K1Lane {
         c[i].mx = run_max(c[i].mx, c[i].cnt);
 #endif
       }
+#endif
 #pragma unroll
     for (int i = 0; i < NS; i++)
       if (__builtin_expect(top[i] >= d.acc_row, 0)) replay16(c[i], s0[i], v[i], pos[i]);
@@ -529,7 +556,14 @@ struct K1Lane {
 #endif
     };
 #endif
-#ifdef K1_ONEBUF  // one 64-B block per chain in registers (fewer VGPRs, more waves)
+#if defined(K1_INPLACE)  // one 64-B block per chain, stepped in place, then reloaded
+    uint4 r0[NS][4];
+    load(r0, 0);
+    for (uint64_t j = 0; j < L; j += 64) {
+      block(j, r0);
+      load(r0, j + 64);
+    }
+#elif defined(K1_ONEBUF)  // one 64-B block per chain in registers (fewer VGPRs, more waves)
     uint4 r0[NS][4];
     load(r0, 0);
     for (uint64_t j = 0; j < L; j += 64) {
