@@ -467,3 +467,39 @@ def test_layer_ranges_with_parallel_subranges(analyzer, monkeypatch, range_kib, 
         except Exception:
             got = "error"
         assert got == want
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_native_layer_skip_dirs_random_trees(analyzer, seed):
+    """Random trees with skipped dirs (.git, --skip-dirs, system dirs) at every depth, files
+    below, beside and as the PARENT of a skipped dir (filepath.Rel(skipDir, file) == ".."
+    counts as under it, tar.go:100-111), dirs listed before and after their files, and
+    unclean names: the native walk (prefix tests for clean paths, Rel otherwise) ==
+    the Python walker (Rel everywhere)."""
+    import random
+    rnd = random.Random(seed)
+    names = ["a", "b", ".git", "vendor", "proc", "q", "x.y", "..", "."]
+    buf = io.BytesIO()
+    with tarfile.open(fileobj=buf, mode="w", format=tarfile.PAX_FORMAT) as tf:
+        for _ in range(400):
+            depth = rnd.randint(1, 4)
+            parts = [rnd.choice(names) for _ in range(depth)]
+            p = "/".join(parts)
+            if rnd.random() < 0.1:
+                p = "./" + p
+            if rnd.random() < 0.05:
+                p = p.replace("/", "//", 1)
+            if rnd.random() < 0.3:
+                _special(tf, p + "/", tarfile.DIRTYPE)
+            else:
+                _reg(tf, p, ("GITHUB_TOKEN=%s\nfile %s\n" % (GHP, p)).encode())
+    tar = buf.getvalue()
+    skip_dirs = ["/vendor", "b/q"]
+    want = []
+    opq, wh = W.LayerTar([], skip_dirs).Walk(io.BytesIO(tar), lambda p, n, rd: (
+        analyzer.Required(p, n) and not A.IsBinary(c := rd(), n) and want.append(("/" + p, c))))
+    lay = W.NativeLayer(analyzer.scanner, tar, skip_dirs=skip_dirs)
+    b = lay.batch
+    got = [(b.path(i), bytes(b.data[int(b.offsets[i]):int(b.offsets[i + 1])])) for i in range(b.nfiles)]
+    assert got == want
+    assert len(want) > 20

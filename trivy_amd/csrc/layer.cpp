@@ -15,6 +15,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <string_view>
 #include <functional>
 #include <memory>
 #include <vector>
@@ -43,7 +44,25 @@ namespace tsg {
 namespace {
 
 // Go path.Clean
+// true when p is what clean(p) returns (no empty, "." or ".." element, no trailing "/"):
+// most archive names are, and the general path below allocates per element
+bool is_clean(const std::string& p) {
+  if (p.empty()) return false;
+  if (p == "/") return true;
+  if (p.back() == '/') return false;
+  size_t start = p[0] == '/' ? 1 : 0;
+  for (size_t k = start; k <= p.size(); k++) {
+    if (k < p.size() && p[k] != '/') continue;
+    const size_t len = k - start;
+    if (len == 0 || (len == 1 && p[start] == '.') || (len == 2 && p[start] == '.' && p[start + 1] == '.'))
+      return false;
+    start = k + 1;
+  }
+  return true;
+}
+
 std::string clean(const std::string& p) {
+  if (is_clean(p)) return p;
   if (p.empty()) return ".";
   const bool rooted = p[0] == '/';
   std::vector<std::string> out;
@@ -461,51 +480,80 @@ Gate make_gate(const tsg_ruleset* rs, const char* const* skip_files, uint32_t n_
 // LayerTar.Walk's per-entry logic (tar.go:45-84) over entries [first, end) in walk order.
 // `skipped` is tar.go:35's skipDirs: it enters with the directories earlier entries added
 // (another rank's, for a range of the layer) and leaves with this run's appended.
+// a clean relative path without "." / ".." elements: Rel against another such path is
+// decided by prefix tests (under_skipped)
+bool simple_rel_path(const std::string& p) { return is_clean(p) && p[0] != '/'; }
+
+// tar.go:100-111 underSkippedDir: filepath.Rel(skipDir, filePath) does not start with
+// "../" for some skip dir (an error ends the search: false).  For simple paths Rel is a
+// prefix question: fp is the dir, below it, or its parent (Rel = "..", which Go also
+// counts); other paths take the general Rel.
+bool under_skipped(const std::vector<std::string>& skipped, const std::vector<uint8_t>& simple, const std::string& fp) {
+  const bool fsimple = simple_rel_path(fp);
+  for (size_t i = 0; i < skipped.size(); i++) {
+    const std::string& s = skipped[i];
+    if (fsimple && simple[i]) {
+      const size_t ns = s.size(), nf = fp.size();
+      if (nf == ns ? fp == s
+                   : nf > ns ? fp[ns] == '/' && fp.compare(0, ns, s) == 0
+                             : s[nf] == '/' && s.compare(0, nf, fp) == 0 && s.find('/', nf + 1) == std::string::npos)
+        return true;
+      continue;
+    }
+    std::string r;
+    if (!rel(s, fp, &r)) return false;
+    if (!starts_with(r, "../")) return true;
+  }
+  return false;
+}
+
+// LayerTar.Walk's per-entry logic (tar.go:45-84) over entries [first, end) in walk order.
+// `skipped` is tar.go:35's skipDirs: it enters with the directories earlier entries added
+// (another rank's, for a range of the layer) and leaves with this run's appended.
 void classify(const std::vector<TarEntry>& entries, size_t first, const Gate& g,
               std::vector<std::string>* skipped, tsg_layer* L, std::vector<Walked>* walked) {
+  // the per-entry path work (Clean) in parallel; the walk's order-dependent logic (skip
+  // dirs accumulate in archive order) sequentially below
+  const size_t n = entries.size() > first ? entries.size() - first : 0;
+  std::vector<std::string> fps(n);
+  pool_for(n, 16, [&](size_t j) { fps[j] = trim_left_slash(clean(entries[first + j].name)); }, 256);
+  std::vector<uint8_t> simple;
+  for (const auto& x : *skipped) simple.push_back(simple_rel_path(x));
   for (size_t i = first; i < entries.size(); i++) {
     const TarEntry& te = entries[i];
     char type = te.type;
     const std::string& name = te.name;
     if (type == 0) type = (!name.empty() && name.back() == '/') ? '5' : '0';
-    const std::string fp = trim_left_slash(clean(name));
-    const size_t k = fp.rfind('/');
-    const std::string fdir = k == std::string::npos ? "" : fp.substr(0, k + 1);
-    const std::string fname = k == std::string::npos ? fp : fp.substr(k + 1);
+    std::string& fp = fps[i - first];  // (already without leading "/")
+    const std::string_view fv(fp);
+    const size_t k = fv.rfind('/');
+    const std::string_view fdir = k == std::string_view::npos ? std::string_view() : fv.substr(0, k + 1);
+    const std::string_view fname = k == std::string_view::npos ? fv : fv.substr(k + 1);
     if (fname == ".wh..wh..opq") {
-      L->opq += fdir;
+      L->opq.append(fdir);
       L->opq += '\0';
       continue;
     }
-    if (starts_with(fname, ".wh.")) {
-      std::string j = fdir + fname.substr(4);
+    if (fname.substr(0, 4) == ".wh.") {
+      std::string j(fdir);
+      j.append(fname.substr(4));
       L->wh += j.empty() ? j : clean(j);
       L->wh += '\0';
       continue;
     }
     if (type == '5') {
-      const std::string d = trim_left_slash(fp);
-      if (base(d) == ".git" || contains(g.skip_dirs, d)) {  // walk.go:56-71
+      // walk.go:56-71 (base(fp) is fname for a non-empty clean path)
+      if ((!fp.empty() && fname == ".git") || contains(g.skip_dirs, fp)) {
         skipped->push_back(fp);
-        continue;
+        simple.push_back(simple_rel_path(fp));
       }
-    } else if (type == '0') {
-      if (contains(g.skip_files, trim_left_slash(fp))) continue;
-    } else {
-      continue;  // links, devices, fifos, sparse, contiguous: no content
+      continue;  // directories carry no content
     }
-    bool under = false;  // tar.go:100-111
-    for (const auto& s : *skipped) {
-      std::string r;
-      if (!rel(s, fp, &r)) break;
-      if (!starts_with(r, "../")) {
-        under = true;
-        break;
-      }
-    }
-    if (under || type == '5') continue;
+    if (type != '0') continue;  // links, devices, fifos, sparse, contiguous: no content
+    if (contains(g.skip_files, fp)) continue;
+    if (under_skipped(*skipped, simple, fp)) continue;
     L->walked++;
-    walked->push_back({te.dpos, te.size, fp});
+    walked->push_back({te.dpos, te.size, std::move(fp)});
   }
 }
 
@@ -568,16 +616,28 @@ int scan_in_pieces(tsg_ctx* ctx, tsg_layer* L, const std::function<uint64_t(size
   std::vector<uint64_t> tickets, got(n, 0);
   int rc = TSG_OK;
   size_t i = 0;
+  // TSG_LAYER_PROF: time waiting for a free slot, writing pieces, submitting, collecting
+  const bool prof = getenv("TSG_LAYER_PROF") != nullptr;
+  double t_acq = 0, t_fill = 0, t_sub = 0;
+  auto now = [] { return std::chrono::steady_clock::now(); };
+  auto ms = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
+    return std::chrono::duration<double, std::milli>(b - a).count();
+  };
   while (i < n && rc == TSG_OK) {
     const size_t a = i;
     while (i < n && (i == a || L->offsets[i + 1] - L->offsets[a] <= piece_bytes)) i++;
     const uint64_t bytes = L->offsets[i] - L->offsets[a];
     const uint64_t pbytes = L->path_offsets[i] - L->path_offsets[a];
     tsg_slot_view v;
+    const auto p0 = now();
     if ((rc = tsg_slot_acquire(ctx, bytes, (uint32_t)(i - a), pbytes, &v))) break;
+    const auto p1 = now();
     pool_for(i - a, 16, [&](size_t k) {
       got[a + k] = fill(a + k, v.data + (L->offsets[a + k] - L->offsets[a]));
     }, 1);
+    const auto p2 = now();
+    t_acq += ms(p0, p1);
+    t_fill += ms(p1, p2);
     uint64_t o = 0;
     v.offsets[0] = 0;
     v.path_offsets[0] = 0;
@@ -590,13 +650,16 @@ int scan_in_pieces(tsg_ctx* ctx, tsg_layer* L, const std::function<uint64_t(size
     }
     if (pbytes) std::memcpy(v.paths, L->paths.data() + L->path_offsets[a], pbytes);
     uint64_t t = 0;
+    const auto p3 = now();
     rc = tsg_slot_submit(ctx, v.id, (uint32_t)(i - a), &t);
     const int rr = tsg_slot_release(ctx, v.id);
+    t_sub += ms(p3, now());
     if (!rc) {
       tickets.push_back(t);
       rc = rr;
     }
   }
+  const auto c0 = now();
   // every submitted piece is collected, also after a failure (nothing stays pending)
   auto res = std::make_unique<tsg_result>();
   res->buf.assign(8, '\0');
@@ -611,6 +674,9 @@ int scan_in_pieces(tsg_ctx* ctx, tsg_layer* L, const std::function<uint64_t(size
     res->buf.append(r->buf, 8, std::string::npos);  // the piece's records (after its header)
     tsg_result_free(r);
   }
+  if (prof)
+    fprintf(stderr, "pieces: %zu pieces, %zu files: slot waits %.1f ms, writes %.1f ms, submits %.1f ms, "
+            "collect after the last submit %.1f ms\n", tickets.size(), n, t_acq, t_fill, t_sub, ms(c0, now()));
   if (rc || crc) return rc ? rc : crc;
   const uint32_t hdr[2] = {0x31475354u, (uint32_t)n};
   std::memcpy(&res->buf[0], hdr, 8);
@@ -770,6 +836,7 @@ extern "C" int tsg_layer_scan(tsg_ctx* ctx, const uint8_t* tar, uint64_t tar_len
   *layer = nullptr;
   *out = nullptr;
   try {
+    const auto t0 = std::chrono::steady_clock::now();
     const Gate g = make_gate(ctx_ruleset(ctx), skip_files, n_skip_files, skip_dirs, n_skip_dirs, config_path);
     auto L = std::make_unique<tsg_layer>();
     std::vector<TarEntry> entries;
@@ -778,10 +845,17 @@ extern "C" int tsg_layer_scan(tsg_ctx* ctx, const uint8_t* tar, uint64_t tar_len
       if (!index_tar(tar, tar_len, &entries, &err))
         return fail(TSG_ERR_ARG, std::string("failed to extract the archive: ") + err);
     }
+    const auto t1 = std::chrono::steady_clock::now();
     std::vector<std::string> skipped;
     std::vector<Walked> walked;
     classify(entries, 0, g, &skipped, L.get(), &walked);
+    const auto t2 = std::chrono::steady_clock::now();
     const std::vector<size_t> kept = gate_kept(tar, g, walked, L.get());
+    if (getenv("TSG_LAYER_PROF"))
+      fprintf(stderr, "layer scan: index %.1f ms, classify %.1f ms, gates %.1f ms\n",
+              std::chrono::duration<double, std::milli>(t1 - t0).count(),
+              std::chrono::duration<double, std::milli>(t2 - t1).count(),
+              std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t2).count());
     constexpr uint64_t kPart = 4ull << 20;  // (a large file is copied by several threads)
     const int rc = scan_in_pieces(ctx, L.get(), [&](size_t k, uint8_t* dst) {
       const Walked& w = walked[kept[k]];
@@ -1072,6 +1146,7 @@ int fs_collect(const tsg_ruleset* rs, const char* root, const char* const* skip_
       directory = k == std::string::npos ? "." : (k == 0 ? "/" : r0.substr(0, k));
     }
     const int T = 16;  // the process-wide host pool (plan.cpp)
+    const auto t_walk0 = std::chrono::steady_clock::now();
     // 1. the walk, one level of directories at a time
     struct Visit {
       std::vector<std::string> children;  // a directory's entries
@@ -1124,6 +1199,7 @@ int fs_collect(const tsg_ruleset* rs, const char* root, const char* const* skip_
       }
       level.swap(next);
     }
+    const auto tw = std::chrono::steady_clock::now();
     std::sort(files.begin(), files.end(), [](const std::unique_ptr<FsFile>& a, const std::unique_ptr<FsFile>& b) {
       return a->fp < b->fp;
     });
@@ -1141,6 +1217,10 @@ int fs_collect(const tsg_ruleset* rs, const char* root, const char* const* skip_
       f.got = f.size <= kSmall ? r : f.size;
       f.keep = !is_binary(f.head.data(), (int64_t)(f.size <= kSmall ? r : std::min<uint64_t>(r, f.size)));
     }, 8);
+    if (getenv("TSG_LAYER_PROF"))
+      fprintf(stderr, "fs: walk %.1f ms, heads %.1f ms (%zu files)\n",
+              std::chrono::duration<double, std::milli>(tw - t_walk0).count(),
+              std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tw).count(), n);
     *out_files = std::move(files);
     *out_walked = walked;
     return TSG_OK;
