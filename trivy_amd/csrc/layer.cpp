@@ -612,7 +612,10 @@ struct Sink {
 int scan_in_pieces(tsg_ctx* ctx, tsg_layer* L, const std::function<uint64_t(size_t, uint8_t*)>& fill,
                    tsg_result** out) {
   const size_t n = L->offsets.size() - 1;
-  const uint64_t piece_bytes = ctx_slot_bytes(ctx);
+  // about 8 pieces (at least 32 MiB, at most a slot), so that even a small input overlaps
+  // its writes with the scans of its first pieces
+  const uint64_t piece_bytes =
+      std::min(ctx_slot_bytes(ctx), std::max<uint64_t>(32ull << 20, L->offsets.back() / 8));
   std::vector<uint64_t> tickets, got(n, 0);
   int rc = TSG_OK;
   size_t i = 0;
@@ -1121,6 +1124,19 @@ uint64_t read_upto(int fd, uint8_t* p, uint64_t n) {
 }
 
 // steps 1-2 (walk, heads) into *files (path order, keep flags) and L's walked count
+// 2. io.ReadAll (secret.go:85) of a small file, IsBinary's head of a large one
+void read_head(FsFile& f) {
+  const int fd = open(f.full.c_str(), O_RDONLY);
+  if (fd < 0) return;  // analyzer.go:411-413: a permission error skips the file
+  const uint64_t want = f.size <= kSmall ? f.size : 300;
+  f.head.resize(want);
+  const uint64_t r = read_upto(fd, f.head.data(), want);
+  close(fd);
+  f.head.resize(r);
+  f.got = f.size <= kSmall ? r : f.size;
+  f.keep = !is_binary(f.head.data(), (int64_t)(f.size <= kSmall ? r : std::min<uint64_t>(r, f.size)));
+}
+
 int fs_collect(const tsg_ruleset* rs, const char* root, const char* const* skip_files, uint32_t n_skip_files,
                const char* const* skip_dirs, uint32_t n_skip_dirs, const char* config_path,
                std::vector<std::unique_ptr<FsFile>>* out_files, uint32_t* out_walked) {
@@ -1189,6 +1205,7 @@ int fs_collect(const tsg_ruleset* rs, const char* root, const char* const* skip_
         v.file->full = path;
         v.file->fp = fp;
         v.file->size = (uint64_t)s2.st_size;
+        read_head(*v.file);  // (in the walk: reads overlap the listing of other dirs)
       }, 8);
       std::vector<std::string> next;
       for (size_t i = 0; i < vis.size(); i++) {
@@ -1204,19 +1221,6 @@ int fs_collect(const tsg_ruleset* rs, const char* root, const char* const* skip_
       return a->fp < b->fp;
     });
     const size_t n = files.size();
-    // 2. heads: io.ReadAll (secret.go:85) of the small files, IsBinary's head of the others
-    pool_for(n, T, [&](size_t i) {
-      FsFile& f = *files[i];
-      const int fd = open(f.full.c_str(), O_RDONLY);
-      if (fd < 0) return;  // analyzer.go:411-413: a permission error skips the file
-      const uint64_t want = f.size <= kSmall ? f.size : 300;
-      f.head.resize(want);
-      const uint64_t r = read_upto(fd, f.head.data(), want);
-      close(fd);
-      f.head.resize(r);
-      f.got = f.size <= kSmall ? r : f.size;
-      f.keep = !is_binary(f.head.data(), (int64_t)(f.size <= kSmall ? r : std::min<uint64_t>(r, f.size)));
-    }, 8);
     if (getenv("TSG_LAYER_PROF"))
       fprintf(stderr, "fs: walk %.1f ms, heads %.1f ms (%zu files)\n",
               std::chrono::duration<double, std::milli>(tw - t_walk0).count(),
