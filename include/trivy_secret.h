@@ -151,7 +151,7 @@ typedef struct tsg_ctx_options {
   int32_t host_threads;      /* resolver threads; <= 0 = 16 */
   uint32_t adapt_mib;        /* first batch of at least this many MiB samples K1's literal
                                 frequencies and stops reporting the frequent ones (their
-                                keyword gates are then checked on the host); 0 = 64,
+                                keyword gates are then checked on the host); 0 = 16,
                                 0xFFFFFFFF = never */
   uint32_t flags;            /* TSG_CTX_* */
   uint32_t slot_mib;         /* default capacity of a pinned slot (tsg_queue batches,

@@ -612,10 +612,12 @@ struct Sink {
 int scan_in_pieces(tsg_ctx* ctx, tsg_layer* L, const std::function<uint64_t(size_t, uint8_t*)>& fill,
                    tsg_result** out) {
   const size_t n = L->offsets.size() - 1;
-  // about 8 pieces (at least 32 MiB, at most a slot), so that even a small input overlaps
-  // its writes with the scans of its first pieces
+  // about 8 pieces of at least 160 MiB (a batch has fixed costs: tools/batch_sizes.py) and
+  // at most a slot
+  // (TSG_PIECE_MIB overrides the floor: measurements)
+  static const uint64_t floor_mib = getenv("TSG_PIECE_MIB") ? std::max(1, atoi(getenv("TSG_PIECE_MIB"))) : 160;
   const uint64_t piece_bytes =
-      std::min(ctx_slot_bytes(ctx), std::max<uint64_t>(32ull << 20, L->offsets.back() / 8));
+      std::min(ctx_slot_bytes(ctx), std::max<uint64_t>(floor_mib << 20, L->offsets.back() / 8));
   std::vector<uint64_t> tickets, got(n, 0);
   int rc = TSG_OK;
   size_t i = 0;
