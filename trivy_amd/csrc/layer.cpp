@@ -1127,13 +1127,10 @@ uint64_t read_upto(int fd, uint8_t* p, uint64_t n) {
 
 // steps 1-2 (walk, heads) into *files (path order, keep flags) and L's walked count
 // 2. io.ReadAll (secret.go:85) of a small file, IsBinary's head of a large one
-void read_head(FsFile& f) {
-  const int fd = open(f.full.c_str(), O_RDONLY);
-  if (fd < 0) return;  // analyzer.go:411-413: a permission error skips the file
+void read_head(FsFile& f, int fd) {
   const uint64_t want = f.size <= kSmall ? f.size : 300;
   f.head.resize(want);
   const uint64_t r = read_upto(fd, f.head.data(), want);
-  close(fd);
   f.head.resize(r);
   f.got = f.size <= kSmall ? r : f.size;
   f.keep = !is_binary(f.head.data(), (int64_t)(f.size <= kSmall ? r : std::min<uint64_t>(r, f.size)));
@@ -1165,56 +1162,112 @@ int fs_collect(const tsg_ruleset* rs, const char* root, const char* const* skip_
     }
     const int T = 16;  // the process-wide host pool (plan.cpp)
     const auto t_walk0 = std::chrono::steady_clock::now();
-    // 1. the walk, one level of directories at a time
-    struct Visit {
-      std::vector<std::string> children;  // a directory's entries
-      std::unique_ptr<FsFile> file;       // a kept regular file
-      bool walked = false;                // a regular file handed to the analyzer
-      int err = 0;                        // opendir errno (not EACCES)
-    };
     std::vector<std::unique_ptr<FsFile>> files;
     uint32_t walked = 0;
-    std::vector<std::string> level{r0};
+    // a regular file at `path` (name relative to the open directory dfd, or dfd < 0): the
+    // walk's file callback, its Required gate and its head; true if walked
+    auto visit_file = [&](int dfd, const char* name, const std::string& path, std::unique_ptr<FsFile>* keep) {
+      if (contains(g.skip_files, trim_left_slash(path))) return false;
+      std::string fp;
+      if (!rel(directory, path, &fp)) fp = path;
+      const int fd = dfd >= 0 ? openat(dfd, name, O_RDONLY | O_NOFOLLOW | O_CLOEXEC)
+                              : open(path.c_str(), O_RDONLY | O_NOFOLLOW | O_CLOEXEC);
+      if (fd < 0) return true;  // analyzer.go:411-413: a permission error skips the file
+      struct stat fs2;
+      if (fstat(fd, &fs2) != 0 || !S_ISREG(fs2.st_mode)) {  // (replaced since the listing)
+        close(fd);
+        return false;
+      }
+      if (g.required(trim_left_slash(fp), (int64_t)fs2.st_size)) {
+        auto f = std::make_unique<FsFile>();
+        f->full = path;
+        f->fp = std::move(fp);
+        f->size = (uint64_t)fs2.st_size;
+        read_head(*f, fd);
+        *keep = std::move(f);
+      }
+      close(fd);
+      return true;
+    };
+    std::vector<std::string> level;
+    {
+      struct stat s0;
+      if (lstat(r0.c_str(), &s0) == 0 && S_ISDIR(s0.st_mode)) {
+        level.push_back(r0);
+      } else if (lstat(r0.c_str(), &s0) == 0 && S_ISREG(s0.st_mode)) {  // fs.go:37-38
+        std::unique_ptr<FsFile> f;
+        walked += visit_file(-1, nullptr, r0, &f);
+        if (f) files.push_back(std::move(f));
+      }
+    }
+    // 1. the walk, one level of directories at a time (at most kDirs open at once): the
+    // level's directories listed in parallel (d_type; lstat only where the file system
+    // does not say), then its regular files opened relative to their directory, in parallel
+    constexpr size_t kDirs = 256;
+    struct Dir {
+      DIR* d = nullptr;
+      int err = 0;                                  // open errno (not EACCES)
+      std::vector<std::string> subdirs;             // cleaned paths
+      std::vector<std::string> names;               // regular files
+    };
+    struct Entry {
+      uint32_t dir;
+      const std::string* name;
+    };
     while (!level.empty()) {
-      std::vector<Visit> vis(level.size());
-      pool_for(level.size(), T, [&](size_t i) {
-        const std::string& path = level[i];
-        Visit& v = vis[i];
-        struct stat s2;
-        if (lstat(path.c_str(), &s2) != 0) return;
-        if (S_ISDIR(s2.st_mode)) {
+      std::vector<std::string> next;
+      for (size_t l0 = 0; l0 < level.size(); l0 += kDirs) {
+        const size_t nd = std::min(kDirs, level.size() - l0);
+        std::vector<Dir> dirs(nd);
+        pool_for(nd, T, [&](size_t i) {
+          const std::string& path = level[l0 + i];
+          Dir& v = dirs[i];
           if (skip_dir(path)) return;
-          DIR* d = opendir(path.c_str());
-          if (!d) {
-            if (errno != EACCES) v.err = errno ? errno : EIO;  // fs.go:48-55: permission errors are ignored
+          const int fd = open(path.c_str(), O_RDONLY | O_DIRECTORY | O_NOFOLLOW | O_CLOEXEC);
+          if (fd < 0 || !(v.d = fdopendir(fd))) {
+            if (fd >= 0) close(fd);
+            // fs.go:48-55: permission errors are ignored; so is a directory gone (or
+            // replaced) since its parent was listed
+            if (errno != EACCES && errno != ENOENT && errno != ENOTDIR && errno != ELOOP) v.err = errno ? errno : EIO;
             return;
           }
-          while (dirent* e = readdir(d)) {
+          const int dfd = dirfd(v.d);
+          while (dirent* e = readdir(v.d)) {
             const char* nm = e->d_name;
             if (!strcmp(nm, ".") || !strcmp(nm, "..")) continue;
-            v.children.push_back(clean(path + "/" + nm));
+            unsigned char t = e->d_type;
+            if (t == DT_UNKNOWN) {
+              struct stat s2;
+              if (fstatat(dfd, nm, &s2, AT_SYMLINK_NOFOLLOW) != 0) continue;
+              t = S_ISDIR(s2.st_mode) ? DT_DIR : S_ISREG(s2.st_mode) ? DT_REG : DT_LNK;
+            }
+            if (t == DT_DIR) v.subdirs.push_back(clean(path + "/" + nm));
+            else if (t == DT_REG) v.names.push_back(nm);
           }
-          closedir(d);
-          return;
+        }, 1);
+        std::vector<Entry> ents;
+        for (size_t i = 0; i < nd; i++) {
+          if (dirs[i].err) {
+            for (auto& v : dirs) if (v.d) closedir(v.d);
+            return fail(TSG_ERR_ARG, "walk error: cannot read " + level[l0 + i]);
+          }
+          for (const auto& nm : dirs[i].names) ents.push_back({(uint32_t)i, &nm});
         }
-        if (!S_ISREG(s2.st_mode)) return;  // fs.go:37-38
-        if (contains(g.skip_files, trim_left_slash(path))) return;
-        std::string fp;
-        if (!rel(directory, path, &fp)) fp = path;
-        v.walked = true;
-        if (!g.required(trim_left_slash(fp), (int64_t)s2.st_size)) return;
-        v.file.reset(new FsFile);
-        v.file->full = path;
-        v.file->fp = fp;
-        v.file->size = (uint64_t)s2.st_size;
-        read_head(*v.file);  // (in the walk: reads overlap the listing of other dirs)
-      }, 8);
-      std::vector<std::string> next;
-      for (size_t i = 0; i < vis.size(); i++) {
-        if (vis[i].err) return fail(TSG_ERR_ARG, "walk error: cannot read " + level[i]);
-        walked += vis[i].walked;
-        if (vis[i].file) files.push_back(std::move(vis[i].file));
-        for (auto& c : vis[i].children) next.push_back(std::move(c));
+        std::vector<std::unique_ptr<FsFile>> got(ents.size());
+        std::vector<uint8_t> wk(ents.size(), 0);
+        pool_for(ents.size(), T, [&](size_t k) {
+          const Dir& v = dirs[ents[k].dir];
+          wk[k] = visit_file(dirfd(v.d), ents[k].name->c_str(), clean(level[l0 + ents[k].dir] + "/" + *ents[k].name),
+                             &got[k]);
+        }, 8);
+        for (size_t k = 0; k < ents.size(); k++) {
+          walked += wk[k];
+          if (got[k]) files.push_back(std::move(got[k]));
+        }
+        for (auto& v : dirs) {
+          if (v.d) closedir(v.d);
+          for (auto& c : v.subdirs) next.push_back(std::move(c));
+        }
       }
       level.swap(next);
     }
