@@ -610,7 +610,7 @@ struct Sink {
 // pieces overlap.  The pieces' results are joined in file order into *out; L's offsets
 // become the files' actual sizes.
 int scan_in_pieces(tsg_ctx* ctx, tsg_layer* L, const std::function<uint64_t(size_t, uint8_t*)>& fill,
-                   tsg_result** out) {
+                   tsg_result** out, const std::vector<uint8_t>* drop) {
   const size_t n = L->offsets.size() - 1;
   // about 8 pieces of at least 160 MiB (a batch has fixed costs: tools/batch_sizes.py) and
   // at most a slot
@@ -685,6 +685,28 @@ int scan_in_pieces(tsg_ctx* ctx, tsg_layer* L, const std::function<uint64_t(size
   if (rc || crc) return rc ? rc : crc;
   const uint32_t hdr[2] = {0x31475354u, (uint32_t)n};
   std::memcpy(&res->buf[0], hdr, 8);
+  if (drop) {  // the files fill() dropped leave the result and L
+    std::vector<size_t> rec;
+    result_record_spans(res->buf, &rec);
+    auto kept = std::make_unique<tsg_result>();
+    kept->buf.assign(8, '\0');
+    std::string paths;
+    std::vector<uint64_t> offs{0}, poffs{0};
+    for (size_t k = 0; k < n; k++) {
+      if ((*drop)[k]) continue;
+      kept->buf.append(res->buf, rec[k], rec[k + 1] - rec[k]);
+      offs.push_back(offs.back() + got[k]);
+      paths.append(L->paths, L->path_offsets[k], L->path_offsets[k + 1] - L->path_offsets[k]);
+      poffs.push_back(paths.size());
+    }
+    const uint32_t h2[2] = {0x31475354u, (uint32_t)(offs.size() - 1)};
+    std::memcpy(&kept->buf[0], h2, 8);
+    L->offsets.swap(offs);
+    L->path_offsets.swap(poffs);
+    L->paths.swap(paths);
+    *out = kept.release();
+    return TSG_OK;
+  }
   for (size_t k = 0; k < n; k++) L->offsets[k + 1] = L->offsets[k] + got[k];
   *out = res.release();
   return TSG_OK;
@@ -872,7 +894,7 @@ extern "C" int tsg_layer_scan(tsg_ctx* ctx, const uint8_t* tar, uint64_t tar_len
         }, 1);
       }
       return w.size;
-    }, out);
+    }, out, nullptr);
     if (rc) return rc;
     *layer = L.release();
     return TSG_OK;
@@ -1136,9 +1158,12 @@ void read_head(FsFile& f, int fd) {
   f.keep = !is_binary(f.head.data(), (int64_t)(f.size <= kSmall ? r : std::min<uint64_t>(r, f.size)));
 }
 
+// heads = false: no file is opened; every file that passes Required is listed with its
+// lstat size (keep, got = size), for a caller that reads files straight into place and
+// applies IsBinary there (tsg_fs_scan)
 int fs_collect(const tsg_ruleset* rs, const char* root, const char* const* skip_files, uint32_t n_skip_files,
                const char* const* skip_dirs, uint32_t n_skip_dirs, const char* config_path,
-               std::vector<std::unique_ptr<FsFile>>* out_files, uint32_t* out_walked) {
+               std::vector<std::unique_ptr<FsFile>>* out_files, uint32_t* out_walked, bool heads = true) {
   {
     Gate g{rs->rs, rs->plan.get(), base(config_path ? config_path : ""), {}, {}};
     for (uint32_t i = 0; i < n_skip_files; i++)  // walk.go:25-33
@@ -1170,6 +1195,24 @@ int fs_collect(const tsg_ruleset* rs, const char* root, const char* const* skip_
       if (contains(g.skip_files, trim_left_slash(path))) return false;
       std::string fp;
       if (!rel(directory, path, &fp)) fp = path;
+      // Required's path tests first (only its size test needs the file): a file they drop
+      // is never opened
+      if (!g.required(trim_left_slash(fp), INT64_MAX)) return true;
+      if (!heads) {
+        struct stat s3;
+        if ((dfd >= 0 ? fstatat(dfd, name, &s3, AT_SYMLINK_NOFOLLOW) : lstat(path.c_str(), &s3)) != 0 ||
+            !S_ISREG(s3.st_mode))
+          return false;  // (gone or replaced since the listing)
+        if (s3.st_size >= 10) {  // (secret.go:113-115)
+          auto f = std::make_unique<FsFile>();
+          f->full = path;
+          f->fp = std::move(fp);
+          f->size = f->got = (uint64_t)s3.st_size;
+          f->keep = true;
+          *keep = std::move(f);
+        }
+        return true;
+      }
       const int fd = dfd >= 0 ? openat(dfd, name, O_RDONLY | O_NOFOLLOW | O_CLOEXEC)
                               : open(path.c_str(), O_RDONLY | O_NOFOLLOW | O_CLOEXEC);
       if (fd < 0) return true;  // analyzer.go:411-413: a permission error skips the file
@@ -1178,7 +1221,7 @@ int fs_collect(const tsg_ruleset* rs, const char* root, const char* const* skip_
         close(fd);
         return false;
       }
-      if (g.required(trim_left_slash(fp), (int64_t)fs2.st_size)) {
+      if (fs2.st_size >= 10) {  // (secret.go:113-115)
         auto f = std::make_unique<FsFile>();
         f->full = path;
         f->fp = std::move(fp);
@@ -1373,17 +1416,42 @@ extern "C" int tsg_fs_scan(tsg_ctx* ctx, const char* root, const char* const* sk
   *layer = nullptr;
   *out = nullptr;
   try {
+    auto now = [] { return std::chrono::steady_clock::now(); };
+    auto ms = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
+      return std::chrono::duration<double, std::milli>(b - a).count();
+    };
+    const auto t0 = now();
     std::vector<std::unique_ptr<tsg::FsFile>> files;
     uint32_t walked = 0;
     int rc = tsg::fs_collect(tsg::ctx_ruleset(ctx), root, skip_files, n_skip_files, skip_dirs, n_skip_dirs,
-                             config_path, &files, &walked);
+                             config_path, &files, &walked, false);
     if (rc) return rc;
+    const auto t1 = now();
     auto L = std::make_unique<tsg_layer>();
     L->walked = walked;
     const std::vector<size_t> kept = tsg::fs_layout(files, L.get());
-    rc = tsg::scan_in_pieces(ctx, L.get(), [&](size_t k, uint8_t* dst) { return tsg::fs_fill(*files[kept[k]], dst); },
-                             out);
+    const auto t2 = now();
+    // every listed file read straight into its place in a piece; an unreadable or binary
+    // one is scanned along (its bytes are there already) and dropped from the results
+    std::vector<uint8_t> drop(kept.size(), 0);
+    rc = tsg::scan_in_pieces(ctx, L.get(), [&](size_t k, uint8_t* dst) -> uint64_t {
+      const tsg::FsFile& f = *files[kept[k]];
+      const int fd = open(f.full.c_str(), O_RDONLY | O_NOFOLLOW | O_CLOEXEC);
+      if (fd < 0) {  // analyzer.go:411-413: a permission error skips the file
+        drop[k] = 1;
+        return 0;
+      }
+      const uint64_t r = tsg::read_upto(fd, dst, f.size);
+      close(fd);
+      if (tsg::is_binary(dst, (int64_t)r)) drop[k] = 1;  // secret.go:78-84 (its first 300 bytes)
+      return r;
+    }, out, &drop);
     if (rc) return rc;
+    const auto t3 = now();
+    files.clear();
+    if (getenv("TSG_LAYER_PROF"))
+      fprintf(stderr, "fs_scan: %.1f ms (walk+heads %.1f, layout %.1f, pieces %.1f, free %.1f)\n", ms(t0, now()),
+              ms(t0, t1), ms(t1, t2), ms(t2, t3), ms(t3, now()));
     *layer = L.release();
     return TSG_OK;
   } catch (const std::bad_alloc&) {
