@@ -27,6 +27,7 @@ for v in "$@"; do
     clspf4_ip) build $v -DK1_CLSPF=4 -DK1_INPLACE ;;
     inplace) build $v -DK1_INPLACE ;;
     u4) build $v -DK1_UNROLL=4 ;;
+    k2twobuf) build $v -DK2_TWOBUF ;;
     nostep) build $v -DK1_EXP_NOSTEP ;;
     noload) build $v -DK1_EXP_NOLOAD ;;
     noload_nolds) build $v -DK1_EXP_NOLOAD -DK1_EXP_NO_CLS -DK1_EXP_NO_TAB ;;

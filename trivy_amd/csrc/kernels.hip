@@ -103,7 +103,7 @@ struct DevDFA {  // K2 rule group
   uint32_t nrules;            // rules in the group
   uint32_t inv_nc;            // ceil(2^32 / nc): state_of(row) = umulhi(row, inv_nc), exact below 2^16
   uint32_t start[4];          // start rows per previous-byte context
-  uint32_t o_cls, o_accs, o_masks, lds_bytes;
+  uint32_t o_cls, o_dead, o_accs, o_masks, lds_bytes;  // LDS layout (stage_dfa)
 };
 
 struct DevK1 {
@@ -1144,6 +1144,16 @@ __device__ __forceinline__ void emit_cand(const K2Args& A, uint32_t file, uint32
   }
 }
 
+#ifdef K2_NOINL  // the rare paths out of line (their registers do not add to the hot loop's)
+#define K2_NOINLINE __attribute__((noinline))
+#else
+#define K2_NOINLINE __forceinline__
+#endif
+#ifdef K2_W
+#define K2_WAVES __attribute__((amdgpu_waves_per_eu(K2_W, 8)))
+#else
+#define K2_WAVES
+#endif
 struct Lane {
   const DevDFA& d;
   const K2Args& A;
@@ -1182,7 +1192,7 @@ struct Lane {
   // run; emitting those one by one, each after a dependent global lookup of the accept
   // mask and the rules, made entries of a few dozen items the kernel's long pole
   // (profiles/r03/d2, r03/k2a: 30-80 items, ~600 candidates, 0.4-0.5 ms).
-  __device__ void replay_emit(uint32_t s0, const uint4 v, int lo, int hi, uint64_t wb) {
+  __device__ K2_NOINLINE void replay_emit(uint32_t s0, const uint4 v, int lo, int hi, uint64_t wb) {
     uint32_t n = 0, r = s0;
 #pragma unroll
     for (int k = 0; k < 16; k++) {
@@ -1234,8 +1244,9 @@ struct Lane {
   }
 
   // matches that started before b: follow them past b (noinject) until they all die
-  __device__ __forceinline__ void tail(uint32_t s, uint64_t fe, uint64_t b) {
+  __device__ K2_NOINLINE void tail(uint32_t s, uint64_t fe, uint64_t b) {
     const uint8_t* data = A.data;
+    const uint8_t* dead = s_cls + (d.o_dead - d.o_cls);  // (staged: stage_dfa)
     if (b >= fe) {
       const uint32_t m = d.eot[state_of(s)];
       if (m) emit(m, fe);
@@ -1245,19 +1256,33 @@ struct Lane {
     // 16 bytes per load (the next word in flight), liveness checked once per word: a dead
     // noinject state is absorbing and accepts nothing, so stepping on inside the word
     // changes no output.  (The batch is padded, so whole-word loads past fe are safe.)
+    // Each word is stepped from registers over its bytes in [q, fe); a word with an accepting
+    // transition is replayed by replay_emit (one atomic for all its records: tails of a
+    // relaxed unbounded rule accept at every byte of a long token).
     uint64_t q = b;
     uint64_t w = q & ~15ull;
     uint4 cur = *(const uint4*)(data + w);
-    while (q < fe && !(d.dead[state_of(s)] & 1)) {
+    while (q < fe && !(dead[state_of(s)] & 1)) {
       // past ext_cap, or in a state whose threads never die (the tail would run to the end
       // of the file): the group's rules over the whole file, on the host
-      if (q - b >= A.ext_cap || (d.dead[state_of(s)] & 2)) {
+      if (q - b >= A.ext_cap || (dead[state_of(s)] & 2)) {
         for (uint32_t k = 0; k < d.nrules; k++) emit_cand(A, file, d.rules[k], kCandWhole);
         return;
       }
       const uint4 nxt = *(const uint4*)(data + w + 16);
       const uint64_t e = min(fe, w + 16);
-      for (; q < e; q++) s = step(s, byte_of(cur, (uint32_t)(q - w)), q);
+      const int lo = (int)(q - w), hi = (int)(e - w);
+      const uint32_t s0 = s;
+      uint32_t any = 0;
+#pragma unroll
+      for (int k = 0; k < 16; k++) {
+        const uint32_t t = s_tab[s + s_cls[byte_of(cur, k)]];
+        const bool in = k >= lo && k < hi;
+        any |= in ? t : 0u;
+        s = in ? (t & 0x7FFFu) : s;
+      }
+      if (__builtin_expect(any & 0x8000u, 0)) replay_emit(s0, cur, lo, hi, w);
+      q = e;
       cur = nxt;
       w += 16;
     }
@@ -1269,7 +1294,7 @@ struct Lane {
       atomicMax(&A.diag[1], n);
       if (n > 4096) atomicAdd(&A.diag[2], 1u);
     }
-    if (q >= fe && !(d.dead[state_of(s)] & 1)) {
+    if (q >= fe && !(dead[state_of(s)] & 1)) {
       const uint32_t m = d.eot[state_of(s)];
       if (m) emit(m, fe);
     }
@@ -1349,6 +1374,8 @@ __device__ __forceinline__ void stage_dfa(const DevDFA& d, uint8_t* smem) {
   for (uint32_t i = threadIdx.x; i < (d.ns * d.nc + 1) / 2; i += blockDim.x) dst[i] = src[i];
   uint8_t* s_cls = smem + d.o_cls;
   for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) s_cls[i] = d.cls[i];
+  uint8_t* s_dead = smem + d.o_dead;
+  for (uint32_t i = threadIdx.x; i < d.ns; i += blockDim.x) s_dead[i] = d.dead[i];
   if (d.state_acc) {
     uint16_t* s_accs = (uint16_t*)(smem + d.o_accs);
     uint64_t* s_masks = (uint64_t*)(smem + d.o_masks);
@@ -1366,7 +1393,8 @@ __device__ __forceinline__ void stage_dfa(const DevDFA& d, uint8_t* smem) {
 // from the start state of its context, its end stops the chain).
 struct K2Item {
   uint32_t s, file;
-  uint64_t fs, fe, a, b, base;
+  uint32_t lo, hi;  // the chunk's bytes inside its file: [base + lo, base + hi)
+  uint64_t fs, base;
 };
 
 __device__ __forceinline__ void k2_list_pair(const DevDFA& d, const K2Args& A, const uint16_t* s_tab,
@@ -1396,12 +1424,12 @@ __device__ __forceinline__ void k2_list_pair(const DevDFA& d, const K2Args& A, c
     const uint2 item = A.items[first + (live[i] ? k : 0)];
     it[i].file = item.x;
     it[i].fs = A.off[item.x];
-    it[i].fe = A.off[item.x + 1];
+    const uint64_t fe = A.off[item.x + 1];
     it[i].base = (uint64_t)item.y * C;
-    it[i].a = max(it[i].fs, it[i].base);
-    it[i].b = min(it[i].fe, it[i].base + C);
-    if (!live[i]) it[i].b = it[i].a;  // a ghost steps nothing and emits nothing
-    it[i].s = it[i].a == it[i].fs ? d.start[0] : d.start[ctx_of(A.data[it[i].a - 1])];
+    const uint64_t a = max(it[i].fs, it[i].base);
+    it[i].lo = (uint32_t)(a - it[i].base);
+    it[i].hi = live[i] ? (uint32_t)(min(fe, it[i].base + C) - it[i].base) : it[i].lo;  // a ghost steps nothing
+    it[i].s = a == it[i].fs ? d.start[0] : d.start[ctx_of(A.data[a - 1])];
   }
   // word q of quad lane t's chunk, for each chain
   const uint8_t* src[2][4];
@@ -1419,16 +1447,15 @@ __device__ __forceinline__ void k2_list_pair(const DevDFA& d, const K2Args& A, c
       if (live[i]) {
         L.file = it[i].file;
         L.fs = it[i].fs;
-        L.piece(it[i].fe, it[i].a, it[i].b);
+        L.piece(A.off[it[i].file + 1], it[i].base + it[i].lo, it[i].base + it[i].hi);
       }
     return;
   }
-  // bytes [wb, wb + 16) of chain c, stepped where they lie in [a, b)
-  auto word = [&](K2Item& c, uint64_t wb, const uint4 v) __attribute__((always_inline)) {
-    // bit k of `live` = byte wb + k lies in [a, b) (the chunk's part inside its file)
-    const int64_t lo64 = (int64_t)c.a - (int64_t)wb, hi64 = (int64_t)c.b - (int64_t)wb;
-    const int32_t lo = (int32_t)max<int64_t>(0, min<int64_t>(16, lo64));
-    const int32_t hi = (int32_t)max<int64_t>(0, min<int64_t>(16, hi64));
+  // bytes [base + o, base + o + 16) of chain c, stepped where they lie in [lo, hi)
+  auto word = [&](K2Item& c, uint32_t o, const uint4 v) __attribute__((always_inline)) {
+    const int32_t lo = min(16, max(0, (int32_t)c.lo - (int32_t)o));
+    const int32_t hi = min(16, max(0, (int32_t)c.hi - (int32_t)o));
+    const uint64_t wb = c.base + o;
     const uint32_t mask = ((1u << hi) - 1u) & ~((1u << lo) - 1u);
     uint32_t s = c.s, any = 0;
     const uint32_t s0 = s;
@@ -1460,10 +1487,18 @@ __device__ __forceinline__ void k2_list_pair(const DevDFA& d, const K2Args& A, c
   quad_transpose4(X, b0, b1);                                                   \
   quad_transpose4(Y, b0, b1);                                                   \
   _Pragma("unroll") for (int w = 0; w < 4; w++) {                              \
-    word(it[0], it[0].base + (J) + 16u * w, X[w]);                              \
-    word(it[1], it[1].base + (J) + 16u * w, Y[w]);                              \
+    word(it[0], (uint32_t)(J) + 16u * w, X[w]);                                 \
+    word(it[1], (uint32_t)(J) + 16u * w, Y[w]);                                 \
   }
   K2_LOAD(x0, y0, 0)
+#ifndef K2_TWOBUF  // one 64-B block per chain, stepped in place, then reloaded (160 VGPRs: 3 waves/SIMD)
+  for (uint64_t j = 0; j < C; j += 64) {
+    K2_BLOCK(x0, y0, j)
+    if (j + 64 < C) {
+      K2_LOAD(x0, y0, j + 64)
+    }
+  }
+#else
   for (uint64_t j = 0; j < C; j += 128) {  // C is a multiple of 128 here
     K2_LOAD(x1, y1, j + 64)
     K2_BLOCK(x0, y0, j)
@@ -1472,6 +1507,7 @@ __device__ __forceinline__ void k2_list_pair(const DevDFA& d, const K2Args& A, c
     }
     K2_BLOCK(x1, y1, j + 64)
   }
+#endif
 #undef K2_LOAD
 #undef K2_BLOCK
   // matches that started in the chunk and run past it (inside the file): follow them
@@ -1480,7 +1516,7 @@ __device__ __forceinline__ void k2_list_pair(const DevDFA& d, const K2Args& A, c
     if (live[i]) {
       L.file = it[i].file;
       L.fs = it[i].fs;
-      L.tail(it[i].s, it[i].fe, it[i].b);
+      L.tail(it[i].s, A.off[it[i].file + 1], it[i].base + it[i].hi);
     }
 }
 
@@ -1576,7 +1612,7 @@ __device__ __forceinline__ void k2_run(const DevDFA* __restrict__ dfas, const K2
   }
 }
 
-__global__ void __launch_bounds__(kBlock) k2_kernel(const DevDFA* __restrict__ dfas, K2Args A) {
+__global__ void __launch_bounds__(kBlock) K2_WAVES k2_kernel(const DevDFA* __restrict__ dfas, K2Args A) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   k2_run<false>(dfas, A, A.entries, *A.nentries, A.claim, smem);
 }
@@ -1677,6 +1713,8 @@ static int make_device_dfa(const DFA& dd, const std::vector<uint32_t>& rules, De
   uint32_t o = align16((uint32_t)(tab.size() * 2));
   v.o_cls = o;
   o += 256;
+  v.o_dead = o;  // the tails' per-word liveness test reads it
+  o += align16((uint32_t)d.nstates);
   v.o_accs = o;
   v.o_masks = o;
   v.state_acc = 0;

@@ -364,7 +364,13 @@ std::unique_ptr<Plan> build_plan(const Ruleset& rs, const PlanOptions& opt, std:
     flush();
   }
 
-  if (tprof) fprintf(stderr, "plan: grouping %.1f ms (%zu groups)\n", tms(tp), p->groups.size());
+  if (tprof) {
+    fprintf(stderr, "plan: grouping %.1f ms (%zu groups)\n", tms(tp), p->groups.size());
+    for (size_t g = 0; g < p->groups.size(); g++)
+      fprintf(stderr, "plan: group %zu: %zu rules, %d states x %d classes (%zu table bytes), events %#x\n", g,
+              p->groups[g].rules.size(), p->groups[g].dfa->nstates, p->groups[g].dfa->nclasses,
+              (size_t)p->groups[g].dfa->nstates * p->groups[g].dfa->nclasses * 2, p->groups[g].events);
+  }
   tp = tnow();
   // ---- K1 automaton: keywords + anchor literals; literal groups share event bits
   std::vector<char> litg(p->groups.size(), 0);
