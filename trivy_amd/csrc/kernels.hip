@@ -1107,6 +1107,7 @@ struct K2Args {
   uint8_t* ovf;
   uint32_t* diag;  // null, or [4]: tail bytes, longest tail, tails over 4 KiB, word replays
   uint32_t* claim;  // [2] next list / dense entry (zeroed per batch)
+  uint32_t word_recs;  // accepting words as one kCandWord record each (groups < 2^14)
   // null, or per entry kTraceW words {start, end (wall clock, 100 MHz), group << 32 | items,
   // XCC_ID << 32 | HW_ID, then (K2_TRACE_CTR builds only) replayed words, candidates,
   // tail bytes, longest tail} written by the block that ran it (TSG_K2_TRACE)
@@ -1177,6 +1178,16 @@ struct Lane {
 
   // the record of an accepting transition (kCandTrans: the host expands its accept mask)
   __device__ __forceinline__ uint32_t trans(uint32_t ix) const { return kCandTrans | (group << 16) | ix; }
+  // An accepting 16-B word as ONE record (kCandWord): the row before byte p, p's offset in
+  // the file; the host replays the word from there to the word's end (or the file's) and
+  // expands every accepting transition on the way (plan.cpp resolve_batch).  Without it
+  // (more groups than 14 bits), replay_emit writes the transitions themselves.
+  __device__ __forceinline__ void accept_word(uint32_t s0, const uint4 v, int lo, int hi, uint64_t wb) {
+    if (A.word_recs)
+      emit_cand(A, file, kCandTrans | kCandWord | (group << 16) | s0, wb + (uint64_t)lo - fs);
+    else
+      replay_emit(s0, v, lo, hi, wb);
+  }
   // one candidate record at idx (see emit_cand)
   __device__ __forceinline__ void put(uint32_t idx, uint32_t rule, uint64_t end) const {
     if (idx < A.cand_cap && end < kCandWhole) {
@@ -1257,7 +1268,7 @@ struct Lane {
     // noinject state is absorbing and accepts nothing, so stepping on inside the word
     // changes no output.  (The batch is padded, so whole-word loads past fe are safe.)
     // Each word is stepped from registers over its bytes in [q, fe); a word with an accepting
-    // transition is replayed by replay_emit (one atomic for all its records: tails of a
+    // transition is recorded by accept_word (one record or atomic for the word: tails of a
     // relaxed unbounded rule accept at every byte of a long token).
     uint64_t q = b;
     uint64_t w = q & ~15ull;
@@ -1281,7 +1292,7 @@ struct Lane {
         any |= in ? t : 0u;
         s = in ? (t & 0x7FFFu) : s;
       }
-      if (__builtin_expect(any & 0x8000u, 0)) replay_emit(s0, cur, lo, hi, w);
+      if (__builtin_expect(any & 0x8000u, 0)) accept_word(s0, cur, lo, hi, w);
       q = e;
       cur = nxt;
       w += 16;
@@ -1471,7 +1482,7 @@ __device__ __forceinline__ void k2_list_pair(const DevDFA& d, const K2Args& A, c
       K2_CTR(0, atomicAdd, 1);
       L.file = c.file;
       L.fs = c.fs;
-      L.replay_emit(s0, v, lo, hi, wb);
+      L.accept_word(s0, v, lo, hi, wb);
     }
     c.s = s;
   };
@@ -2028,14 +2039,17 @@ static const void* k1_fn_ns(uint32_t kw_words, uint32_t lds_class, uint32_t rep)
 }
 
 // independent K1 chains per lane: 2 (quad-transposed loads keep two 64-byte blocks per
-// chain in registers), or 4 with TSG_K1_NS=4 (measurements)
+// chain in registers), or 3 / 4 with TSG_K1_NS=3 / 4 (measurements)
 static uint32_t k1_streams() {
-  static const uint32_t ns = (getenv("TSG_K1_NS") && atoi(getenv("TSG_K1_NS")) == 4) ? 4u : 2u;
+  static const uint32_t ns = getenv("TSG_K1_NS") && (atoi(getenv("TSG_K1_NS")) == 3 || atoi(getenv("TSG_K1_NS")) == 4)
+                                 ? (uint32_t)atoi(getenv("TSG_K1_NS"))
+                                 : 2u;
   return ns;
 }
 
 static const void* k1_fn(uint32_t kw_words, uint32_t lds_class, uint32_t rep, uint32_t ns) {
-  return ns == 2 ? k1_fn_ns<2>(kw_words, lds_class, rep) : k1_fn_ns<4>(kw_words, lds_class, rep);
+  return ns == 2 ? k1_fn_ns<2>(kw_words, lds_class, rep)
+                 : ns == 3 ? k1_fn_ns<3>(kw_words, lds_class, rep) : k1_fn_ns<4>(kw_words, lds_class, rep);
 }
 
 static int launch_k1(DeviceRules* r, const K1Args& A, hipStream_t st) {
@@ -2472,6 +2486,8 @@ int enqueue_scan(DeviceRules* r, LaneState* l, const ScanInput& in, HostOut* out
     static const bool diag = getenv("TSG_K2_DIAG") != nullptr;
     A.diag = diag ? l->counts + 8 : nullptr;
     A.claim = l->counts + 12;
+    static const bool no_words = getenv("TSG_K2_NO_WORDREC") != nullptr;  // (measurements)
+    A.word_recs = G <= 0x3FFF && !no_words;
     static const bool trace = getenv("TSG_K2_TRACE") != nullptr;
     if (trace && (rc = ensure(&l->etrace, &l->etrace_cap, (size_t)entries_cap * kTraceW))) return rc;
     if (trace) HIP_TRY(hipMemsetAsync(l->etrace, 0, sizeof(unsigned long long) * entries_cap * kTraceW, st));

@@ -796,6 +796,7 @@ void resolve_batch(const Ruleset& rs, const Plan& plan, const BatchView& b,
   std::vector<Candidate> expanded;
   const Candidate* kc = ko.cand;
   size_t nkc = ko.ncand;
+  const bool words = plan.groups.size() <= 0x3FFF;  // kCandWord records (kernels.hip accept_word)
   {
     size_t ntrans = 0;
     for (size_t i = 0; i < nkc; i++) ntrans += (kc[i].rule & kCandTrans) && kc[i].end != kCandWhole;
@@ -807,11 +808,28 @@ void resolve_batch(const Ruleset& rs, const Plan& plan, const BatchView& b,
           expanded.push_back(c);
           continue;
         }
-        const uint32_t g = (c.rule >> 16) & 0x7FFFu, ix = c.rule & 0xFFFFu;
+        const bool word = words && (c.rule & kCandWord);
+        const uint32_t g = (c.rule >> 16) & (words ? 0x3FFFu : 0x7FFFu), ix = c.rule & 0xFFFFu;
         if (g >= plan.groups.size()) continue;
         const GroupPlan& gp = plan.groups[g];
         const DFA& d = *gp.dfa;
         const uint32_t ncd = (uint32_t)std::max(2, d.nclasses);  // the device's row width
+        if (word) {  // kCandWord: replay the word from row ix at byte `end` to the word's end
+          size_t st = ix / ncd;
+          if (st >= (size_t)d.nstates || c.file >= F) continue;
+          const uint64_t f0 = b.offsets[c.file], flen = b.offsets[c.file + 1] - f0;
+          const uint64_t pend = std::min<uint64_t>(flen, (((f0 + c.end) | 15) + 1) - f0);
+          for (uint64_t p = c.end; p < pend; p++) {
+            const size_t e = st * d.nclasses + d.cls[b.data[f0 + p]];
+            if (d.acc[e]) {
+              const auto& m = d.masks[d.acc[e]];
+              for (size_t k = 0; k < gp.rules.size(); k++)
+                if ((m[k / 64] >> (k % 64)) & 1) expanded.push_back({c.file, gp.rules[k], (uint32_t)p});
+            }
+            st = d.next[e];
+          }
+          continue;
+        }
         const size_t st = ix / ncd, cl = std::min<size_t>(ix % ncd, (size_t)d.nclasses - 1);
         if (st >= (size_t)d.nstates) continue;
         const auto& m = d.masks[d.acc[st * d.nclasses + cl]];

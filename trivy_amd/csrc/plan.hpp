@@ -116,6 +116,9 @@ constexpr uint32_t kCandWhole = 0xFFFFFFFFu;
 // `end` accepts, and its accept mask names the rules (expanded on the host, so the kernel
 // looks up no mask per accepting byte)
 constexpr uint32_t kCandTrans = 0x80000000u;
+// with kCandTrans: a whole accepting 16-B word {file, kCandTrans | kCandWord | group << 16 |
+// row before the byte at end, end}; the host replays it (groups then have 14 bits)
+constexpr uint32_t kCandWord = 0x40000000u;
 struct Candidate {
   uint32_t file;
   uint32_t rule;
