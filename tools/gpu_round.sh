@@ -13,6 +13,10 @@ tail -1 $out/gpu_tests.log
 echo "== smoke" && timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke()" > $out/smoke.log 2>&1 || { tail $out/smoke.log; exit 2; }
 cat $out/smoke.log
 tools/gpu_bench_prof.sh $tag || exit 3
+# the headline line again, now with the FETCH_SIZE record of this device code (roofline.traffic)
+mkdir -p profiles/pmc && cp $out/pmc_builtin.json profiles/pmc/builtin.json && \
+  echo "== bench (with traffic)" && timeout -k 10 400 python -u bench.py > $out/bench_final.json 2> $out/bench_final.err || { tail $out/bench_final.err; exit 10; }
+tail -c 1500 $out/bench_final.json
 echo "== configs[3]" && timeout -k 10 400 python -u bench.py --rules user1000 --steps 2 --warmup 1 --cpu-mib 16 > $out/bench_user1000.json 2> $out/bench_user1000.err || { tail $out/bench_user1000.err; exit 4; }
 echo "== configs[4]" && timeout -k 10 400 python -u bench.py --rules allow-exclude --steps 2 --warmup 1 --cpu-mib 256 > $out/bench_allow.json 2> $out/bench_allow.err || { tail $out/bench_allow.err; exit 5; }
 echo "== configs[0]" && timeout -k 10 400 python -u tools/fs_bench.py > $out/fs_bench.json 2> $out/fs_bench.err || { tail $out/fs_bench.err; exit 6; }
