@@ -423,7 +423,11 @@ int tsg_fs_pack_slot(tsg_ctx* ctx, const char* root, const char* const* skip_fil
  * size; each piece is written straight into a pinned slot and submitted while the next one
  * is written, so ingest, upload, kernels and host resolution overlap.  *out holds one record
  * per kept file in the order of *layer's paths (tsg_result format); *layer carries the paths,
- * offsets, opq, wh and walked count (its data view is NULL: the bytes lived in the slots). */
+ * offsets, opq, wh and walked count (its data view is NULL: the bytes lived in the slots).
+ * tsg_fs_scan opens no file during its walk: every file that passes Required is listed with
+ * its lstat size and read straight into its place in a piece; a file that is binary
+ * (IsBinary on the bytes read) or cannot be opened is scanned along and then left out of
+ * *out and *layer, which therefore equal tsg_fs_pack's batch and its scan. */
 int tsg_layer_scan(tsg_ctx* ctx, const uint8_t* tar, uint64_t tar_len,
                    const char* const* skip_files, uint32_t n_skip_files,
                    const char* const* skip_dirs, uint32_t n_skip_dirs, const char* config_path,

@@ -28,6 +28,8 @@ for v in "$@"; do
     inplace) build $v -DK1_INPLACE ;;
     u4) build $v -DK1_UNROLL=4 ;;
     k2twobuf) build $v -DK2_TWOBUF ;;
+    x1) build $v -DK1X_WORDS=1 ;;
+    x8) build $v -DK1X_WORDS=8 ;;
     nostep) build $v -DK1_EXP_NOSTEP ;;
     noload) build $v -DK1_EXP_NOLOAD ;;
     noload_nolds) build $v -DK1_EXP_NOLOAD -DK1_EXP_NO_CLS -DK1_EXP_NO_TAB ;;

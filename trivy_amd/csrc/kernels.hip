@@ -698,6 +698,10 @@ __device__ void k1x_verify_at(const DevK1X& x, const K1XArgs& A, uint64_t p, uin
 }
 
 constexpr int kK1XBlock = 512;
+#ifndef K1X_WORDS
+#define K1X_WORDS 4
+#endif
+constexpr int kXWords = K1X_WORDS;  // words per lane per round (k1x_kernel)
 
 __device__ __forceinline__ uint32_t k1x_hits(const uint32_t* s_bm, const uint32_t (&d)[5]) {
   uint32_t hits = 0;
@@ -722,33 +726,52 @@ __global__ void __launch_bounds__(kK1XBlock) k1x_kernel(DevK1X x, K1XArgs A) {
   uint2* list = A.list + (size_t)blockIdx.x * slice;
   const uint64_t nwords = (A.total + 15) / 16;
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-  uint64_t wi = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  // one word ahead in registers (the batch is padded with zero bytes past its end)
-  uint4 v = make_uint4(0, 0, 0, 0);
-  uint32_t nx = 0;
-  if (wi < nwords) {
-    v = *(const uint4*)(A.data + wi * 16);
-    nx = *(const uint32_t*)(A.data + wi * 16 + 16);
-  }
-  for (; wi < nwords; wi += stride) {
-    const uint32_t d[5] = {x_lower4(v.x), x_lower4(v.y), x_lower4(v.z), x_lower4(v.w), x_lower4(nx)};
-    if (wi + stride < nwords) {
-      v = *(const uint4*)(A.data + (wi + stride) * 16);
-      nx = *(const uint32_t*)(A.data + (wi + stride) * 16 + 16);
+  // kXWords words per lane per round (each load coalesced across the wave), the next
+  // round's words in flight while this round is hashed: at 2 waves per SIMD (the 128 KiB
+  // bitmap) one word ahead left every round waiting for HBM
+  constexpr int U = kXWords;
+  uint4 v[U];
+  uint32_t nx[U];
+  auto load = [&](uint64_t w0) __attribute__((always_inline)) {
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const uint64_t w = w0 + (uint64_t)u * stride;
+      // (the batch is padded with zero bytes past its end)
+      v[u] = w < nwords ? *(const uint4*)(A.data + w * 16) : make_uint4(0, 0, 0, 0);
+      nx[u] = w < nwords ? *(const uint32_t*)(A.data + w * 16 + 16) : 0u;
     }
-    uint32_t hits = k1x_hits(s_bm, d);
-    // positions past the batch end never count (their window holds pad bytes)
-    const uint64_t p0 = wi * 16;
-    if (p0 + 16 > A.total) hits &= (1u << (uint32_t)(A.total - p0)) - 1u;
-    if (__builtin_expect(hits != 0, 0)) {
-      const uint32_t slot = atomicAdd(s_n, 1u);
-      if (slot < slice) {
-        list[slot] = make_uint2((uint32_t)wi, hits);
-      } else {
-        for (uint32_t t = hits; t; t &= t - 1) {
-          const int k = __builtin_ctz(t);
-          const uint32_t w = (k & 3) ? __builtin_amdgcn_alignbyte(d[k / 4 + 1], d[k / 4], k & 3) : d[k / 4];
-          k1x_verify_at(x, A, p0 + k, w);
+  };
+  uint64_t wi = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  load(wi);
+  for (; wi < nwords; wi += (uint64_t)U * stride) {
+    uint4 cv[U];
+    uint32_t cn[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      cv[u] = v[u];
+      cn[u] = nx[u];
+    }
+    load(wi + (uint64_t)U * stride);
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const uint64_t w = wi + (uint64_t)u * stride;
+      if (w >= nwords) break;
+      const uint32_t d[5] = {x_lower4(cv[u].x), x_lower4(cv[u].y), x_lower4(cv[u].z), x_lower4(cv[u].w),
+                             x_lower4(cn[u])};
+      uint32_t hits = k1x_hits(s_bm, d);
+      // positions past the batch end never count (their window holds pad bytes)
+      const uint64_t p0 = w * 16;
+      if (p0 + 16 > A.total) hits &= (1u << (uint32_t)(A.total - p0)) - 1u;
+      if (__builtin_expect(hits != 0, 0)) {
+        const uint32_t slot = atomicAdd(s_n, 1u);
+        if (slot < slice) {
+          list[slot] = make_uint2((uint32_t)w, hits);
+        } else {
+          for (uint32_t t = hits; t; t &= t - 1) {
+            const int k = __builtin_ctz(t);
+            const uint32_t wd = (k & 3) ? __builtin_amdgcn_alignbyte(d[k / 4 + 1], d[k / 4], k & 3) : d[k / 4];
+            k1x_verify_at(x, A, p0 + k, wd);
+          }
         }
       }
     }
