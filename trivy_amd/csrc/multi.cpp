@@ -135,6 +135,11 @@ int tsg_multi_create(const int* devices, uint32_t n, const tsg_ruleset* rs, cons
       m->ctx.push_back(c);
     }
     m->piece_bytes = (uint64_t)(opt && opt->slot_mib ? opt->slot_mib : 256) << 20;
+    // one context's resolution fans out over 16 threads; N devices in one process get up to
+    // 16 per device (as many as the machine has), so their batches resolve side by side
+    const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+    const int per = opt && opt->host_threads > 0 ? opt->host_threads : 16;
+    pool_reserve((int)std::min<unsigned>(hw, (unsigned)per * n) - 1);
     *out = m.release();
     return TSG_OK;
   } catch (const std::bad_alloc&) {

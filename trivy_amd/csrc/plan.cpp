@@ -623,6 +623,8 @@ class Pool {
     return *p;
   }
   // runs j on the caller and up to `helpers` pool threads; returns when all are done
+  // at least n worker threads (more concurrent jobs can then run side by side)
+  void reserve(int n) { grow(std::min(n, 256)); }
   void run(PJob& j, int helpers) {
     grow(helpers);
     {
@@ -691,6 +693,8 @@ static void parallel_for(size_t n, int nthreads, F f, size_t grain = 64) {
   j.grain = grain;
   Pool::get().run(j, std::min(nthreads, 256) - 1);
 }
+
+void pool_reserve(int threads) { Pool::get().reserve(threads); }
 
 void pool_for(size_t n, int nthreads, const std::function<void(size_t)>& f, size_t grain) {
   parallel_for(n, nthreads, f, grain);

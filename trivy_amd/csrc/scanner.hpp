@@ -116,6 +116,8 @@ void result_record_spans(const std::string& b, std::vector<size_t>* rec);
 
 // f(i) for i in [0, n) on the process-wide worker pool (plan.cpp), `grain` indices a claim
 void pool_for(size_t n, int nthreads, const std::function<void(size_t)>& f, size_t grain);
+// the process-wide resolver pool holds at least this many worker threads
+void pool_reserve(int threads);
 // Global.AllowPath (scanner.go:55-57): the plan's path DFA for ASCII paths, else the exact VM
 struct Plan;
 bool path_allowed(const Ruleset& rs, const Plan* plan, const char* p, size_t n);
