@@ -74,6 +74,9 @@ constexpr int kK1Seg = 8;         // K1: consecutive chunks per chain
 constexpr int kK1Lds[3] = {52, 80, 156};
 constexpr int kK1BlocksPerCU[3] = {3, 2, 1};
 constexpr __host__ __device__ int k1_threads(int ldsk) { return ldsk == 156 ? 1024 : 512; }
+// class 1 without the replicated class table (TSG_K1_NOREP=2, measurements): two blocks of
+// 10 waves per CU (20 waves; 100 VGPRs allow 5 per SIMD)
+constexpr int kK1Threads1NoRep = 640;
 // K1 LDS image: the byte -> class table, then the transition table.  The class table is
 // replicated per lane of a 32-lane half (K1_REP layout, [byte][lane & 31] words: every lane
 // reads its own bank, so the class read never conflicts) when the automaton leaves room for
@@ -592,8 +595,8 @@ struct K1Lane {
 // K1 LDS image (static, so every table address is a constant): the class words at 0 (REP:
 // byte b's word for lane l at (b * 32 + l % 32) * 4; else at b * 4), the transitions after
 // them.  Accept masks stay in global memory (rare path).
-template <int KWW, int LDSK, int NS, bool REP>
-__global__ void __launch_bounds__(k1_threads(LDSK)) __attribute__((amdgpu_waves_per_eu(K1_WAVES, 8))) k1_kernel(DevK1 d, K1Args A) {
+template <int KWW, int LDSK, int NS, bool REP, int TPB>
+__global__ void __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(K1_WAVES, 8))) k1_kernel(DevK1 d, K1Args A) {
   __shared__ __attribute__((aligned(16))) uint8_t smem[LDSK * 1024];
   constexpr uint32_t kTabOff = REP ? kK1RepBytes : 1024;
   static_assert(!REP || LDSK * 1024 > (int)kK1RepBytes, "K1_REP needs room for the automaton");
@@ -1926,8 +1929,12 @@ static int make_device_k1(const Plan& p, DevK1* out, std::vector<void*>* allocs,
   const int lc = k1_lds_class(host->tab.size() * 2);
   v.lds_class = (uint32_t)(lc >> 1);
   v.rep = (uint32_t)(lc & 1);
-  if (getenv("TSG_K1_NOREP") && v.rep && host->tab.size() * 2 + 1024 <= (size_t)kK1Lds[v.lds_class] * 1024)
+  if (getenv("TSG_K1_NOREP") && atoi(getenv("TSG_K1_NOREP")) == 2 && host->tab.size() * 2 + 1024 <= (size_t)kK1Lds[1] * 1024) {
+    v.lds_class = 1;  // (measurements: no replicated class table, two blocks per CU)
+    v.rep = 0;
+  } else if (getenv("TSG_K1_NOREP") && v.rep && host->tab.size() * 2 + 1024 <= (size_t)kK1Lds[v.lds_class] * 1024) {
     v.rep = 0;  // (measurements: the 256-word class table in the same LDS class)
+  }
   if (v.lds_class > 2) return fail(TSG_ERR_INTERNAL, "keyword automaton exceeds LDS");
   return TSG_OK;
 }
@@ -2043,12 +2050,12 @@ static int ensure(T** p, size_t* cap, size_t n) {
   return TSG_OK;
 }
 
-template <int LDSK, int NS, bool REP>
+template <int LDSK, int NS, bool REP, int TPB = k1_threads(LDSK)>
 static const void* k1_fn_w(uint32_t kw_words) {
-  if (kw_words <= 1) return (const void*)k1_kernel<1, LDSK, NS, REP>;
-  if (kw_words <= 2) return (const void*)k1_kernel<2, LDSK, NS, REP>;
-  if (kw_words <= 4) return (const void*)k1_kernel<4, LDSK, NS, REP>;
-  return (const void*)k1_kernel<8, LDSK, NS, REP>;
+  if (kw_words <= 1) return (const void*)k1_kernel<1, LDSK, NS, REP, TPB>;
+  if (kw_words <= 2) return (const void*)k1_kernel<2, LDSK, NS, REP, TPB>;
+  if (kw_words <= 4) return (const void*)k1_kernel<4, LDSK, NS, REP, TPB>;
+  return (const void*)k1_kernel<8, LDSK, NS, REP, TPB>;
 }
 
 // (the 256-word class table only in the largest class: smaller automata always fit REP)
@@ -2056,13 +2063,20 @@ template <int NS>
 static const void* k1_fn_ns(uint32_t kw_words, uint32_t lds_class, uint32_t rep) {
   switch (lds_class) {
     case 0: return k1_fn_w<kK1Lds[0], NS, true>(kw_words);
-    case 1: return k1_fn_w<kK1Lds[1], NS, true>(kw_words);
+    case 1: return rep ? k1_fn_w<kK1Lds[1], NS, true>(kw_words) : k1_fn_w<kK1Lds[1], NS, false, kK1Threads1NoRep>(kw_words);
     default: return rep ? k1_fn_w<kK1Lds[2], NS, true>(kw_words) : k1_fn_w<kK1Lds[2], NS, false>(kw_words);
   }
 }
 
 // independent K1 chains per lane: 2 (quad-transposed loads keep two 64-byte blocks per
 // chain in registers), or 3 / 4 with TSG_K1_NS=3 / 4 (measurements)
+// consecutive chunks per chain (TSG_K1_SEG overrides, 1..kK1Seg: measurements)
+static uint32_t k1_seg() {
+  static const uint32_t seg = getenv("TSG_K1_SEG") ? std::min<uint32_t>(kK1Seg, std::max(1, atoi(getenv("TSG_K1_SEG"))))
+                                                  : (uint32_t)kK1Seg;
+  return seg;
+}
+
 static uint32_t k1_streams() {
   static const uint32_t ns = getenv("TSG_K1_NS") && (atoi(getenv("TSG_K1_NS")) == 3 || atoi(getenv("TSG_K1_NS")) == 4)
                                  ? (uint32_t)atoi(getenv("TSG_K1_NS"))
@@ -2080,7 +2094,7 @@ static int launch_k1(DeviceRules* r, const K1Args& A, hipStream_t st) {
   // automaton once); TSG_K1_GRID overrides the blocks per CU (measurements)
   static const int gmul = getenv("TSG_K1_GRID") ? atoi(getenv("TSG_K1_GRID")) : 0;
   const uint32_t lc = std::min<uint32_t>(r->k1.lds_class, 2);
-  const int threads = k1_threads(kK1Lds[lc]);
+  const int threads = (lc == 1 && !r->k1.rep) ? kK1Threads1NoRep : k1_threads(kK1Lds[lc]);
   const uint64_t cap = (uint64_t)r->grid / 8 * (gmul > 0 ? gmul : kK1BlocksPerCU[lc]);
   const int grid = (int)std::min<uint64_t>((A.nitems + threads - 1) / threads, cap);
   DevK1 d = r->k1;
@@ -2106,7 +2120,7 @@ static int adapt_k1(DeviceRules* r, LaneState* l, uint64_t total, uint32_t nfile
   const uint64_t nsamp = (k1_items + step - 1) / step;
   HIP_TRY(hipMemsetAsync(r->d_hits, 0, sizeof(uint32_t) * ns, l->st));
   K1Args A{l->data_alloc + kPad, l->off, l->chunk_file, total, nchunks, nsamp, step, r->chunk,
-           nfiles, l->kw, l->ev_bits, r->d_hits, k1_streams(), (uint32_t)kK1Seg};
+           nfiles, l->kw, l->ev_bits, r->d_hits, k1_streams(), k1_seg()};
   int rc;
   if ((rc = launch_k1(r, A, l->st))) return rc;
   std::vector<uint32_t> hits(ns);
@@ -2417,13 +2431,13 @@ int enqueue_scan(DeviceRules* r, LaneState* l, const ScanInput& in, HostOut* out
 
   // ---- K1
   const uint32_t k1s = k1_streams();
-  const uint64_t k1_items = (nchunks + (uint64_t)k1s * kK1Seg - 1) / ((uint64_t)k1s * kK1Seg);
+  const uint64_t k1_items = (nchunks + (uint64_t)k1s * k1_seg() - 1) / ((uint64_t)k1s * k1_seg());
   const uint64_t adapt_bytes = r->adapt_mib == 0xFFFFFFFFu ? ~0ull : (uint64_t)(r->adapt_mib ? r->adapt_mib : 16) << 20;
   if (!r->adapted && k1_items >= 64 && total >= adapt_bytes)
     if ((rc = adapt_k1(r, l, total, F, nchunks, k1_items))) return rc;
   if (k1_items) {
     K1Args A{data, l->off, l->chunk_file, total, nchunks, k1_items, 1, C, F, l->kw, l->ev_bits, nullptr, k1s,
-             (uint32_t)kK1Seg};
+             k1_seg()};
     if ((rc = launch_k1(r, A, st))) return rc;
   }
   if (r->has_k1x && total) {  // the hashed literals of a large rule set, after K1's stores
