@@ -115,3 +115,24 @@ def test_fold_runes_unbounded_rules_emulated_vs_exact(builtin, chunk):
     want = builtin.ScanBatch(batch, nthreads=8)
     assert builtin.ScanBatch(batch, emulate_chunk=chunk) == want
     assert sum(len(w["Findings"] or []) for w in want) > 50
+
+
+@pytest.mark.parametrize("chunk", [64, 256])
+def test_word_records_emulated_vs_exact(builtin, chunk, monkeypatch):
+    """K2's word records (kernels.hip Lane::accept_word: one record per accepting 16-B word,
+    in the chunk and in the tail) as the emulation writes them (TSG_EMU_WORDREC): the host's
+    replay and expansion of each word (plan.cpp resolve_batch) gives the exact results, on
+    the seeded corpus, on fold-rune files and on accept-dense long tokens."""
+    monkeypatch.setenv("TSG_EMU_WORDREC", "1")
+    batch, _ = corpus.make_corpus(3 << 20, seed=70 + chunk, plants_per_mib=60)
+    assert builtin.ScanBatch(batch, emulate_chunk=chunk) == builtin.ScanBatch(batch, nthreads=8)
+    fb = fold_corpus(5)
+    assert builtin.ScanBatch(fb, emulate_chunk=chunk) == builtin.ScanBatch(fb, nthreads=8)
+    rng = np.random.default_rng(chunk)
+    tok = "".join(rng.choice(list("abcdefghijklmnopqrstuvwxyz0123456789"), 3000))
+    files = [("a/dense%d.env" % i, ("x" * (i * 7) + "api_key = '%s'\nSECRET_KEY=%s\ngithub_token: ghp_%s\n"
+                                    % (tok, tok[:40 + i], tok[:36])).encode()) for i in range(24)]
+    dense = S.Batch.from_args([S.ScanArgs(FilePath=p, Content=c) for p, c in files])
+    want = builtin.ScanBatch(dense, nthreads=8)
+    assert builtin.ScanBatch(dense, emulate_chunk=chunk) == want
+    assert sum(len(w["Findings"] or []) for w in want) > 0

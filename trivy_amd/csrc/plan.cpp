@@ -1314,9 +1314,65 @@ void k1x_reference(const Plan& plan, const BatchView& bv, uint32_t chunk, std::v
   }
 }
 
+// The list kernel's output form for one item (kernels.hip k2_list_pair / Lane::tail with
+// word records): an accepting 16-B word (batch-aligned; its part inside [a, b) or the tail)
+// becomes one kCandWord record {file, group, row before its first byte, that byte's offset};
+// a tail stops at a word boundary past ext_cap or in an immortal state (kCandWhole for the
+// group's rules); end-of-text accepts are per-rule candidates.  TSG_EMU_WORDREC selects it
+// (tests: it drives resolve_batch's word expansion without a device).
+static void emulate_words(const DFA& d, uint32_t gi, const std::vector<uint32_t>& rules, const uint8_t* data,
+                          uint32_t f, uint64_t fs, uint64_t fe, uint64_t a, uint64_t b, uint32_t ext_cap,
+                          std::vector<Candidate>* out) {
+  const uint32_t nc = (uint32_t)d.nclasses, ncd = std::max<uint32_t>(2, nc);
+  auto word_rec = [&](uint32_t s0, uint64_t p0) {
+    out->push_back({f, kCandTrans | kCandWord | (gi << 16) | (s0 * ncd), (uint32_t)(p0 - fs)});
+  };
+  auto eot = [&](uint32_t s) {
+    if (!d.eot_acc[s]) return;
+    const auto& m = d.masks[d.eot_acc[s]];
+    for (size_t k = 0; k < rules.size(); k++)
+      if ((m[k / 64] >> (k % 64)) & 1) out->push_back({f, rules[k], (uint32_t)(fe - fs)});
+  };
+  // bytes [p, e) of one word from state s: the state after them, accept seen
+  auto step = [&](uint32_t& s, uint64_t p, uint64_t e) {
+    bool acc = false;
+    for (; p < e; p++) {
+      const size_t x = (size_t)s * nc + d.cls[data[p]];
+      acc |= d.acc[x] != 0;
+      s = d.next[x];
+    }
+    return acc;
+  };
+  uint32_t s = (a == fs) ? d.start[kCtxBOT] : d.start[DFA::ctx_of(data[a - 1], d)];
+  for (uint64_t p = a; p < b;) {
+    const uint64_t e = std::min<uint64_t>(b, (p | 15) + 1);
+    const uint32_t s0 = s;
+    if (step(s, p, e)) word_rec(s0, p);
+    p = e;
+  }
+  if (b >= fe) {
+    eot(s);
+    return;
+  }
+  s = d.to_noinject[s];
+  uint64_t q = b;
+  while (q < fe && !d.dead[s]) {
+    if (q - b >= ext_cap || (s < d.immortal.size() && d.immortal[s])) {
+      for (uint32_t r : rules) out->push_back({f, r, kCandWhole});
+      return;
+    }
+    const uint64_t e = std::min<uint64_t>(fe, (q | 15) + 1);
+    const uint32_t s0 = s;
+    if (step(s, q, e)) word_rec(s0, q);
+    q = e;
+  }
+  if (q >= fe && !d.dead[s]) eot(s);
+}
+
 void emulate_kernels(const Plan& plan, const BatchView& bv, uint32_t chunk, uint32_t ext_cap,
                      KernelOutput* ko, std::vector<uint64_t>* group_item_bytes) {
   const uint32_t F = bv.nfiles;
+  const bool word_recs = getenv("TSG_EMU_WORDREC") != nullptr && plan.groups.size() <= 0x3FFF;
   std::vector<uint32_t> ev;
   k1_reference(plan, bv, chunk, &ko->kw, &ev);
   ko->cand.clear();
@@ -1340,6 +1396,10 @@ void emulate_kernels(const Plan& plan, const BatchView& bv, uint32_t chunk, uint
         if (!need) continue;
         const uint64_t a = std::max<uint64_t>(fs, c * chunk), b = std::min<uint64_t>(fe, (c + 1) * chunk);
         if (group_item_bytes) (*group_item_bytes)[gi] += b - a;
+        if (word_recs) {
+          emulate_words(d, (uint32_t)gi, g.rules, bv.data, f, fs, fe, a, b, ext_cap, &ko->cand);
+          continue;
+        }
         bool o = run_segment(d, bv.data, fs, fe, a, b, ext_cap, [&](uint32_t mi, uint64_t pos) {
           const auto& m = d.masks[mi];
           for (size_t k = 0; k < g.rules.size(); k++)
