@@ -397,6 +397,14 @@ void tsg_layer_range_free(tsg_layer_range* range);
 int tsg_fs_pack(const tsg_ruleset* rs, const char* root, const char* const* skip_files,
                 uint32_t n_skip_files, const char* const* skip_dirs, uint32_t n_skip_dirs,
                 const char* config_path, tsg_layer** out);
+/* One rank's share of a tree (configs[0] over several GPUs, one process each): every rank
+ * lists the tree (no file opened), the listed files in path order are cut into `world`
+ * contiguous runs of about equal bytes, and only this rank's run is read, IsBinary-gated
+ * and packed.  Concatenated in rank order the shards are tsg_fs_pack's batch; walked is the
+ * whole tree's. */
+int tsg_fs_pack_shard(const tsg_ruleset* rs, const char* root, const char* const* skip_files,
+                      uint32_t n_skip_files, const char* const* skip_dirs, uint32_t n_skip_dirs,
+                      const char* config_path, uint32_t rank, uint32_t world, tsg_layer** out);
 /* Ingest straight into a pinned slot: tsg_layer_pack / tsg_layer_range_pack /
  * tsg_fs_pack whose kept files are written into a slot acquired from ctx instead of pageable
  * memory, so no second copy precedes the upload: a layer's files are copied once, tar ->

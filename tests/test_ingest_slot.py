@@ -208,3 +208,21 @@ def test_pipelined_scan_errors_leave_no_pending(scanner, tmp_path):
     paths, res, _, _, _ = W.scan_layer_pipelined(ctx, layer_bytes())
     assert len(paths) == len(res) > 0
     ctx.close()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_fs_pack_shard_union_is_fs_pack(tmp_path, scanner, world):
+    """tsg_fs_pack_shard: each rank reads only its contiguous byte run of the listed tree;
+    the shards in rank order are tsg_fs_pack's batch (files, bytes, paths), walked is the
+    whole tree's."""
+    root = str(tmp_path / "t")
+    _tree(root)
+    configs.source_tree(os.path.join(root, "src"), 2 << 20, seed=3)
+    ref = W.NativeFS(scanner, root)
+    parts = [W.NativeFS(scanner, root, rank=r, world=world) for r in range(world)]
+    paths = [p.batch.path(i) for p in parts for i in range(p.batch.nfiles)]
+    assert paths == [ref.batch.path(i) for i in range(ref.batch.nfiles)]
+    data = b"".join(bytes(p.batch.data[:int(p.batch.offsets[-1])]) for p in parts)
+    assert data == bytes(ref.batch.data[:int(ref.batch.offsets[-1])])
+    assert all(p.walked == ref.walked for p in parts)
+    assert min(p.batch.nfiles for p in parts) > 0

@@ -152,3 +152,66 @@ def test_two_ranks_layer_gpu(tmp_path):
     procs, outs = _run_layer_ranks(tmp_path, device=0, nbytes=6 << 20)
     assert all(p.returncode == 0 for p in procs), outs
     assert "OK" in outs[0]
+
+
+FS_WORKER = textwrap.dedent("""
+    import sys
+    sys.path.insert(0, %(root)r)
+    import torch.distributed as dist
+    from tests.helpers import canon_secret
+    from trivy_amd import analyzer as A, configs, secret as S, walker as W
+    from trivy_amd.shard import scan_fs_sharded
+    rank = int(sys.argv[1])
+    dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%(port)d",
+                            rank=rank, world_size=2)
+    root = %(tree)r
+    if rank == 0:
+        configs.source_tree(root, 2 << 20, seed=23)
+    dist.barrier()
+    an = A.SecretAnalyzer(S.NewScanner(None), "")
+    device = %(device)r
+    out = scan_fs_sharded(an, root, rank, 2, dist=dist, device=device,
+                          emulate_chunk=0 if device is not None else 64)
+    if rank == 0:
+        want = W.analyze_fs(an, root)
+        assert [canon_secret(s) for s in out] == [canon_secret(s) for s in want]
+        assert len(out) > 10
+        print("OK", len(out))
+    else:
+        assert out is None
+    dist.destroy_process_group()
+""")
+
+
+def _run_fs_ranks(tmp_path, device=None):
+    port = _free_port()
+    script = tmp_path / "wf.py"
+    script.write_text(FS_WORKER % {"root": ROOT, "port": port, "tree": str(tmp_path / "tree"),
+                                   "device": device})
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    procs = [subprocess.Popen([sys.executable, str(script), str(r)], cwd=ROOT, env=env,
+                              stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+             for r in range(2)]
+    try:
+        outs = [p.communicate(timeout=240)[0] for p in procs]
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    return procs, outs
+
+
+def test_two_ranks_fs_gloo(tmp_path):
+    """configs[0] over 2 ranks: each reads only its byte run of the tree (tsg_fs_pack_shard);
+    rank 0's gathered findings == the single-process fs analysis."""
+    procs, outs = _run_fs_ranks(tmp_path)
+    assert all(p.returncode == 0 for p in procs), outs
+    assert "OK" in outs[0]
+
+
+@pytest.mark.gpu
+def test_two_ranks_fs_gpu(tmp_path):
+    """The same with both ranks scanning on the one GPU (as bench.py --gpus N would on N)."""
+    procs, outs = _run_fs_ranks(tmp_path, device=0)
+    assert all(p.returncode == 0 for p in procs), outs
+    assert "OK" in outs[0]

@@ -158,6 +158,9 @@ SIGNATURES = [
     ("tsg_layer_range_free", None, [_P]),
     ("tsg_fs_pack", C.c_int, [_P, C.c_char_p, C.POINTER(C.c_char_p), C.c_uint32,
                               C.POINTER(C.c_char_p), C.c_uint32, C.c_char_p, C.POINTER(_P)]),
+    ("tsg_fs_pack_shard", C.c_int, [_P, C.c_char_p, C.POINTER(C.c_char_p), C.c_uint32,
+                                    C.POINTER(C.c_char_p), C.c_uint32, C.c_char_p, C.c_uint32,
+                                    C.c_uint32, C.POINTER(_P)]),
     ("tsg_layer_pack_slot", C.c_int, [_P, _P, C.c_uint64, C.POINTER(C.c_char_p), C.c_uint32,
                                       C.POINTER(C.c_char_p), C.c_uint32, C.c_char_p,
                                       C.POINTER(C.c_uint32), C.POINTER(_P)]),

@@ -1402,6 +1402,74 @@ int fs_pack(const tsg_ruleset* rs, const char* root, const char* const* skip_fil
 }  // namespace
 }  // namespace tsg
 
+// One rank's share of a tree (SURVEY.md §8e, configs[0] over several GPUs): every rank lists
+// the tree (no file is opened: Required's path tests and lstat sizes), the listed files in
+// path order are cut into `world` contiguous runs of about equal bytes, and only this rank's
+// run is read, IsBinary-gated and packed.  The union over the ranks, in rank order, is
+// tsg_fs_pack's batch; walked is the whole tree's.
+extern "C" int tsg_fs_pack_shard(const tsg_ruleset* rs, const char* root, const char* const* skip_files,
+                                 uint32_t n_skip_files, const char* const* skip_dirs, uint32_t n_skip_dirs,
+                                 const char* config_path, uint32_t rank, uint32_t world, tsg_layer** out) {
+  if (!rs || !root || !out || world == 0 || rank >= world) return fail(TSG_ERR_ARG, "bad argument");
+  *out = nullptr;
+  try {
+    std::vector<std::unique_ptr<tsg::FsFile>> files;
+    uint32_t walked = 0;
+    int rc = tsg::fs_collect(rs, root, skip_files, n_skip_files, skip_dirs, n_skip_dirs, config_path, &files,
+                             &walked, false);
+    if (rc) return rc;
+    uint64_t all = 0;
+    for (const auto& f : files) all += f->size;
+    std::vector<size_t> mine;
+    uint64_t p = 0;
+    for (size_t i = 0; i < files.size(); i++) {  // owner of the file's first byte
+      const uint64_t r = all ? (uint64_t)((unsigned __int128)p * world / all) : i * world / files.size();
+      if (r == rank) mine.push_back(i);
+      p += files[i]->size;
+    }
+    // read this rank's files whole (in parallel), then IsBinary on what was read
+    std::vector<std::vector<uint8_t>> body(mine.size());
+    std::vector<uint8_t> keep(mine.size(), 0);
+    tsg::pool_for(mine.size(), 16, [&](size_t k) {
+      const tsg::FsFile& f = *files[mine[k]];
+      const int fd = open(f.full.c_str(), O_RDONLY | O_NOFOLLOW | O_CLOEXEC);
+      if (fd < 0) return;  // analyzer.go:411-413: a permission error skips the file
+      body[k].resize(f.size);
+      body[k].resize(tsg::read_upto(fd, body[k].data(), f.size));
+      close(fd);
+      keep[k] = !tsg::is_binary(body[k].data(), (int64_t)body[k].size());
+    }, 4);
+    auto L = std::make_unique<tsg_layer>();
+    L->walked = walked;
+    uint64_t total = 0;
+    for (size_t k = 0; k < mine.size(); k++)
+      if (keep[k]) {
+        total += body[k].size();
+        L->offsets.push_back(total);
+        L->paths += files[mine[k]]->fp;
+        L->path_offsets.push_back(L->paths.size());
+      }
+    tsg::Sink sink;
+    uint8_t* dst = sink.reserve(L.get(), total, (uint32_t)(L->offsets.size() - 1), L->paths.size());
+    std::vector<size_t> kept;
+    for (size_t k = 0; k < mine.size(); k++)
+      if (keep[k]) kept.push_back(k);
+    tsg::pool_for(kept.size(), 16, [&](size_t j) {
+      const auto& b = body[kept[j]];
+      if (!b.empty()) std::memcpy(dst + L->offsets[j], b.data(), b.size());
+    }, 16);
+    sink.finish(L.get());
+    *out = L.release();
+    return TSG_OK;
+  } catch (const tsg::SinkError& e) {
+    return fail(e.rc, e.msg);
+  } catch (const std::bad_alloc&) {
+    return fail(TSG_ERR_NOMEM, "out of memory");
+  } catch (const std::exception& e) {
+    return fail(TSG_ERR_INTERNAL, e.what());
+  }
+}
+
 extern "C" int tsg_fs_pack(const tsg_ruleset* rs, const char* root, const char* const* skip_files,
                            uint32_t n_skip_files, const char* const* skip_dirs, uint32_t n_skip_dirs,
                            const char* config_path, tsg_layer** out) {

@@ -119,10 +119,52 @@ def scan_layer_sharded(analyzer, tar, rank, world, dist=None, device=None, emula
     return secrets, lay.opq, lay.wh
 
 
+def scan_fs_sharded(analyzer, root, rank, world, dist=None, device=None, emulate_chunk=0,
+                    skip_files=(), skip_dirs=()):
+    """BASELINE configs[0] over `world` ranks (one process per GPU): every rank lists the
+    tree and reads only its contiguous byte run of the listed files (tsg_fs_pack_shard:
+    no rank holds another's file contents), scans it, and rank 0 gathers the files with
+    findings (sparse) and returns them sorted as AnalysisResult.Sort does; the other ranks
+    return None.  A failure on one rank raises on every rank (one status all-gather before
+    the gather), so no rank is left waiting in a collective."""
+    from .walker import NativeFS
+
+    def pack_scan():
+        fs = NativeFS(analyzer.scanner, root, skip_files, skip_dirs, analyzer.configPath,
+                      rank=rank, world=world)
+        b = fs.batch
+        if b.nfiles == 0:
+            return []
+        if device is not None or emulate_chunk:
+            local = analyzer.scanner.ScanBatch(b, device=device, emulate_chunk=emulate_chunk)
+        else:
+            local = analyzer.scanner.ScanBatch(b, nthreads=16)
+        return [r for r in local if r and r["Findings"]]
+
+    if world == 1 or dist is None:
+        return findings_sorted(pack_scan())
+    mine = None
+    try:
+        mine = pack_scan()
+        status = ("ok", "")
+    except Exception as e:  # noqa: BLE001 - forwarded to every rank
+        status = ("err", "rank %d: %s" % (rank, e))
+    sts = [None] * world
+    dist.all_gather_object(sts, status)
+    bad = [m for k, m in sts if k == "err"]
+    if bad:
+        raise RuntimeError("; ".join(bad))
+    gathered = [None] * world if rank == 0 else None
+    dist.gather_object(mine, gathered, dst=0)
+    if rank != 0:
+        return None
+    return findings_sorted([r for part in gathered for r in part])
+
+
 def findings_sorted(results):
     """The secrets of AnalysisResult after Sort: files with findings, by path."""
     from .analyzer import sort_secrets
     return sort_secrets([r for r in results if r and r["Findings"]])
 
 
-__all__ = ["lpt_shards", "scan_sharded", "scan_layer_sharded", "findings_sorted", "S"]
+__all__ = ["lpt_shards", "scan_sharded", "scan_layer_sharded", "scan_fs_sharded", "findings_sorted", "S"]

@@ -383,18 +383,25 @@ def pack_layer_ranges(scanner, tar, world, skip_files=(), skip_dirs=(), config_p
 
 class NativeFS(NativeLayer):
     """tsg_fs_pack: walker.FS.Walk + the fs artifact's relative paths + `Required` +
-    `IsBinary` over a directory tree, files read in parallel and packed in path order."""
+    `IsBinary` over a directory tree, files read in parallel and packed in path order
+    (world > 1: tsg_fs_pack_shard, only this rank's contiguous byte run is read)."""
 
-    def __init__(self, scanner, root, skip_files=(), skip_dirs=(), config_path=""):
+    def __init__(self, scanner, root, skip_files=(), skip_dirs=(), config_path="", rank=0, world=1):
         L = N.lib()
         self._h = None
         enc = lambda xs: (C.c_char_p * max(1, len(xs)))(
             *[x.encode("utf-8", "surrogateescape") for x in xs])
         sf, sd = enc(list(skip_files)), enc(list(skip_dirs))
         h = C.c_void_p()
-        N.check(L.tsg_fs_pack(scanner.handle, root.encode("utf-8", "surrogateescape"), sf,
-                              len(skip_files), sd, len(skip_dirs),
-                              config_path.encode("utf-8", "surrogateescape"), C.byref(h)))
+        if world > 1:  # tsg_fs_pack_shard: this rank's contiguous byte run of the tree
+            N.check(L.tsg_fs_pack_shard(scanner.handle, root.encode("utf-8", "surrogateescape"), sf,
+                                        len(skip_files), sd, len(skip_dirs),
+                                        config_path.encode("utf-8", "surrogateescape"), rank, world,
+                                        C.byref(h)))
+        else:
+            N.check(L.tsg_fs_pack(scanner.handle, root.encode("utf-8", "surrogateescape"), sf,
+                                  len(skip_files), sd, len(skip_dirs),
+                                  config_path.encode("utf-8", "surrogateescape"), C.byref(h)))
         self._h = h
         v = N.LayerView()
         N.check(L.tsg_layer_get(h, C.byref(v)))
