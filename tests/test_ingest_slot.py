@@ -226,3 +226,34 @@ def test_fs_pack_shard_union_is_fs_pack(tmp_path, scanner, world):
     assert data == bytes(ref.batch.data[:int(ref.batch.offsets[-1])])
     assert all(p.walked == ref.walked for p in parts)
     assert min(p.batch.nfiles for p in parts) > 0
+
+
+@pytest.mark.parametrize("seed", [1, 2])
+def test_fs_scan_drops_binary_across_pieces(tmp_path, scanner, seed):
+    """tsg_fs_scan reads every listed file into its piece and drops the binary ones when the
+    pieces are joined: with many binary files (some before, between and after text files,
+    some at piece boundaries of 1 MiB slots) the joined result equals scanning tsg_fs_pack's
+    batch, file for file."""
+    rng = np.random.default_rng(seed)
+    root = str(tmp_path / "t")
+    os.makedirs(root)
+    tok = "ghp_" + "aB3dE5fG7hI9jK1lM3nO5pQ7rS9tU1vW3xY5"
+    for i in range(120):
+        d = os.path.join(root, "d%d" % (i % 7))
+        os.makedirs(d, exist_ok=True)
+        n = int(rng.integers(10, 300_000))
+        if rng.random() < 0.4:  # binary: a control byte in the first 300 bytes
+            body = bytes(rng.integers(0, 256, n, dtype=np.uint8))
+            body = body[:5] + b"\x01" + body[6:]
+        else:
+            body = (b"line of text %d\n" % i) * (n // 16) + ("GITHUB_TOKEN=%s\n" % tok).encode()
+        with open(os.path.join(d, "f%03d.txt" % i), "wb") as f:
+            f.write(body)
+    ctx = S.GpuContext(scanner, 0, emulate=True, slot_mib=1)
+    ref = W.NativeFS(scanner, root)
+    paths, res, _, _, walked = W.scan_fs_pipelined(ctx, root)
+    assert paths == [ref.batch.path(i) for i in range(ref.batch.nfiles)]
+    assert res == scanner.ScanBatch(ref.batch)
+    assert walked == ref.walked == 120
+    assert 40 < len(paths) < 100
+    ctx.close()
