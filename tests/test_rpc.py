@@ -79,3 +79,28 @@ def test_round_trip_scan_output():
             return [norm(v) for v in x]
         return x
     assert back == norm(secrets)
+
+
+def test_reference_golden_round_trip():
+    """The findings of the reference's own integration golden
+    (integration/testdata/secrets.json.golden) through ConvertToRPCSecrets, the wire and
+    ConvertFromRPCSecrets: every field survives (Layer: Digest/DiffID/CreatedBy as
+    present; the golden's `Deleted` field is not a field of this revision's message)."""
+    import json
+    import os
+    from tests.conftest import ROOT
+    g = json.load(open(os.path.join(ROOT, "tests/golden/reference/integration/secrets.json.golden")))
+    secrets = [{"FilePath": r["Target"], "Findings": r["Secrets"]} for r in g["Results"]]
+    wire = [m.SerializeToString() for m in rpc.ConvertToRPCSecrets(secrets)]
+    back = rpc.ConvertFromRPCSecrets([rpc.Secret.FromString(w) for w in wire])
+    assert len(back) == len(secrets) and sum(len(s["Findings"]) for s in back) == 2
+    for got, want in zip(back, secrets):
+        assert got["FilePath"] == want["FilePath"]
+        for gf, wf in zip(got["Findings"], want["Findings"]):
+            for k in ("RuleID", "Category", "Severity", "Title", "StartLine", "EndLine", "Match"):
+                assert gf[k] == wf[k], k
+            assert gf["Layer"] == {k: v for k, v in (wf.get("Layer") or {}).items() if v}
+            for gl, wl in zip(gf["Code"]["Lines"], wf["Code"]["Lines"]):
+                for k in ("Number", "Content", "IsCause", "Annotation", "Truncated", "FirstCause", "LastCause"):
+                    assert gl[k] == wl[k], k
+                assert gl["Highlighted"] == wl.get("Highlighted", "")
