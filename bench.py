@@ -4,7 +4,12 @@
     python bench.py [--gpus N] [--steps K] [--warmup W] [--gb G]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
 
-Workload (per rank, weak scaling): the 83 builtin rules over a seeded synthetic corpus of
+GPUs: under torchrun, one rank per GPU (rank r drives device LOCAL_RANK; WORLD_SIZE must
+equal --gpus).  Without torchrun, --gpus N makes this one process drive devices 0..N-1
+through tsg_multi (the form a single trivy process binds, image.go:210-234), one host
+thread per device.  Fewer visible GPUs than asked is an error, never a silent fallback.
+
+Workload (per GPU, weak scaling): the 83 builtin rules over a seeded synthetic corpus of
 --gb GiB (default 10: BASELINE configs[1]) of mixed code/config text files with planted
 secrets.  The corpus is packed once, before timing, into the context's pinned host slots
 (--batch-mib each; the ingest of SURVEY.md §8f writes files straight into such slots).
@@ -233,27 +238,112 @@ def fill_slots(ctx, batch, batch_bytes):
     return slots
 
 
+def _visible_gpus():
+    """HIP devices this process can see (counting does not initialise the GPU)."""
+    try:
+        import torch
+        return torch.cuda.device_count()
+    except ImportError:
+        return 0
+
+
+class DeviceRun:
+    """One device's share of the job: its context, its pinned slots (filled before timing),
+    and the pipelined submit / collect loop over them."""
+
+    def __init__(self, ctx, slots, info, depth, log):
+        self.ctx, self.slots, self.info, self.depth, self.log = ctx, slots, info, depth, log
+        self.step_findings = []  # (files with findings, findings) of every step, warmup included
+
+    def run(self, steps, verbose=True):
+        """`steps` scans of the share, pipelined across step boundaries (batches of step k+1
+        are submitted while step k's last ones resolve); every result is collected."""
+        import collections
+        import ctypes as C
+        from trivy_amd import _native as N
+        L = N.lib()
+        q = collections.deque()
+        per_step = [[0, 0] for _ in range(steps)]
+
+        def collect():
+            t, k = q.popleft()
+            out = C.c_void_p()
+            N.check(L.tsg_batch_collect(self.ctx.handle, t, C.byref(out)))
+            ff, nf = _summary(out)
+            L.tsg_result_free(out)
+            per_step[k][0] += ff
+            per_step[k][1] += nf
+
+        for k in range(steps):
+            if verbose:
+                self.log("step %d/%d" % (k + 1, steps))
+            for sid, nf, _ in self.slots:
+                t = C.c_uint64()
+                N.check(L.tsg_slot_submit(self.ctx.handle, sid, nf, C.byref(t)))
+                q.append((t.value, k))
+                while len(q) >= self.depth:
+                    collect()
+        while q:
+            collect()
+        self.step_findings.extend(tuple(x) for x in per_step)
+
+    def release(self):
+        for sid, _, _ in self.slots:
+            self.ctx.release_slot(sid)
+
+
+STAT_SUMS = ("batches", "sum_bytes", "sum_k1_ms", "sum_gate_ms", "sum_k2_ms", "sum_h2d_ms", "sum_d2h_ms",
+             "sum_resolve_ms", "sum_prep_ms", "sum_meta_ms")
+
+
+def _gbs(nbytes, ms):
+    """GB/s, or None without a time (emulated contexts record no kernel times)"""
+    return nbytes / (ms / 1e3) / 1e9 if ms else None
+
+
+def _frac(gbs):
+    return round(gbs / HBM_PEAK_GBS, 4) if gbs is not None else None
+
+
+def _r(x, n=1):
+    return round(x, n) if x is not None else None
+
+
+def _delta(st, st0):
+    return {k: st[k] - st0[k] for k in STAT_SUMS}
+
+
+def _device_ms(d):
+    """All of a batch's device work but the batch's own H2D and the wait for the other
+    lane: the metadata H2D, prep, K1 (+K1X), gates, K2 and the outputs kernel."""
+    return d["sum_meta_ms"] + d["sum_prep_ms"] + d["sum_k1_ms"] + d["sum_gate_ms"] + d["sum_k2_ms"] + d["sum_d2h_ms"]
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="GPUs: under torchrun one rank per GPU (WORLD_SIZE must equal it); "
+                         "otherwise this one process drives devices 0..N-1 (tsg_multi)")
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--gb", type=float, default=10.0, help="GiB of corpus per rank")
+    ap.add_argument("--gb", type=float, default=10.0, help="GiB of corpus per GPU")
     ap.add_argument("--batch-mib", type=int, default=1024, help="bytes per pinned slot / batch")
     ap.add_argument("--chunk", type=int, default=0)
     ap.add_argument("--seed", type=int, default=2)
-    ap.add_argument("--depth", type=int, default=4, help="batches in flight")
+    ap.add_argument("--depth", type=int, default=4, help="batches in flight per GPU")
     ap.add_argument("--host-threads", type=int, default=0,
                     help="host resolution pool threads (0: library default, 16)")
     ap.add_argument("--cpu-mib", type=int, default=1024, help="CPU baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--strong", action="store_true",
-                    help="strong scaling: --gb is the whole job's corpus, split over the ranks "
-                         "(each rank generates and scans its 1/N share); default: --gb per rank")
+                    help="strong scaling: --gb is the whole job's corpus, split over the GPUs "
+                         "(each generates and scans its 1/N share); default: --gb per GPU")
     ap.add_argument("--rules", default="builtin", choices=["builtin", "user1000", "allow-exclude"],
                     help="rule set: builtin (configs[1]), builtin + 1,000 user rules "
                          "(configs[3]), allow rules + exclude blocks over text and binary "
                          "blobs (configs[4])")
+    ap.add_argument("--emulate", action="store_true",
+                    help="tests only: emulated contexts (the kernels' algorithm on the CPU), no GPU")
     ap.add_argument("--e2e", choices=["fs", "layer"], default=None,
                     help="end-to-end ingest + scan instead of the configs[1] line: 'fs' = a "
                          "seeded source tree on disk (configs[0] shape, --e2e-mib), 'layer' = a "
@@ -266,92 +356,122 @@ def main():
         return main_e2e(args)
 
     T0 = time.perf_counter()
+    if args.gpus < 1:
+        raise SystemExit("bench: --gpus must be >= 1")
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    if ws > 1 and args.gpus != ws:  # (before any rendezvous)
+        raise SystemExit("bench: --gpus %d under torchrun with WORLD_SIZE=%d: one rank per GPU, "
+                         "so they must be equal" % (args.gpus, ws))
     dist, rank, world, local = _dist()
+    # devices this process drives: its rank's GPU, or 0..N-1 in one process
+    devices = [local] if world > 1 else list(range(args.gpus))
+    ngpus = world if world > 1 else args.gpus
+    if not args.emulate:
+        vis = _visible_gpus()
+        if vis < max(devices) + 1:
+            raise SystemExit("bench: --gpus %d needs device %d, but this process sees %d GPU(s); "
+                             "refusing to run on fewer" % (args.gpus, max(devices), vis))
     from trivy_amd import corpus
     from trivy_amd import secret as S
     from trivy_amd import _native as N
     L = N.lib()
 
-    nbytes = int(args.gb * (1 << 30) / (world if args.strong else 1))
-    t0 = time.perf_counter()
-    sc, extra, binary_frac, workload, nrules = rule_set(args.rules)
-    compile_s = time.perf_counter() - t0
-    t0 = time.perf_counter()
-    batch, info = corpus.make_corpus(nbytes, seed=args.seed + 1000 * rank, plants_per_mib=1.0,
-                                     extra_plants=extra, extra_per_mib=2.0 if extra else 0.0,
-                                     binary_frac=binary_frac)
-    gen_s = time.perf_counter() - t0
-    dev = 0
-    if world > 1:  # one rank per GPU; more ranks than GPUs share them round-robin (rehearsals)
-        import torch
-        dev = local % max(1, torch.cuda.device_count())
-    batch_bytes = args.batch_mib << 20
-    nslots = -(-nbytes // batch_bytes) + 2
-    ctx = S.GpuContext(sc, dev, chunk_bytes=args.chunk, host_threads=args.host_threads,
-                       max_slots=nslots + 2)
-    t0 = time.perf_counter()
-    slots = fill_slots(ctx, batch, batch_bytes)
-    pack_s = time.perf_counter() - t0
-
     def log(msg):
         print("[bench rank %d %.1fs] %s" % (rank, time.perf_counter() - T0, msg), file=sys.stderr, flush=True)
 
-    log("corpus %.2f GiB (%d files) in %.1fs, rules compiled in %.1fs, packed in %.1fs"
-        % (info["bytes"] / (1 << 30), info["files"], gen_s, compile_s, pack_s))
+    nbytes = int(args.gb * (1 << 30) / (ngpus if args.strong else 1))  # per GPU
+    t0 = time.perf_counter()
+    sc, extra, binary_frac, workload, nrules = rule_set(args.rules)
+    compile_s = time.perf_counter() - t0
+    batch_bytes = args.batch_mib << 20
+    nslots = -(-nbytes // batch_bytes) + 2
+    multi = None
+    if len(devices) > 1 or args.emulate:
+        multi = S.MultiGpu(sc, devices, host_threads=args.host_threads, emulate=args.emulate,
+                           max_slots=nslots + 2, chunk_bytes=args.chunk)
+        ctxs = [multi.context(i) for i in range(len(devices))]
+    else:
+        ctxs = [S.GpuContext(sc, devices[0], chunk_bytes=args.chunk, host_threads=args.host_threads,
+                             max_slots=nslots + 2)]
+    # each GPU's share: a corpus of its own (seeded by its global GPU index), packed into that
+    # device's pinned slots before timing; the first GPU's stays for the CPU sample
+    runs, gen_s, pack_s, batch0, info0 = [], 0.0, 0.0, None, None
+    for i, ctx in enumerate(ctxs):
+        g = rank if world > 1 else i
+        t0 = time.perf_counter()
+        batch, info = corpus.make_corpus(nbytes, seed=args.seed + 1000 * g, plants_per_mib=1.0,
+                                         extra_plants=extra, extra_per_mib=2.0 if extra else 0.0,
+                                         binary_frac=binary_frac)
+        gen_s += time.perf_counter() - t0
+        t0 = time.perf_counter()
+        slots = fill_slots(ctx, batch, batch_bytes)
+        pack_s += time.perf_counter() - t0
+        runs.append(DeviceRun(ctx, slots, info, args.depth, log))
+        if i == 0:
+            info0, batch0 = info, batch
+        batch = None
+        log("GPU %d: corpus %.2f GiB (%d files), packed" % (devices[i], info["bytes"] / (1 << 30), info["files"]))
+    log("generated in %.1fs, rules compiled in %.1fs, packed in %.1fs" % (gen_s, compile_s, pack_s))
 
-    import collections
     import ctypes as C
-    step_findings = []  # (files with findings, findings) of every step, warmup included
+    import threading
 
-    def collect(q, per_step):
-        t, k = q.popleft()
-        out = C.c_void_p()
-        N.check(L.tsg_batch_collect(ctx.handle, t, C.byref(out)))
-        ff, nf = _summary(out)
-        L.tsg_result_free(out)
-        per_step[k][0] += ff
-        per_step[k][1] += nf
+    def run_all(steps):
+        """every device's share, one host thread per device (the native calls release the GIL)"""
+        if len(runs) == 1:
+            runs[0].run(steps)
+            return
+        errs = []
 
-    def run(steps):
-        """`steps` scans of the corpus, pipelined across step boundaries (batches of step
-        k+1 are submitted while step k's last ones resolve); every result is collected."""
-        q = collections.deque()
-        per_step = [[0, 0] for _ in range(steps)]
-        for k in range(steps):
-            log("step %d/%d" % (k + 1, steps))
-            for sid, nf, _ in slots:
-                t = C.c_uint64()
-                N.check(L.tsg_slot_submit(ctx.handle, sid, nf, C.byref(t)))
-                q.append((t.value, k))
-                while len(q) >= args.depth:
-                    collect(q, per_step)
-        while q:
-            collect(q, per_step)
-        step_findings.extend(tuple(x) for x in per_step)
+        def one(r, verbose):
+            try:
+                r.run(steps, verbose)
+            except BaseException as e:  # noqa: BLE001 (re-raised below)
+                errs.append(e)
+        th = [threading.Thread(target=one, args=(r, i == 0)) for i, r in enumerate(runs)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        if errs:
+            raise errs[0]
 
-    run(args.warmup)
-    st0 = ctx.stats()
+    run_all(args.warmup)
+    st0 = [r.ctx.stats() for r in runs]
     _barrier(dist)
     t0 = time.perf_counter()
-    run(args.steps)
+    run_all(args.steps)
     _barrier(dist)
     dt = time.perf_counter() - t0
-    st = ctx.stats()
+    st = [r.ctx.stats() for r in runs]
     dt = _reduce(dist, dt, "MAX")
-    total_bytes = _reduce(dist, float(info["bytes"]), "SUM") * args.steps
-    d = {k: st[k] - st0[k] for k in ("batches", "sum_bytes", "sum_k1_ms", "sum_gate_ms", "sum_k2_ms",
-                                      "sum_h2d_ms", "sum_d2h_ms", "sum_resolve_ms")}
+    local_bytes = float(sum(r.info["bytes"] for r in runs))
+    total_bytes = _reduce(dist, local_bytes, "SUM") * args.steps
+    ds = [_delta(a, b) for a, b in zip(st, st0)]
+    # pooled over this process's devices (per-batch means), and per device for the aggregate
+    d = {k: sum(x[k] for x in ds) for k in STAT_SUMS}
     nbat = max(1, d["batches"])
-    k1_gbs = d["sum_bytes"] / (d["sum_k1_ms"] / 1e3) / 1e9
-    dev_ms = d["sum_k1_ms"] + d["sum_gate_ms"] + d["sum_k2_ms"]
+    k1_gbs = _gbs(d["sum_bytes"], d["sum_k1_ms"])
+    kern_ms = d["sum_k1_ms"] + d["sum_gate_ms"] + d["sum_k2_ms"]
+    dev_ms = _device_ms(d)
     launch_bytes = d["sum_bytes"] / nbat
-    k2_read = st["k2_bytes"]  # last batch: chunk bytes K2 read
+    # SURVEY §8d aggregate: N_total / max_g(t_g) / (8 TB/s x G), t_g = a GPU's device time
+    # over the timed steps (K1 alone, K1 + gates + K2, and all device work)
+    agg = {}
+    for key, fn in (("k1", lambda x: x["sum_k1_ms"]),
+                    ("k1_gates_k2", lambda x: x["sum_k1_ms"] + x["sum_gate_ms"] + x["sum_k2_ms"]),
+                    ("device", _device_ms)):
+        tmax = _reduce(dist, max(fn(x) for x in ds), "MAX") / 1e3
+        agg[key + "_frac"] = round(total_bytes / tmax / (HBM_PEAK_GBS * 1e9 * ngpus), 4) if tmax else None
+    last = st[0]
+    k2_read = last["k2_bytes"]  # last batch of the first device: chunk bytes K2 read
     pmc = _traffic_record(args.rules, int(launch_bytes))
+    ngpus_s = "x%d" % ngpus
     line = {
         "metric": "secret-scan GB/s (builtin rules) at 1/2/4/8 MI355X; % of HBM peak",
         "value": round(total_bytes / dt / 1e9, 3),
         "unit": "GB/s",
-        "n_gpus": world,
+        "n_gpus": ngpus,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(dt / args.steps * 1e3, 3),
@@ -359,18 +479,24 @@ def main():
         "scaling": "strong" if args.strong else "weak",
         "vs_baseline": None,
         "dtype": "u8",
-        "data": "synthetic (seeded corpus, trivy_amd/corpus.py) in pinned host memory; every "
+        "data": "synthetic (seeded corpus per GPU, trivy_amd/corpus.py) in pinned host memory; every "
                 "step moves every byte host->HBM (H2D inside the timed region)",
         "config": {"workload": workload % (nbytes / (1 << 30)) + (
-                       "; strong scaling: a %.1f GiB job split over %d ranks" % (args.gb, world)
+                       "; strong scaling: a %.1f GiB job split over %d GPUs" % (args.gb, ngpus)
                        if args.strong else ""),
-                   "files_per_gpu": info["files"], "bytes_per_gpu": info["bytes"],
+                   "files_per_gpu": info0["files"], "bytes_per_gpu": info0["bytes"],
                    "job_bytes": int(total_bytes / args.steps),
-                   "batches_per_step": len(slots), "batch_bytes": batch_bytes,
-                   "rules": nrules, "parallelism": "file-sharded x%d, no collective" % world},
+                   "batches_per_step": sum(len(r.slots) for r in runs), "batch_bytes": batch_bytes,
+                   "rules": nrules,
+                   "parallelism": ("file-sharded %s, one process per GPU (torchrun), no collective" % ngpus_s
+                                   if world > 1 else
+                                   "file-sharded %s, one process driving %d device(s) (tsg_multi), no "
+                                   "collective" % (ngpus_s, len(devices))) + (
+                                       ", EMULATED contexts (no GPU)" if args.emulate else ""),
+                   "devices": devices if world == 1 else None},
         "roofline": {"bound": "hbm", "kernel": "K1 keyword automaton (k1_kernel)",
-                     "achieved": round(k1_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(k1_gbs / HBM_PEAK_GBS, 4),
+                     "achieved": _r(k1_gbs), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": _frac(k1_gbs),
                      "traffic": pmc["k1_bytes_per_launch"] if pmc else None,
                      "algorithmic_bytes_per_launch": int(launch_bytes),
                      "traffic_source": pmc["csv"] if pmc else
@@ -378,48 +504,66 @@ def main():
                      "in profiles/pmc/",
                      "traffic_calibration": "FETCH_SIZE KiB x 1024 / 0.922 (K1's quad-transposed "
                                             "64-B loads; profiles/r02/fetch_calib.json)",
-                     "k1_gates_k2_frac": round(d["sum_bytes"] / (dev_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4)},
-        "kernels": {"k1_GBps": round(k1_gbs, 1),
-                    "k2_GBps_on_item_bytes": round(k2_read / (st["k2_ms"] / 1e3) / 1e9, 1)
-                    if st["k2_ms"] else None,
-                    "k1_gates_k2_GBps": round(d["sum_bytes"] / (dev_ms / 1e3) / 1e9, 1),
-                    "k1_ms_per_batch": round(d["sum_k1_ms"] / nbat, 3),
-                    "gates_ms_per_batch": round(d["sum_gate_ms"] / nbat, 3),
-                    "k2_ms_per_batch": round(d["sum_k2_ms"] / nbat, 3),
-                    "k2_item_bytes_last_batch": k2_read, "k2_entries_last_batch": st["k2_launches"],
-                    "candidates_last_batch": st["candidates"],
-                    "groups_skipped_last_batch": st["groups_skipped"],
-                    "k2_diag_last_batch": {k: st[k] for k in ("k2_tail_bytes", "k2_tail_max",
-                                                               "k2_long_tails", "k2_replays")}},
-        "pipeline": {"h2d_GBps": round(d["sum_bytes"] / (d["sum_h2d_ms"] / 1e3) / 1e9, 2),
+                     "k1_gates_k2_frac": _frac(_gbs(d["sum_bytes"], kern_ms)),
+                     "device_frac": _frac(_gbs(d["sum_bytes"], dev_ms)),
+                     "aggregate": dict(agg, gpus=ngpus,
+                                       definition="job bytes / max over GPUs of that GPU's device "
+                                                  "ms (HIP events) / (8 TB/s x GPUs)")},
+        "kernels": {"k1_GBps": _r(k1_gbs),
+                    "k2_GBps_on_item_bytes": round(k2_read / (last["k2_ms"] / 1e3) / 1e9, 1)
+                    if last["k2_ms"] else None,
+                    "k1_gates_k2_GBps": _r(_gbs(d["sum_bytes"], kern_ms)),
+                    "device_GBps": _r(_gbs(d["sum_bytes"], dev_ms)),
+                    "device_ms_per_batch": round(dev_ms / nbat, 4),
+                    "meta_h2d_ms_per_batch": round(d["sum_meta_ms"] / nbat, 4),
+                    "prep_ms_per_batch": round(d["sum_prep_ms"] / nbat, 4),
+                    "k1_ms_per_batch": round(d["sum_k1_ms"] / nbat, 4),
+                    "gates_ms_per_batch": round(d["sum_gate_ms"] / nbat, 4),
+                    "k2_ms_per_batch": round(d["sum_k2_ms"] / nbat, 4),
+                    "outputs_ms_per_batch": round(d["sum_d2h_ms"] / nbat, 4),
+                    "per_device": [{"device": dv, "batches": x["batches"],
+                                    "k1_ms": round(x["sum_k1_ms"], 3),
+                                    "k1_gates_k2_ms": round(x["sum_k1_ms"] + x["sum_gate_ms"] + x["sum_k2_ms"], 3),
+                                    "device_ms": round(_device_ms(x), 3)}
+                                   for dv, x in zip(devices, ds)],
+                    "k2_item_bytes_last_batch": k2_read, "k2_entries_last_batch": last["k2_launches"],
+                    "candidates_last_batch": last["candidates"],
+                    "groups_skipped_last_batch": last["groups_skipped"],
+                    "k2_diag_last_batch": {k: last[k] for k in ("k2_tail_bytes", "k2_tail_max",
+                                                                 "k2_long_tails", "k2_replays")}},
+        "pipeline": {"h2d_GBps": _r(_gbs(d["sum_bytes"], d["sum_h2d_ms"]), 2),
                      "h2d_ms_per_batch": round(d["sum_h2d_ms"] / nbat, 3),
-                     "d2h_ms_per_batch": round(d["sum_d2h_ms"] / nbat, 3),
                      "resolve_ms_per_batch": round(d["sum_resolve_ms"] / nbat, 3),
                      "depth": args.depth, "lanes": 2,
                      "gen_s": round(gen_s, 2), "pack_into_pinned_s": round(pack_s, 2),
                      "rule_compile_s": round(compile_s, 2)},
     }
     log("timed %d steps: %.3f s" % (args.steps, dt))
-    # every step must have produced the same findings (the timed loop reads every result)
-    if len(set(step_findings)) != 1:
-        raise SystemExit("bench: findings differ between steps: %s" % step_findings)
-    line["checks"] = {"findings_per_step": step_findings[0][1],
-                      "files_with_findings_per_step": step_findings[0][0],
-                      "steps_checked": len(step_findings)}
+    # every step of every device must have produced the same findings as its warmup steps
+    # (the timed loop reads every result)
+    for dv, r in zip(devices, runs):
+        if len(set(r.step_findings)) != 1:
+            raise SystemExit("bench: findings differ between steps on device %d: %s" % (dv, r.step_findings))
+    line["checks"] = {"findings_per_step": sum(r.step_findings[0][1] for r in runs),
+                      "files_with_findings_per_step": sum(r.step_findings[0][0] for r in runs),
+                      "steps_checked": len(runs[0].step_findings)}
     if rank == 0 and not args.no_cpu_baseline:
         nt = args.host_threads or 16
-        exact, opt, sub, exact_bytes = cpu_baselines(sc, batch, args.cpu_mib << 20, nt)
+        exact, opt, sub, exact_bytes = cpu_baselines(sc, batch0, args.cpu_mib << 20, nt)
         line["cpu_baseline"], line["cpu_optimised"] = exact, opt
         out = C.c_void_p()
-        N.check(L.tsg_scan_batch(ctx.handle, *sub.ptrs(), C.byref(out)))
+        N.check(L.tsg_scan_batch(ctxs[0].handle, *sub.ptrs(), C.byref(out)))
         if _raw(out) != exact_bytes:
             raise SystemExit("bench: the device result of the cpu_baseline sample differs from "
                              "the exact CPU path")
         line["checks"]["sample_device_eq_exact_cpu"] = True
         line["checks"]["sample_files"] = sub.nfiles
-    for sid, _, _ in slots:
-        ctx.release_slot(sid)
-    ctx.close()
+    for r in runs:
+        r.release()
+    for c in ctxs:
+        c.close()
+    if multi is not None:
+        multi.close()
     if rank == 0:
         print(json.dumps(line), flush=True)
     if dist is not None:

@@ -218,7 +218,7 @@ int tsg_batch_kernels(tsg_ctx* ctx, uint32_t slot_id, uint32_t nfiles, uint32_t*
 typedef struct tsg_stats {
   double k1_ms;          /* K1 literal automaton + run counters, last collected batch (HIP events) */
   double k2_ms;          /* K2 rule-group DFAs (the persistent work-list launch) */
-  double aux_ms;         /* D2H of the outputs */
+  double aux_ms;         /* the outputs kernel (results into pinned, host-mapped memory) */
   double resolve_ms;     /* host exact resolution (wall) */
   uint64_t bytes;        /* content bytes of the batch */
   uint64_t k2_bytes;     /* chunk bytes K2 scans (items listed x chunk) */
@@ -239,6 +239,10 @@ typedef struct tsg_stats {
    * followed past chunk ends, the longest such tail, tails over 4 KiB, words replayed for
    * accepts */
   uint32_t k2_tail_bytes, k2_tail_max, k2_long_tails, k2_replays;
+  /* the rest of a batch's device work (HIP events on its lane): the prep kernel (zero fills,
+   * coarse file map) and the H2D of the offsets / paths; aux_ms / sum_d2h_ms above are the
+   * outputs kernel (results written into pinned, host-mapped memory) */
+  double prep_ms, meta_ms, sum_prep_ms, sum_meta_ms;
 } tsg_stats;
 int tsg_ctx_get_stats(const tsg_ctx* ctx, tsg_stats* out);
 

@@ -136,3 +136,28 @@ def test_word_records_emulated_vs_exact(builtin, chunk, monkeypatch):
     want = builtin.ScanBatch(dense, nthreads=8)
     assert builtin.ScanBatch(dense, emulate_chunk=chunk) == want
     assert sum(len(w["Findings"] or []) for w in want) > 0
+
+
+@pytest.mark.parametrize("chunk", [64, 256])
+def test_fold_rune_then_immortal_tail_emulated_vs_exact(chunk):
+    """A (?i) user rule with a (?s).* loop, matched through a U+212A: after the file's last
+    folding rune the resolver's combined fold-DFA pass follows its threads in noinject mode,
+    and a thread inside `(?s).*` never dies (DFA::immortal).  That pass stops there; the
+    rule must then be resolved over the whole file, or every match end past that point (the
+    `omega` far after the rune) is lost (plan.cpp resolve_batch)."""
+    doc = {"rules": [{"id": "kilo-omega", "category": "user", "title": "kilo to omega", "severity": "HIGH",
+                      "regex": r"(?i)kilo(?P<secret>(?s).*)omega", "secret-group-name": "secret",
+                      "keywords": ["omega"]}]}
+    sc = S.NewScanner(S.config_from_dict(doc))
+    rng = np.random.default_rng(9)
+    args = []
+    for i in range(40):
+        pad = "".join(rng.choice(list("abcdefgh \n=:"), int(rng.integers(10, 300))))
+        far = "".join(rng.choice(list("abcdefgh \n=:"), int(rng.integers(100, 3000))))
+        head = "Kilo" if i % 2 == 0 else "KILO"
+        body = pad + head + far + "OMEGA" + pad + ("K" if i % 3 == 0 else "")
+        args.append(S.ScanArgs("u/%d.txt" % i, body.encode()))
+    batch = S.Batch.from_args(args)
+    want = sc.ScanBatch(batch, nthreads=4)
+    assert sum(len(w["Findings"] or []) for w in want) == len(args)
+    assert sc.ScanBatch(batch, emulate_chunk=chunk) == want

@@ -79,7 +79,9 @@ class Stats(C.Structure):
                 ("sum_h2d_ms", C.c_double), ("sum_d2h_ms", C.c_double),
                 ("sum_resolve_ms", C.c_double), ("wait_ms", C.c_double),
                 ("k2_tail_bytes", C.c_uint32), ("k2_tail_max", C.c_uint32),
-                ("k2_long_tails", C.c_uint32), ("k2_replays", C.c_uint32)]
+                ("k2_long_tails", C.c_uint32), ("k2_replays", C.c_uint32),
+                ("prep_ms", C.c_double), ("meta_ms", C.c_double),
+                ("sum_prep_ms", C.c_double), ("sum_meta_ms", C.c_double)]
 
 
 # (name, restype, argtypes) -- every symbol include/trivy_secret.h declares

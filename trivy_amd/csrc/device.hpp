@@ -5,9 +5,10 @@
 // DeviceLane (its own HIP stream and HBM buffers); enqueue_scan puts the whole device part
 // of a batch on that stream with no host round trip:
 //
-//   H2D (pinned slot -> HBM)  chunk->file map  K1  path gate  keyword gates  event-chunk
-//   compaction  item counts  item layout (device-side)  item lists  K2  candidate copy-out
-//   (to pinned, mapped host memory)  D2H of keyword bits / overflow / path / skip flags
+//   H2D (pinned slot -> HBM) and one H2D of the offsets / paths  prep (zero fills, coarse
+//   file map)  K1  path gate  keyword gates  event-chunk compaction  item counts  item
+//   layout (device-side)  item lists  K2  outputs (candidates, keyword bits, overflow /
+//   path / skip flags, counters: written straight into pinned, host-mapped memory)
 //
 // and records the batch's completion event.  Two lanes per device let the H2D of one batch
 // overlap the kernels of the other.
@@ -24,25 +25,31 @@ namespace tsg {
 
 struct DeviceRules;
 
-// Pinned host memory of one batch's device outputs (written by the lane's stream).
+// Pinned host memory of one batch: the staging of its offsets / path offsets / paths (one
+// H2D), and its device outputs, which the outputs kernel writes straight into host-mapped
+// memory (no runtime D2H copy).
 struct HostOut {
+  uint8_t* blk = nullptr;       // host-mapped block: counts | gskip | ovf | pathok | kw
+  uint8_t* blk_dev = nullptr;   // its device address
   uint32_t* kw = nullptr;       // [files_cap * kw_words]
   uint8_t* ovf = nullptr;       // [files_cap] 1 = resolve the file whole
   uint8_t* pathok = nullptr;    // [files_cap] Global.AllowPath: 0 / 1 / 2 = host decides
   uint8_t* gskip = nullptr;     // [groups] 1 = K2 skipped the group (item capacity)
   Candidate* cand = nullptr;    // [cand_cap] host-mapped: K2 candidates copied out
   Candidate* cand_dev = nullptr;  // device address of `cand`
-  uint32_t* counts = nullptr;   // [16] host-mapped: 0 candidates, 1 event chunks, 2 K2 list
-                                // entries, 3 dense entries, 5 items, 6 entries, 7 skipped
-                                // groups, 8-11 K2 diagnostics (TSG_K2_DIAG)
-  uint32_t* counts_dev = nullptr;
+  uint32_t* counts = nullptr;   // [16] 0 candidates, 1 event chunks, 2 K2 list entries,
+                                // 3 dense entries, 5 items, 6 entries, 7 skipped groups,
+                                // 8-11 K2 diagnostics (TSG_K2_DIAG)
+  uint8_t* meta = nullptr;      // pinned staging: offsets [F+1] | path offsets [F+1] | paths
+  size_t meta_cap = 0;
   uint32_t files_cap = 0, cand_cap = 0, groups = 0, kw_words = 0;
-  // stage boundaries of the batch on its lane's stream: H2D | wait for the previous
-  // batch's kernels | K1 | gates | K2 | D2H; ev[kEvDone] completes the batch
-  hipEvent_t ev[7] = {};
+  // stage boundaries of the batch on its lane's stream: data H2D | metadata H2D | wait for
+  // the previous batch's kernels | prep | K1 | gates | K2 | outputs; ev[kEvDone] completes
+  // the batch
+  hipEvent_t ev[9] = {};
 };
 
-constexpr int kEvDone = 6;
+constexpr int kEvDone = 8;
 // per-batch K2 diagnostics (K2 work that is not the chunks themselves)
 struct K2Diag {
   unsigned long long tail_bytes, tail_max, long_tails, replays;
@@ -58,7 +65,7 @@ struct ScanInput {
 };
 
 struct ScanTimes {  // HIP-event milliseconds of one batch on its lane
-  float h2d = 0, wait = 0, k1 = 0, gates = 0, k2 = 0, d2h = 0;
+  float h2d = 0, meta = 0, wait = 0, prep = 0, k1 = 0, gates = 0, k2 = 0, out = 0;
 };
 
 struct LaneState;  // HBM buffers + stream + events of one lane

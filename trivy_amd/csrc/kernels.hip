@@ -140,21 +140,90 @@ __device__ __forceinline__ uint32_t byte_of(const uint4 v, uint32_t k) {
   return (w >> ((k & 3) * 8)) & 0xFF;
 }
 
-// chunk_file[c] = the file holding byte c*C (the last file starting at or before it; empty
-// files never hold a byte), for every chunk of the padded chunk range: one thread per
-// chunk, a binary search over the offsets (balanced, unlike a thread per file)
-__global__ void chunk_file_kernel(const uint64_t* __restrict__ off, uint32_t nfiles, uint32_t chunk,
-                                  uint64_t nchunks_pad, uint32_t* __restrict__ chunk_file) {
-  const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= nchunks_pad) return;
-  const uint64_t p = c * chunk;
-  uint32_t lo = 0, hi = nfiles;  // invariant: off[lo] <= p (off[0] = 0), answer in [lo, hi)
-  while (hi - lo > 1) {
+// ---------------------------------------------------------------- file map
+// The coarse file map: cf[k] = the file holding batch byte k << kCfShift (the last file
+// starting at or before it; empty files never hold a byte).  The file holding byte p then
+// lies in [cf[k], cf[k + 1]] for k = p >> kCfShift, found by a short binary search over the
+// offsets.  Every caller is on a sparse path (K1 accepts, K1X hits, event chunks, dense
+// entries), so one entry per 16 KiB replaces a full per-chunk map (17 MB per GiB batch).
+constexpr uint32_t kCfShift = 14;
+
+__device__ __forceinline__ uint32_t bsearch_file(const uint64_t* __restrict__ off, uint32_t lo, uint32_t hi,
+                                                 uint64_t p) {
+  while (hi - lo > 1) {  // invariant: off[lo] <= p, the answer in [lo, hi)
     const uint32_t mid = (lo + hi) >> 1;
     if (off[mid] <= p) lo = mid;
     else hi = mid;
   }
-  chunk_file[c] = lo;
+  return lo;
+}
+
+__device__ __forceinline__ uint32_t file_of(const uint32_t* __restrict__ cf, const uint64_t* __restrict__ off,
+                                            uint32_t nfiles, uint64_t p) {
+  const uint64_t k = p >> kCfShift;
+  return bsearch_file(off, cf[k], min(nfiles, cf[k + 1] + 1), p);
+}
+
+// ---------------------------------------------------------------- per-batch preparation
+// One kernel replaces the per-batch runtime fills: it zeroes the lane's output and counter
+// buffers and the zero tail after the batch (K1's chains read past its end), and builds the
+// coarse file map.  (Each fill was a runtime kernel of its own, ~7 us each, 16 per batch.)
+constexpr int kPrepZeros = 10;
+struct PrepArgs {
+  const uint64_t* off;
+  uint32_t nfiles;
+  uint64_t ncf;  // entries of cf
+  uint32_t* cf;
+  uint8_t* zp[kPrepZeros];  // byte ranges to zero
+  uint64_t zn[kPrepZeros];
+  uint32_t nz;
+};
+
+__device__ __forceinline__ void zero_range(uint8_t* p, uint64_t n, uint64_t tid, uint64_t nth) {
+  const uint64_t a = min<uint64_t>(n, (16 - ((uintptr_t)p & 15)) & 15);  // bytes before 16-B alignment
+  const uint64_t body = (n - a) / 16;
+  for (uint64_t i = tid; i < a; i += nth) p[i] = 0;
+  uint4* q = (uint4*)(p + a);
+  for (uint64_t i = tid; i < body; i += nth) q[i] = make_uint4(0, 0, 0, 0);
+  uint8_t* t = p + a + body * 16;
+  for (uint64_t i = tid; i < n - a - body * 16; i += nth) t[i] = 0;
+}
+
+__global__ void __launch_bounds__(256) prep_kernel(PrepArgs A) {
+  const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x, nth = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t k = tid; k < A.ncf; k += nth) A.cf[k] = bsearch_file(A.off, 0, A.nfiles, k << kCfShift);
+  for (uint32_t z = 0; z < A.nz; z++) zero_range(A.zp[z], A.zn[z], tid, nth);
+}
+
+// ---------------------------------------------------------------- outputs to the host
+// One kernel writes a batch's outputs straight into pinned, host-mapped memory: the
+// candidate records (their count is only known on the device) and the small per-file /
+// per-group arrays (keyword bits, overflow, path and skip flags, counters).  It replaces
+// the candidate copy kernel and five runtime D2H copies.  Every range starts 16-B aligned
+// on both sides (host_out_alloc, hipMalloc).
+constexpr int kOutCopies = 5;
+struct OutArgs {
+  const uint32_t* count;  // device candidate count
+  uint32_t cand_cap;
+  const uint8_t* cand;  // DevCand records
+  uint8_t* cand_host;
+  const uint8_t* src[kOutCopies];
+  uint8_t* dst[kOutCopies];
+  uint64_t n[kOutCopies];
+  uint32_t nc;
+};
+
+__device__ __forceinline__ void copy_range(uint8_t* __restrict__ d, const uint8_t* __restrict__ s, uint64_t n,
+                                           uint64_t tid, uint64_t nth) {
+  const uint64_t body = n / 16;
+  for (uint64_t i = tid; i < body; i += nth) ((uint4*)d)[i] = ((const uint4*)s)[i];
+  for (uint64_t i = body * 16 + tid; i < n; i += nth) d[i] = s[i];
+}
+
+__global__ void __launch_bounds__(256) outputs_kernel(OutArgs A) {
+  const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x, nth = (uint64_t)gridDim.x * blockDim.x;
+  copy_range(A.cand_host, A.cand, (uint64_t)min(*A.count, A.cand_cap) * 12u, tid, nth);
+  for (uint32_t c = 0; c < A.nc; c++) copy_range(A.dst[c], A.src[c], A.n[c], tid, nth);
 }
 
 // ---------------------------------------------------------------- Global.AllowPath
@@ -216,7 +285,7 @@ __device__ __forceinline__ uint32_t run_max(uint32_t a, uint32_t b) {
 struct K1Args {
   const uint8_t* data;
   const uint64_t* off;
-  const uint32_t* chunk_file;
+  const uint32_t* cf;  // coarse file map (file_of)
   uint64_t total, nchunks, nitems, item_step;
   uint32_t chunk, nfiles;
   uint32_t* kw;    // [nfiles * kw_words]
@@ -295,8 +364,7 @@ struct K1Lane {
     const uint32_t* m = s_masks + (size_t)s_accs[id] * d.mw;
     c.evl |= m[d.kw_words];
     if (q >= A.total) return;
-    uint32_t f = A.chunk_file[q / A.chunk];  // file holding the chunk's first byte
-    while (A.off[f + 1] <= q) f++;
+    const uint32_t f = file_of(A.cf, A.off, A.nfiles, q);
     const uint64_t avail = q - A.off[f] + 1;  // bytes of f up to and including q
     uint32_t* kwf = A.kw + (size_t)f * d.kw_words;
     for (uint32_t w = 0; w < d.kw_words; w++) {
@@ -648,7 +716,7 @@ struct DevK1X {
 struct K1XArgs {
   const uint8_t* data;
   const uint64_t* off;
-  const uint32_t* chunk_file;
+  const uint32_t* cf;  // coarse file map (file_of)
   uint64_t total;
   uint32_t chunk, nfiles;
   uint32_t* kw;
@@ -689,8 +757,7 @@ __device__ void k1x_verify_at(const DevK1X& x, const K1XArgs& A, uint64_t p, uin
         if (x.ev[i]) atomicOr(&A.ev[q / A.chunk], x.ev[i]);
         const int32_t k = x.kwid[i];
         if (k >= 0) {
-          uint32_t f = A.chunk_file[q / A.chunk];
-          while (A.off[f + 1] <= q) f++;
+          const uint32_t f = file_of(A.cf, A.off, A.nfiles, q);
           if (p >= A.off[f]) atomicOr(&A.kw[(size_t)f * x.kw_words + k / 32], 1u << (k % 32));
         }
       }
@@ -839,7 +906,7 @@ __global__ void ggate_kernel(const uint32_t* __restrict__ kw, uint32_t F, uint32
 
 struct ItemArgs {
   const uint64_t* off;
-  const uint32_t* chunk_file;
+  const uint32_t* cf;  // coarse file map (file_of)
   const uint32_t* ev;
   const uint32_t* evlist;           // chunks with event bits (ev_compact_kernel)
   const uint32_t* nev;              // [1] length of evlist
@@ -910,7 +977,7 @@ __device__ __forceinline__ void gen_items(const ItemArgs& A, uint64_t t, V visit
     const uint64_t e = A.evlist[t];
     const uint32_t evb = A.ev[e] & ~kEvAlways;
     const uint64_t ce = (e + 1) * C;
-    for (uint32_t f = A.chunk_file[e]; f < A.F && A.off[f] < ce; f++) {
+    for (uint32_t f = file_of(A.cf, A.off, A.F, e * C); f < A.F && A.off[f] < ce; f++) {
       const uint64_t fs = A.off[f], fe = A.off[f + 1];
       if (fe == fs) continue;
       const uint64_t fc0 = fs / C;
@@ -1115,9 +1182,9 @@ __global__ void __launch_bounds__(kLayoutBlock) layout_kernel(LayoutArgs A) {
 struct K2Args {
   const uint8_t* data;
   const uint64_t* off;
-  const uint32_t* chunk_file;
+  const uint32_t* cf;  // coarse file map (file_of)
   uint64_t total, nchunks;
-  uint32_t chunk, ext_cap;
+  uint32_t chunk, ext_cap, nfiles;
   const uint32_t* kw;
   uint32_t kw_words;
   const uint32_t* gmask;    // [G * kw_words] keyword gate of each group (dense entries)
@@ -1569,7 +1636,7 @@ __device__ __forceinline__ void k2_dense_entry(const DevDFA& d, const K2Args& A,
   if (c0 >= (uint64_t)en.y + en.z) return;
   uint64_t a = c0 * A.chunk;
   const uint64_t b = min((c0 + kStreams) * A.chunk, A.total);
-  uint32_t f = A.chunk_file[c0];
+  uint32_t f = file_of(A.cf, A.off, A.nfiles, a);
   {
     const uint64_t fs = A.off[f], fe = A.off[f + 1];
     if (b == a + (uint64_t)kStreams * A.chunk && a >= fs && b <= fe) {  // common case: one file
@@ -1657,13 +1724,6 @@ __global__ void __launch_bounds__(kBlock) K2_WAVES k2_kernel(const DevDFA* __res
 __global__ void __launch_bounds__(kBlock) k2_dense_kernel(const DevDFA* __restrict__ dfas, K2Args A) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   k2_run<true>(dfas, A, A.dentries, *A.ndentries, A.claim + 1, smem);
-}
-
-// the candidates of a batch to pinned, mapped host memory (their count is only known here)
-__global__ void cand_copy_kernel(const DevCand* __restrict__ src, const uint32_t* __restrict__ count, uint32_t cap,
-                                 DevCand* __restrict__ dst) {
-  const uint32_t n = min(*count, cap);
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) dst[i] = src[i];
 }
 
 // ---------------------------------------------------------------- host side
@@ -1987,10 +2047,13 @@ struct LaneState {
   hipStream_t st = nullptr;
   uint8_t* data_alloc = nullptr;  // kPad | batch | tail
   size_t data_cap = 0;
-  uint64_t* off = nullptr;
-  size_t off_cap = 0;
-  uint32_t* chunk_file = nullptr;
-  size_t chunk_cap = 0;
+  uint8_t* meta = nullptr;        // offsets | path offsets | paths (one H2D per batch)
+  size_t meta_cap = 0;
+  const uint64_t* off = nullptr;  // into meta (last batch)
+  const uint64_t* poff = nullptr;
+  const uint8_t* paths = nullptr;
+  uint32_t* cf = nullptr;         // coarse file map (file_of)
+  size_t cf_cap = 0;
   uint32_t* ev_bits = nullptr;
   size_t ev_cap = 0;
   uint2* xlist = nullptr;  // K1X hit records
@@ -2005,10 +2068,6 @@ struct LaneState {
   size_t ggate_cap = 0;
   uint8_t* ovf = nullptr;
   size_t ovf_cap = 0;
-  uint8_t* paths = nullptr;
-  size_t paths_cap = 0;
-  uint64_t* poff = nullptr;
-  size_t poff_cap = 0;
   uint8_t* pathok = nullptr;
   size_t pathok_cap = 0;
   uint2* items = nullptr;
@@ -2032,7 +2091,7 @@ struct LaneState {
     if (!d) return;
     (void)hipSetDevice(d->device);
     if (st) (void)hipStreamSynchronize(st);
-    void* bufs[] = {data_alloc, off, chunk_file, ev_bits, xlist, xcount, evlist, kw, ggate, ovf, paths, poff, pathok,
+    void* bufs[] = {data_alloc, meta, cf, ev_bits, xlist, xcount, evlist, kw, ggate, ovf, pathok,
                     items, entries, dentries, cand, counts, gcount, cursor, base, kind, gskip, etrace};
     for (void* b : bufs) (void)hipFree(b);
     if (st) (void)hipStreamDestroy(st);
@@ -2045,7 +2104,7 @@ static int ensure(T** p, size_t* cap, size_t n) {
   if (*p) HIP_TRY(hipFree(*p));  // (hipFree waits for the device)
   *p = nullptr;
   const size_t alloc = std::max<size_t>(n + n / 8, 16);
-  HIP_TRY(hipMalloc((void**)p, alloc * sizeof(T)));
+  HIP_TRY(hipMalloc((void**)p, (alloc * sizeof(T) + 15) & ~(size_t)15));
   *cap = alloc;
   return TSG_OK;
 }
@@ -2119,7 +2178,7 @@ static int adapt_k1(DeviceRules* r, LaneState* l, uint64_t total, uint32_t nfile
   const uint64_t step = std::max<uint64_t>(1, k1_items / 16384);
   const uint64_t nsamp = (k1_items + step - 1) / step;
   HIP_TRY(hipMemsetAsync(r->d_hits, 0, sizeof(uint32_t) * ns, l->st));
-  K1Args A{l->data_alloc + kPad, l->off, l->chunk_file, total, nchunks, nsamp, step, r->chunk,
+  K1Args A{l->data_alloc + kPad, l->off, l->cf, total, nchunks, nsamp, step, r->chunk,
            nfiles, l->kw, l->ev_bits, r->d_hits, k1_streams(), k1_seg()};
   int rc;
   if ((rc = launch_k1(r, A, l->st))) return rc;
@@ -2319,6 +2378,17 @@ int lane_create(DeviceRules* d, LaneState** out) {
 void lane_destroy(LaneState* l) { delete l; }
 hipStream_t lane_stream(LaneState* l) { return l->st; }
 
+static size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+void host_out_free(HostOut* o) {
+  void* ps[] = {o->blk, o->cand, o->meta};
+  for (void* p : ps)
+    if (p) (void)hipHostFree(p);
+  for (auto& e : o->ev)
+    if (e) (void)hipEventDestroy(e);
+  *o = HostOut{};
+}
+
 int host_out_alloc(const DeviceRules* d, uint32_t files_cap, HostOut* o) {
   HIP_TRY(hipSetDevice(d->device));
   HostOut h;
@@ -2326,26 +2396,30 @@ int host_out_alloc(const DeviceRules* d, uint32_t files_cap, HostOut* o) {
   h.cand_cap = 1u << 22;
   h.groups = std::max<uint32_t>(1, (uint32_t)d->groups.size());
   h.kw_words = (uint32_t)d->plan->kw_words;
-  HIP_TRY(hipHostMalloc((void**)&h.kw, sizeof(uint32_t) * (size_t)h.files_cap * h.kw_words, hipHostMallocDefault));
-  HIP_TRY(hipHostMalloc((void**)&h.ovf, h.files_cap, hipHostMallocDefault));
-  HIP_TRY(hipHostMalloc((void**)&h.pathok, h.files_cap, hipHostMallocDefault));
-  HIP_TRY(hipHostMalloc((void**)&h.gskip, h.groups, hipHostMallocDefault));
-  HIP_TRY(hipHostMalloc((void**)&h.cand, sizeof(Candidate) * (size_t)h.cand_cap, hipHostMallocMapped));
-  HIP_TRY(hipHostGetDevicePointer((void**)&h.cand_dev, h.cand, 0));
-  HIP_TRY(hipHostMalloc((void**)&h.counts, sizeof(uint32_t) * 16, hipHostMallocMapped));
-  HIP_TRY(hipHostGetDevicePointer((void**)&h.counts_dev, h.counts, 0));
-  for (auto& e : h.ev) HIP_TRY(hipEventCreate(&e));
+  // one host-mapped block for the small outputs (each part 256-B aligned): counts | gskip |
+  // ovf | pathok | kw
+  const size_t o_gskip = 256, o_ovf = o_gskip + al256(h.groups), o_path = o_ovf + al256(h.files_cap),
+               o_kw = o_path + al256(h.files_cap),
+               bytes = o_kw + al256(sizeof(uint32_t) * (size_t)h.files_cap * h.kw_words);
+  auto fail_free = [&](hipError_t e, const char* what) {
+    host_out_free(&h);
+    return fail(TSG_ERR_GPU, std::string(what) + ": " + hipGetErrorString(e));
+  };
+  hipError_t e;
+  if ((e = hipHostMalloc((void**)&h.blk, bytes, hipHostMallocMapped)) != hipSuccess) return fail_free(e, "hipHostMalloc");
+  if ((e = hipHostGetDevicePointer((void**)&h.blk_dev, h.blk, 0)) != hipSuccess) return fail_free(e, "hipHostGetDevicePointer");
+  h.counts = (uint32_t*)h.blk;
+  h.gskip = h.blk + o_gskip;
+  h.ovf = h.blk + o_ovf;
+  h.pathok = h.blk + o_path;
+  h.kw = (uint32_t*)(h.blk + o_kw);
+  if ((e = hipHostMalloc((void**)&h.cand, sizeof(Candidate) * (size_t)h.cand_cap, hipHostMallocMapped)) != hipSuccess)
+    return fail_free(e, "hipHostMalloc");
+  if ((e = hipHostGetDevicePointer((void**)&h.cand_dev, h.cand, 0)) != hipSuccess) return fail_free(e, "hipHostGetDevicePointer");
+  for (auto& ev : h.ev)
+    if ((e = hipEventCreate(&ev)) != hipSuccess) return fail_free(e, "hipEventCreate");
   *o = h;
   return TSG_OK;
-}
-
-void host_out_free(HostOut* o) {
-  void* ps[] = {o->kw, o->ovf, o->pathok, o->gskip, o->cand, o->counts};
-  for (void* p : ps)
-    if (p) (void)hipHostFree(p);
-  for (auto& e : o->ev)
-    if (e) (void)hipEventDestroy(e);
-  *o = HostOut{};
 }
 
 int enqueue_scan(DeviceRules* r, LaneState* l, const ScanInput& in, HostOut* out) {
@@ -2366,10 +2440,17 @@ int enqueue_scan(DeviceRules* r, LaneState* l, const ScanInput& in, HostOut* out
   const size_t tail = (size_t)kK1MaxStreams * kK1Seg * C + kPad;
   if ((rc = ensure(&l->data_alloc, &l->data_cap, (size_t)total + kPad + tail))) return rc;
   uint8_t* data = l->data_alloc + kPad;
-  if ((rc = ensure(&l->off, &l->off_cap, (size_t)F + 1))) return rc;
+  const bool paths_dev = r->has_pathdfa && F;
+  const uint64_t P = paths_dev ? in.poff[F] : 0;
+  const size_t meta_bytes = sizeof(uint64_t) * ((size_t)F + 1) * (paths_dev ? 2 : 1) + P;
+  if ((rc = ensure(&l->meta, &l->meta_cap, meta_bytes))) return rc;
+  l->off = (const uint64_t*)l->meta;
+  l->poff = l->off + F + 1;
+  l->paths = (const uint8_t*)(l->poff + F + 1);
   const uint64_t k1_item_chunks = (uint64_t)kK1MaxStreams * kK1Seg;
   const uint64_t nchunks_pad = (nchunks + k1_item_chunks - 1) / k1_item_chunks * k1_item_chunks + 1;
-  if ((rc = ensure(&l->chunk_file, &l->chunk_cap, (size_t)nchunks_pad))) return rc;
+  const uint64_t ncf = (total >> kCfShift) + 2;
+  if ((rc = ensure(&l->cf, &l->cf_cap, (size_t)ncf))) return rc;
   if ((rc = ensure(&l->ev_bits, &l->ev_cap, (size_t)nchunks_pad))) return rc;
   // K1X hit records: one per 256 bytes (a lane-word with a hit past that verifies inline)
   if (r->has_k1x && (rc = ensure(&l->xlist, &l->xlist_cap, (size_t)(total / 256 + 65536)))) return rc;
@@ -2378,6 +2459,7 @@ int enqueue_scan(DeviceRules* r, LaneState* l, const ScanInput& in, HostOut* out
   if ((rc = ensure(&l->kw, &l->kw_cap, (size_t)F * W + 1))) return rc;
   if ((rc = ensure(&l->ggate, &l->ggate_cap, (size_t)F * r->GW + 1))) return rc;
   if ((rc = ensure(&l->ovf, &l->ovf_cap, (size_t)F + 1))) return rc;
+  if ((rc = ensure(&l->pathok, &l->pathok_cap, (size_t)F + 1))) return rc;
   // item capacity: twice the batch's chunks (the builtin rules list ~11 % of them); over
   // it, groups are skipped (kGroupSkip) and resolved on the host, never dropped
   const uint64_t items_cap = std::max<uint64_t>(2 * nchunks, 1u << 16);
@@ -2392,42 +2474,62 @@ int enqueue_scan(DeviceRules* r, LaneState* l, const ScanInput& in, HostOut* out
     HIP_TRY(hipMalloc((void**)&l->cand, sizeof(DevCand) * (size_t)out->cand_cap));
     l->cand_cap = out->cand_cap;
   }
-  if (r->has_pathdfa && F) {
-    if ((rc = ensure(&l->paths, &l->paths_cap, (size_t)in.poff[F] + 1))) return rc;
-    if ((rc = ensure(&l->poff, &l->poff_cap, (size_t)F + 1))) return rc;
-    if ((rc = ensure(&l->pathok, &l->pathok_cap, (size_t)F))) return rc;
+  // ---- the batch's offsets, path offsets and paths side by side in pinned staging (the
+  // HostOut is this submission's alone until its job ends), for one H2D
+  if (out->meta_cap < meta_bytes) {
+    if (out->meta) HIP_TRY(hipHostFree(out->meta));
+    out->meta = nullptr;
+    out->meta_cap = 0;
+    const size_t cap = std::max<size_t>(meta_bytes + meta_bytes / 8, 1 << 20);
+    HIP_TRY(hipHostMalloc((void**)&out->meta, cap, hipHostMallocDefault));
+    out->meta_cap = cap;
+  }
+  std::memcpy(out->meta, in.off, sizeof(uint64_t) * ((size_t)F + 1));
+  if (paths_dev) {
+    std::memcpy(out->meta + sizeof(uint64_t) * ((size_t)F + 1), in.poff, sizeof(uint64_t) * ((size_t)F + 1));
+    if (P) std::memcpy(out->meta + sizeof(uint64_t) * 2 * ((size_t)F + 1), in.paths, P);
   }
 
-  // ---- H2D from the pinned slot
+  // ---- H2D from the pinned slot: the batch, then its metadata (two runtime copies)
   HIP_TRY(hipEventRecord(out->ev[0], st));
-  HIP_TRY(hipMemsetAsync(l->data_alloc, 0, kPad, st));
   if (total) HIP_TRY(hipMemcpyAsync(data, in.data, total, hipMemcpyHostToDevice, st));
-  HIP_TRY(hipMemsetAsync(data + total, 0, tail, st));
-  HIP_TRY(hipMemcpyAsync(l->off, in.off, sizeof(uint64_t) * (F + 1), hipMemcpyHostToDevice, st));
-  if (r->has_pathdfa && F) {
-    if (in.poff[F]) HIP_TRY(hipMemcpyAsync(l->paths, in.paths, in.poff[F], hipMemcpyHostToDevice, st));
-    HIP_TRY(hipMemcpyAsync(l->poff, in.poff, sizeof(uint64_t) * (F + 1), hipMemcpyHostToDevice, st));
-  }
-  if (F) {
-    chunk_file_kernel<<<(uint32_t)((nchunks_pad + 255) / 256), 256, 0, st>>>(l->off, F, C, nchunks_pad, l->chunk_file);
-    HIP_TRY(hipGetLastError());
-    HIP_TRY(hipMemsetAsync(l->kw, 0, sizeof(uint32_t) * (size_t)F * W, st));
-    HIP_TRY(hipMemsetAsync(l->ovf, 0, F, st));
-  }
-  HIP_TRY(hipMemsetAsync(l->counts, 0, sizeof(uint32_t) * 16, st));
-  if (G) {
-    HIP_TRY(hipMemsetAsync(l->gcount, 0, sizeof(uint32_t) * G, st));
-    HIP_TRY(hipMemsetAsync(l->cursor, 0, sizeof(uint32_t) * G, st));
-    HIP_TRY(hipMemsetAsync(l->gskip, 0, G, st));
-    HIP_TRY(hipMemsetAsync(l->kind, 0, G, st));
-  }
-
   HIP_TRY(hipEventRecord(out->ev[1], st));
+  HIP_TRY(hipMemcpyAsync(l->meta, out->meta, meta_bytes, hipMemcpyHostToDevice, st));
+  HIP_TRY(hipEventRecord(out->ev[2], st));
   // the kernels of consecutive batches run one after the other (each has the whole chip;
   // their HIP-event times are the kernels' own), while this lane's H2D above overlapped
   // the previous batch's kernels on the other lane
   if (r->kernels_done_valid) HIP_TRY(hipStreamWaitEvent(st, r->kernels_done, 0));
-  HIP_TRY(hipEventRecord(out->ev[2], st));
+  HIP_TRY(hipEventRecord(out->ev[3], st));
+
+  // ---- prep: zero fills and the coarse file map, one kernel
+  {
+    PrepArgs PA{};
+    PA.off = l->off;
+    PA.nfiles = F;
+    PA.ncf = F ? ncf : 0;
+    PA.cf = l->cf;
+    auto zero = [&](void* ptr, uint64_t n) {
+      if (n) {
+        PA.zp[PA.nz] = (uint8_t*)ptr;
+        PA.zn[PA.nz++] = n;
+      }
+    };
+    zero(l->data_alloc, kPad);
+    zero(data + total, tail);
+    zero(l->kw, sizeof(uint32_t) * (uint64_t)F * W);
+    zero(l->ovf, F);
+    zero(l->counts, sizeof(uint32_t) * 16);
+    zero(l->gcount, sizeof(uint32_t) * G);
+    zero(l->cursor, sizeof(uint32_t) * G);
+    zero(l->gskip, G);
+    zero(l->kind, G);
+    const uint64_t work = std::max<uint64_t>({PA.ncf, (uint64_t)F * W / 4, tail / 16, 1});
+    const int pgrid = (int)std::min<uint64_t>((work + 255) / 256, (uint64_t)r->grid);
+    prep_kernel<<<pgrid, 256, 0, st>>>(PA);
+    HIP_TRY(hipGetLastError());
+  }
+  HIP_TRY(hipEventRecord(out->ev[4], st));
 
   // ---- K1
   const uint32_t k1s = k1_streams();
@@ -2436,26 +2538,26 @@ int enqueue_scan(DeviceRules* r, LaneState* l, const ScanInput& in, HostOut* out
   if (!r->adapted && k1_items >= 64 && total >= adapt_bytes)
     if ((rc = adapt_k1(r, l, total, F, nchunks, k1_items))) return rc;
   if (k1_items) {
-    K1Args A{data, l->off, l->chunk_file, total, nchunks, k1_items, 1, C, F, l->kw, l->ev_bits, nullptr, k1s,
+    K1Args A{data, l->off, l->cf, total, nchunks, k1_items, 1, C, F, l->kw, l->ev_bits, nullptr, k1s,
              k1_seg()};
     if ((rc = launch_k1(r, A, st))) return rc;
   }
   if (r->has_k1x && total) {  // the hashed literals of a large rule set, after K1's stores
     const int xg = (int)std::max<uint64_t>(1, std::min<uint64_t>((total / 16 + kK1XBlock - 1) / kK1XBlock,
                                                                    (uint64_t)r->cus));
-    K1XArgs X{data, l->off, l->chunk_file, total, C, F, l->kw, l->ev_bits, l->xlist, l->xcount,
+    K1XArgs X{data, l->off, l->cf, total, C, F, l->kw, l->ev_bits, l->xlist, l->xcount,
               (uint32_t)std::min<size_t>(l->xlist_cap, 0xFFFFFFFFu)};
     k1x_kernel<<<xg, kK1XBlock, (1u << kXBits) / 8 + 16, st>>>(r->k1x, X);
     HIP_TRY(hipGetLastError());
     k1x_verify_kernel<<<r->grid, kBlock, 0, st>>>(r->k1x, X, (uint32_t)xg);
     HIP_TRY(hipGetLastError());
   }
-  HIP_TRY(hipEventRecord(out->ev[3], st));
+  HIP_TRY(hipEventRecord(out->ev[5], st));
 
   // ---- gates, items, device-side layout
   ItemArgs IA{};
   IA.off = l->off;
-  IA.chunk_file = l->chunk_file;
+  IA.cf = l->cf;
   IA.ev = l->ev_bits;
   IA.ggate = l->ggate;
   IA.gofbit = r->d_gofbit;
@@ -2475,7 +2577,7 @@ int enqueue_scan(DeviceRules* r, LaneState* l, const ScanInput& in, HostOut* out
   IA.base = l->base;
   IA.items = l->items;
   const bool work = F && G && nchunks;
-  if (r->has_pathdfa && F) {
+  if (paths_dev) {
     path_allow_kernel<<<(F + 255) / 256, 256, 0, st>>>(r->pathdfa, l->paths, l->poff, F, l->pathok);
     HIP_TRY(hipGetLastError());
   }
@@ -2495,18 +2597,19 @@ int enqueue_scan(DeviceRules* r, LaneState* l, const ScanInput& in, HostOut* out
     hipLaunchKernelGGL(items_emit_kernel, dim3(igrid), dim3(kBlock), 2 * G * sizeof(uint32_t) + 16, st, IA);
     HIP_TRY(hipGetLastError());
   }
-  HIP_TRY(hipEventRecord(out->ev[4], st));
+  HIP_TRY(hipEventRecord(out->ev[6], st));
 
   // ---- K2 over the work list
   if (work) {
     K2Args A{};
     A.data = data;
     A.off = l->off;
-    A.chunk_file = l->chunk_file;
+    A.cf = l->cf;
     A.total = total;
     A.nchunks = nchunks;
     A.chunk = C;
     A.ext_cap = r->ext_cap;
+    A.nfiles = F;
     A.kw = l->kw;
     A.kw_words = W;
     A.gmask = r->d_gmask;
@@ -2536,33 +2639,47 @@ int enqueue_scan(DeviceRules* r, LaneState* l, const ScanInput& in, HostOut* out
                        (const DevDFA*)r->d_groups, A);
     HIP_TRY(hipGetLastError());
   }
-  HIP_TRY(hipEventRecord(out->ev[5], st));
+  HIP_TRY(hipEventRecord(out->ev[7], st));
   HIP_TRY(hipEventRecord(r->kernels_done, st));
   r->kernels_done_valid = true;
 
-  // ---- results to the pinned host buffers
-  cand_copy_kernel<<<64, 256, 0, st>>>(l->cand, l->counts, out->cand_cap, (DevCand*)out->cand_dev);
-  HIP_TRY(hipGetLastError());
-  HIP_TRY(hipMemcpyAsync(out->counts, l->counts, sizeof(uint32_t) * 16, hipMemcpyDeviceToHost, st));
-  if (F) {
-    HIP_TRY(hipMemcpyAsync(out->kw, l->kw, sizeof(uint32_t) * (size_t)F * W, hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipMemcpyAsync(out->ovf, l->ovf, F, hipMemcpyDeviceToHost, st));
-    if (r->has_pathdfa) HIP_TRY(hipMemcpyAsync(out->pathok, l->pathok, F, hipMemcpyDeviceToHost, st));
+  // ---- outputs straight into the pinned, host-mapped block (no runtime copies)
+  {
+    OutArgs OA{};
+    OA.count = l->counts;
+    OA.cand_cap = out->cand_cap;
+    OA.cand = (const uint8_t*)l->cand;
+    OA.cand_host = (uint8_t*)out->cand_dev;
+    auto copy = [&](void* host, const void* dev, uint64_t n) {
+      if (n) {
+        OA.dst[OA.nc] = out->blk_dev + ((uint8_t*)host - out->blk);
+        OA.src[OA.nc] = (const uint8_t*)dev;
+        OA.n[OA.nc++] = n;
+      }
+    };
+    copy(out->counts, l->counts, sizeof(uint32_t) * 16);
+    copy(out->kw, l->kw, sizeof(uint32_t) * (uint64_t)F * W);
+    copy(out->ovf, l->ovf, F);
+    if (paths_dev) copy(out->pathok, l->pathok, F);
+    copy(out->gskip, l->gskip, G);
+    outputs_kernel<<<128, 256, 0, st>>>(OA);
+    HIP_TRY(hipGetLastError());
   }
-  if (G) HIP_TRY(hipMemcpyAsync(out->gskip, l->gskip, G, hipMemcpyDeviceToHost, st));
   HIP_TRY(hipEventRecord(out->ev[kEvDone], st));
   return TSG_OK;
 }
 
 int batch_times(const HostOut* o, ScanTimes* t) {
-  float x[6] = {0, 0, 0, 0, 0, 0};
-  for (int k = 0; k < 6; k++) HIP_TRY(hipEventElapsedTime(&x[k], o->ev[k], o->ev[k + 1]));
+  float x[kEvDone] = {};
+  for (int k = 0; k < kEvDone; k++) HIP_TRY(hipEventElapsedTime(&x[k], o->ev[k], o->ev[k + 1]));
   t->h2d = x[0];
-  t->wait = x[1];
-  t->k1 = x[2];
-  t->gates = x[3];
-  t->k2 = x[4];
-  t->d2h = x[5];
+  t->meta = x[1];
+  t->wait = x[2];
+  t->prep = x[3];
+  t->k1 = x[4];
+  t->gates = x[5];
+  t->k2 = x[6];
+  t->out = x[7];
   return TSG_OK;
 }
 

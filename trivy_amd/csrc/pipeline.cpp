@@ -257,7 +257,9 @@ void update_stats(tsg_ctx* c, const Batch& b) {
   s.k2_ms = b.t.k2;
   s.gate_ms = b.t.gates;
   s.h2d_ms = b.t.h2d;
-  s.aux_ms = b.t.d2h;
+  s.aux_ms = b.t.out;
+  s.prep_ms = b.t.prep;
+  s.meta_ms = b.t.meta;
   s.resolve_ms = b.resolve_ms;
   s.bytes = b.bytes;
   s.candidates = b.counts[0];
@@ -279,7 +281,9 @@ void update_stats(tsg_ctx* c, const Batch& b) {
   s.sum_gate_ms += b.t.gates;
   s.sum_k2_ms += b.t.k2;
   s.sum_h2d_ms += b.t.h2d;
-  s.sum_d2h_ms += b.t.d2h;
+  s.sum_d2h_ms += b.t.out;
+  s.sum_prep_ms += b.t.prep;
+  s.sum_meta_ms += b.t.meta;
   s.sum_resolve_ms += b.resolve_ms;
 }
 

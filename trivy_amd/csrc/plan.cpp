@@ -1119,7 +1119,10 @@ void resolve_batch(const Ruleset& rs, const Plan& plan, const BatchView& b,
         if (any) {
           const uint64_t td = prof ? __rdtsc() : 0;
           const int64_t q0 = fold.front(), q1 = fold.back();
-          run_segment(fd, content, 0, (uint64_t)n, 0, (uint64_t)std::min<int64_t>(n, q1 + 1), ~0u,
+          // (true: the tail past the last rune reached a state whose threads never die,
+          // e.g. a (?s).* rule, and stopped there: its later ends are unknown, so every
+          // wanted rule is resolved over the whole file instead)
+          const bool cut = run_segment(fd, content, 0, (uint64_t)n, 0, (uint64_t)std::min<int64_t>(n, q1 + 1), ~0u,
                       [&](uint32_t mi, uint64_t pos) {
                         if ((int64_t)pos < q0) return;
                         const auto& m = fd.masks[mi];
@@ -1133,7 +1136,12 @@ void resolve_batch(const Ruleset& rs, const Plan& plan, const BatchView& b,
               const uint32_t r = plan.fold_rules[k];
               done[r] = 1;
               wptr[r] = &wins[r];
-              normalize(wins[r]);
+              if (cut) {
+                wins[r].whole = true;
+                wins[r].iv.clear();
+              } else {
+                normalize(wins[r]);
+              }
             }
         }
       }

@@ -395,6 +395,7 @@ class GpuContext:
                  host_threads=0, adapt_mib=0, emulate=False, slot_mib=0, max_slots=0):
         import threading
         self._h = None
+        self._owned = True
         self.scanner = scanner
         self.chunk = chunk_bytes or 256
         opt = N.CtxOptions(chunk_bytes, ext_cap, cand_capacity, host_threads, adapt_mib,
@@ -407,6 +408,23 @@ class GpuContext:
         self._lock = threading.Lock()
         self._fifo = []         # (ticket, paths) of this object's uncollected submissions
         self._paths = {}        # ticket -> paths
+
+    @classmethod
+    def borrowed(cls, scanner, handle, chunk_bytes=0):
+        """A view of a context owned elsewhere (a device of a MultiGpu): same methods, and
+        close() leaves the context itself alone."""
+        import threading
+        self = cls.__new__(cls)
+        self._h = handle
+        self._owned = False
+        self.scanner = scanner
+        self.chunk = chunk_bytes or 256
+        self._upload = None
+        self._k1 = None
+        self._lock = threading.Lock()
+        self._fifo = []
+        self._paths = {}
+        return self
 
     @property
     def handle(self):
@@ -531,7 +549,8 @@ class GpuContext:
             if self._upload is not None:
                 N.lib().tsg_slot_release(self._h, self._upload[0])
                 self._upload = None
-            N.lib().tsg_ctx_destroy(self._h)
+            if self._owned:
+                N.lib().tsg_ctx_destroy(self._h)
             self._h = None
 
     def __del__(self):
@@ -543,10 +562,12 @@ class MultiGpu:
     node's GPUs, pkg/fanal/artifact/image/image.go:210-234).  scan_batch() shards a batch's
     files LPT by bytes over the devices and returns the results in input order."""
 
-    def __init__(self, scanner, devices, slot_mib=0, host_threads=0, emulate=False, max_slots=0):
+    def __init__(self, scanner, devices, slot_mib=0, host_threads=0, emulate=False, max_slots=0,
+                 chunk_bytes=0):
         self._h = None
         self.scanner = scanner
-        opt = N.CtxOptions(0, 0, 0, host_threads, 0, N.TSG_CTX_EMULATE if emulate else 0,
+        self.chunk = chunk_bytes or 256
+        opt = N.CtxOptions(chunk_bytes, 0, 0, host_threads, 0, N.TSG_CTX_EMULATE if emulate else 0,
                            slot_mib, max_slots)
         devs = (C.c_int * len(devices))(*[int(d) for d in devices])
         h = C.c_void_p()
@@ -559,6 +580,12 @@ class MultiGpu:
         out = C.c_void_p()
         N.check(N.lib().tsg_multi_scan_batch(self._h, *batch.ptrs(), C.byref(out)))
         return self.scanner.decode(out, GpuContext._paths_of(batch))
+
+    def context(self, i):
+        """The i-th device's context (owned by this object) as a GpuContext view."""
+        h = C.c_void_p()
+        N.check(N.lib().tsg_multi_ctx(self._h, int(i), C.byref(h)))
+        return GpuContext.borrowed(self.scanner, h, self.chunk)
 
     def stats(self, i):
         s = N.Stats()
