@@ -351,6 +351,9 @@ def main():
                          "(Required, IsBinary), packs straight into a pinned slot and scans")
     ap.add_argument("--e2e-mib", type=int, default=0, help="e2e input size (default fs 200, layer 2048)")
     ap.add_argument("--e2e-slot-mib", type=int, default=0, help="e2e piece / slot size (0: 256)")
+    ap.add_argument("--piece-mib", type=int, default=0,
+                    help="e2e: piece floor of tsg_fs_scan / tsg_layer_scan (the 'piece_mib' test knob; "
+                         "0: the library's 160)")
     args = ap.parse_args()
     if args.e2e:
         return main_e2e(args)
@@ -588,6 +591,8 @@ def main_e2e(args):
     from trivy_amd import secret as S
     from trivy_amd import walker as W
     L = N.lib()
+    if args.piece_mib:
+        N.knob("piece_mib", args.piece_mib)
     an = A.SecretAnalyzer()
     an.Init("")
     sc = an.scanner

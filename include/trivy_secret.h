@@ -284,6 +284,23 @@ void tsg_multi_destroy(tsg_multi* m);
 
 const char* tsg_last_error(void);
 
+/* ---- test and measurement knobs ----
+ * Process-wide switches that change how (never what) the library computes, for tests and
+ * measurements only.  They are set through this call alone: the library reads no
+ * environment variable that changes a plan, a kernel or a result (the profiling switches
+ * TSG_PROF, TSG_PROF2, TSG_LAYER_PROF, TSG_K2_DIAG, TSG_K2_TRACE and TSG_DEBUG_RESOLVE only
+ * add timings, counters or traces).  value NULL or "" resets the knob.
+ *   "tar_range_kib"   sub-range floor of the parallel tar index walk (default 64 MiB)
+ *   "piece_mib"       piece floor of tsg_layer_scan / tsg_fs_scan (default 160)
+ *   "pike_only"       "1": the Go-regexp matcher uses the Pike VM alone (no backtracker)
+ *   "no_k1x"          "1": a rule set too large for K1's automaton is not split onto K1X
+ *   "emu_wordrec"     "1": emulated K2 writes one record per accepting 16-B word, as the
+ *                     kernel does (tsg_scan_batch_emulated, TSG_CTX_EMULATE contexts)
+ *   "emu_kw_unknown"  comma-separated keywords the emulated K1 leaves to the host, as
+ *                     after its adaptation (tsg_scan_batch_emulated)
+ * Returns TSG_ERR_ARG for an unknown name. */
+int tsg_test_knob(const char* name, const char* value);
+
 /* ---- test hooks: the Go-regexp engine and the DFA builder in isolation ---- */
 typedef struct tsg_regex tsg_regex;
 int tsg_regex_compile(const char* src, tsg_regex** out, char* err, size_t err_len);

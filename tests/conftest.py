@@ -18,3 +18,17 @@ def pytest_configure(config):
 @pytest.fixture(scope="session")
 def golden_dir():
     return GOLDEN
+
+
+@pytest.fixture
+def knob():
+    """Set library test knobs (tsg_test_knob) for one test; every one is reset afterwards."""
+    from trivy_amd import _native as N
+    names = []
+
+    def set_(name, value):
+        N.knob(name, value)
+        names.append(name)
+    yield set_
+    for n in names:
+        N.knob(n, None)

@@ -58,14 +58,14 @@ def test_fold_runes_exact_vs_oracle(builtin):
 
 
 @pytest.mark.parametrize("unknown", ["key,secret,token", "api,pass,access"])
-def test_unknown_keywords_exact_gate(builtin, unknown, monkeypatch):
+def test_unknown_keywords_exact_gate(builtin, unknown, knob):
     """After K1 adaptation frequent keywords are not reported; their gates are decided on
     the host with the ASCII case-folded search (no bytes.ToLower of the file) unless the
     file holds U+0130/U+212A.  Emulated here by clearing those keyword bits."""
-    monkeypatch.setenv("TSG_EMU_KW_UNKNOWN", unknown)
+    knob("emu_kw_unknown", unknown)
     batch = fold_corpus(4, nbytes=1 << 20, plants=300, frac=0.2)
     got = builtin.ScanBatch(batch, emulate_chunk=64)
-    monkeypatch.delenv("TSG_EMU_KW_UNKNOWN")
+    knob("emu_kw_unknown", None)
     assert got == builtin.ScanBatch(batch, nthreads=8)
 
 
@@ -118,12 +118,12 @@ def test_fold_runes_unbounded_rules_emulated_vs_exact(builtin, chunk):
 
 
 @pytest.mark.parametrize("chunk", [64, 256])
-def test_word_records_emulated_vs_exact(builtin, chunk, monkeypatch):
+def test_word_records_emulated_vs_exact(builtin, chunk, knob):
     """K2's word records (kernels.hip Lane::accept_word: one record per accepting 16-B word,
-    in the chunk and in the tail) as the emulation writes them (TSG_EMU_WORDREC): the host's
+    in the chunk and in the tail) as the emulation writes them ("emu_wordrec" knob): the host's
     replay and expansion of each word (plan.cpp resolve_batch) gives the exact results, on
     the seeded corpus, on fold-rune files and on accept-dense long tokens."""
-    monkeypatch.setenv("TSG_EMU_WORDREC", "1")
+    knob("emu_wordrec", 1)
     batch, _ = corpus.make_corpus(3 << 20, seed=70 + chunk, plants_per_mib=60)
     assert builtin.ScanBatch(batch, emulate_chunk=chunk) == builtin.ScanBatch(batch, nthreads=8)
     fb = fold_corpus(5)

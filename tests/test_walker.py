@@ -288,7 +288,7 @@ def test_native_layer_malformed_pax(analyzer):
 
 
 @pytest.mark.parametrize("range_kib", [1, 3, 17, 1 << 20])
-def test_native_layer_parallel_index_matches_sequential(analyzer, monkeypatch, range_kib):
+def test_native_layer_parallel_index_matches_sequential(analyzer, knob, range_kib):
     """The speculative parallel tar index (ranges walked from the first plausible header,
     stitched to the true chain) gives exactly the sequential walk: PAX / GNU long-name
     groups straddling range borders, and members whose data holds tar headers (a tar
@@ -304,9 +304,9 @@ def test_native_layer_parallel_index_matches_sequential(analyzer, monkeypatch, r
             if i % 9 == 0:
                 _reg(tf, "nested/layer%d.tar.txt" % i, inner)  # headers inside file data
     tar = buf.getvalue()
-    monkeypatch.delenv("TSG_TAR_RANGE_KIB", raising=False)
+    knob("tar_range_kib", None)
     seq = W.NativeLayer(analyzer.scanner, tar)
-    monkeypatch.setenv("TSG_TAR_RANGE_KIB", str(range_kib))
+    knob("tar_range_kib", range_kib)
     par = W.NativeLayer(analyzer.scanner, tar)
     b1, b2 = seq.batch, par.batch
     assert b1.nfiles == b2.nfiles >= 60 and par.walked == seq.walked
@@ -319,9 +319,9 @@ def test_native_layer_parallel_index_matches_sequential(analyzer, monkeypatch, r
         except Exception as e:
             return ("error", str(e))
     for cut in (len(tar) // 2, len(tar) // 2 + 100, len(tar) // 3 + 700, len(tar) - 700):
-        monkeypatch.delenv("TSG_TAR_RANGE_KIB")
+        knob("tar_range_kib", None)
         want = outcome(tar[:cut])
-        monkeypatch.setenv("TSG_TAR_RANGE_KIB", str(range_kib))
+        knob("tar_range_kib", range_kib)
         assert outcome(tar[:cut]) == want, cut
 
 
@@ -442,25 +442,25 @@ def test_layer_ranges_errors(analyzer):
 
 @pytest.mark.parametrize("range_kib", [1, 7])
 @pytest.mark.parametrize("world", [2, 3])
-def test_layer_ranges_with_parallel_subranges(analyzer, monkeypatch, range_kib, world):
+def test_layer_ranges_with_parallel_subranges(analyzer, knob, range_kib, world):
     """Each rank's range is itself walked in speculative parallel sub-ranges (walk_par)."""
     tar = _nested_tar()
-    monkeypatch.delenv("TSG_TAR_RANGE_KIB", raising=False)
+    knob("tar_range_kib", None)
     whole = W.NativeLayer(analyzer.scanner, tar)
     wb = whole.batch
-    monkeypatch.setenv("TSG_TAR_RANGE_KIB", str(range_kib))
+    knob("tar_range_kib", range_kib)
     paths, blobs, walked, opq, wh = _union(W.pack_layer_ranges(analyzer.scanner, tar, world))
     assert paths == [wb.path(i) for i in range(wb.nfiles)]
     assert blobs == [bytes(wb.data[int(wb.offsets[i]):int(wb.offsets[i + 1])]) for i in range(wb.nfiles)]
     assert (walked, opq, wh) == (whole.walked, whole.opq, whole.wh)
     for cut in (len(tar) // 2 + 100, len(tar) - 700):
-        monkeypatch.delenv("TSG_TAR_RANGE_KIB")
+        knob("tar_range_kib", None)
         try:
             W.NativeLayer(analyzer.scanner, tar[:cut])
             want = "ok"
         except Exception:
             want = "error"
-        monkeypatch.setenv("TSG_TAR_RANGE_KIB", str(range_kib))
+        knob("tar_range_kib", range_kib)
         try:
             W.pack_layer_ranges(analyzer.scanner, tar[:cut], world)
             got = "ok"

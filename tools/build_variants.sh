@@ -1,5 +1,5 @@
-# Build measurement variants of libtrivy_secret.so: the same sources with other K1
-# compile-time settings (select one with TSG_LIB_VARIANT=<name>, e.g. tools/gpu_sweep.sh).
+# Build measurement variants of libtrivy_secret.so: the same sources with other compile-time
+# settings (select one with TSG_LIB_VARIANT=<name>).  Every variant computes the same results.
 #   usage: tools/build_variants.sh NAME...
 set -e
 cd "$(dirname "$0")/.."
@@ -14,25 +14,12 @@ build() {
 }
 for v in "$@"; do
   case $v in
-    ob4w4) build $v -DK1_UNROLL=4 ;;
-    nolds) build $v -DK1_EXP_NO_CLS -DK1_EXP_NO_TAB ;;
-    noruns) build $v -DK1_EXP_NO_RUNS ;;
-    nocls) build $v -DK1_EXP_NO_CLS ;;
-    notab) build $v -DK1_EXP_NO_TAB ;;
-    k2ctr) build $v -DK2_TRACE_CTR ;;
-    coal) build $v -DK1_EXP_COAL ;;
-    clspf8) build $v -DK1_CLSPF=8 ;;
-    clspf8_ip) build $v -DK1_CLSPF=8 -DK1_INPLACE ;;
-    clspf4) build $v -DK1_CLSPF=4 ;;
-    clspf4_ip) build $v -DK1_CLSPF=4 -DK1_INPLACE ;;
-    inplace) build $v -DK1_INPLACE ;;
-    u4) build $v -DK1_UNROLL=4 ;;
-    k2twobuf) build $v -DK2_TWOBUF ;;
-    x1) build $v -DK1X_WORDS=1 ;;
+    g2) build $v -DK1_GROUP=2 ;;         # K1: class reads of 2 / 8 / 16 bytes in flight
+    g8) build $v -DK1_GROUP=8 ;;
+    g16) build $v -DK1_GROUP=16 ;;
+    k2ctr) build $v -DK2_TRACE_CTR ;;    # K2: per-entry counters (TSG_K2_TRACE)
+    k2noinl) build $v -DK2_NOINL ;;      # K2: rare paths out of line
+    x1) build $v -DK1X_WORDS=1 ;;        # K1X: words per lane per round
     x8) build $v -DK1X_WORDS=8 ;;
-    nostep) build $v -DK1_EXP_NOSTEP ;;
-    noload) build $v -DK1_EXP_NOLOAD ;;
-    noload_nolds) build $v -DK1_EXP_NOLOAD -DK1_EXP_NO_CLS -DK1_EXP_NO_TAB ;;
-    nolds_coal) build $v -DK1_EXP_NO_CLS -DK1_EXP_NO_TAB -DK1_EXP_COAL ;;
   esac
 done

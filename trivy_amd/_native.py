@@ -127,6 +127,7 @@ SIGNATURES = [
     ("tsg_multi_get_stats", C.c_int, [_P, C.c_uint32, C.POINTER(Stats)]),
     ("tsg_multi_destroy", None, [_P]),
     ("tsg_last_error", C.c_char_p, []),
+    ("tsg_test_knob", C.c_int, [C.c_char_p, C.c_char_p]),
     ("tsg_regex_compile", C.c_int, [C.c_char_p, C.POINTER(_P), C.c_char_p, C.c_size_t]),
     ("tsg_regex_free", None, [_P]),
     ("tsg_regex_num_slots", C.c_int, [_P]),
@@ -207,6 +208,11 @@ class NativeError(RuntimeError):
     def __init__(self, code, msg):
         super().__init__("%s (code %d)" % (msg, code))
         self.code = code
+
+
+def knob(name, value=None):
+    """tsg_test_knob: set (value) or reset (None) a process-wide test / measurement knob."""
+    check(lib().tsg_test_knob(name.encode(), None if value is None else str(value).encode()))
 
 
 def check(rc):

@@ -211,7 +211,8 @@ int tsg_scan_batch_emulated(const tsg_ruleset* rs, const uint8_t* data, const ui
     KernelOutput ko;
     auto t0 = std::chrono::steady_clock::now();
     emulate_kernels(*rs->plan, b, chunk, 1u << 16, &ko);
-    if (const char* u = getenv("TSG_EMU_KW_UNKNOWN")) {
+    const std::string u = knob_kw_unknown();
+    if (!u.empty()) {
       // test hook: as after K1 adaptation, these keywords' bits are not reported and their
       // gates are checked exactly on the host
       const Plan& p = *rs->plan;

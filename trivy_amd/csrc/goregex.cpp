@@ -1,5 +1,6 @@
 // Go 1.19 regexp dialect: parser, compiler and Pike VM.  See goregex.hpp.
 #include "goregex.hpp"
+#include "internal.hpp"
 
 #include <algorithm>
 #include <cstdlib>
@@ -1632,7 +1633,7 @@ struct TwoPass {
       : whole(p, 2), sub(p, submatch_ ? p.nslots : 2), bt(p, submatch_ ? p.nslots : 2), submatch(submatch_),
         nslots(p.nslots), engine(engine_) {}
   bool run(const uint8_t* b, size_t n, int64_t pos, int64_t start_hi) {
-    if (engine != 1 && bt.fits(n, pos) && !(engine == 0 && getenv_pike())) {
+    if (engine != 1 && bt.fits(n, pos) && !(engine == 0 && pike_only())) {
       mode = 2;
       return bt.run(b, n, pos, start_hi);
     }
@@ -1647,8 +1648,8 @@ struct TwoPass {
   const std::vector<int64_t>& matchcap() const {
     return mode == 2 ? bt.matchcap() : mode == 1 ? sub.matchcap() : whole.matchcap();
   }
-  static bool getenv_pike() {
-    static const bool v = getenv("TSG_PIKE_ONLY") != nullptr;  // tests: the Pike VM alone
+  static bool pike_only() {
+    const bool v = knobs().pike_only.load() != 0;  // tests: the Pike VM alone ("pike_only" knob)
     return v;
   }
 };

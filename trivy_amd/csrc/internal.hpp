@@ -1,6 +1,9 @@
 // Shared internals of the C ABI (capi.cpp, gpu.hip).
 #pragma once
+#include <atomic>
+#include <cstdint>
 #include <memory>
+#include <mutex>
 #include <string>
 
 #include "../../include/trivy_secret.h"
@@ -23,4 +26,13 @@ int fail(int code, const std::string& msg);
 const tsg_ruleset* ctx_ruleset(const tsg_ctx* c);
 // bytes of a default pinned slot (tsg_ctx_options.slot_mib)
 uint64_t ctx_slot_bytes(const tsg_ctx* c);
+
+// test and measurement knobs (knobs.cpp, tsg_test_knob); 0 = default
+struct Knobs {
+  std::atomic<int64_t> tar_range_kib{0}, piece_mib{0}, pike_only{0}, no_k1x{0}, emu_wordrec{0};
+  std::mutex m;
+  std::string emu_kw_unknown;
+};
+Knobs& knobs();
+std::string knob_kw_unknown();
 }  // namespace tsg

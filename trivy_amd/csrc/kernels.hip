@@ -48,44 +48,18 @@ enum : uint8_t { kGroupNone = 0, kGroupList = 1, kGroupDense = 2, kGroupSkip = 3
       return fail(TSG_ERR_GPU, std::string(#x) + ": " + hipGetErrorString(e_));       \
   } while (0)
 
-// K1 registers: one 64-B block per chain, stepped in place and then reloaded, with the byte
-// loop unrolled 8 ways keeps a lane at 100 VGPRs: 4 waves per SIMD hide the dependent LDS
-// chain (2.1 -> 2.5 TB/s against two blocks in flight, 16-way unroll and 206 VGPRs at 2
-// waves per SIMD, profiles/r02/k1_experiments/occupancy_sweep.txt; in place instead of a
-// copy of the block: 0.400 -> 0.385 ms per GiB, profiles/r03/k1).  K1_ONEBUF / K1_TWOBUF
-// restore the older layouts.
-#ifndef K1_UNROLL
-#define K1_UNROLL 8
-#endif
-#if !defined(K1_TWOBUF) && !defined(K1_ONEBUF)
-#define K1_INPLACE  // one 64-B block per chain, stepped in place then reloaded (100 VGPRs)
-#endif
-#ifdef K1_EXP_COAL  // timing experiment only (wrong results): wave-coalesced loads
-#define K1_ADDR(a, i, off) \
-  (((a) / ((uint64_t)NS * L * 64) * ((uint64_t)NS * L * 64)) + ((uint64_t)((off) / 16) * NS + (i)) * 1024 + (threadIdx.x & 63) * 16)
-#else
-#define K1_ADDR(a, i, off) ((a) + (uint64_t)(i) * L + (off))
-#endif
-constexpr int kStreams = 4;       // K2 dense: chunks per lane
-constexpr int kK1MaxStreams = 8;  // K1: chains per lane, the largest variant
-constexpr int kK1Seg = 8;         // K1: consecutive chunks per chain
-// static LDS size classes of the K1 kernel (KiB): 3, 2 or 1 blocks per CU, of 512, 512 and
-// 1024 threads (16 waves per CU at K1_WAVES = 4 per SIMD, whose registers bound a lane)
+constexpr int kStreams = 4;  // K2 dense: chunks per lane
+constexpr int kK1Chains = 2;  // K1: chains per lane (independent dependent-LDS chains)
+constexpr int kK1Seg = 8;     // K1: consecutive chunks per chain
+// legacy K1 layout: static LDS size classes (KiB): 3, 2 or 1 blocks per CU, of 512, 512
+// and 1024 threads (16 waves per CU at 4 per SIMD, whose registers bound a lane)
 constexpr int kK1Lds[3] = {52, 80, 156};
 constexpr int kK1BlocksPerCU[3] = {3, 2, 1};
 constexpr __host__ __device__ int k1_threads(int ldsk) { return ldsk == 156 ? 1024 : 512; }
-// class 1 without the replicated class table (TSG_K1_NOREP=2, measurements): two blocks of
-// 10 waves per CU (20 waves; 100 VGPRs allow 5 per SIMD)
-constexpr int kK1Threads1NoRep = 640;
-// K1 LDS image: the byte -> class table, then the transition table.  The class table is
-// replicated per lane of a 32-lane half (K1_REP layout, [byte][lane & 31] words: every lane
-// reads its own bank, so the class read never conflicts) when the automaton leaves room for
-// it; otherwise 256 words (K1 tables of more than 124 KiB).
+// legacy class words replicated per lane of a 32-lane half ([byte][lane & 31] words: every
+// lane reads its own bank) when the automaton leaves room for it; else 256 words
 constexpr uint32_t kK1RepBytes = 256 * 32 * 4;
 constexpr int kBlock = 256;
-#ifndef K1_WAVES
-#define K1_WAVES 4
-#endif
 constexpr int kPad = 256;     // zero bytes before and after the batch in HBM (>= K1 warm-up)
 constexpr int kMaxBack = 16;  // event windows up to this many chunks; larger -> whole file
 
@@ -111,16 +85,22 @@ struct DevDFA {  // K2 rule group
 
 struct DevK1 {
   // States are renumbered so that the ones whose arrival must be reported (they end a
-  // literal) come last, and a state is named by its row (id * nc): next = tab[row + class]
-  // needs no multiply, and "arrival reports" is next >= acc_row.
-  const uint16_t* tab;    // [ns * nc] row of the next state
-  const uint32_t* cls;    // [256] class * 2 | 0xFF00 if in run class D | 0xFFFF0000 if in U
+  // literal) come last, and a state is named by its row: next = tab[row + class] needs no
+  // multiply, and "arrival reports" is next >= acc_row.  Packed layout: a row is the byte
+  // offset of its first entry in the LDS table, the class entry holds class * 2 + the
+  // table's LDS offset; legacy: a row is the entry index (id * stride).
+  const uint16_t* tab;    // [ns * stride] row of the next state
+  const uint32_t* cls;    // legacy: [256] class * 2 | 0xFF00 if in run class D | 0xFFFF0000 if in U
+  const uint32_t* pcls;   // packed: [256 * 2] {class * 2 + kK1PTab, in D | in U << 16}
   const uint16_t* accs;   // [ns] accept-mask index of the literals a state ends
   const uint32_t* masks;  // [nmasks * mw] keyword words (kw_words), then the event word
-  uint32_t nc, ns, nmasks, mw, kw_words, start, warm, kU, kD;  // start: row; kD = threshold << 8
+  uint32_t nc, ns, nmasks, mw, kw_words, start, warm, kU, kD;  // start: row; kD legacy: threshold << 8
   uint32_t acc_row;
-  uint32_t lds_class;  // index into kK1Lds
-  uint32_t rep;        // class table replicated per lane (K1_REP layout)
+  uint32_t row_unit;   // row of state id = id * row_unit
+  uint32_t tab_words;  // dwords of the transition table (staged into LDS)
+  uint32_t packed;     // layout (see above)
+  uint32_t lds_class;  // legacy: index into kK1Lds
+  uint32_t rep;        // legacy: class table replicated per lane (K1_REP layout)
   const uint16_t* kw_len;  // [kw_words * 32] byte length of each keyword (rare path)
   uint32_t kw_maxlen;      // longest keyword: an occurrence ending this far into a file fits
 };
@@ -263,15 +243,43 @@ __global__ void path_allow_kernel(DevPathDFA d, const uint8_t* __restrict__ path
 
 // ---------------------------------------------------------------- K1
 typedef unsigned short us2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));  // 8-byte aligned: one ds_read_b64
 
-// K1 class table in LDS.  The class word of a byte is class * 2 (low byte) | 0xFF00 if the
-// byte is in run class D | 0xFFFF0000 if in U.  Text bytes of 32 lanes fall on 32 banks by
-// their value (byte mod 32), which cost 2.3 extra LDS cycles per class read
-// (profiles/r03/d1: SQ of a build without transition reads; tools/k1_banksim.py agrees), so
-// the table is replicated per lane where it fits (K1_REP).
+// Two LDS layouts of the literal automaton.
+//
+// Packed (K1P, every rule set whose automaton rows fit 16-bit byte offsets; the builtin
+// rules: 515 states x 46 entries): per byte ONE ds_read_b64 of the byte's class entry and
+// ONE ds_read_u16 of the transition, and four VALU ops:
+//   a   = v_perm(word, lane8, sel)     the entry's address b * 256 + (lane % 32) * 8, built
+//                                      from the byte in place (no extract, no shift)
+//   e   = class entry {class * 2 + kK1PTab, keep}
+//   s   = tab[s + e.x]                 s is the row's byte offset: no scale, no mask
+//   cnt = cnt * keep + keep  (v_pk_mad_u16, saturating)   keep = {in D, in U}: the two run
+//                                      counters grow by one or drop to zero in one op
+//   mx  = max(mx, cnt), top = max(top, s) (every other byte: v_max3)
+// against 7.9 for the legacy layout (profiles/r03: bfe + shift + or for the class address,
+// a mask and a shift for the transition address, an add, an and and a max for the
+// counters, and per-byte dword selects of a half-unrolled loop).  The class entries are
+// replicated per lane of a 32-lane half ([byte][lane % 32], 8 B each: 32 lanes read 256
+// contiguous bytes, conflict-free), 64 KiB; the transitions follow at kK1PTab.
+//
+// Legacy (automata too large for 16-bit byte offsets, e.g. a large user rule set): class
+// words (class * 2 | 0xFF00 if in D | 0xFFFF0000 if in U), replicated per lane where the
+// automaton leaves room (K1_REP), the transition table after them, rows as entry indices.
+constexpr uint32_t kK1PTab = 256 * 256;  // packed: class entries below, transitions above
+constexpr int kK1PLdsK = 128;            // packed: static LDS image, KiB (1 block of 1024 per CU)
+#ifndef K1_GROUP
+#define K1_GROUP 4  // K1 bytes per scheduling group (fast16)
+#endif
 
-// run counters: high half = U run length, low half = D run length << 8 (both saturating);
-// m (the byte's class word) keeps the halves of the classes the byte belongs to
+__device__ __forceinline__ uint32_t pk_mad_sat(uint32_t cnt, uint32_t keep) {
+  uint32_t r;
+  asm("v_pk_mad_u16 %0, %1, %2, %2 clamp" : "=v"(r) : "v"(cnt), "v"(keep));
+  return r;
+}
+
+// legacy run counters: high half = U run length, low half = D run length << 8 (both
+// saturating); m (the byte's class word) keeps the halves of the classes the byte is in
 __device__ __forceinline__ uint32_t run_step(uint32_t cnt, uint32_t m) {
   const us2 inc = {(unsigned short)0x0100, (unsigned short)0x0001};
   us2 c = __builtin_elementwise_add_sat(__builtin_bit_cast(us2, cnt), inc);
@@ -291,8 +299,7 @@ struct K1Args {
   uint32_t* kw;    // [nfiles * kw_words]
   uint32_t* ev;    // [nchunks, padded to whole items]
   uint32_t* hits;  // [ns] arrivals per accepting state (sampling pass) or null
-  uint32_t streams;  // chains per lane
-  uint32_t seg;      // consecutive chunks per chain
+  uint32_t seg;    // consecutive chunks per chain
 };
 
 // one chain = one segment of consecutive chunks: automaton row, run counters, the running
@@ -341,27 +348,39 @@ struct K1Chain {
   uint32_t s, cnt, mx, evl;
 };
 
-template <int KWW, bool REP>
+__device__ __forceinline__ uint32_t word_of(const uint4 v, int k) {  // (k constant: no select)
+  return k < 4 ? v.x : k < 8 ? v.y : k < 12 ? v.z : v.w;
+}
+
+template <int KWW, bool PACKED, bool REP>
 struct K1Lane {
   const DevK1& d;
   const K1Args& A;
-  const uint16_t* s_tab;
-  const uint32_t* s_cls;  // REP: this lane's column of the replicated table
-  const uint16_t* s_accs;
-  const uint32_t* s_masks;
+  const uint8_t* smem;    // the block's LDS image
+  const uint8_t* s_tab;   // legacy: the transition table
+  const uint32_t* s_cls;  // legacy: this lane's column of the class words (REP) or the table
+  uint32_t lane8;         // packed: (lane % 32) * 8
 
-  // the class word of byte b
-  __device__ __forceinline__ uint32_t cls(uint32_t b) const { return REP ? s_cls[b << 5] : s_cls[b]; }
-  // m's low byte is the byte's class * 2: the entry's byte offset is 2 * row + m[7:0]
-  __device__ __forceinline__ uint32_t next(uint32_t s, uint32_t m) const {
-    return *(const uint16_t*)((const uint8_t*)s_tab + (s + s + (m & 0xFFu)));
+  // byte k (0..3) of dword w: the chain's row s and run counters cnt step once
+  __device__ __forceinline__ void step(uint32_t& s, uint32_t& cnt, uint32_t w, int k) const {
+    if constexpr (PACKED) {
+      const uint32_t a = __builtin_amdgcn_perm(w, lane8, 0x0C0C0000u | ((4u + (uint32_t)k) << 8));
+      const u32x2 e = *(const u32x2*)(smem + a);
+      s = *(const uint16_t*)(smem + s + e.x);
+      cnt = pk_mad_sat(cnt, e.y);
+    } else {
+      const uint32_t b = (w >> (8 * k)) & 0xFFu;
+      const uint32_t m = REP ? s_cls[b << 5] : s_cls[b];
+      s = *(const uint16_t*)(s_tab + (s + s + (m & 0xFFu)));
+      cnt = run_step(cnt, m);
+    }
   }
   // arrival in reporting row r with batch byte q: keyword bits of q's file (each keyword
   // only if it starts inside that file), event bits of the chain's chunk
   __device__ __forceinline__ void accept(K1Chain& c, uint32_t r, uint64_t q) {
-    const uint32_t id = r / d.nc;
+    const uint32_t id = r / d.row_unit;
     if (A.hits && q < A.total) atomicAdd(&A.hits[id], 1u);
-    const uint32_t* m = s_masks + (size_t)s_accs[id] * d.mw;
+    const uint32_t* m = d.masks + (size_t)d.accs[id] * d.mw;
     c.evl |= m[d.kw_words];
     if (q >= A.total) return;
     const uint32_t f = file_of(A.cf, A.off, A.nfiles, q);
@@ -385,14 +404,22 @@ struct K1Lane {
   }
   // the word at batch byte p again, byte by byte from row s, reporting every arrival
   __device__ __forceinline__ void replay16(K1Chain& c, uint32_t s, const uint4 v, uint64_t p) {
+    uint32_t cnt = 0;
 #pragma unroll 1
     for (uint32_t k = 0; k < 16; k++) {
-      s = next(s, cls(byte_of(v, k)));
+      const uint32_t w = k < 4 ? v.x : k < 8 ? v.y : k < 12 ? v.z : v.w;
+      if constexpr (PACKED) {
+        const u32x2 e = *(const u32x2*)(smem + ((((w >> (8 * (k & 3))) & 0xFFu) << 8) | lane8));
+        s = *(const uint16_t*)(smem + s + e.x);
+      } else {
+        step(s, cnt, w, (int)(k & 3));
+      }
       if (s >= d.acc_row) accept(c, s, p + k);
     }
   }
-  // NS chains, 16 bytes each, interleaved byte by byte; a word in which a chain reached a
-  // reporting row is replayed on the rare path.  pos[i]: batch byte of chain i's word.
+  // NS chains, 16 bytes each, interleaved byte by byte (fully unrolled: constant byte
+  // positions); a word in which a chain reached a reporting row is replayed on the rare
+  // path.  pos[i]: batch byte of chain i's word.
   template <int NS>
   __device__ __forceinline__ void fast16(K1Chain (&c)[NS], const uint4 (&v)[NS], const uint64_t (&pos)[NS]) {
     uint32_t s0[NS], top[NS];
@@ -401,133 +428,28 @@ struct K1Lane {
       s0[i] = c[i].s;
       top[i] = 0;
     }
-#ifdef K1_CLSPF
-    // the word's class words first (they do not depend on the state): their LDS reads are
-    // all in flight together instead of each one in front of its transition
-    constexpr int G = K1_CLSPF;  // bytes per prefetch group
-#pragma unroll 1
-    for (int k0 = 0; k0 < 16; k0 += G) {
-      uint32_t mw[NS][G];
 #pragma unroll
-      for (int k = 0; k < G; k++)
-#pragma unroll
-        for (int i = 0; i < NS; i++) mw[i][k] = cls(byte_of(v[i], k0 + k));
-#pragma unroll
-      for (int k = 0; k < G; k++)
-#pragma unroll
-        for (int i = 0; i < NS; i++) {
-          const uint32_t m = mw[i][k];
-          c[i].s = next(c[i].s, m);
-          top[i] = max(top[i], c[i].s);
-          c[i].cnt = run_step(c[i].cnt, m);
-          c[i].mx = run_max(c[i].mx, c[i].cnt);
-        }
-      __builtin_amdgcn_sched_barrier(0);  // (the next group's reads stay behind this one)
-    }
-#else
-#pragma unroll(NS > 4 ? K1_UNROLL / 4 : K1_UNROLL)
-    for (int k = 0; k < 16; k++)
+    for (int k = 0; k < 16; k++) {
 #pragma unroll
       for (int i = 0; i < NS; i++) {
-#ifdef K1_EXP_NO_CLS  // timing experiments only: wrong results
-        const uint32_t m = (byte_of(v[i], k) & 0x3Fu) * 2u;
-#else
-        const uint32_t m = cls(byte_of(v[i], k));
-#endif
-#ifdef K1_EXP_NO_TAB
-        c[i].s = (c[i].s + m) & 0x3FFFu;
-#else
-        c[i].s = next(c[i].s, m);
-#endif
+        step(c[i].s, c[i].cnt, word_of(v[i], k), k & 3);
         top[i] = max(top[i], c[i].s);
-#ifndef K1_EXP_NO_RUNS
-        c[i].cnt = run_step(c[i].cnt, m);
         c[i].mx = run_max(c[i].mx, c[i].cnt);
-#endif
       }
-#endif
+      // the class reads of K1_GROUP bytes in flight at a time: hoisting all 16 bytes' reads
+      // ahead of the chain (what the scheduler does unbounded) needs 2 registers per byte
+      // and chain and spills at the 128 VGPRs of 4 waves per SIMD
+      if ((k + 1) % K1_GROUP == 0) __builtin_amdgcn_sched_barrier(0);
+    }
 #pragma unroll
     for (int i = 0; i < NS; i++)
       if (__builtin_expect(top[i] >= d.acc_row, 0)) replay16(c[i], s0[i], v[i], pos[i]);
   }
 
-  // item = NS segments of A.seg consecutive chunks from a; chain i walks segment i (its
-  // state carries from one chunk to the next, so only the segment start needs the warm-up
-  // replay), the NS chains interleaved byte by byte
-  template <int NS>
-  __device__ void item(uint64_t a) {
-    const uint8_t* data = A.data;
-    const uint32_t C = A.chunk;
-    const uint64_t L = (uint64_t)C * A.seg;  // segment bytes
-    const uint64_t c0 = a / C;
-    K1Chain c[NS];
-#pragma unroll
-    for (int i = 0; i < NS; i++) {
-      c[i].s = d.start;
-      c[i].cnt = 0;
-      c[i].mx = 0;
-      c[i].evl = 0;
-    }
-    // warm-up: the d.warm bytes before each segment (the front pad before byte 0), with
-    // no reporting: afterwards row and counters equal those of the one-stream run
-    for (uint32_t j = 0; j < d.warm; j += 16) {
-      uint4 v[NS];
-#pragma unroll
-      for (int i = 0; i < NS; i++) v[i] = *(const uint4*)(data + a + (uint64_t)i * L - d.warm + j);
-#pragma unroll
-      for (int k = 0; k < 16; k++)
-#pragma unroll
-        for (int i = 0; i < NS; i++) {
-          const uint32_t m = cls(byte_of(v[i], k));
-          c[i].s = next(c[i].s, m);
-          c[i].cnt = run_step(c[i].cnt, m);
-        }
-    }
-    // Four words in flight per chain, each register set consumed in place (the loop body
-    // is unrolled four times): a set is refilled right after its word is stepped, so a
-    // load has three words of work to land, and no register copy waits on a pending load.
-    uint32_t jc = 0;   // offset inside the current chunk
-    uint64_t ci = c0;  // chunk index of chain 0
-    auto word = [&](uint64_t j, const uint4 (&v)[NS]) {
-      uint64_t pos[NS];
-#pragma unroll
-      for (int i = 0; i < NS; i++) pos[i] = a + (uint64_t)i * L + j;
-      fast16<NS>(c, v, pos);
-      jc += 16;
-      if (jc == C) {  // chunk end (uniform across the lane's chains): its event bits
-#pragma unroll
-        for (int i = 0; i < NS; i++) {
-          A.ev[ci + (uint64_t)i * A.seg] = c[i].evl | run_bits(c[i].mx);
-          c[i].evl = 0;
-          c[i].mx = 0;
-        }
-        jc = 0;
-        ci++;
-      }
-    };
-    auto load = [&](uint4 (&v)[NS], uint64_t j) {
-#pragma unroll
-      for (int i = 0; i < NS; i++) v[i] = *(const uint4*)(data + K1_ADDR(a, i, j));
-    };
-    uint4 b0[NS], b1[NS], b2[NS], b3[NS];
-    load(b0, 0);
-    load(b1, 16);
-    load(b2, 32);
-    load(b3, 48);
-    for (uint64_t j = 0; j < L; j += 64) {  // L is a multiple of 128
-      word(j, b0);
-      load(b0, j + 64);
-      word(j + 16, b1);
-      load(b1, j + 80);
-      word(j + 32, b2);
-      load(b2, j + 96);
-      word(j + 48, b3);
-      load(b3, j + 112);
-    }
-  }
-
-  // The same walk with quad-transposed loads (see quad_transpose): quad lane t walks item
-  // it0 + t of ib bytes (a ghost lane past the last item repeats it0 and stores nothing).
+  // An item = NS segments of A.seg consecutive chunks; quad lane t walks item it0 + t of ib
+  // bytes (a ghost lane past the last item repeats it0 and stores nothing).  Chain i walks
+  // segment i (its state carries from one chunk to the next, so only the segment start
+  // needs the warm-up replay of the d.warm bytes before it); loads are quad-transposed.
   template <int NS>
   __device__ __forceinline__ void item_quad(uint64_t it0, uint64_t ib, uint32_t q) {
     const uint8_t* data = A.data;
@@ -545,6 +467,8 @@ struct K1Lane {
       c[i].mx = 0;
       c[i].evl = 0;
     }
+    // warm-up: the d.warm bytes before each segment (the front pad before byte 0), with
+    // no reporting: afterwards row and counters equal those of the one-stream run
     for (uint32_t j = 0; j < d.warm; j += 16) {
       uint4 v[NS];
 #pragma unroll
@@ -552,11 +476,7 @@ struct K1Lane {
 #pragma unroll
       for (int k = 0; k < 16; k++)
 #pragma unroll
-        for (int i = 0; i < NS; i++) {
-          const uint32_t m = cls(byte_of(v[i], k));
-          c[i].s = next(c[i].s, m);
-          c[i].cnt = run_step(c[i].cnt, m);
-        }
+        for (int i = 0; i < NS; i++) step(c[i].s, c[i].cnt, word_of(v[i], k), k & 3);
     }
     const uint8_t* src[4];  // word q of quad lane t's item
 #pragma unroll
@@ -567,12 +487,7 @@ struct K1Lane {
       uint64_t pos[NS];
 #pragma unroll
       for (int i = 0; i < NS; i++) pos[i] = ghost ? A.total : a + (uint64_t)i * L + jw;
-      #ifdef K1_EXP_NOSTEP  // timing experiment only (wrong results): no byte steps, the words folded
-#pragma unroll
-      for (int ii = 0; ii < NS; ii++) c[ii].s ^= v[ii].x ^ v[ii].y ^ v[ii].z ^ v[ii].w;
-#else
       fast16<NS>(c, v, pos);
-#endif
       jc += 16;
       if (jc == C) {
         if (!ghost)
@@ -605,90 +520,55 @@ struct K1Lane {
       word(j + 32, v2);
       word(j + 48, v3);
     };
-#ifdef K1_EXP_COAL  // timing experiment only (wrong results): the wave's bytes, each load instruction 1 KiB contiguous
-    const uint64_t wbase = (it0 + q - (threadIdx.x & 63)) * ib + (threadIdx.x & 63) * 16, wlim = A.nitems * ib - 16;
     auto load = [&](uint4 (&r)[NS][4], uint64_t j) __attribute__((always_inline)) {
 #pragma unroll
       for (int i = 0; i < NS; i++)
 #pragma unroll
-        for (int t = 0; t < 4; t++)
-          r[i][t] = *(const uint4*)(data + min(wlim, wbase + (((uint64_t)i * (L / 64) + j / 64) * 4 + t) * 1024));
+        for (int t = 0; t < 4; t++) r[i][t] = *(const uint4*)(src[t] + ((uint64_t)i * L + j));
     };
-#else
-    auto load = [&](uint4 (&r)[NS][4], uint64_t j) __attribute__((always_inline)) {
-#pragma unroll
-      for (int i = 0; i < NS; i++)
-#pragma unroll
-        for (int t = 0; t < 4; t++)
-#ifdef K1_EXP_NOLOAD  // timing experiment only (wrong results): register data instead of loads
-          r[i][t] = make_uint4((uint32_t)j * 0x9E3779B1u + t, (uint32_t)j + i * 77u, (uint32_t)(j >> 3) ^ 0x5bd1e995u, (uint32_t)j * 31u + q);
-#else
-          r[i][t] = *(const uint4*)(src[t] + ((uint64_t)i * L + j));
-#endif
-    };
-#endif
-#if defined(K1_INPLACE)  // one 64-B block per chain, stepped in place, then reloaded
+    // one 64-B block per chain, stepped in place, then reloaded (profiles/r03/k1: 0.400 ->
+    // 0.385 ms per GiB against a copy of the block)
     uint4 r0[NS][4];
     load(r0, 0);
     for (uint64_t j = 0; j < L; j += 64) {
       block(j, r0);
       load(r0, j + 64);
     }
-#elif defined(K1_ONEBUF)  // one 64-B block per chain in registers (fewer VGPRs, more waves)
-    uint4 r0[NS][4];
-    load(r0, 0);
-    for (uint64_t j = 0; j < L; j += 64) {
-      uint4 cur[NS][4];
-#pragma unroll
-      for (int i = 0; i < NS; i++)
-#pragma unroll
-        for (int t = 0; t < 4; t++) cur[i][t] = r0[i][t];
-      load(r0, j + 64);
-      block(j, cur);
-    }
-#else
-    uint4 r0[NS][4], r1[NS][4];
-    load(r0, 0);
-    load(r1, 64);
-    for (uint64_t j = 0; j < L; j += 128) {  // L is a multiple of 128
-      block(j, r0);
-      load(r0, j + 128);
-      block(j + 64, r1);
-      load(r1, j + 192);
-    }
-#endif
   }
 };
 
-// K1 LDS image (static, so every table address is a constant): the class words at 0 (REP:
-// byte b's word for lane l at (b * 32 + l % 32) * 4; else at b * 4), the transitions after
-// them.  Accept masks stay in global memory (rare path).
-template <int KWW, int LDSK, int NS, bool REP, int TPB>
-__global__ void __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(K1_WAVES, 8))) k1_kernel(DevK1 d, K1Args A) {
+// The K1 kernel: every block stages the automaton once (a persistent grid), then its quads
+// walk 4 consecutive items together (uniform trip count inside a quad).  Accept masks stay
+// in global memory (rare path).  LDSK: the static LDS image in KiB.
+template <int KWW, bool PACKED, int LDSK, bool REP, int TPB>
+__global__ void __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(4, 8))) k1_kernel(DevK1 d, K1Args A) {
+  constexpr int NS = kK1Chains;
   __shared__ __attribute__((aligned(16))) uint8_t smem[LDSK * 1024];
-  constexpr uint32_t kTabOff = REP ? kK1RepBytes : 1024;
-  static_assert(!REP || LDSK * 1024 > (int)kK1RepBytes, "K1_REP needs room for the automaton");
-  uint32_t* s_cls = (uint32_t*)smem;
-  uint16_t* s_tab = (uint16_t*)(smem + kTabOff);
-  {
-    const uint32_t* src = (const uint32_t*)d.tab;
-    uint32_t* dst = (uint32_t*)s_tab;
-    for (uint32_t i = threadIdx.x; i < (d.ns * d.nc + 1) / 2; i += blockDim.x) dst[i] = src[i];
+  const uint32_t* tsrc = (const uint32_t*)d.tab;
+  if constexpr (PACKED) {
+    static_assert(LDSK * 1024 >= (int)kK1PTab + 65536, "packed K1 image: 64 KiB of class entries + 64 KiB of rows");
+    u32x2* dst = (u32x2*)smem;  // [byte][lane % 32]
+    const u32x2* src = (const u32x2*)d.pcls;
+    for (uint32_t i = threadIdx.x; i < 256u * 32u; i += blockDim.x) dst[i] = src[i >> 5];
+    uint32_t* tdst = (uint32_t*)(smem + kK1PTab);
+    for (uint32_t i = threadIdx.x; i < d.tab_words; i += blockDim.x) tdst[i] = tsrc[i];
+  } else {
+    constexpr uint32_t kTabOff = REP ? kK1RepBytes : 1024;
+    static_assert(!REP || LDSK * 1024 > (int)kK1RepBytes, "K1_REP needs room for the automaton");
+    uint32_t* s_cls = (uint32_t*)smem;
+    uint32_t* tdst = (uint32_t*)(smem + kTabOff);
+    for (uint32_t i = threadIdx.x; i < d.tab_words; i += blockDim.x) tdst[i] = tsrc[i];
     for (uint32_t i = threadIdx.x; i < (REP ? 256u * 32u : 256u); i += blockDim.x) s_cls[i] = d.cls[REP ? i >> 5 : i];
   }
   __syncthreads();
-  K1Lane<KWW, REP> L{d, A, s_tab, s_cls + (REP ? (threadIdx.x & 31) : 0), d.accs, d.masks};
+  const uint32_t lane = threadIdx.x & 31;
+  K1Lane<KWW, PACKED, REP> L{d, A, smem, smem + (REP ? kK1RepBytes : 1024), (const uint32_t*)smem + (REP ? lane : 0),
+                             lane * 8};
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-#ifdef K1_NO_QUAD
-  for (uint64_t it = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; it < A.nitems; it += stride)
-    L.template item<NS>(it * A.item_step * NS * A.seg * A.chunk);
-#else
-  // quads walk 4 consecutive items together (uniform trip count inside a quad)
   const uint32_t q = threadIdx.x & 3;
   const uint64_t ib = (uint64_t)A.item_step * NS * A.seg * A.chunk;
   for (uint64_t it0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) & ~3ull; it0 < A.nitems; it0 += stride)
     L.template item_quad<NS>(it0, ib, q);
-#endif
 }
 
 // ---------------------------------------------------------------- K1X
@@ -1581,7 +1461,7 @@ __device__ __forceinline__ void k2_list_pair(const DevDFA& d, const K2Args& A, c
   };
   // two 64-byte blocks of both chains in registers (x: chain 0, y: chain 1; 0: current,
   // 1: next), named individually so they stay in VGPRs
-  uint4 x0[4], y0[4], x1[4], y1[4];
+  uint4 x0[4], y0[4];
 #define K2_LOAD(X, Y, J)                                                        \
   _Pragma("unroll") for (int t = 0; t < 4; t++) {                              \
     X[t] = *(const uint4*)(src[0][t] + (J));                                     \
@@ -1595,23 +1475,13 @@ __device__ __forceinline__ void k2_list_pair(const DevDFA& d, const K2Args& A, c
     word(it[1], (uint32_t)(J) + 16u * w, Y[w]);                                 \
   }
   K2_LOAD(x0, y0, 0)
-#ifndef K2_TWOBUF  // one 64-B block per chain, stepped in place, then reloaded (160 VGPRs: 3 waves/SIMD)
+  // one 64-B block per chain, stepped in place, then reloaded (160 VGPRs: 3 waves/SIMD)
   for (uint64_t j = 0; j < C; j += 64) {
     K2_BLOCK(x0, y0, j)
     if (j + 64 < C) {
       K2_LOAD(x0, y0, j + 64)
     }
   }
-#else
-  for (uint64_t j = 0; j < C; j += 128) {  // C is a multiple of 128 here
-    K2_LOAD(x1, y1, j + 64)
-    K2_BLOCK(x0, y0, j)
-    if (j + 128 < C) {
-      K2_LOAD(x0, y0, j + 128)
-    }
-    K2_BLOCK(x1, y1, j + 64)
-  }
-#endif
 #undef K2_LOAD
 #undef K2_BLOCK
   // matches that started in the chunk and run past it (inside the file): follow them
@@ -1827,54 +1697,54 @@ static int make_device_dfa(const DFA& dd, const std::vector<uint32_t>& rules, De
 }
 
 // perf experiments only (results are not exact): bit 0 strips the K1 accept flags
-static int k1_debug() {
-  const char* e = getenv("TSG_K1_DEBUG");
-  return e ? atoi(e) : 0;
-}
-
 struct K1Host {  // host copies of the K1 tables (adaptation rebuilds the device table)
   std::vector<uint16_t> tab, accs;
   std::vector<uint32_t> masks;
   std::vector<uint32_t> order;  // device state id -> automaton state
   uint32_t stride = 0;          // row stride of tab (>= the class count)
+  uint32_t unit = 1;            // row of state id = id * stride * unit (packed: 2, bytes)
 };
 
-// Device numbering of the K1 automaton: states whose arrival is reported (they end a
-// literal, and are not `quiet`) last; rows = id * nc.
-// Row stride (u16 entries) of the K1 table: the class count padded to 2 mod 4, so a row is
-// an odd number of dwords and equal classes of different rows fall in different LDS banks
-// (ds_read_u16 banks are dword mod 32).  Padding is skipped when it would need a larger LDS
-// image or overflow the 16-bit rows.  TSG_K1_STRIDE=0 turns it off (measurements).
-// K1 LDS class of a transition table of tab_bytes (2 * the class count for the REP layout,
-// preferred; 3 = too large)
+// K1 LDS class of a legacy transition table of tab_bytes (2 * the class count for the REP
+// layout, preferred; 3 = too large)
 static int k1_lds_class(size_t tab_bytes) {
   for (int k = 0; k < 3; k++)
     if (tab_bytes + kK1RepBytes <= (size_t)kK1Lds[k] * 1024) return 2 * k + 1;
   return tab_bytes + 1024 <= (size_t)kK1Lds[2] * 1024 ? 2 * 2 : 2 * 3;
 }
 
+// the packed layout holds rows as 16-bit byte offsets: ns * stride u16 entries in 64 KiB
+static bool k1_packed_fits(size_t ns, size_t rs) { return ns * rs * 2 <= 65536; }
+
+// Row stride (u16 entries) of the K1 table: the class count padded to 2 mod 4, so a row is
+// an odd number of dwords and equal classes of different rows fall in different LDS banks
+// (ds_read_u16 banks are dword mod 32).  Padding is skipped when it would change the
+// layout (packed -> legacy, or a larger legacy LDS image) or overflow the 16-bit rows.
 static size_t k1_stride(size_t nc, size_t ns) {
-  const char* e = getenv("TSG_K1_STRIDE");
-  if (e && atoi(e) == 0) return nc;
   size_t rs = nc;
   while (rs % 4 != 2) rs++;
   auto tab = [&](size_t r) { return (ns * r + (ns * r & 1)) * 2; };
+  if (k1_packed_fits(ns, nc)) return k1_packed_fits(ns, rs) ? rs : nc;
   if ((ns - 1) * rs > 0xFFFF || k1_lds_class(tab(rs)) != k1_lds_class(tab(nc))) return nc;
   return rs;
 }
 
+// Device numbering of the K1 automaton: states whose arrival is reported (they end a
+// literal, and are not `quiet`) last; rows = id * stride * unit.
 static int k1_tables(const Plan& p, const std::vector<uint8_t>& quiet, K1Host* h, uint32_t* start_row,
                      uint32_t* acc_row) {
   const DFA& d = *p.kw_dfa;
   const size_t nc = d.nclasses, ns = d.nstates;
   const size_t rs = k1_stride(nc, ns);
   h->stride = (uint32_t)rs;
-  if ((ns - 1) * rs > 0xFFFF) return fail(TSG_ERR_INTERNAL, "keyword automaton too large for 16-bit rows");
+  h->unit = k1_packed_fits(ns, rs) ? 2 : 1;
+  const size_t row = rs * h->unit;
+  if ((ns - 1) * row > 0xFFFF) return fail(TSG_ERR_INTERNAL, "keyword automaton too large for 16-bit rows");
   std::vector<uint32_t> newid(ns);
   h->order.clear();
   for (int pass = 0; pass < 2; pass++)
     for (size_t st = 0; st < ns; st++) {
-      const bool rep = d.eot_acc[st] && !quiet[st] && !(k1_debug() & 1);
+      const bool rep = d.eot_acc[st] && !quiet[st];
       if (rep == (pass == 1)) {
         newid[st] = (uint32_t)h->order.size();
         h->order.push_back((uint32_t)st);
@@ -1883,7 +1753,7 @@ static int k1_tables(const Plan& p, const std::vector<uint8_t>& quiet, K1Host* h
   uint32_t first_rep = (uint32_t)ns;
   for (size_t i = 0; i < ns; i++) {
     const uint32_t st = h->order[i];
-    if (d.eot_acc[st] && !quiet[st] && !(k1_debug() & 1)) {
+    if (d.eot_acc[st] && !quiet[st]) {
       first_rep = (uint32_t)i;
       break;
     }
@@ -1893,10 +1763,10 @@ static int k1_tables(const Plan& p, const std::vector<uint8_t>& quiet, K1Host* h
   for (size_t i = 0; i < ns; i++) {
     const uint32_t st = h->order[i];
     h->accs[i] = (uint16_t)d.eot_acc[st];
-    for (size_t c = 0; c < nc; c++) h->tab[i * rs + c] = (uint16_t)(newid[d.next[st * nc + c]] * rs);
+    for (size_t c = 0; c < nc; c++) h->tab[i * rs + c] = (uint16_t)(newid[d.next[st * nc + c]] * row);
   }
-  *start_row = newid[d.start[kCtxBOT]] * (uint32_t)rs;
-  *acc_row = first_rep * (uint32_t)rs;
+  *start_row = newid[d.start[kCtxBOT]] * (uint32_t)row;
+  *acc_row = first_rep * (uint32_t)row;
   return TSG_OK;
 }
 
@@ -1956,9 +1826,13 @@ static int make_device_k1(const Plan& p, DevK1* out, std::vector<void*>* allocs,
   DevK1& v = *out;
   int rc;
   if ((rc = k1_tables(p, std::vector<uint8_t>(d.nstates, 0), host, &v.start, &v.acc_row))) return rc;
-  std::vector<uint32_t> cls(256);
-  for (int b = 0; b < 256; b++)
+  v.packed = host->unit == 2 ? 1u : 0u;
+  std::vector<uint32_t> cls(256), pcls(512);
+  for (int b = 0; b < 256; b++) {
     cls[b] = (uint32_t)d.cls[b] * 2 | ((p.run_cls[b] & 2) ? 0xFF00u : 0u) | ((p.run_cls[b] & 1) ? 0xFFFF0000u : 0u);
+    pcls[2 * b] = (uint32_t)d.cls[b] * 2 + kK1PTab;
+    pcls[2 * b + 1] = ((p.run_cls[b] & 2) ? 1u : 0u) | ((p.run_cls[b] & 1) ? 1u << 16 : 0u);
+  }
   const uint32_t W = (uint32_t)p.kw_words, mw = W + 1;
   std::vector<uint32_t> masks((size_t)d.masks.size() * mw, 0);
   for (size_t m = 0; m < d.masks.size(); m++) {
@@ -1968,16 +1842,19 @@ static int make_device_k1(const Plan& p, DevK1* out, std::vector<void*>* allocs,
   }
   if ((rc = upload_vec(host->tab, &v.tab, allocs))) return rc;
   if ((rc = upload_vec(cls, &v.cls, allocs))) return rc;
+  if ((rc = upload_vec(pcls, &v.pcls, allocs))) return rc;
   if ((rc = upload_vec(host->accs, &v.accs, allocs))) return rc;
   if ((rc = upload_vec(masks, &v.masks, allocs))) return rc;
   v.nc = host->stride;  // the kernel's row stride
+  v.row_unit = host->stride * host->unit;
+  v.tab_words = (uint32_t)(host->tab.size() / 2);
   v.ns = (uint32_t)d.nstates;
   v.nmasks = (uint32_t)d.masks.size();
   v.mw = mw;
   v.kw_words = W;
   v.warm = (uint32_t)p.warm;
   v.kU = (uint32_t)p.run_k[0];
-  v.kD = (uint32_t)p.run_k[1] << 8;
+  v.kD = v.packed ? (uint32_t)p.run_k[1] : (uint32_t)p.run_k[1] << 8;
   std::vector<uint16_t> kwlen((size_t)W * 32, 0);
   v.kw_maxlen = 1;
   for (int k = 0; k < p.n_kw; k++) {
@@ -1989,13 +1866,7 @@ static int make_device_k1(const Plan& p, DevK1* out, std::vector<void*>* allocs,
   const int lc = k1_lds_class(host->tab.size() * 2);
   v.lds_class = (uint32_t)(lc >> 1);
   v.rep = (uint32_t)(lc & 1);
-  if (getenv("TSG_K1_NOREP") && atoi(getenv("TSG_K1_NOREP")) == 2 && host->tab.size() * 2 + 1024 <= (size_t)kK1Lds[1] * 1024) {
-    v.lds_class = 1;  // (measurements: no replicated class table, two blocks per CU)
-    v.rep = 0;
-  } else if (getenv("TSG_K1_NOREP") && v.rep && host->tab.size() * 2 + 1024 <= (size_t)kK1Lds[v.lds_class] * 1024) {
-    v.rep = 0;  // (measurements: the 256-word class table in the same LDS class)
-  }
-  if (v.lds_class > 2) return fail(TSG_ERR_INTERNAL, "keyword automaton exceeds LDS");
+  if (!v.packed && v.lds_class > 2) return fail(TSG_ERR_INTERNAL, "keyword automaton exceeds LDS");
   return TSG_OK;
 }
 
@@ -2109,57 +1980,43 @@ static int ensure(T** p, size_t* cap, size_t n) {
   return TSG_OK;
 }
 
-template <int LDSK, int NS, bool REP, int TPB = k1_threads(LDSK)>
+template <bool PACKED, int LDSK, bool REP, int TPB>
 static const void* k1_fn_w(uint32_t kw_words) {
-  if (kw_words <= 1) return (const void*)k1_kernel<1, LDSK, NS, REP, TPB>;
-  if (kw_words <= 2) return (const void*)k1_kernel<2, LDSK, NS, REP, TPB>;
-  if (kw_words <= 4) return (const void*)k1_kernel<4, LDSK, NS, REP, TPB>;
-  return (const void*)k1_kernel<8, LDSK, NS, REP, TPB>;
+  if (kw_words <= 1) return (const void*)k1_kernel<1, PACKED, LDSK, REP, TPB>;
+  if (kw_words <= 2) return (const void*)k1_kernel<2, PACKED, LDSK, REP, TPB>;
+  if (kw_words <= 4) return (const void*)k1_kernel<4, PACKED, LDSK, REP, TPB>;
+  return (const void*)k1_kernel<8, PACKED, LDSK, REP, TPB>;
 }
 
-// (the 256-word class table only in the largest class: smaller automata always fit REP)
-template <int NS>
-static const void* k1_fn_ns(uint32_t kw_words, uint32_t lds_class, uint32_t rep) {
-  switch (lds_class) {
-    case 0: return k1_fn_w<kK1Lds[0], NS, true>(kw_words);
-    case 1: return rep ? k1_fn_w<kK1Lds[1], NS, true>(kw_words) : k1_fn_w<kK1Lds[1], NS, false, kK1Threads1NoRep>(kw_words);
-    default: return rep ? k1_fn_w<kK1Lds[2], NS, true>(kw_words) : k1_fn_w<kK1Lds[2], NS, false>(kw_words);
+// the kernel of a layout and its block size / blocks per CU
+static const void* k1_fn(const DevK1& k, int* threads, int* per_cu) {
+  if (k.packed) {
+    *threads = 1024;
+    *per_cu = 1;
+    return k1_fn_w<true, kK1PLdsK, true, 1024>(k.kw_words);
+  }
+  const uint32_t lc = std::min<uint32_t>(k.lds_class, 2);
+  *threads = k1_threads(kK1Lds[lc]);
+  *per_cu = kK1BlocksPerCU[lc];
+  switch (lc) {
+    case 0: return k1_fn_w<false, kK1Lds[0], true, k1_threads(kK1Lds[0])>(k.kw_words);
+    case 1: return k1_fn_w<false, kK1Lds[1], true, k1_threads(kK1Lds[1])>(k.kw_words);
+    default:
+      return k.rep ? k1_fn_w<false, kK1Lds[2], true, k1_threads(kK1Lds[2])>(k.kw_words)
+                   : k1_fn_w<false, kK1Lds[2], false, k1_threads(kK1Lds[2])>(k.kw_words);
   }
 }
 
-// independent K1 chains per lane: 2 (quad-transposed loads keep two 64-byte blocks per
-// chain in registers), or 3 / 4 with TSG_K1_NS=3 / 4 (measurements)
-// consecutive chunks per chain (TSG_K1_SEG overrides, 1..kK1Seg: measurements)
-static uint32_t k1_seg() {
-  static const uint32_t seg = getenv("TSG_K1_SEG") ? std::min<uint32_t>(kK1Seg, std::max(1, atoi(getenv("TSG_K1_SEG"))))
-                                                  : (uint32_t)kK1Seg;
-  return seg;
-}
-
-static uint32_t k1_streams() {
-  static const uint32_t ns = getenv("TSG_K1_NS") && (atoi(getenv("TSG_K1_NS")) == 3 || atoi(getenv("TSG_K1_NS")) == 4)
-                                 ? (uint32_t)atoi(getenv("TSG_K1_NS"))
-                                 : 2u;
-  return ns;
-}
-
-static const void* k1_fn(uint32_t kw_words, uint32_t lds_class, uint32_t rep, uint32_t ns) {
-  return ns == 2 ? k1_fn_ns<2>(kw_words, lds_class, rep)
-                 : ns == 3 ? k1_fn_ns<3>(kw_words, lds_class, rep) : k1_fn_ns<4>(kw_words, lds_class, rep);
-}
-
+// a persistent grid of the resident blocks (each block stages the automaton once)
 static int launch_k1(DeviceRules* r, const K1Args& A, hipStream_t st) {
-  // a persistent grid of the resident blocks of the LDS class (each block stages the
-  // automaton once); TSG_K1_GRID overrides the blocks per CU (measurements)
-  static const int gmul = getenv("TSG_K1_GRID") ? atoi(getenv("TSG_K1_GRID")) : 0;
-  const uint32_t lc = std::min<uint32_t>(r->k1.lds_class, 2);
-  const int threads = (lc == 1 && !r->k1.rep) ? kK1Threads1NoRep : k1_threads(kK1Lds[lc]);
-  const uint64_t cap = (uint64_t)r->grid / 8 * (gmul > 0 ? gmul : kK1BlocksPerCU[lc]);
+  int threads = 0, per_cu = 0;
+  const void* fn = k1_fn(r->k1, &threads, &per_cu);
+  const uint64_t cap = (uint64_t)r->cus * per_cu;
   const int grid = (int)std::min<uint64_t>((A.nitems + threads - 1) / threads, cap);
   DevK1 d = r->k1;
   K1Args a = A;
   void* args[] = {&d, &a};
-  HIP_TRY(hipLaunchKernel(k1_fn(r->k1.kw_words, r->k1.lds_class, r->k1.rep, A.streams), dim3(grid), dim3(threads), args, 0, st));
+  HIP_TRY(hipLaunchKernel(fn, dim3(grid), dim3(threads), args, 0, st));
   HIP_TRY(hipGetLastError());
   return TSG_OK;
 }
@@ -2179,14 +2036,14 @@ static int adapt_k1(DeviceRules* r, LaneState* l, uint64_t total, uint32_t nfile
   const uint64_t nsamp = (k1_items + step - 1) / step;
   HIP_TRY(hipMemsetAsync(r->d_hits, 0, sizeof(uint32_t) * ns, l->st));
   K1Args A{l->data_alloc + kPad, l->off, l->cf, total, nchunks, nsamp, step, r->chunk,
-           nfiles, l->kw, l->ev_bits, r->d_hits, k1_streams(), k1_seg()};
+           nfiles, l->kw, l->ev_bits, r->d_hits, (uint32_t)kK1Seg};
   int rc;
   if ((rc = launch_k1(r, A, l->st))) return rc;
   std::vector<uint32_t> hits(ns);
   HIP_TRY(hipMemcpyAsync(hits.data(), r->d_hits, sizeof(uint32_t) * ns, hipMemcpyDeviceToHost, l->st));
   HIP_TRY(hipStreamSynchronize(l->st));
   r->adapted = true;
-  const uint64_t sample_bytes = nsamp * A.streams * A.seg * r->chunk;
+  const uint64_t sample_bytes = nsamp * kK1Chains * A.seg * r->chunk;
   uint64_t tot = 0;
   std::vector<uint32_t> order;
   for (uint32_t s = 0; s < ns; s++)
@@ -2195,9 +2052,7 @@ static int adapt_k1(DeviceRules* r, LaneState* l, uint64_t total, uint32_t nfile
       order.push_back(s);
     }
   std::sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return hits[a] > hits[b]; });
-  // reporting budget: one arrival per 4 KiB (TSG_K1_ADAPT_BYTES overrides: measurements)
-  static const uint64_t per = getenv("TSG_K1_ADAPT_BYTES") ? std::max(1, atoi(getenv("TSG_K1_ADAPT_BYTES"))) : 4096;
-  const uint64_t budget = sample_bytes / per;
+  const uint64_t budget = sample_bytes / 4096;  // reporting budget: one arrival per 4 KiB
   std::vector<uint8_t> hot(p.kw_dfa->nstates, 0);  // automaton states that stop reporting
   auto kw_unknown = std::make_shared<std::vector<uint8_t>>(p.n_kw, 0);
   uint32_t ev_hot = 0, nhot = 0;
@@ -2437,7 +2292,7 @@ int enqueue_scan(DeviceRules* r, LaneState* l, const ScanInput& in, HostOut* out
   l->nchunks = nchunks;
   int rc;
   // ---- buffers (grown on demand; growing waits for the device)
-  const size_t tail = (size_t)kK1MaxStreams * kK1Seg * C + kPad;
+  const size_t tail = (size_t)kK1Chains * kK1Seg * C + kPad;
   if ((rc = ensure(&l->data_alloc, &l->data_cap, (size_t)total + kPad + tail))) return rc;
   uint8_t* data = l->data_alloc + kPad;
   const bool paths_dev = r->has_pathdfa && F;
@@ -2447,7 +2302,7 @@ int enqueue_scan(DeviceRules* r, LaneState* l, const ScanInput& in, HostOut* out
   l->off = (const uint64_t*)l->meta;
   l->poff = l->off + F + 1;
   l->paths = (const uint8_t*)(l->poff + F + 1);
-  const uint64_t k1_item_chunks = (uint64_t)kK1MaxStreams * kK1Seg;
+  const uint64_t k1_item_chunks = (uint64_t)kK1Chains * kK1Seg;
   const uint64_t nchunks_pad = (nchunks + k1_item_chunks - 1) / k1_item_chunks * k1_item_chunks + 1;
   const uint64_t ncf = (total >> kCfShift) + 2;
   if ((rc = ensure(&l->cf, &l->cf_cap, (size_t)ncf))) return rc;
@@ -2532,14 +2387,12 @@ int enqueue_scan(DeviceRules* r, LaneState* l, const ScanInput& in, HostOut* out
   HIP_TRY(hipEventRecord(out->ev[4], st));
 
   // ---- K1
-  const uint32_t k1s = k1_streams();
-  const uint64_t k1_items = (nchunks + (uint64_t)k1s * k1_seg() - 1) / ((uint64_t)k1s * k1_seg());
+  const uint64_t k1_items = (nchunks + k1_item_chunks - 1) / k1_item_chunks;
   const uint64_t adapt_bytes = r->adapt_mib == 0xFFFFFFFFu ? ~0ull : (uint64_t)(r->adapt_mib ? r->adapt_mib : 16) << 20;
   if (!r->adapted && k1_items >= 64 && total >= adapt_bytes)
     if ((rc = adapt_k1(r, l, total, F, nchunks, k1_items))) return rc;
   if (k1_items) {
-    K1Args A{data, l->off, l->cf, total, nchunks, k1_items, 1, C, F, l->kw, l->ev_bits, nullptr, k1s,
-             k1_seg()};
+    K1Args A{data, l->off, l->cf, total, nchunks, k1_items, 1, C, F, l->kw, l->ev_bits, nullptr, (uint32_t)kK1Seg};
     if ((rc = launch_k1(r, A, st))) return rc;
   }
   if (r->has_k1x && total) {  // the hashed literals of a large rule set, after K1's stores
@@ -2626,8 +2479,7 @@ int enqueue_scan(DeviceRules* r, LaneState* l, const ScanInput& in, HostOut* out
     static const bool diag = getenv("TSG_K2_DIAG") != nullptr;
     A.diag = diag ? l->counts + 8 : nullptr;
     A.claim = l->counts + 12;
-    static const bool no_words = getenv("TSG_K2_NO_WORDREC") != nullptr;  // (measurements)
-    A.word_recs = G <= 0x3FFF && !no_words;
+    A.word_recs = G <= 0x3FFF;
     static const bool trace = getenv("TSG_K2_TRACE") != nullptr;
     if (trace && (rc = ensure(&l->etrace, &l->etrace_cap, (size_t)entries_cap * kTraceW))) return rc;
     if (trace) HIP_TRY(hipMemsetAsync(l->etrace, 0, sizeof(unsigned long long) * entries_cap * kTraceW, st));

@@ -369,10 +369,9 @@ uint64_t walk_tar(const uint8_t* tar, uint64_t tar_len, uint64_t pos, uint64_t s
 // groups, return value); index_tar is walk_par(0, tar_len).
 uint64_t walk_par(const uint8_t* tar, uint64_t tar_len, uint64_t pos0, uint64_t stop, std::vector<TarEntry>* out,
                   std::vector<uint64_t>* groups, std::string* err) {
-  // ranges of at least 64 MiB (TSG_TAR_RANGE_KIB lowers it: tests of the stitching)
-  const uint64_t kMinRange =
-      getenv("TSG_TAR_RANGE_KIB") ? std::max(1ull, strtoull(getenv("TSG_TAR_RANGE_KIB"), nullptr, 10)) << 10
-                                  : 64ull << 20;
+  // ranges of at least 64 MiB (the "tar_range_kib" knob lowers it: tests of the stitching)
+  const int64_t kib = knobs().tar_range_kib.load();
+  const uint64_t kMinRange = kib > 0 ? (uint64_t)kib << 10 : 64ull << 20;
   const uint64_t span = stop > pos0 ? stop - pos0 : 0;
   const int T = (int)std::min<uint64_t>(16, std::max<uint64_t>(1, span / kMinRange));
   if (T == 1) return walk_tar(tar, tar_len, pos0, stop, out, groups, err);
@@ -615,8 +614,8 @@ int scan_in_pieces(tsg_ctx* ctx, tsg_layer* L, const std::function<uint64_t(size
   const size_t n = L->offsets.size() - 1;
   // about 8 pieces of at least 160 MiB (a batch has fixed costs: tools/batch_sizes.py) and
   // at most a slot
-  // (TSG_PIECE_MIB overrides the floor: measurements)
-  static const uint64_t floor_mib = getenv("TSG_PIECE_MIB") ? std::max(1, atoi(getenv("TSG_PIECE_MIB"))) : 160;
+  // (the "piece_mib" knob overrides the floor: measurements)
+  const uint64_t floor_mib = knobs().piece_mib.load() > 0 ? (uint64_t)knobs().piece_mib.load() : 160;
   const uint64_t piece_bytes =
       std::min(ctx_slot_bytes(ctx), std::max<uint64_t>(floor_mib << 20, L->offsets.back() / 8));
   std::vector<uint64_t> tickets, got(n, 0);

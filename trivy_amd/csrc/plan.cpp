@@ -1,5 +1,6 @@
 // GPU plan construction, host resolver, CPU batch path and kernel emulation.
 #include "plan.hpp"
+#include "internal.hpp"
 #include <deque>
 #include <condition_variable>
 #include <mutex>
@@ -474,7 +475,7 @@ std::unique_ptr<Plan> build_plan(const Ruleset& rs, const PlanOptions& opt, std:
     return k1_estimate(with_anchors) <= 4 * (size_t)opt.max_kw_table_bytes && build_k1(with_anchors);
   };
   bool k1_ok = (opt.anchors && try_k1(true)) || try_k1(false);
-  if (!k1_ok && !getenv("TSG_NO_K1X")) {
+  if (!k1_ok && !knobs().no_k1x.load()) {
     // Too many literal bytes for an LDS-resident automaton (large user rule sets): the
     // keywords and anchors of >= 4 bytes go to the hashed prefilter (K1X), the short
     // ones stay in the automaton.  Keyword bits stay exact, anchors keep their events.
@@ -1380,7 +1381,7 @@ static void emulate_words(const DFA& d, uint32_t gi, const std::vector<uint32_t>
 void emulate_kernels(const Plan& plan, const BatchView& bv, uint32_t chunk, uint32_t ext_cap,
                      KernelOutput* ko, std::vector<uint64_t>* group_item_bytes) {
   const uint32_t F = bv.nfiles;
-  const bool word_recs = getenv("TSG_EMU_WORDREC") != nullptr && plan.groups.size() <= 0x3FFF;
+  const bool word_recs = knobs().emu_wordrec.load() && plan.groups.size() <= 0x3FFF;
   std::vector<uint32_t> ev;
   k1_reference(plan, bv, chunk, &ko->kw, &ev);
   ko->cand.clear();
