@@ -243,6 +243,8 @@ typedef struct tsg_stats {
    * coarse file map) and the H2D of the offsets / paths; aux_ms / sum_d2h_ms above are the
    * outputs kernel (results written into pinned, host-mapped memory) */
   double prep_ms, meta_ms, sum_prep_ms, sum_meta_ms;
+  uint64_t k1_records;   /* last batch: 16-byte words in which K1 reached a reporting state
+                            (replayed by the accept kernel) */
 } tsg_stats;
 int tsg_ctx_get_stats(const tsg_ctx* ctx, tsg_stats* out);
 

@@ -243,3 +243,40 @@ def test_queue_flush_and_idle_close(builtin):
     assert res == [builtin.Scan(a)]
     q.close()
     ctx.close()
+
+
+def test_slot_holders_waiting_for_each_other_fail(builtin):
+    """Two callers that each hold one of the context's slots and then ask for another wait
+    for each other: the second one to ask fails (TSG_ERR_ARG) instead of both waiting
+    forever; once it gives its slot back, the first one gets it."""
+    from trivy_amd import _native as N
+    ctx = S.GpuContext(builtin, 0, emulate=True, max_slots=2)
+    a = ctx.acquire_slot(1 << 20, 16, 1024)[0]
+    got, errs = [], []
+    b_has = threading.Event()
+
+    def second():
+        b = ctx.acquire_slot(1 << 20, 16, 1024)[0]
+        b_has.set()
+        try:
+            got.append(ctx.acquire_slot(1 << 20, 16, 1024)[0])  # waits for `a` (held, waiting)
+        except N.NativeError as e:
+            errs.append(e)
+        finally:
+            ctx.release_slot(b)
+
+    t = threading.Thread(target=second)
+    t.start()
+    b_has.wait(10)
+    try:
+        third = ctx.acquire_slot(1 << 20, 16, 1024)[0]  # both slots held: one of us must fail
+        ctx.release_slot(third)
+    except N.NativeError as e:
+        errs.append(e)
+    ctx.release_slot(a)
+    t.join(20)
+    assert not t.is_alive()
+    assert len(errs) >= 1 and all(e.code == N.TSG_ERR_ARG for e in errs)
+    for sid in got:
+        ctx.release_slot(sid)
+    ctx.close()

@@ -14,9 +14,9 @@ build() {
 }
 for v in "$@"; do
   case $v in
-    g2) build $v -DK1_GROUP=2 ;;         # K1: class reads of 2 / 8 / 16 bytes in flight
-    g8) build $v -DK1_GROUP=8 ;;
-    g16) build $v -DK1_GROUP=16 ;;
+    legacy) build $v -DK1_LEGACY ;;      # K1: the legacy layout (class words, index rows)
+    ns3) build $v -DK1_CHAINS=3 ;;       # K1: chains per lane
+    ns4) build $v -DK1_CHAINS=4 ;;
     k2ctr) build $v -DK2_TRACE_CTR ;;    # K2: per-entry counters (TSG_K2_TRACE)
     k2noinl) build $v -DK2_NOINL ;;      # K2: rare paths out of line
     x1) build $v -DK1X_WORDS=1 ;;        # K1X: words per lane per round

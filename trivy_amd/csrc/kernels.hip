@@ -49,7 +49,10 @@ enum : uint8_t { kGroupNone = 0, kGroupList = 1, kGroupDense = 2, kGroupSkip = 3
   } while (0)
 
 constexpr int kStreams = 4;  // K2 dense: chunks per lane
-constexpr int kK1Chains = 2;  // K1: chains per lane (independent dependent-LDS chains)
+#ifndef K1_CHAINS
+#define K1_CHAINS 2
+#endif
+constexpr int kK1Chains = K1_CHAINS;  // K1: chains per lane (independent dependent-LDS chains)
 constexpr int kK1Seg = 8;     // K1: consecutive chunks per chain
 // legacy K1 layout: static LDS size classes (KiB): 3, 2 or 1 blocks per CU, of 512, 512
 // and 1024 threads (16 waves per CU at 4 per SIMD, whose registers bound a lane)
@@ -268,9 +271,7 @@ typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));  // 8-byte aligned: 
 // automaton leaves room (K1_REP), the transition table after them, rows as entry indices.
 constexpr uint32_t kK1PTab = 256 * 256;  // packed: class entries below, transitions above
 constexpr int kK1PLdsK = 128;            // packed: static LDS image, KiB (1 block of 1024 per CU)
-#ifndef K1_GROUP
-#define K1_GROUP 4  // K1 bytes per scheduling group (fast16)
-#endif
+
 
 __device__ __forceinline__ uint32_t pk_mad_sat(uint32_t cnt, uint32_t keep) {
   uint32_t r;
@@ -300,6 +301,9 @@ struct K1Args {
   uint32_t* ev;    // [nchunks, padded to whole items]
   uint32_t* hits;  // [ns] arrivals per accepting state (sampling pass) or null
   uint32_t seg;    // consecutive chunks per chain
+  uint2* rec;      // words with an arrival past the blocks' LDS lists: {batch byte / 16, row before it}
+  uint32_t* rec_n;   // [2] records in rec, blocks done (both zeroed per launch)
+  uint32_t rec_cap;  // >= the batch's 16-byte words
 };
 
 // one chain = one segment of consecutive chunks: automaton row, run counters, the running
@@ -352,6 +356,31 @@ __device__ __forceinline__ uint32_t word_of(const uint4 v, int k) {  // (k const
   return k < 4 ? v.x : k < 8 ? v.y : k < 12 ? v.z : v.w;
 }
 
+// K1 arrival in reporting row r at batch byte q: keyword bits of q's file (each keyword only
+// if it starts inside that file), event bits of the chunk (into evl)
+__device__ __forceinline__ void k1_accept(const DevK1& d, const K1Args& A, uint32_t& evl, uint32_t r, uint64_t q) {
+  const uint32_t id = r / d.row_unit;
+  if (A.hits && q < A.total) atomicAdd(&A.hits[id], 1u);
+  const uint32_t* m = d.masks + (size_t)d.accs[id] * d.mw;
+  evl |= m[d.kw_words];
+  if (q >= A.total) return;
+  const uint32_t f = file_of(A.cf, A.off, A.nfiles, q);
+  const uint64_t avail = q - A.off[f] + 1;  // bytes of f up to and including q
+  uint32_t* kwf = A.kw + (size_t)f * d.kw_words;
+  for (uint32_t w = 0; w < d.kw_words; w++) {
+    uint32_t bits = m[w];
+    if (!bits) continue;
+    if (avail < d.kw_maxlen) {
+      for (uint32_t t = bits; t; t &= t - 1) {
+        const uint32_t k = __builtin_ctz(t);
+        if (d.kw_len[w * 32 + k] > avail) bits &= ~(1u << k);
+      }
+      if (!bits) continue;
+    }
+    atomicOr(&kwf[w], bits);
+  }
+}
+
 template <int KWW, bool PACKED, bool REP>
 struct K1Lane {
   const DevK1& d;
@@ -360,6 +389,9 @@ struct K1Lane {
   const uint8_t* s_tab;   // legacy: the transition table
   const uint32_t* s_cls;  // legacy: this lane's column of the class words (REP) or the table
   uint32_t lane8;         // packed: (lane % 32) * 8
+  uint2* s_rec;           // the block's list of words with an arrival (LDS), and its length
+  uint32_t* s_nrec;
+  uint32_t rec_lds;       // its capacity
 
   // byte k (0..3) of dword w: the chain's row s and run counters cnt step once
   __device__ __forceinline__ void step(uint32_t& s, uint32_t& cnt, uint32_t w, int k) const {
@@ -375,47 +407,8 @@ struct K1Lane {
       cnt = run_step(cnt, m);
     }
   }
-  // arrival in reporting row r with batch byte q: keyword bits of q's file (each keyword
-  // only if it starts inside that file), event bits of the chain's chunk
-  __device__ __forceinline__ void accept(K1Chain& c, uint32_t r, uint64_t q) {
-    const uint32_t id = r / d.row_unit;
-    if (A.hits && q < A.total) atomicAdd(&A.hits[id], 1u);
-    const uint32_t* m = d.masks + (size_t)d.accs[id] * d.mw;
-    c.evl |= m[d.kw_words];
-    if (q >= A.total) return;
-    const uint32_t f = file_of(A.cf, A.off, A.nfiles, q);
-    const uint64_t avail = q - A.off[f] + 1;  // bytes of f up to and including q
-    uint32_t* kwf = A.kw + (size_t)f * d.kw_words;
-    for (uint32_t w = 0; w < d.kw_words; w++) {
-      uint32_t bits = m[w];
-      if (!bits) continue;
-      if (avail < d.kw_maxlen) {
-        for (uint32_t t = bits; t; t &= t - 1) {
-          const uint32_t k = __builtin_ctz(t);
-          if (d.kw_len[w * 32 + k] > avail) bits &= ~(1u << k);
-        }
-        if (!bits) continue;
-      }
-      atomicOr(&kwf[w], bits);
-    }
-  }
   __device__ __forceinline__ uint32_t run_bits(uint32_t mx) const {
     return ((mx >> 16) >= d.kU ? kEvRunU : 0u) | ((mx & 0xFFFFu) >= d.kD ? kEvRunD : 0u);
-  }
-  // the word at batch byte p again, byte by byte from row s, reporting every arrival
-  __device__ __forceinline__ void replay16(K1Chain& c, uint32_t s, const uint4 v, uint64_t p) {
-    uint32_t cnt = 0;
-#pragma unroll 1
-    for (uint32_t k = 0; k < 16; k++) {
-      const uint32_t w = k < 4 ? v.x : k < 8 ? v.y : k < 12 ? v.z : v.w;
-      if constexpr (PACKED) {
-        const u32x2 e = *(const u32x2*)(smem + ((((w >> (8 * (k & 3))) & 0xFFu) << 8) | lane8));
-        s = *(const uint16_t*)(smem + s + e.x);
-      } else {
-        step(s, cnt, w, (int)(k & 3));
-      }
-      if (s >= d.acc_row) accept(c, s, p + k);
-    }
   }
   // NS chains, 16 bytes each, interleaved byte by byte (fully unrolled: constant byte
   // positions); a word in which a chain reached a reporting row is replayed on the rare
@@ -429,21 +422,50 @@ struct K1Lane {
       top[i] = 0;
     }
 #pragma unroll
-    for (int k = 0; k < 16; k++) {
+    for (int k = 0; k < 16; k++)
 #pragma unroll
       for (int i = 0; i < NS; i++) {
         step(c[i].s, c[i].cnt, word_of(v[i], k), k & 3);
         top[i] = max(top[i], c[i].s);
         c[i].mx = run_max(c[i].mx, c[i].cnt);
       }
-      // the class reads of K1_GROUP bytes in flight at a time: hoisting all 16 bytes' reads
-      // ahead of the chain (what the scheduler does unbounded) needs 2 registers per byte
-      // and chain and spills at the 128 VGPRs of 4 waves per SIMD
-      if ((k + 1) % K1_GROUP == 0) __builtin_amdgcn_sched_barrier(0);
-    }
 #pragma unroll
-    for (int i = 0; i < NS; i++)
-      if (__builtin_expect(top[i] >= d.acc_row, 0)) replay16(c[i], s0[i], v[i], pos[i]);
+    for (int i = 0; i < NS; i++) defer(top[i] >= d.acc_row && pos[i] < A.total, s0[i], pos[i]);
+  }
+  // A word in which the chain reached a reporting row is recorded {word, row before it} in
+  // the block's LDS list and replayed once the block's items are done (k1_kernel), not
+  // replayed here: a 16-step serial replay that the whole wave would wait for.  Past the LDS
+  // list a record goes to the global list, which the block that finishes last replays.
+  __device__ __forceinline__ void defer(bool hit, uint32_t s0, uint64_t p) {
+    const unsigned long long m = __ballot(hit);
+    if (m == 0) return;
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t leader = (uint32_t)__builtin_ctzll(m);
+    uint32_t base = 0;
+    if (lane == leader) base = atomicAdd(s_nrec, (uint32_t)__popcll(m));
+    base = __shfl(base, (int)leader);
+    if (hit) {
+      const uint32_t idx = base + (uint32_t)__popcll(m & ((1ull << lane) - 1));
+      const uint2 r = make_uint2((uint32_t)(p >> 4), s0);
+      if (idx < rec_lds) {
+        s_rec[idx] = r;
+      } else {
+        const uint32_t g = atomicAdd(A.rec_n, 1u);
+        if (g < A.rec_cap) A.rec[g] = r;
+      }
+    }
+  }
+  // one recorded word again, byte by byte from row s: every arrival sets its keyword bits;
+  // returns the word's event bits
+  __device__ __forceinline__ uint32_t replay(uint32_t s, uint64_t p) const {
+    const uint4 v = *(const uint4*)(A.data + p);
+    uint32_t evl = 0, cnt = 0;
+#pragma unroll 1
+    for (uint32_t k = 0; k < 16; k++) {
+      step(s, cnt, k < 4 ? v.x : k < 8 ? v.y : k < 12 ? v.z : v.w, (int)(k & 3));
+      if (s >= d.acc_row) k1_accept(d, A, evl, s, p + k);
+    }
+    return evl;
   }
 
   // An item = NS segments of A.seg consecutive chunks; quad lane t walks item it0 + t of ib
@@ -483,11 +505,7 @@ struct K1Lane {
     for (int t = 0; t < 4; t++) src[t] = data + (it0 + t < A.nitems ? it0 + t : it0) * ib + 16u * q;
     uint32_t jc = 0;
     uint64_t ci = c0;
-    auto word = [&](uint64_t jw, const uint4 (&v)[NS]) __attribute__((always_inline)) {
-      uint64_t pos[NS];
-#pragma unroll
-      for (int i = 0; i < NS; i++) pos[i] = ghost ? A.total : a + (uint64_t)i * L + jw;
-      fast16<NS>(c, v, pos);
+    auto word_end = [&]() __attribute__((always_inline)) {
       jc += 16;
       if (jc == C) {
         if (!ghost)
@@ -501,6 +519,13 @@ struct K1Lane {
         jc = 0;
         ci++;
       }
+    };
+    auto word = [&](uint64_t jw, const uint4 (&v)[NS]) __attribute__((always_inline)) {
+      uint64_t pos[NS];
+#pragma unroll
+      for (int i = 0; i < NS; i++) pos[i] = ghost ? A.total : a + (uint64_t)i * L + jw;
+      fast16<NS>(c, v, pos);
+      word_end();
     };
     // 64 bytes of every chain at j: transpose, then the 4 words in order (each word's
     // registers picked with constant indices so the arrays stay in VGPRs)
@@ -544,6 +569,11 @@ template <int KWW, bool PACKED, int LDSK, bool REP, int TPB>
 __global__ void __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(4, 8))) k1_kernel(DevK1 d, K1Args A) {
   constexpr int NS = kK1Chains;
   __shared__ __attribute__((aligned(16))) uint8_t smem[LDSK * 1024];
+  // the block's arrival words: what the 160 KiB of LDS leave beside the image, at most 2048
+  constexpr int kRecLds = (160 * 1024 - LDSK * 1024 - 64) / 8 < 2048 ? (160 * 1024 - LDSK * 1024 - 64) / 8 : 2048;
+  __shared__ uint2 s_rec[kRecLds];
+  __shared__ uint32_t s_nrec, s_last;
+  if (threadIdx.x == 0) s_nrec = 0;
   const uint32_t* tsrc = (const uint32_t*)d.tab;
   if constexpr (PACKED) {
     static_assert(LDSK * 1024 >= (int)kK1PTab + 65536, "packed K1 image: 64 KiB of class entries + 64 KiB of rows");
@@ -562,13 +592,67 @@ __global__ void __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(4, 8))
   }
   __syncthreads();
   const uint32_t lane = threadIdx.x & 31;
-  K1Lane<KWW, PACKED, REP> L{d, A, smem, smem + (REP ? kK1RepBytes : 1024), (const uint32_t*)smem + (REP ? lane : 0),
-                             lane * 8};
+  K1Lane<KWW, PACKED, REP> L{d,        A,         smem, smem + (REP ? kK1RepBytes : 1024), (const uint32_t*)smem + (REP ? lane : 0),
+                             lane * 8, s_rec, &s_nrec, (uint32_t)kRecLds};
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   const uint32_t q = threadIdx.x & 3;
   const uint64_t ib = (uint64_t)A.item_step * NS * A.seg * A.chunk;
   for (uint64_t it0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) & ~3ull; it0 < A.nitems; it0 += stride)
     L.template item_quad<NS>(it0, ib, q);
+  // The block's recorded words: after the barrier every event word of the block's chunks
+  // is stored (each chunk belongs to one chain of this block), so the records' event bits
+  // are ORed after them; the replays run from the tables already in LDS.
+  __syncthreads();
+  const uint32_t n = min(s_nrec, (uint32_t)kRecLds);
+  for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
+    const uint64_t p = (uint64_t)s_rec[i].x << 4;
+    const uint32_t evl = L.replay(s_rec[i].y, p);
+    if (evl) atomicOr(&A.ev[p / A.chunk], evl);
+  }
+  // the global list (records past the LDS lists, rare): replayed by the last block to finish,
+  // when every block's event words are stored.  Every block counts itself done (a block that
+  // finished early cannot know whether a later one will append).  The adaptation's sampling
+  // pass, whose list is long, leaves it to k1_list_kernel.
+  if (!A.hits) {
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      __threadfence();
+      s_last = atomicAdd(A.rec_n + 1, 1u) == gridDim.x - 1;
+    }
+    __syncthreads();
+    if (s_last && *(volatile uint32_t*)A.rec_n != 0) {
+      __threadfence();
+      const uint32_t g = min(*(volatile uint32_t*)A.rec_n, A.rec_cap);
+      for (uint32_t i = threadIdx.x; i < g; i += blockDim.x) {
+        const volatile uint32_t* r = (const volatile uint32_t*)(A.rec + i);
+        const uint64_t p = (uint64_t)r[0] << 4;
+        const uint32_t evl = L.replay(r[1], p);
+        if (evl) atomicOr(&A.ev[p / A.chunk], evl);
+      }
+    }
+  }
+}
+
+// The global list of K1's sampling pass (adapt_k1): one record per thread, tables in global
+// memory (L2-resident); after K1, so the event bits are ORed after its stores.
+__global__ void __launch_bounds__(256) k1_list_kernel(DevK1 d, K1Args A) {
+  const uint32_t n = min(*A.rec_n, A.rec_cap);
+  const uint8_t* tab = (const uint8_t*)d.tab;
+  for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < n; e += gridDim.x * blockDim.x) {
+    const uint2 r = A.rec[e];
+    const uint64_t p = (uint64_t)r.x << 4;
+    const uint4 v = *(const uint4*)(A.data + p);
+    uint32_t s = r.y, evl = 0;
+#pragma unroll 1
+    for (uint32_t k = 0; k < 16; k++) {
+      const uint32_t w = k < 4 ? v.x : k < 8 ? v.y : k < 12 ? v.z : v.w;
+      const uint32_t b = (w >> (8 * (k & 3))) & 0xFFu;
+      // packed rows are byte offsets, legacy rows entry indices (DevK1)
+      s = d.packed ? *(const uint16_t*)(tab + s + (d.pcls[2 * b] - kK1PTab)) : *(const uint16_t*)(tab + 2 * s + (d.cls[b] & 0xFFu));
+      if (s >= d.acc_row) k1_accept(d, A, evl, s, p + k);
+    }
+    if (evl) atomicOr(&A.ev[p / A.chunk], evl);
+  }
 }
 
 // ---------------------------------------------------------------- K1X
@@ -1714,7 +1798,15 @@ static int k1_lds_class(size_t tab_bytes) {
 }
 
 // the packed layout holds rows as 16-bit byte offsets: ns * stride u16 entries in 64 KiB
-static bool k1_packed_fits(size_t ns, size_t rs) { return ns * rs * 2 <= 65536; }
+static bool k1_packed_fits(size_t ns, size_t rs) {
+#ifdef K1_LEGACY  // measurement builds: the legacy layout for every automaton
+  (void)ns;
+  (void)rs;
+  return false;
+#else
+  return ns * rs * 2 <= 65536;
+#endif
+}
 
 // Row stride (u16 entries) of the K1 table: the class count padded to 2 mod 4, so a row is
 // an odd number of dwords and equal classes of different rows fall in different LDS banks
@@ -1925,6 +2017,8 @@ struct LaneState {
   const uint8_t* paths = nullptr;
   uint32_t* cf = nullptr;         // coarse file map (file_of)
   size_t cf_cap = 0;
+  uint2* k1rec = nullptr;         // K1's words with an arrival past the blocks' LDS lists
+  size_t k1rec_cap = 0;
   uint32_t* ev_bits = nullptr;
   size_t ev_cap = 0;
   uint2* xlist = nullptr;  // K1X hit records
@@ -1962,7 +2056,7 @@ struct LaneState {
     if (!d) return;
     (void)hipSetDevice(d->device);
     if (st) (void)hipStreamSynchronize(st);
-    void* bufs[] = {data_alloc, meta, cf, ev_bits, xlist, xcount, evlist, kw, ggate, ovf, pathok,
+    void* bufs[] = {data_alloc, meta, cf, k1rec, ev_bits, xlist, xcount, evlist, kw, ggate, ovf, pathok,
                     items, entries, dentries, cand, counts, gcount, cursor, base, kind, gskip, etrace};
     for (void* b : bufs) (void)hipFree(b);
     if (st) (void)hipStreamDestroy(st);
@@ -2018,6 +2112,7 @@ static int launch_k1(DeviceRules* r, const K1Args& A, hipStream_t st) {
   void* args[] = {&d, &a};
   HIP_TRY(hipLaunchKernel(fn, dim3(grid), dim3(threads), args, 0, st));
   HIP_TRY(hipGetLastError());
+  HIP_TRY(hipGetLastError());
   return TSG_OK;
 }
 
@@ -2035,12 +2130,17 @@ static int adapt_k1(DeviceRules* r, LaneState* l, uint64_t total, uint32_t nfile
   const uint64_t step = std::max<uint64_t>(1, k1_items / 16384);
   const uint64_t nsamp = (k1_items + step - 1) / step;
   HIP_TRY(hipMemsetAsync(r->d_hits, 0, sizeof(uint32_t) * ns, l->st));
+  HIP_TRY(hipMemsetAsync(l->counts + 14, 0, 2 * sizeof(uint32_t), l->st));
   K1Args A{l->data_alloc + kPad, l->off, l->cf, total, nchunks, nsamp, step, r->chunk,
-           nfiles, l->kw, l->ev_bits, r->d_hits, (uint32_t)kK1Seg};
+           nfiles, l->kw, l->ev_bits, r->d_hits, (uint32_t)kK1Seg, l->k1rec, l->counts + 14,
+           (uint32_t)std::min<size_t>(l->k1rec_cap, 0xFFFFFFFFu)};
   int rc;
   if ((rc = launch_k1(r, A, l->st))) return rc;
+  k1_list_kernel<<<r->grid, 256, 0, l->st>>>(r->k1, A);  // the sampling pass's global list
+  HIP_TRY(hipGetLastError());
   std::vector<uint32_t> hits(ns);
   HIP_TRY(hipMemcpyAsync(hits.data(), r->d_hits, sizeof(uint32_t) * ns, hipMemcpyDeviceToHost, l->st));
+  HIP_TRY(hipMemsetAsync(l->counts + 14, 0, 2 * sizeof(uint32_t), l->st));  // (the real pass records anew)
   HIP_TRY(hipStreamSynchronize(l->st));
   r->adapted = true;
   const uint64_t sample_bytes = nsamp * kK1Chains * A.seg * r->chunk;
@@ -2306,6 +2406,10 @@ int enqueue_scan(DeviceRules* r, LaneState* l, const ScanInput& in, HostOut* out
   const uint64_t nchunks_pad = (nchunks + k1_item_chunks - 1) / k1_item_chunks * k1_item_chunks + 1;
   const uint64_t ncf = (total >> kCfShift) + 2;
   if ((rc = ensure(&l->cf, &l->cf_cap, (size_t)ncf))) return rc;
+  // K1 arrival words: at most one record per 16-byte word of the batch (8 B per 16: HBM is
+  // plentiful, and only the records written are traffic; the adaptation keeps them near one
+  // per 4 KiB), so the list never overflows
+  if ((rc = ensure(&l->k1rec, &l->k1rec_cap, (size_t)(total / 16 + 16)))) return rc;
   if ((rc = ensure(&l->ev_bits, &l->ev_cap, (size_t)nchunks_pad))) return rc;
   // K1X hit records: one per 256 bytes (a lane-word with a hit past that verifies inline)
   if (r->has_k1x && (rc = ensure(&l->xlist, &l->xlist_cap, (size_t)(total / 256 + 65536)))) return rc;
@@ -2392,7 +2496,8 @@ int enqueue_scan(DeviceRules* r, LaneState* l, const ScanInput& in, HostOut* out
   if (!r->adapted && k1_items >= 64 && total >= adapt_bytes)
     if ((rc = adapt_k1(r, l, total, F, nchunks, k1_items))) return rc;
   if (k1_items) {
-    K1Args A{data, l->off, l->cf, total, nchunks, k1_items, 1, C, F, l->kw, l->ev_bits, nullptr, (uint32_t)kK1Seg};
+    K1Args A{data, l->off, l->cf, total, nchunks, k1_items, 1, C, F, l->kw, l->ev_bits, nullptr, (uint32_t)kK1Seg,
+             l->k1rec, l->counts + 14, (uint32_t)std::min<size_t>(l->k1rec_cap, 0xFFFFFFFFu)};
     if ((rc = launch_k1(r, A, st))) return rc;
   }
   if (r->has_k1x && total) {  // the hashed literals of a large rule set, after K1's stores

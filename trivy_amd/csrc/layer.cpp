@@ -31,6 +31,21 @@
 
 #include "internal.hpp"
 
+namespace tsg {
+namespace {
+// open / openat that waits out a full descriptor table (EMFILE / ENFILE: concurrent walks
+// of wide trees, each holding directory and file descriptors) instead of treating it as an
+// unreadable file, which the walk would skip; another error is returned as it is
+int open_at_retry(int dfd, const char* path, int flags) {
+  for (int tries = 0;; tries++) {
+    const int fd = dfd >= 0 ? openat(dfd, path, flags) : open(path, flags);
+    if (fd >= 0 || (errno != EMFILE && errno != ENFILE) || tries >= 5000) return fd;
+    std::this_thread::sleep_for(std::chrono::microseconds(500));
+  }
+}
+}  // namespace
+}  // namespace tsg
+
 struct tsg_layer {
   std::unique_ptr<uint8_t[]> data;  // not zero-filled: every byte is copied in
   const uint8_t* ext = nullptr;     // the kept files in a context's pinned slot (*_pack_slot)
@@ -1213,8 +1228,7 @@ int fs_collect(const tsg_ruleset* rs, const char* root, const char* const* skip_
         }
         return true;
       }
-      const int fd = dfd >= 0 ? openat(dfd, name, O_RDONLY | O_NOFOLLOW | O_CLOEXEC)
-                              : open(path.c_str(), O_RDONLY | O_NOFOLLOW | O_CLOEXEC);
+      const int fd = open_at_retry(dfd, dfd >= 0 ? name : path.c_str(), O_RDONLY | O_NOFOLLOW | O_CLOEXEC);
       if (fd < 0) return true;  // analyzer.go:411-413: a permission error skips the file
       struct stat fs2;
       if (fstat(fd, &fs2) != 0 || !S_ISREG(fs2.st_mode)) {  // (replaced since the listing)
@@ -1243,10 +1257,12 @@ int fs_collect(const tsg_ruleset* rs, const char* root, const char* const* skip_
         if (f) files.push_back(std::move(f));
       }
     }
-    // 1. the walk, one level of directories at a time (at most kDirs open at once): the
+    // 1. the walk, one level of directories at a time (at most kDirs open at once, so that
+    // concurrent walks stay well inside a 1024-descriptor limit; a full table is waited out,
+    // open_at_retry): the
     // level's directories listed in parallel (d_type; lstat only where the file system
     // does not say), then its regular files opened relative to their directory, in parallel
-    constexpr size_t kDirs = 256;
+    constexpr size_t kDirs = 64;
     struct Dir {
       DIR* d = nullptr;
       int err = 0;                                  // open errno (not EACCES)
@@ -1266,7 +1282,7 @@ int fs_collect(const tsg_ruleset* rs, const char* root, const char* const* skip_
           const std::string& path = level[l0 + i];
           Dir& v = dirs[i];
           if (skip_dir(path)) return;
-          const int fd = open(path.c_str(), O_RDONLY | O_DIRECTORY | O_NOFOLLOW | O_CLOEXEC);
+          const int fd = open_at_retry(-1, path.c_str(), O_RDONLY | O_DIRECTORY | O_NOFOLLOW | O_CLOEXEC);
           if (fd < 0 || !(v.d = fdopendir(fd))) {
             if (fd >= 0) close(fd);
             // fs.go:48-55: permission errors are ignored; so is a directory gone (or
@@ -1352,7 +1368,7 @@ uint64_t fs_fill(FsFile& f, uint8_t* dst) {
     if (f.got) std::memcpy(dst, f.head.data(), f.got);
     return f.got;
   }
-  const int fd = open(f.full.c_str(), O_RDONLY);
+  const int fd = open_at_retry(-1, f.full.c_str(), O_RDONLY | O_CLOEXEC);
   const uint64_t r = fd < 0 ? 0 : read_upto(fd, dst, f.got);
   if (fd >= 0) close(fd);
   return r;
@@ -1431,7 +1447,7 @@ extern "C" int tsg_fs_pack_shard(const tsg_ruleset* rs, const char* root, const 
     std::vector<uint8_t> keep(mine.size(), 0);
     tsg::pool_for(mine.size(), 16, [&](size_t k) {
       const tsg::FsFile& f = *files[mine[k]];
-      const int fd = open(f.full.c_str(), O_RDONLY | O_NOFOLLOW | O_CLOEXEC);
+      const int fd = tsg::open_at_retry(-1, f.full.c_str(), O_RDONLY | O_NOFOLLOW | O_CLOEXEC);
       if (fd < 0) return;  // analyzer.go:411-413: a permission error skips the file
       body[k].resize(f.size);
       body[k].resize(tsg::read_upto(fd, body[k].data(), f.size));
@@ -1504,7 +1520,7 @@ extern "C" int tsg_fs_scan(tsg_ctx* ctx, const char* root, const char* const* sk
     std::vector<uint8_t> drop(kept.size(), 0);
     rc = tsg::scan_in_pieces(ctx, L.get(), [&](size_t k, uint8_t* dst) -> uint64_t {
       const tsg::FsFile& f = *files[kept[k]];
-      const int fd = open(f.full.c_str(), O_RDONLY | O_NOFOLLOW | O_CLOEXEC);
+      const int fd = tsg::open_at_retry(-1, f.full.c_str(), O_RDONLY | O_NOFOLLOW | O_CLOEXEC);
       if (fd < 0) {  // analyzer.go:411-413: a permission error skips the file
         drop[k] = 1;
         return 0;

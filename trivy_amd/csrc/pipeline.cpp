@@ -24,6 +24,7 @@
 #include <deque>
 #include <functional>
 #include <map>
+#include <set>
 #include <memory>
 #include <mutex>
 #include <thread>
@@ -108,14 +109,24 @@ struct tsg_ctx {
   std::vector<char> out_busy;
   std::map<uint64_t, std::shared_ptr<Batch>> pending;  // submitted, uncollected, by ticket
   uint64_t next_ticket = 1;
-  int jobs = 0;                                // host job threads running (any API)
+  int jobs = 0;                                // host jobs submitted and not finished (any API)
   tsg_stats stats{};
+  // completion threads: a fixed set (one per device lane; 4 for an emulated context) takes
+  // the submitted host jobs in order; each job waits for its batch's device completion,
+  // then resolves it on the process-wide pool
+  std::deque<std::function<void()>> jq;
+  std::vector<std::thread> workers;
+  bool stopping = false;
+  std::multiset<std::thread::id> slot_waiters;  // threads waiting in slot_take
 
   ~tsg_ctx() {
     {
       std::unique_lock<std::mutex> lk(m);
       cv.wait(lk, [&] { return jobs == 0; });
+      stopping = true;
     }
+    cv.notify_all();
+    for (auto& t : workers) t.join();
     if (!emulate) (void)hipSetDevice(device);
     for (auto* l : lanes) lane_destroy(l);
     for (auto& o : outs) host_out_free(&o);
@@ -204,14 +215,22 @@ int slot_take(tsg_ctx* c, std::unique_lock<std::mutex>& lk, int owner, uint64_t 
       *id = (uint32_t)pick;
       return TSG_OK;
     }
-    // nothing will free a slot if no job is running and every slot is held by this very
-    // thread (a queue batch's slot is submitted as soon as its last writer is done; other
-    // threads release theirs)
-    bool others = false;
+    // Nothing will free a slot if no job is running and every held slot's holder is this
+    // thread or another thread that is itself waiting here (two callers that each hold a
+    // slot and ask for another): fail instead of waiting forever.  (A queue batch's slot is
+    // submitted as soon as its last writer is done; an upload's holder is copying.)
     const auto me = std::this_thread::get_id();
-    for (const auto& sl : c->slots) others |= sl->owner == kQueue || (sl->owner != kFree && sl->holder != me);
-    if (c->jobs == 0 && !others) return fail(TSG_ERR_ARG, "every pinned slot is held by the caller");
+    bool progress = c->jobs != 0;
+    for (const auto& sl : c->slots) {
+      if (sl->owner == kFree) continue;
+      progress |= sl->owner == kQueue || sl->owner == kUpload ||
+                  (sl->holder != me && !c->slot_waiters.count(sl->holder));
+    }
+    if (!progress)
+      return fail(TSG_ERR_ARG, "every pinned slot is held by a caller that is waiting for another slot");
+    c->slot_waiters.insert(me);
     c->cv.wait(lk);
+    c->slot_waiters.erase(c->slot_waiters.find(me));
   }
 }
 
@@ -274,6 +293,7 @@ void update_stats(tsg_ctx* c, const Batch& b) {
   s.k2_tail_max = b.counts[9];
   s.k2_long_tails = b.counts[10];
   s.k2_replays = b.counts[11];
+  s.k1_records = b.counts[14];
   s.k1_hot_states = c->dr ? device_rules_hot_states(c->dr) : 0;
   s.batches++;
   s.sum_bytes += b.bytes;
@@ -351,13 +371,28 @@ void run_job(tsg_ctx* c, std::shared_ptr<Batch> b, BatchView view, HostOut ho,
   }
   b.reset();  // (the last reference may be this thread's)
   std::lock_guard<std::mutex> g(c->m);
-  c->jobs--;  // after this the context may be destroyed: nothing below touches it
+  c->jobs--;  // after this the context may be destroyed: only its completion thread (joined
+              // by the destructor) touches it again
   c->cv.notify_all();
 }
 
-// submit nfiles files of slot `sid` (lock held); the job runs on a thread of its own,
-// which mostly waits for the lane's completion event (the resolution itself fans out on
-// the process-wide pool)
+// a completion thread of the context: takes queued host jobs until the context stops
+void job_worker(tsg_ctx* c) {
+  std::unique_lock<std::mutex> lk(c->m);
+  for (;;) {
+    c->cv.wait(lk, [&] { return c->stopping || !c->jq.empty(); });
+    if (c->jq.empty()) return;  // stopping, nothing left
+    auto job = std::move(c->jq.front());
+    c->jq.pop_front();
+    lk.unlock();
+    job();
+    lk.lock();
+  }
+}
+
+// submit nfiles files of slot `sid` (lock held); the job is queued for the context's
+// completion threads, where it mostly waits for the lane's completion event (the
+// resolution itself fans out on the process-wide pool)
 int submit_locked(tsg_ctx* c, uint32_t sid, uint32_t nfiles, bool keep_result,
                   std::function<void(const std::shared_ptr<Batch>&)> on_done, std::shared_ptr<Batch>* out) {
   Slot& s = *c->slots[sid];
@@ -386,16 +421,17 @@ int submit_locked(tsg_ctx* c, uint32_t sid, uint32_t nfiles, bool keep_result,
   s.inflight++;
   c->jobs++;
   try {
-    std::thread(run_job, c, b, view, ho, kwu).detach();
-  } catch (const std::exception& ex) {  // no thread: the enqueued device work is waited for here
+    c->jq.push_back([c, b, view, ho, kwu] { run_job(c, b, view, ho, kwu); });
+  } catch (const std::exception& ex) {  // no room: the enqueued device work is waited for here
     s.inflight--;
     c->jobs--;
     if (b->out >= 0) {
       (void)hipEventSynchronize(ho.ev[kEvDone]);
       c->out_busy[b->out] = 0;
     }
-    return fail(TSG_ERR_INTERNAL, std::string("cannot start a batch job: ") + ex.what());
+    return fail(TSG_ERR_INTERNAL, std::string("cannot queue a batch job: ") + ex.what());
   }
+  c->cv.notify_all();
   b->ticket = c->next_ticket++;
   *out = b;
   return TSG_OK;
@@ -565,6 +601,8 @@ int tsg_ctx_create(int device, const tsg_ruleset* rs, const tsg_ctx_options* opt
         c->lanes.push_back(l);
       }
     }
+    const size_t nw = c->emulate ? 4 : c->lanes.size();
+    for (size_t i = 0; i < nw; i++) c->workers.emplace_back(job_worker, c.get());
     *out = c.release();
     return TSG_OK;
   });

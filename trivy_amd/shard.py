@@ -88,9 +88,21 @@ def scan_layer_sharded(analyzer, tar, rank, world, dist=None, device=None, emula
             return [v for _, v in out]
 
         holder = {}
-        guarded(lambda: holder.setdefault("rng", LayerRange(tar, rank, world)) and None)
+
+        def make_range():
+            holder["rng"] = LayerRange(tar, rank, world)
+            return None
+        guarded(make_range)
         rng = holder["rng"]
-        guarded(lambda: layer_chain(rng, rank, world, allgather) and None)
+        # every rank's range info, gathered in a guarded step of its own: inside layer_chain
+        # every collective is then entered by all ranks (its only failures are raised on
+        # every rank, after the same all-gathers)
+        infos = guarded(lambda: rng.info)
+
+        def chain():
+            holder["pos"] = layer_chain(rng, rank, world, allgather, infos=infos)
+            return None
+        guarded(chain)
         dirs = guarded(lambda: rng.dirs(skip_dirs))
         prior = [d for r in range(rank) for d in dirs[r]]
 

@@ -334,11 +334,12 @@ def layer_chain_step(infos, confirmed):
     return ("done", out)
 
 
-def layer_chain(rng, rank, world, allgather):
+def layer_chain(rng, rank, world, allgather, infos=None):
     """Fix the true chain across ranks (allgather(obj) -> list over ranks) and sync `rng` to
     it; returns this rank's entry position.  Raises the archive error of the chain on every
-    rank, as one sequential walk fails."""
-    infos = allgather(rng.info)
+    rank, as one sequential walk fails.  infos: every rank's rng.info, when already gathered."""
+    if infos is None:
+        infos = allgather(rng.info)
     confirmed = {}
     while True:
         st = layer_chain_step(infos, confirmed)
