@@ -471,3 +471,90 @@ def test_pipelined_layer_and_fs_scan_gpu(tmp_path):
     assert paths == [ref.batch.path(i) for i in range(ref.batch.nfiles)]
     assert res == sc.ScanBatch(ref.batch, nthreads=16)
     ctx.close()
+
+
+def _plant_lines(data, plants):
+    """(rule, start line) of each planted secret, counted independently of the scanner.
+    Lines are numbered on the censored content (scanner.go:389-392, 445-502; the multi-line
+    private-key fixture of scanner_test.go:476-496): each private-key block's secret group
+    (its newline after BEGIN, the six body lines and the newline before END) becomes one
+    line of '*', so every later plant moves up 7 lines per block before it."""
+    rules = {"github": "github-pat", "aws": "aws-access-key-id", "slack": "slack-access-token"}
+    out = set()
+    pems = sorted(at for name, at in plants.items() if name not in rules)
+    for name, at in plants.items():
+        rule = rules.get(name, "private-key")
+        # the secret's line: the plant starts with a newline except the first one
+        first = at + (0 if at == 0 else 1)
+        before = sum(1 for p in pems if p < at)
+        out.add((rule, data.count(b"\n", 0, first) + 1 - 7 * before))
+    return out
+
+
+def test_layer_large_entries_gpu():
+    """configs[2]'s large entries ("some entries >= 200 MiB",
+    walker/tar.go:137-167 spills them to a temp file; here they are one piece of their own
+    in a grown pinned slot): a seeded layer with a 200 MiB and a 24 MiB text entry through
+    tsg_layer_scan.  Every file equals the exact CPU path except the 200 MiB one (the exact
+    path takes minutes on one file), which equals the GPU algorithm emulated on the CPU and
+    holds exactly the planted findings at their independently counted lines: the first
+    line, the middle, private-key blocks across the 2 MiB / 16 MiB / middle boundaries,
+    and the last bytes of the file."""
+    from trivy_amd import analyzer as A
+    from trivy_amd import configs
+    from trivy_amd import walker as W
+    an = A.SecretAnalyzer()
+    an.Init("")
+    sc = an.scanner
+    big = (200 << 20, 24 << 20)
+    tar = configs.layer_tar(8 << 20, seed=9, binary_frac=0.05, big=big)
+    ctx = S.GpuContext(sc, 0)
+    ref = W.NativeLayer(sc, tar)
+    paths, res, opq, wh, walked = W.scan_layer_pipelined(ctx, tar)
+    ctx.close()
+    want_paths = [ref.batch.path(i) for i in range(ref.batch.nfiles)]
+    assert paths == want_paths and (opq, wh, walked) == (ref.opq, ref.wh, ref.walked)
+    bigi = [want_paths.index("/opt/big/text%d.log" % k) for k in range(len(big))]
+    b = ref.batch
+    small = [i for i in range(b.nfiles) if i != bigi[0]]
+    sub = S.Batch.from_args([S.ScanArgs(b.path(i), bytes(b.data[int(b.offsets[i]):int(b.offsets[i + 1])]))
+                             for i in small])
+    exact = sc.ScanBatch(sub, nthreads=16)
+    assert [res[i] for i in small] == exact
+    for k, size in enumerate(big):
+        i = bigi[k]
+        data, plants = configs.big_text(size, seed=9 + k)
+        assert bytes(b.data[int(b.offsets[i]):int(b.offsets[i + 1])]) == data
+        got = res[i]
+        assert {(f["RuleID"], f["StartLine"]) for f in got["Findings"]} == _plant_lines(data, plants)
+        if k == 0:
+            emu = sc.ScanBatch(S.Batch.from_args([S.ScanArgs(paths[i], data)]), emulate_chunk=256)
+            assert [got] == emu
+
+
+def test_file_larger_than_slot_gpu():
+    """A file larger than the context's pinned slot (slot_mib=1: a 3 MiB file, and a 1 MiB
+    one just over it) gets a piece of its own; the slot and the lane's HBM buffers grow on
+    the device (layer.cpp scan_in_pieces, tsg_slot_acquire).  Every file == the oracle."""
+    from oracle import secret as O
+    from trivy_amd import analyzer as A
+    from trivy_amd import configs
+    from trivy_amd import walker as W
+    an = A.SecretAnalyzer()
+    an.Init("")
+    sc = an.scanner
+    tar = configs.layer_tar(2 << 20, seed=12, binary_frac=0.0, big=(3 << 20, (1 << 20) + 4096))
+    ctx = S.GpuContext(sc, 0, slot_mib=1)
+    paths, res, _, _, _ = W.scan_layer_pipelined(ctx, tar)
+    ctx.close()
+    ref = W.NativeLayer(sc, tar)
+    b = ref.batch
+    assert paths == [b.path(i) for i in range(b.nfiles)]
+    osc = O.NewScanner(None)
+    nfind = 0
+    for i in range(b.nfiles):
+        c = bytes(b.data[int(b.offsets[i]):int(b.offsets[i + 1])])
+        want = canon_secret(osc.Scan(paths[i], c))
+        assert canon_secret(res[i]) == want, paths[i]
+        nfind += len(want["Findings"] or [])
+    assert "/opt/big/text0.log" in paths and nfind > 20

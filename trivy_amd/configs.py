@@ -136,11 +136,65 @@ def mixed_batch(doc, nbytes, seed, plants_per_file=0.3, binary_frac=0.0):
     return args
 
 
-def layer_tar(nbytes, seed=3, binary_frac=0.05):
+_LOREM = (b"lorem ipsum dolor sit amet consectetur adipiscing elit sed do eiusmod tempor "
+          b"incididunt ut labore et dolore magna aliqua enim ad minim veniam quis nostrud "
+          b"exercitation ullamco laboris nisi aliquip ex ea commodo consequat duis aute irure in "
+          b"reprehenderit voluptate velit esse cillum fugiat nulla pariatur excepteur sint "
+          b"occaecat cupidatat non proident sunt culpa qui officia deserunt mollit anim id est "
+          b"laborum").split()
+
+
+def big_text(nbytes, seed=7):
+    """A large text entry ("some entries >= 200 MiB"): filler words
+    that hold no rule keyword, and secrets planted at known places: a GitHub token in the
+    first line, an AWS key at the middle, private-key blocks straddling the 2 MiB / 16 MiB /
+    middle offsets (K1 segments, K2 chunks and items, ingest pieces all break inside them),
+    a Slack token near the end and a private-key block whose END line is the file's last
+    bytes.  Returns (bytes, {plant name: byte offset})."""
+    rng = np.random.default_rng(seed)
+    idx = rng.integers(0, len(_LOREM), size=nbytes // 5 + 16)
+    parts, n = [], 0
+    for k, i in enumerate(idx):
+        w = _LOREM[i] + (b"\n" if k % 12 == 11 else b" ")
+        parts.append(w)
+        n += len(w)
+        if n >= nbytes:
+            break
+    buf = bytearray(b"".join(parts)[:nbytes])
+    alnum = string.ascii_letters + string.digits
+    upper = string.ascii_uppercase + "234567"
+    b64 = string.ascii_letters + string.digits + "+/"
+
+    def pem():
+        lines = ["".join(rng.choice(list(b64), size=64)) for _ in range(6)]
+        return ("-----BEGIN RSA PRIVATE KEY-----\n" + "\n".join(lines) + "\n-----END RSA PRIVATE KEY-----").encode()
+
+    plants = {}
+
+    def put(name, at, blob):
+        at = max(0, min(at, len(buf) - len(blob)))
+        buf[at:at + len(blob)] = blob
+        plants[name] = at
+    put("github", 0, ("GITHUB_TOKEN=ghp_%s\n" % "".join(rng.choice(list(alnum), size=36))).encode())
+    put("aws", nbytes // 2 + 4096, ("\naws_access_key_id = AKIA%s\n" % "".join(rng.choice(list(upper), size=16))).encode())
+    for name, at in (("pem_2mib", 2 << 20), ("pem_16mib", 16 << 20), ("pem_mid", nbytes // 2)):
+        if at + 1024 < nbytes:
+            blob = b"\n" + pem() + b"\n"
+            put(name, at - len(blob) // 2, blob)
+    put("slack", nbytes - 4096, ("\nSLACK=xoxb-%s-%s-%s\n" % (
+        "".join(rng.choice(list(string.digits), size=12)), "".join(rng.choice(list(string.digits), size=12)),
+        "".join(rng.choice(list(alnum), size=24)))).encode())
+    blob = b"\n" + pem()
+    put("pem_end", len(buf) - len(blob), blob)
+    return bytes(buf), plants
+
+
+def layer_tar(nbytes, seed=3, binary_frac=0.05, big=()):
     """configs[2] (SURVEY.md §8d "Config 3"): an uncompressed image-layer tar built from the
     seeded corpus, with directory entries, symlinks/hardlinks (no content), whiteouts,
     an opaque marker, a system dir (`proc/`, skipped by the walker), `.git` and
-    `node_modules` trees, binary blobs and PAX long names.  Returns the tar bytes."""
+    `node_modules` trees, binary blobs and PAX long names; `big`: sizes of large text entries
+    (big_text), written between the corpus files.  Returns the tar bytes."""
     import io
     import tarfile
     from trivy_amd import corpus
@@ -192,6 +246,13 @@ def layer_tar(nbytes, seed=3, binary_frac=0.05):
                 if rng.random() < 0.5:
                     blob = c[:300].replace(b"\0", b" ") + blob
                 add(tf, "blob/%d.dat" % i, tarfile.REGTYPE, blob)
+            for k, size in enumerate(big):
+                if i == (k + 1) * base.nfiles // (len(big) + 1):
+                    if "opt/big" not in dirs:
+                        dirs.add("opt/big")
+                        add(tf, "opt/", tarfile.DIRTYPE)
+                        add(tf, "opt/big/", tarfile.DIRTYPE)
+                    add(tf, "opt/big/text%d.log" % k, tarfile.REGTYPE, big_text(size, seed=seed + k)[0])
         add(tf, "etc/.wh..wh..opq", tarfile.REGTYPE)
         add(tf, "etc/.wh.hostname", tarfile.REGTYPE)
     return buf.getvalue()
