@@ -351,6 +351,11 @@ def main():
                          "(Required, IsBinary), packs straight into a pinned slot and scans")
     ap.add_argument("--e2e-mib", type=int, default=0, help="e2e input size (default fs 200, layer 2048)")
     ap.add_argument("--e2e-slot-mib", type=int, default=0, help="e2e piece / slot size (0: 256)")
+    ap.add_argument("--binary-frac", type=float, default=0.0,
+                    help="e2e fs: share of the tree's bytes that are binary blobs (configs[4]: 0.3)")
+    ap.add_argument("--binary-text-head", type=float, default=0.5,
+                    help="e2e fs: share of the binary blobs that start with 300 bytes of text, so "
+                         "IsBinary passes them to Scan (configs[4]: 0.5)")
     ap.add_argument("--piece-mib", type=int, default=0,
                     help="e2e: piece floor of tsg_fs_scan / tsg_layer_scan (the 'piece_mib' test knob; "
                          "0: the library's 160)")
@@ -593,18 +598,31 @@ def main_e2e(args):
     L = N.lib()
     if args.piece_mib:
         N.knob("piece_mib", args.piece_mib)
+    tmp = tempfile.mkdtemp(prefix="tsg_e2e_")
     an = A.SecretAnalyzer()
-    an.Init("")
+    extra = None
+    if args.rules == "builtin":
+        an.Init("")
+    else:  # the rule set as a trivy-secret.yaml outside the scanned input (secret.go:62-76)
+        import numpy as np
+        import yaml
+        doc = configs.user_rules_doc(1000, seed=4) if args.rules == "user1000" else configs.allow_exclude_doc()
+        cfg_path = os.path.join(tmp, "trivy-secret.yaml")
+        with open(cfg_path, "w") as f:
+            yaml.safe_dump(doc, f)
+        an.Init(cfg_path)
+        extra = rule_set(args.rules)[1]
     sc = an.scanner
     mib = args.e2e_mib or (200 if args.e2e == "fs" else 2048)
-    tmp = None
     cfg = an.configPath.encode()
     none = (C.c_char_p * 1)()
     t0 = time.perf_counter()
+    tree_info = None
     if args.e2e == "fs":
-        tmp = tempfile.mkdtemp(prefix="tsg_e2e_")
         root = os.path.join(tmp, "tree")
-        configs.source_tree(root, mib << 20, seed=args.seed)
+        tree_info = configs.source_tree(root, mib << 20, seed=args.seed, binary_frac=args.binary_frac,
+                                        binary_text_head=args.binary_text_head, extra_plants=extra,
+                                        extra_per_mib=2.0 if extra else 0.0)
         in_bytes = sum(os.path.getsize(os.path.join(d, f)) for d, _, fs in os.walk(root) for f in fs)
 
         def one_call(ctx, out):
@@ -612,8 +630,12 @@ def main_e2e(args):
             N.check(L.tsg_fs_scan(ctx.handle, root.encode(), none, 0, none, 0, cfg, C.byref(h), C.byref(out)))
             L.tsg_layer_free(h)
         unpiped = lambda ctx: W.SlotIngest.fs(ctx, root, config_path=an.configPath)  # noqa: E731
-        ref = W.NativeFS(sc, root)
+        ref = W.NativeFS(sc, root, config_path=an.configPath)
         what = "seeded source tree on local disk (page cache warm), %d MiB, configs[0] shape" % mib
+        if args.binary_frac:
+            what += ("; %.0f%% of the bytes binary blobs (%d files, %d with a text head that IsBinary "
+                     "passes, the rest dropped), configs[4] mix" % (
+                         100 * args.binary_frac, tree_info["binary_files"], tree_info["binary_text_head_files"]))
     else:
         tar = configs.layer_tar(mib << 20, seed=args.seed)
         in_bytes = len(tar)
@@ -626,10 +648,10 @@ def main_e2e(args):
                                      C.byref(h), C.byref(out)))
             L.tsg_layer_free(h)
         unpiped = lambda ctx: W.SlotIngest.layer(ctx, tar, config_path=an.configPath)  # noqa: E731
-        ref = W.NativeLayer(sc, tar)
+        ref = W.NativeLayer(sc, tar, config_path=an.configPath)
         what = "seeded uncompressed layer tar in host memory, %d MiB, configs[2] shape" % mib
     gen_s = time.perf_counter() - t0
-    ctx = S.GpuContext(sc, 0, host_threads=args.host_threads, slot_mib=args.e2e_slot_mib)
+    ctx = S.GpuContext(sc, 0, host_threads=args.host_threads, slot_mib=args.e2e_slot_mib, emulate=args.emulate)
     scanned = int(ref.batch.offsets[-1])
 
     def step(check=False):
@@ -665,16 +687,17 @@ def main_e2e(args):
     L.tsg_result_free(out)
     g.release()
     ctx.close()
-    if tmp:
-        shutil.rmtree(tmp, ignore_errors=True)
+    shutil.rmtree(tmp, ignore_errors=True)
     line = {"metric": "end-to-end secret scan (ingest + scan) GB/s of input, 1 MI355X",
             "value": round(in_bytes * args.steps / dt / 1e9, 3), "unit": "GB/s", "n_gpus": 1,
             "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(dt / args.steps * 1e3, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "u8",
             "data": "synthetic: " + what,
-            "config": {"workload": "e2e-" + args.e2e, "input_bytes": in_bytes, "scanned_bytes": scanned,
+            "config": {"workload": "e2e-" + args.e2e + ("" if args.rules == "builtin" else "-" + args.rules),
+                       "input_bytes": in_bytes, "scanned_bytes": scanned,
                        "files_scanned": ref.batch.nfiles, "findings": summ0[1], "rules": len(sc.Rules),
+                       "rule_set": args.rules, "binary_frac": args.binary_frac,
                        "piece_mib": args.e2e_slot_mib or 256,
                        "api": "tsg_fs_scan" if args.e2e == "fs" else "tsg_layer_scan"},
             "unpipelined": {"ingest_ms": round((b - a) * 1e3, 2),

@@ -67,3 +67,18 @@ def test_torchrun_two_ranks_emulated():
     assert line["n_gpus"] == 2
     assert "torchrun" in line["config"]["parallelism"]
     assert line["config"]["job_bytes"] == 2 * line["config"]["bytes_per_gpu"]
+
+
+def test_e2e_fs_configs4_mix_emulated():
+    """configs[4]'s mix in the timed end-to-end path: 30 % of the tree's bytes binary blobs,
+    half of them with a text head that IsBinary (utils.go:71-89) passes to Scan, under the
+    allow-rule / exclude-block rule set loaded from a trivy-secret.yaml; the first step's
+    results must equal the exact CPU path's (the bench checks it and fails otherwise)."""
+    r = _run(["--e2e", "fs", "--e2e-mib", "8", "--rules", "allow-exclude", "--binary-frac", "0.3",
+              "--binary-text-head", "0.5", "--emulate", "--steps", "1", "--warmup", "1"])
+    line = _line(r)
+    assert line["checks"]["step1_eq_exact_cpu"] is True
+    assert line["config"]["rule_set"] == "allow-exclude" and line["config"]["binary_frac"] == 0.3
+    assert "with a text head" in line["data"] and line["config"]["findings"] > 0
+    # the dropped half is read (input bytes) but not scanned
+    assert line["config"]["scanned_bytes"] < 0.9 * line["config"]["input_bytes"]

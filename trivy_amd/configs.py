@@ -258,13 +258,19 @@ def layer_tar(nbytes, seed=3, binary_frac=0.05, big=()):
     return buf.getvalue()
 
 
-def source_tree(root, nbytes=200 << 20, seed=0):
+def source_tree(root, nbytes=200 << 20, seed=0, binary_frac=0.0, binary_text_head=0.5, extra_plants=None,
+                extra_per_mib=0.0):
     """configs[0] (SURVEY.md §8d "Config 1"): a seeded source tree on disk for `trivy fs
     --scanners secret`.  Files come from the corpus generator (log-normal sizes, median
     6 KiB; every builtin rule planted, near misses included; md/test/vendor/example/docs
     paths that the builtin allow rules cover), plus explicit AWS / GitHub / Slack tokens,
     and entries the walker or `Required` skips: a .git dir, node_modules, lockfiles, a
-    tiny file.  Returns {"files": written regular files, "bytes": their total}."""
+    tiny file.  binary_frac: that share of the tree's bytes are binary blobs (random bytes,
+    sizes like the text files', under bin/); binary_text_head of them start with 300 bytes
+    of text, so utils.IsBinary (utils.go:71-89) passes them to Scan, the others it drops
+    (configs[4]: 30 %, half with a text head).  extra_plants / extra_per_mib: lines planted
+    on top (a user rule set's, configs.plant_lines).  Returns {"files": written regular
+    files, "bytes": their total, "binary_files", "binary_text_head_files"}."""
     import os
     from trivy_amd import corpus
     rng = np.random.default_rng(seed)
@@ -281,8 +287,10 @@ def source_tree(root, nbytes=200 << 20, seed=0):
         "".join(rng.choice(list(string.ascii_uppercase + string.digits), size=8)),
         "".join(rng.choice(list(_ALNUM), size=24))) for _ in range(4)]
     extra = [x for t in zip(aws, gh, slack) for x in t] + aws[8:] + gh[8:] + slack[8:]
-    b, info = corpus.make_corpus(nbytes, seed=seed, plants_per_mib=5.0,
-                                 extra_plants=extra, extra_per_mib=8.0)
+    text_bytes = int(nbytes * (1.0 - binary_frac))
+    b, info = corpus.make_corpus(text_bytes, seed=seed, plants_per_mib=5.0,
+                                 extra_plants=extra + list(extra_plants or []),
+                                 extra_per_mib=8.0 + extra_per_mib)
     nfiles, total = 0, 0
     for i in range(b.nfiles):
         p = os.path.join(root, b.path(i))
@@ -292,6 +300,28 @@ def source_tree(root, nbytes=200 << 20, seed=0):
             f.write(data.tobytes())
         nfiles += 1
         total += len(data)
+    nbin = nhead = 0
+    if binary_frac > 0:
+        # blob sizes drawn like the text files' (from the corpus offsets), random content
+        sizes = np.diff(b.offsets.astype(np.int64))
+        left = nbytes - text_bytes
+        os.makedirs(os.path.join(root, "bin"), exist_ok=True)
+        while left > 0:
+            n = int(min(left, max(16, sizes[int(rng.integers(0, len(sizes)))])))
+            blob = rng.integers(0, 256, size=n, dtype=np.uint8)
+            if rng.random() < binary_text_head:
+                i = int(rng.integers(0, b.nfiles))
+                head = b.data[int(b.offsets[i]):int(b.offsets[i]) + min(300, n)]
+                blob[:len(head)] = head
+                if len(head) < min(300, n):  # a short text file: printable filler after it
+                    blob[len(head):min(300, n)] = ord("x")
+                nhead += 1
+            with open(os.path.join(root, "bin", "blob%06d.dat" % nbin), "wb") as f:
+                f.write(blob.tobytes())
+            nbin += 1
+            nfiles += 1
+            total += n
+            left -= n
     planted = "\n".join(aws[:2] + gh[:2] + slack[:2]).encode()
     for rel in (".git/config", "node_modules/pkg/index.js", "package-lock.json", "go.sum",
                 "src/tiny.txt"):
@@ -301,4 +331,5 @@ def source_tree(root, nbytes=200 << 20, seed=0):
             f.write(planted if rel != "src/tiny.txt" else b"AKIA")
         nfiles += 1
         total += len(planted) if rel != "src/tiny.txt" else 4
-    return {"files": nfiles, "bytes": total, "planted": info["planted"], "seed": seed}
+    return {"files": nfiles, "bytes": total, "planted": info["planted"], "seed": seed,
+            "binary_files": nbin, "binary_text_head_files": nhead}
