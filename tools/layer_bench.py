@@ -3,7 +3,7 @@
 (trivy_amd.configs.layer_tar) through the native ingest (tsg_layer_pack: tar walk +
 Required + IsBinary + packing) and a GPU scan of the packed batch.
 
-    python tools/layer_bench.py [GiB] [scans]
+    python tools/layer_bench.py [GiB] [scans] [--emulate]
 """
 import json
 import os
@@ -19,8 +19,10 @@ from trivy_amd import walker as W  # noqa: E402
 
 
 def main():
-    gib = float(sys.argv[1]) if len(sys.argv) > 1 else 1.0
-    scans = int(sys.argv[2]) if len(sys.argv) > 2 else 3
+    emulate = "--emulate" in sys.argv  # (a CPU check of the harness: no GPU)
+    argv = [a for a in sys.argv[1:] if a != "--emulate"]
+    gib = float(argv[0]) if argv else 1.0
+    scans = int(argv[1]) if len(argv) > 1 else 3
     t0 = time.time()
     tar = configs.layer_tar(int(gib * (1 << 30)), seed=3)
     gen_s = time.time() - t0
@@ -32,7 +34,7 @@ def main():
         packs.append(time.perf_counter() - t)
     b = lay.batch
     scanned = int(b.offsets[-1])
-    ctx = S.GpuContext(an.scanner, 0)
+    ctx = S.GpuContext(an.scanner, 0, emulate=emulate)
     t = time.perf_counter()
     ctx.upload(b)
     up_s = time.perf_counter() - t
@@ -43,43 +45,82 @@ def main():
         res = an.scanner.ScanBatch(b, ctx=ctx)
         times.append(time.perf_counter() - t)
     nfind = sum(len(r["Findings"] or []) for r in res)
-    # configs[2] over W GPUs: (a) every rank indexes the whole chain and packs only its byte
-    # run (tsg_layer_pack_shard); the slowest rank's pack time, measured here rank by rank
+    # configs[2] over W GPUs, rank by rank in this one process (each rank is its own process
+    # on its own GPU in the deployment; here the slowest rank's time is what bounds them):
+    # (a) every rank indexes the whole chain and packs only its byte run (tsg_layer_pack_shard);
+    # (b) the distributed index (tsg_layer_range_*): each rank walks only its byte range, the
+    #     exchange simulated in-process (layer_chain_step), then sync + dirs + pack.
+    # Round 3 timed each world once and packed into fresh pageable memory: a pack faults its
+    # whole output in (~44 k minor faults per quarter of a 1 GiB layer, about a third of its
+    # time) and single calls stalled for 0.1-0.25 s now and then (host noise: the same fault
+    # count, a different rank each time), which made the slowest rank non-monotonic.  Now
+    # each world runs REPS times (median of the slowest rank), and (b) also packs into a
+    # pinned slot of the context (tsg_layer_range_pack_slot), as the product ingest does,
+    # whose memory is faulted in once.
+    import resource
+    import statistics
+
+    def minflt():
+        return resource.getrusage(resource.RUSAGE_SELF).ru_minflt
+
+    REPS = 3
     shard = {}
     for world in (2, 4, 8):
-        worst = 0.0
-        for rank in range(world):
-            t = time.perf_counter()
-            W.NativeLayer(an.scanner, tar, rank=rank, world=world)
-            worst = max(worst, time.perf_counter() - t)
-        # distributed index (tsg_layer_range_*): each rank walks only its byte range; the
-        # exchange is simulated in-process (layer_chain_step); per-rank time = its walk +
-        # sync + dirs + pack, measured rank by rank
-        rngs, walk_t = [], []
-        for rank in range(world):
-            t = time.perf_counter()
-            rngs.append(W.LayerRange(tar, rank, world))
-            walk_t.append(time.perf_counter() - t)
-        infos, confirmed = [g.info for g in rngs], {}
-        while True:
-            st = W.layer_chain_step(infos, confirmed)
-            if st[0] == "done":
-                break
-            confirmed[st[1]] = rngs[st[1]].sync(st[2])
-        worst_r, prior, resync = 0.0, [], len(confirmed)
-        for rank, g in enumerate(rngs):
-            t = time.perf_counter()
-            g.sync(st[1][rank])
-            d = g.dirs()
-            lay_r = g.pack(an.scanner, (), (), prior, "")
-            worst_r = max(worst_r, walk_t[rank] + time.perf_counter() - t)
-            prior = prior + d
-            del lay_r
-        shard[str(world)] = {"slowest_rank_pack_s": round(worst, 4),
-                             "per_rank_ingest_GBps_of_tar": round(len(tar) / worst / 1e9, 2),
-                             "range_index_slowest_rank_s": round(worst_r, 4),
-                             "range_index_per_rank_GBps_of_tar": round(len(tar) / worst_r / 1e9, 2),
-                             "range_index_resyncs": resync}
+        rows = []
+        for _ in range(REPS):
+            worst = 0.0
+            for rank in range(world):
+                t = time.perf_counter()
+                W.NativeLayer(an.scanner, tar, rank=rank, world=world)
+                worst = max(worst, time.perf_counter() - t)
+            rngs, walk_t = [], []
+            for rank in range(world):
+                t = time.perf_counter()
+                rngs.append(W.LayerRange(tar, rank, world))
+                walk_t.append(time.perf_counter() - t)
+            infos, confirmed = [g.info for g in rngs], {}
+            while True:
+                st = W.layer_chain_step(infos, confirmed)
+                if st[0] == "done":
+                    break
+                confirmed[st[1]] = rngs[st[1]].sync(st[2])
+            worst_r = worst_s = 0.0
+            stage_r = stage_s = None
+            prior, resync, faults = [], len(confirmed), 0
+            for rank, g in enumerate(rngs):
+                t = time.perf_counter()
+                g.sync(st[1][rank])
+                d = g.dirs()
+                t1 = time.perf_counter()
+                f0 = minflt()
+                lay_r = g.pack(an.scanner, (), (), prior, "")
+                t2 = time.perf_counter()
+                faults = max(faults, minflt() - f0)
+                del lay_r
+                sl = W.SlotIngest.layer_range(ctx, g, (), (), prior, "")
+                t3 = time.perf_counter()
+                sl.release()
+                tot = walk_t[rank] + (t1 - t) + (t2 - t1)
+                tot_s = walk_t[rank] + (t1 - t) + (t3 - t2)
+                if tot > worst_r:
+                    worst_r, stage_r = tot, (walk_t[rank], t1 - t, t2 - t1)
+                if tot_s > worst_s:
+                    worst_s, stage_s = tot_s, (walk_t[rank], t1 - t, t3 - t2)
+                prior = prior + d
+            rows.append((worst, worst_r, worst_s, stage_r, stage_s, resync, faults))
+        med = lambda k: statistics.median(r[k] for r in rows)  # noqa: E731
+        mid = sorted(rows, key=lambda r: r[2])[len(rows) // 2]
+        shard[str(world)] = {"slowest_rank_pack_s": round(med(0), 4),
+                             "per_rank_ingest_GBps_of_tar": round(len(tar) / med(0) / 1e9, 2),
+                             "range_index_slowest_rank_s": round(med(1), 4),
+                             "range_index_per_rank_GBps_of_tar": round(len(tar) / med(1) / 1e9, 2),
+                             "range_index_slot_slowest_rank_s": round(med(2), 4),
+                             "range_index_slot_per_rank_GBps_of_tar": round(len(tar) / med(2) / 1e9, 2),
+                             "slot_slowest_rank_stages_s": {"walk": round(mid[4][0], 4), "sync_dirs": round(mid[4][1], 4),
+                                                            "pack_slot": round(mid[4][2], 4)},
+                             "pageable_pack_minor_faults_max": int(med(6)),
+                             "runs_slowest_rank_s": [[round(r[0], 4), round(r[1], 4), round(r[2], 4)] for r in rows],
+                             "range_index_resyncs": rows[-1][5]}
     pack_s = min(packs)
     scan_s = min(times)
     print(json.dumps({
