@@ -240,11 +240,9 @@ typedef struct tsg_stats {
    * accepts */
   uint32_t k2_tail_bytes, k2_tail_max, k2_long_tails, k2_replays;
   /* the rest of a batch's device work (HIP events on its lane): the prep kernel (zero fills,
-   * coarse file map) and the H2D of the offsets / paths; aux_ms / sum_d2h_ms above are the
+   * coarse file map) and the H2D of the file offsets; aux_ms / sum_d2h_ms above are the
    * outputs kernel (results written into pinned, host-mapped memory) */
   double prep_ms, meta_ms, sum_prep_ms, sum_meta_ms;
-  uint64_t k1_records;   /* last batch: 16-byte words in which K1 reached a reporting state
-                            (replayed by the accept kernel) */
 } tsg_stats;
 int tsg_ctx_get_stats(const tsg_ctx* ctx, tsg_stats* out);
 

@@ -15,6 +15,8 @@ build() {
 for v in "$@"; do
   case $v in
     legacy) build $v -DK1_LEGACY ;;      # K1: the legacy layout (class words, index rows)
+    u16) build $v -DK1_UNROLL=16 ;;      # K1: bytes unrolled per word
+    u4) build $v -DK1_UNROLL=4 ;;
     ns3) build $v -DK1_CHAINS=3 ;;       # K1: chains per lane
     ns4) build $v -DK1_CHAINS=4 ;;
     k2ctr) build $v -DK2_TRACE_CTR ;;    # K2: per-entry counters (TSG_K2_TRACE)

@@ -41,7 +41,7 @@ def main():
            "k1_GBps": round(nb / med("k1_ms") / 1e6, 1),
            "dev_GBps": round(nb / (med("k1_ms") + med("gate_ms") + med("k2_ms")) / 1e6, 1),
            "k2_items": rows[-1]["k2_items"], "k2_entries": rows[-1]["k2_launches"],
-           "candidates": rows[-1]["candidates"], "k1_records": rows[-1]["k1_records"]}
+           "candidates": rows[-1]["candidates"]}
     print(json.dumps(out), flush=True)
 
 

@@ -81,8 +81,7 @@ class Stats(C.Structure):
                 ("k2_tail_bytes", C.c_uint32), ("k2_tail_max", C.c_uint32),
                 ("k2_long_tails", C.c_uint32), ("k2_replays", C.c_uint32),
                 ("prep_ms", C.c_double), ("meta_ms", C.c_double),
-                ("sum_prep_ms", C.c_double), ("sum_meta_ms", C.c_double),
-                ("k1_records", C.c_uint64)]
+                ("sum_prep_ms", C.c_double), ("sum_meta_ms", C.c_double)]
 
 
 # (name, restype, argtypes) -- every symbol include/trivy_secret.h declares

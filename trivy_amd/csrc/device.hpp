@@ -5,10 +5,10 @@
 // DeviceLane (its own HIP stream and HBM buffers); enqueue_scan puts the whole device part
 // of a batch on that stream with no host round trip:
 //
-//   H2D (pinned slot -> HBM) and one H2D of the offsets / paths  prep (zero fills, coarse
-//   file map)  K1  path gate  keyword gates  event-chunk compaction  item counts  item
-//   layout (device-side)  item lists  K2  outputs (candidates, keyword bits, overflow /
-//   path / skip flags, counters: written straight into pinned, host-mapped memory)
+//   H2D (pinned slot -> HBM) and one H2D of the file offsets  prep (zero fills, coarse file
+//   map)  K1  keyword gates  event-chunk compaction  item counts  item layout
+//   (device-side)  item lists  K2  outputs (candidates, keyword bits, overflow / skip
+//   flags, counters: written straight into pinned, host-mapped memory)
 //
 // and records the batch's completion event.  Two lanes per device let the H2D of one batch
 // overlap the kernels of the other.
@@ -25,25 +25,21 @@ namespace tsg {
 
 struct DeviceRules;
 
-// Pinned host memory of one batch: the staging of its offsets / path offsets / paths (one
-// H2D), and its device outputs, which the outputs kernel writes straight into host-mapped
-// memory (no runtime D2H copy).
+// Pinned host memory of one batch's device outputs, which the outputs kernel writes straight
+// into host-mapped memory (no runtime D2H copy).
 struct HostOut {
-  uint8_t* blk = nullptr;       // host-mapped block: counts | gskip | ovf | pathok | kw
+  uint8_t* blk = nullptr;       // host-mapped block: counts | gskip | ovf | kw
   uint8_t* blk_dev = nullptr;   // its device address
   uint32_t* kw = nullptr;       // [files_cap * kw_words]
   uint8_t* ovf = nullptr;       // [files_cap] 1 = resolve the file whole
-  uint8_t* pathok = nullptr;    // [files_cap] Global.AllowPath: 0 / 1 / 2 = host decides
   uint8_t* gskip = nullptr;     // [groups] 1 = K2 skipped the group (item capacity)
   Candidate* cand = nullptr;    // [cand_cap] host-mapped: K2 candidates copied out
   Candidate* cand_dev = nullptr;  // device address of `cand`
   uint32_t* counts = nullptr;   // [16] 0 candidates, 1 event chunks, 2 K2 list entries,
                                 // 3 dense entries, 5 items, 6 entries, 7 skipped groups,
                                 // 8-11 K2 diagnostics (TSG_K2_DIAG)
-  uint8_t* meta = nullptr;      // pinned staging: offsets [F+1] | path offsets [F+1] | paths
-  size_t meta_cap = 0;
   uint32_t files_cap = 0, cand_cap = 0, groups = 0, kw_words = 0;
-  // stage boundaries of the batch on its lane's stream: data H2D | metadata H2D | wait for
+  // stage boundaries of the batch on its lane's stream: data H2D | offsets H2D | wait for
   // the previous batch's kernels | prep | K1 | gates | K2 | outputs; ev[kEvDone] completes
   // the batch
   hipEvent_t ev[9] = {};

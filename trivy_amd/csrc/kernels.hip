@@ -52,6 +52,9 @@ constexpr int kStreams = 4;  // K2 dense: chunks per lane
 #ifndef K1_CHAINS
 #define K1_CHAINS 2
 #endif
+#ifndef K1_UNROLL
+#define K1_UNROLL 8  // K1: bytes of a word unrolled (8 of 16: profiles/r04/k1g, 0.394 ms against 0.420 for 16)
+#endif
 constexpr int kK1Chains = K1_CHAINS;  // K1: chains per lane (independent dependent-LDS chains)
 constexpr int kK1Seg = 8;     // K1: consecutive chunks per chain
 // legacy K1 layout: static LDS size classes (KiB): 3, 2 or 1 blocks per CU, of 512, 512
@@ -209,41 +212,6 @@ __global__ void __launch_bounds__(256) outputs_kernel(OutArgs A) {
   for (uint32_t c = 0; c < A.nc; c++) copy_range(A.dst[c], A.src[c], A.n[c], tid, nth);
 }
 
-// ---------------------------------------------------------------- Global.AllowPath
-// One thread per file runs the allow-path DFA of the rule set over its path (the host's
-// path_allowed, plan.cpp): 1 = some global allow-path regexp matches, 0 = none, 2 = the
-// path holds a non-ASCII byte (the DFA is exact on ASCII paths only; the host decides).
-struct DevPathDFA {
-  const uint32_t* next;  // [ns * nc]
-  const uint32_t* acc;   // [ns * nc] accept-mask index of the transition (0 = none)
-  const uint32_t* eot;   // [ns] accept at end of text
-  const uint8_t* cls;    // [256]
-  uint32_t nc, start;
-};
-
-__global__ void path_allow_kernel(DevPathDFA d, const uint8_t* __restrict__ paths,
-                                  const uint64_t* __restrict__ poff, uint32_t nfiles, uint8_t* __restrict__ out) {
-  const uint32_t f = blockIdx.x * blockDim.x + threadIdx.x;
-  if (f >= nfiles) return;
-  const uint64_t a = poff[f], b = poff[f + 1];
-  bool ascii = true;
-  for (uint64_t p = a; p < b; p++) ascii &= paths[p] < 0x80;
-  if (!ascii) {
-    out[f] = 2;
-    return;
-  }
-  uint32_t s = d.start;
-  for (uint64_t p = a; p < b; p++) {
-    const uint32_t e = s * d.nc + d.cls[paths[p]];
-    if (d.acc[e]) {
-      out[f] = 1;
-      return;
-    }
-    s = d.next[e];
-  }
-  out[f] = d.eot[s] ? 1 : 0;
-}
-
 // ---------------------------------------------------------------- K1
 typedef unsigned short us2 __attribute__((ext_vector_type(2)));
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));  // 8-byte aligned: one ds_read_b64
@@ -301,9 +269,6 @@ struct K1Args {
   uint32_t* ev;    // [nchunks, padded to whole items]
   uint32_t* hits;  // [ns] arrivals per accepting state (sampling pass) or null
   uint32_t seg;    // consecutive chunks per chain
-  uint2* rec;      // words with an arrival past the blocks' LDS lists: {batch byte / 16, row before it}
-  uint32_t* rec_n;   // [2] records in rec, blocks done (both zeroed per launch)
-  uint32_t rec_cap;  // >= the batch's 16-byte words
 };
 
 // one chain = one segment of consecutive chunks: automaton row, run counters, the running
@@ -389,9 +354,6 @@ struct K1Lane {
   const uint8_t* s_tab;   // legacy: the transition table
   const uint32_t* s_cls;  // legacy: this lane's column of the class words (REP) or the table
   uint32_t lane8;         // packed: (lane % 32) * 8
-  uint2* s_rec;           // the block's list of words with an arrival (LDS), and its length
-  uint32_t* s_nrec;
-  uint32_t rec_lds;       // its capacity
 
   // byte k (0..3) of dword w: the chain's row s and run counters cnt step once
   __device__ __forceinline__ void step(uint32_t& s, uint32_t& cnt, uint32_t w, int k) const {
@@ -421,7 +383,7 @@ struct K1Lane {
       s0[i] = c[i].s;
       top[i] = 0;
     }
-#pragma unroll
+#pragma unroll(K1_UNROLL)
     for (int k = 0; k < 16; k++)
 #pragma unroll
       for (int i = 0; i < NS; i++) {
@@ -429,34 +391,14 @@ struct K1Lane {
         top[i] = max(top[i], c[i].s);
         c[i].mx = run_max(c[i].mx, c[i].cnt);
       }
+    // a word in which a chain reached a reporting row is replayed byte by byte (rare: the
+    // adaptation keeps arrivals near one per 4 KiB); a ghost word (pos = total) reports nothing
 #pragma unroll
-    for (int i = 0; i < NS; i++) defer(top[i] >= d.acc_row && pos[i] < A.total, s0[i], pos[i]);
+    for (int i = 0; i < NS; i++)
+      if (__builtin_expect(top[i] >= d.acc_row && pos[i] < A.total, 0)) c[i].evl |= replay(s0[i], pos[i]);
   }
-  // A word in which the chain reached a reporting row is recorded {word, row before it} in
-  // the block's LDS list and replayed once the block's items are done (k1_kernel), not
-  // replayed here: a 16-step serial replay that the whole wave would wait for.  Past the LDS
-  // list a record goes to the global list, which the block that finishes last replays.
-  __device__ __forceinline__ void defer(bool hit, uint32_t s0, uint64_t p) {
-    const unsigned long long m = __ballot(hit);
-    if (m == 0) return;
-    const uint32_t lane = threadIdx.x & 63;
-    const uint32_t leader = (uint32_t)__builtin_ctzll(m);
-    uint32_t base = 0;
-    if (lane == leader) base = atomicAdd(s_nrec, (uint32_t)__popcll(m));
-    base = __shfl(base, (int)leader);
-    if (hit) {
-      const uint32_t idx = base + (uint32_t)__popcll(m & ((1ull << lane) - 1));
-      const uint2 r = make_uint2((uint32_t)(p >> 4), s0);
-      if (idx < rec_lds) {
-        s_rec[idx] = r;
-      } else {
-        const uint32_t g = atomicAdd(A.rec_n, 1u);
-        if (g < A.rec_cap) A.rec[g] = r;
-      }
-    }
-  }
-  // one recorded word again, byte by byte from row s: every arrival sets its keyword bits;
-  // returns the word's event bits
+  // the word at batch byte p again, byte by byte from row s: every arrival sets its keyword
+  // bits; returns the word's event bits
   __device__ __forceinline__ uint32_t replay(uint32_t s, uint64_t p) const {
     const uint4 v = *(const uint4*)(A.data + p);
     uint32_t evl = 0, cnt = 0;
@@ -569,11 +511,6 @@ template <int KWW, bool PACKED, int LDSK, bool REP, int TPB>
 __global__ void __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(4, 8))) k1_kernel(DevK1 d, K1Args A) {
   constexpr int NS = kK1Chains;
   __shared__ __attribute__((aligned(16))) uint8_t smem[LDSK * 1024];
-  // the block's arrival words: what the 160 KiB of LDS leave beside the image, at most 2048
-  constexpr int kRecLds = (160 * 1024 - LDSK * 1024 - 64) / 8 < 2048 ? (160 * 1024 - LDSK * 1024 - 64) / 8 : 2048;
-  __shared__ uint2 s_rec[kRecLds];
-  __shared__ uint32_t s_nrec, s_last;
-  if (threadIdx.x == 0) s_nrec = 0;
   const uint32_t* tsrc = (const uint32_t*)d.tab;
   if constexpr (PACKED) {
     static_assert(LDSK * 1024 >= (int)kK1PTab + 65536, "packed K1 image: 64 KiB of class entries + 64 KiB of rows");
@@ -592,67 +529,13 @@ __global__ void __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(4, 8))
   }
   __syncthreads();
   const uint32_t lane = threadIdx.x & 31;
-  K1Lane<KWW, PACKED, REP> L{d,        A,         smem, smem + (REP ? kK1RepBytes : 1024), (const uint32_t*)smem + (REP ? lane : 0),
-                             lane * 8, s_rec, &s_nrec, (uint32_t)kRecLds};
+  K1Lane<KWW, PACKED, REP> L{d, A, smem, smem + (REP ? kK1RepBytes : 1024), (const uint32_t*)smem + (REP ? lane : 0),
+                             lane * 8};
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   const uint32_t q = threadIdx.x & 3;
   const uint64_t ib = (uint64_t)A.item_step * NS * A.seg * A.chunk;
   for (uint64_t it0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) & ~3ull; it0 < A.nitems; it0 += stride)
     L.template item_quad<NS>(it0, ib, q);
-  // The block's recorded words: after the barrier every event word of the block's chunks
-  // is stored (each chunk belongs to one chain of this block), so the records' event bits
-  // are ORed after them; the replays run from the tables already in LDS.
-  __syncthreads();
-  const uint32_t n = min(s_nrec, (uint32_t)kRecLds);
-  for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
-    const uint64_t p = (uint64_t)s_rec[i].x << 4;
-    const uint32_t evl = L.replay(s_rec[i].y, p);
-    if (evl) atomicOr(&A.ev[p / A.chunk], evl);
-  }
-  // the global list (records past the LDS lists, rare): replayed by the last block to finish,
-  // when every block's event words are stored.  Every block counts itself done (a block that
-  // finished early cannot know whether a later one will append).  The adaptation's sampling
-  // pass, whose list is long, leaves it to k1_list_kernel.
-  if (!A.hits) {
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      __threadfence();
-      s_last = atomicAdd(A.rec_n + 1, 1u) == gridDim.x - 1;
-    }
-    __syncthreads();
-    if (s_last && *(volatile uint32_t*)A.rec_n != 0) {
-      __threadfence();
-      const uint32_t g = min(*(volatile uint32_t*)A.rec_n, A.rec_cap);
-      for (uint32_t i = threadIdx.x; i < g; i += blockDim.x) {
-        const volatile uint32_t* r = (const volatile uint32_t*)(A.rec + i);
-        const uint64_t p = (uint64_t)r[0] << 4;
-        const uint32_t evl = L.replay(r[1], p);
-        if (evl) atomicOr(&A.ev[p / A.chunk], evl);
-      }
-    }
-  }
-}
-
-// The global list of K1's sampling pass (adapt_k1): one record per thread, tables in global
-// memory (L2-resident); after K1, so the event bits are ORed after its stores.
-__global__ void __launch_bounds__(256) k1_list_kernel(DevK1 d, K1Args A) {
-  const uint32_t n = min(*A.rec_n, A.rec_cap);
-  const uint8_t* tab = (const uint8_t*)d.tab;
-  for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < n; e += gridDim.x * blockDim.x) {
-    const uint2 r = A.rec[e];
-    const uint64_t p = (uint64_t)r.x << 4;
-    const uint4 v = *(const uint4*)(A.data + p);
-    uint32_t s = r.y, evl = 0;
-#pragma unroll 1
-    for (uint32_t k = 0; k < 16; k++) {
-      const uint32_t w = k < 4 ? v.x : k < 8 ? v.y : k < 12 ? v.z : v.w;
-      const uint32_t b = (w >> (8 * (k & 3))) & 0xFFu;
-      // packed rows are byte offsets, legacy rows entry indices (DevK1)
-      s = d.packed ? *(const uint16_t*)(tab + s + (d.pcls[2 * b] - kK1PTab)) : *(const uint16_t*)(tab + 2 * s + (d.cls[b] & 0xFFu));
-      if (s >= d.acc_row) k1_accept(d, A, evl, s, p + k);
-    }
-    if (evl) atomicOr(&A.ev[p / A.chunk], evl);
-  }
 }
 
 // ---------------------------------------------------------------- K1X
@@ -1985,8 +1868,6 @@ struct DeviceRules {
   std::vector<unsigned long long> h_gofbit;
   std::vector<DevDFA> groups;
   DevDFA* d_groups = nullptr;
-  DevPathDFA pathdfa{};
-  bool has_pathdfa = false;
   uint32_t* d_gmask = nullptr;
   uint32_t* d_galways = nullptr;
   unsigned long long* d_kwg = nullptr;   // [n_kw * GW] groups each keyword bit gates
@@ -2010,15 +1891,11 @@ struct LaneState {
   hipStream_t st = nullptr;
   uint8_t* data_alloc = nullptr;  // kPad | batch | tail
   size_t data_cap = 0;
-  uint8_t* meta = nullptr;        // offsets | path offsets | paths (one H2D per batch)
+  uint8_t* meta = nullptr;        // the batch's file offsets (one H2D per batch)
   size_t meta_cap = 0;
   const uint64_t* off = nullptr;  // into meta (last batch)
-  const uint64_t* poff = nullptr;
-  const uint8_t* paths = nullptr;
   uint32_t* cf = nullptr;         // coarse file map (file_of)
   size_t cf_cap = 0;
-  uint2* k1rec = nullptr;         // K1's words with an arrival past the blocks' LDS lists
-  size_t k1rec_cap = 0;
   uint32_t* ev_bits = nullptr;
   size_t ev_cap = 0;
   uint2* xlist = nullptr;  // K1X hit records
@@ -2033,8 +1910,6 @@ struct LaneState {
   size_t ggate_cap = 0;
   uint8_t* ovf = nullptr;
   size_t ovf_cap = 0;
-  uint8_t* pathok = nullptr;
-  size_t pathok_cap = 0;
   uint2* items = nullptr;
   size_t items_cap = 0;
   uint4* entries = nullptr;
@@ -2056,7 +1931,7 @@ struct LaneState {
     if (!d) return;
     (void)hipSetDevice(d->device);
     if (st) (void)hipStreamSynchronize(st);
-    void* bufs[] = {data_alloc, meta, cf, k1rec, ev_bits, xlist, xcount, evlist, kw, ggate, ovf, pathok,
+    void* bufs[] = {data_alloc, meta, cf, ev_bits, xlist, xcount, evlist, kw, ggate, ovf,
                     items, entries, dentries, cand, counts, gcount, cursor, base, kind, gskip, etrace};
     for (void* b : bufs) (void)hipFree(b);
     if (st) (void)hipStreamDestroy(st);
@@ -2130,17 +2005,12 @@ static int adapt_k1(DeviceRules* r, LaneState* l, uint64_t total, uint32_t nfile
   const uint64_t step = std::max<uint64_t>(1, k1_items / 16384);
   const uint64_t nsamp = (k1_items + step - 1) / step;
   HIP_TRY(hipMemsetAsync(r->d_hits, 0, sizeof(uint32_t) * ns, l->st));
-  HIP_TRY(hipMemsetAsync(l->counts + 14, 0, 2 * sizeof(uint32_t), l->st));
   K1Args A{l->data_alloc + kPad, l->off, l->cf, total, nchunks, nsamp, step, r->chunk,
-           nfiles, l->kw, l->ev_bits, r->d_hits, (uint32_t)kK1Seg, l->k1rec, l->counts + 14,
-           (uint32_t)std::min<size_t>(l->k1rec_cap, 0xFFFFFFFFu)};
+           nfiles, l->kw, l->ev_bits, r->d_hits, (uint32_t)kK1Seg};
   int rc;
   if ((rc = launch_k1(r, A, l->st))) return rc;
-  k1_list_kernel<<<r->grid, 256, 0, l->st>>>(r->k1, A);  // the sampling pass's global list
-  HIP_TRY(hipGetLastError());
   std::vector<uint32_t> hits(ns);
   HIP_TRY(hipMemcpyAsync(hits.data(), r->d_hits, sizeof(uint32_t) * ns, hipMemcpyDeviceToHost, l->st));
-  HIP_TRY(hipMemsetAsync(l->counts + 14, 0, 2 * sizeof(uint32_t), l->st));  // (the real pass records anew)
   HIP_TRY(hipStreamSynchronize(l->st));
   r->adapted = true;
   const uint64_t sample_bytes = nsamp * kK1Chains * A.seg * r->chunk;
@@ -2221,21 +2091,6 @@ int device_rules_create(int device, const Plan& p, uint32_t chunk, uint32_t ext_
     HIP_TRY(hipFuncSetAttribute((const void*)k1x_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (1 << kXBits) / 8 + 16));
   HIP_TRY(hipMalloc((void**)&r->d_hits, sizeof(uint32_t) * r->k1.ns));
-  if (const DFA* pd = p.allow_path_dfa.get()) {
-    const uint32_t* t = nullptr;
-    if ((rc = upload_vec(pd->next, &t, &r->tables))) return rc;
-    r->pathdfa.next = t;
-    if ((rc = upload_vec(pd->acc, &t, &r->tables))) return rc;
-    r->pathdfa.acc = t;
-    if ((rc = upload_vec(pd->eot_acc, &t, &r->tables))) return rc;
-    r->pathdfa.eot = t;
-    const uint8_t* cl = nullptr;
-    if ((rc = upload_vec(std::vector<uint8_t>(pd->cls, pd->cls + 256), &cl, &r->tables))) return rc;
-    r->pathdfa.cls = cl;
-    r->pathdfa.nc = (uint32_t)pd->nclasses;
-    r->pathdfa.start = pd->start[kCtxBOT];
-    r->has_pathdfa = true;
-  }
   const uint32_t G = (uint32_t)p.groups.size();
   if (G > 0x7FFF) return fail(TSG_ERR_INTERNAL, "more K2 groups than transition records can name");
   r->GW = std::max<uint32_t>(1, (G + 63) / 64);
@@ -2336,7 +2191,7 @@ hipStream_t lane_stream(LaneState* l) { return l->st; }
 static size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 void host_out_free(HostOut* o) {
-  void* ps[] = {o->blk, o->cand, o->meta};
+  void* ps[] = {o->blk, o->cand};
   for (void* p : ps)
     if (p) (void)hipHostFree(p);
   for (auto& e : o->ev)
@@ -2352,9 +2207,8 @@ int host_out_alloc(const DeviceRules* d, uint32_t files_cap, HostOut* o) {
   h.groups = std::max<uint32_t>(1, (uint32_t)d->groups.size());
   h.kw_words = (uint32_t)d->plan->kw_words;
   // one host-mapped block for the small outputs (each part 256-B aligned): counts | gskip |
-  // ovf | pathok | kw
-  const size_t o_gskip = 256, o_ovf = o_gskip + al256(h.groups), o_path = o_ovf + al256(h.files_cap),
-               o_kw = o_path + al256(h.files_cap),
+  // ovf | kw
+  const size_t o_gskip = 256, o_ovf = o_gskip + al256(h.groups), o_kw = o_ovf + al256(h.files_cap),
                bytes = o_kw + al256(sizeof(uint32_t) * (size_t)h.files_cap * h.kw_words);
   auto fail_free = [&](hipError_t e, const char* what) {
     host_out_free(&h);
@@ -2366,7 +2220,6 @@ int host_out_alloc(const DeviceRules* d, uint32_t files_cap, HostOut* o) {
   h.counts = (uint32_t*)h.blk;
   h.gskip = h.blk + o_gskip;
   h.ovf = h.blk + o_ovf;
-  h.pathok = h.blk + o_path;
   h.kw = (uint32_t*)(h.blk + o_kw);
   if ((e = hipHostMalloc((void**)&h.cand, sizeof(Candidate) * (size_t)h.cand_cap, hipHostMallocMapped)) != hipSuccess)
     return fail_free(e, "hipHostMalloc");
@@ -2395,21 +2248,13 @@ int enqueue_scan(DeviceRules* r, LaneState* l, const ScanInput& in, HostOut* out
   const size_t tail = (size_t)kK1Chains * kK1Seg * C + kPad;
   if ((rc = ensure(&l->data_alloc, &l->data_cap, (size_t)total + kPad + tail))) return rc;
   uint8_t* data = l->data_alloc + kPad;
-  const bool paths_dev = r->has_pathdfa && F;
-  const uint64_t P = paths_dev ? in.poff[F] : 0;
-  const size_t meta_bytes = sizeof(uint64_t) * ((size_t)F + 1) * (paths_dev ? 2 : 1) + P;
+  const size_t meta_bytes = sizeof(uint64_t) * ((size_t)F + 1);
   if ((rc = ensure(&l->meta, &l->meta_cap, meta_bytes))) return rc;
   l->off = (const uint64_t*)l->meta;
-  l->poff = l->off + F + 1;
-  l->paths = (const uint8_t*)(l->poff + F + 1);
   const uint64_t k1_item_chunks = (uint64_t)kK1Chains * kK1Seg;
   const uint64_t nchunks_pad = (nchunks + k1_item_chunks - 1) / k1_item_chunks * k1_item_chunks + 1;
   const uint64_t ncf = (total >> kCfShift) + 2;
   if ((rc = ensure(&l->cf, &l->cf_cap, (size_t)ncf))) return rc;
-  // K1 arrival words: at most one record per 16-byte word of the batch (8 B per 16: HBM is
-  // plentiful, and only the records written are traffic; the adaptation keeps them near one
-  // per 4 KiB), so the list never overflows
-  if ((rc = ensure(&l->k1rec, &l->k1rec_cap, (size_t)(total / 16 + 16)))) return rc;
   if ((rc = ensure(&l->ev_bits, &l->ev_cap, (size_t)nchunks_pad))) return rc;
   // K1X hit records: one per 256 bytes (a lane-word with a hit past that verifies inline)
   if (r->has_k1x && (rc = ensure(&l->xlist, &l->xlist_cap, (size_t)(total / 256 + 65536)))) return rc;
@@ -2418,7 +2263,6 @@ int enqueue_scan(DeviceRules* r, LaneState* l, const ScanInput& in, HostOut* out
   if ((rc = ensure(&l->kw, &l->kw_cap, (size_t)F * W + 1))) return rc;
   if ((rc = ensure(&l->ggate, &l->ggate_cap, (size_t)F * r->GW + 1))) return rc;
   if ((rc = ensure(&l->ovf, &l->ovf_cap, (size_t)F + 1))) return rc;
-  if ((rc = ensure(&l->pathok, &l->pathok_cap, (size_t)F + 1))) return rc;
   // item capacity: twice the batch's chunks (the builtin rules list ~11 % of them); over
   // it, groups are skipped (kGroupSkip) and resolved on the host, never dropped
   const uint64_t items_cap = std::max<uint64_t>(2 * nchunks, 1u << 16);
@@ -2433,27 +2277,12 @@ int enqueue_scan(DeviceRules* r, LaneState* l, const ScanInput& in, HostOut* out
     HIP_TRY(hipMalloc((void**)&l->cand, sizeof(DevCand) * (size_t)out->cand_cap));
     l->cand_cap = out->cand_cap;
   }
-  // ---- the batch's offsets, path offsets and paths side by side in pinned staging (the
-  // HostOut is this submission's alone until its job ends), for one H2D
-  if (out->meta_cap < meta_bytes) {
-    if (out->meta) HIP_TRY(hipHostFree(out->meta));
-    out->meta = nullptr;
-    out->meta_cap = 0;
-    const size_t cap = std::max<size_t>(meta_bytes + meta_bytes / 8, 1 << 20);
-    HIP_TRY(hipHostMalloc((void**)&out->meta, cap, hipHostMallocDefault));
-    out->meta_cap = cap;
-  }
-  std::memcpy(out->meta, in.off, sizeof(uint64_t) * ((size_t)F + 1));
-  if (paths_dev) {
-    std::memcpy(out->meta + sizeof(uint64_t) * ((size_t)F + 1), in.poff, sizeof(uint64_t) * ((size_t)F + 1));
-    if (P) std::memcpy(out->meta + sizeof(uint64_t) * 2 * ((size_t)F + 1), in.paths, P);
-  }
-
-  // ---- H2D from the pinned slot: the batch, then its metadata (two runtime copies)
+  // ---- H2D from the pinned slot: the batch, then its file offsets (two runtime copies; the
+  // paths stay on the host, where Global.AllowPath is settled per file, scanner.go:343-347)
   HIP_TRY(hipEventRecord(out->ev[0], st));
   if (total) HIP_TRY(hipMemcpyAsync(data, in.data, total, hipMemcpyHostToDevice, st));
   HIP_TRY(hipEventRecord(out->ev[1], st));
-  HIP_TRY(hipMemcpyAsync(l->meta, out->meta, meta_bytes, hipMemcpyHostToDevice, st));
+  HIP_TRY(hipMemcpyAsync(l->meta, in.off, meta_bytes, hipMemcpyHostToDevice, st));
   HIP_TRY(hipEventRecord(out->ev[2], st));
   // the kernels of consecutive batches run one after the other (each has the whole chip;
   // their HIP-event times are the kernels' own), while this lane's H2D above overlapped
@@ -2496,8 +2325,7 @@ int enqueue_scan(DeviceRules* r, LaneState* l, const ScanInput& in, HostOut* out
   if (!r->adapted && k1_items >= 64 && total >= adapt_bytes)
     if ((rc = adapt_k1(r, l, total, F, nchunks, k1_items))) return rc;
   if (k1_items) {
-    K1Args A{data, l->off, l->cf, total, nchunks, k1_items, 1, C, F, l->kw, l->ev_bits, nullptr, (uint32_t)kK1Seg,
-             l->k1rec, l->counts + 14, (uint32_t)std::min<size_t>(l->k1rec_cap, 0xFFFFFFFFu)};
+    K1Args A{data, l->off, l->cf, total, nchunks, k1_items, 1, C, F, l->kw, l->ev_bits, nullptr, (uint32_t)kK1Seg};
     if ((rc = launch_k1(r, A, st))) return rc;
   }
   if (r->has_k1x && total) {  // the hashed literals of a large rule set, after K1's stores
@@ -2535,10 +2363,6 @@ int enqueue_scan(DeviceRules* r, LaneState* l, const ScanInput& in, HostOut* out
   IA.base = l->base;
   IA.items = l->items;
   const bool work = F && G && nchunks;
-  if (paths_dev) {
-    path_allow_kernel<<<(F + 255) / 256, 256, 0, st>>>(r->pathdfa, l->paths, l->poff, F, l->pathok);
-    HIP_TRY(hipGetLastError());
-  }
   if (work) {
     ggate_kernel<<<(F + 255) / 256, 256, 0, st>>>(l->kw, F, W, r->d_kwg, r->d_galw, r->GW, l->ggate);
     HIP_TRY(hipGetLastError());
@@ -2617,7 +2441,6 @@ int enqueue_scan(DeviceRules* r, LaneState* l, const ScanInput& in, HostOut* out
     copy(out->counts, l->counts, sizeof(uint32_t) * 16);
     copy(out->kw, l->kw, sizeof(uint32_t) * (uint64_t)F * W);
     copy(out->ovf, l->ovf, F);
-    if (paths_dev) copy(out->pathok, l->pathok, F);
     copy(out->gskip, l->gskip, G);
     outputs_kernel<<<128, 256, 0, st>>>(OA);
     HIP_TRY(hipGetLastError());

@@ -293,7 +293,6 @@ void update_stats(tsg_ctx* c, const Batch& b) {
   s.k2_tail_max = b.counts[9];
   s.k2_long_tails = b.counts[10];
   s.k2_replays = b.counts[11];
-  s.k1_records = b.counts[14];
   s.k1_hot_states = c->dr ? device_rules_hot_states(c->dr) : 0;
   s.batches++;
   s.sum_bytes += b.bytes;
@@ -333,7 +332,7 @@ void run_job(tsg_ctx* c, std::shared_ptr<Batch> b, BatchView view, HostOut ho,
       kv.ncand = std::min<uint32_t>(ho.counts[0], ho.cand_cap);
       kv.overflow = ho.ovf;
       kv.kw_unknown = kwu ? kwu->data() : nullptr;
-      kv.path_ok = rs->plan->allow_path_dfa ? ho.pathok : nullptr;
+      kv.path_ok = nullptr;  // Global.AllowPath on the host (plan.cpp path_allowed)
       kv.group_skipped = skipped ? ho.gskip : nullptr;
     }
     const auto t0 = std::chrono::steady_clock::now();
