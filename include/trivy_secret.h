@@ -294,6 +294,8 @@ const char* tsg_last_error(void);
  *   "piece_mib"       piece floor of tsg_layer_scan / tsg_fs_scan (default 160)
  *   "pike_only"       "1": the Go-regexp matcher uses the Pike VM alone (no backtracker)
  *   "no_k1x"          "1": a rule set too large for K1's automaton is not split onto K1X
+ *   "x_step"          1, 2 or 4: the K1X window step of the next plans (default: the widest
+ *                     step whose K1 automaton fits the packed table)
  *   "emu_wordrec"     "1": emulated K2 writes one record per accepting 16-B word, as the
  *                     kernel does (tsg_scan_batch_emulated, TSG_CTX_EMULATE contexts)
  *   "emu_kw_unknown"  comma-separated keywords the emulated K1 leaves to the host, as

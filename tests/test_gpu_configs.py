@@ -36,14 +36,9 @@ def test_user_rules_1000_compile(user1000):
     assert info["n_rules"] == 1083 and info["n_groups"] > 0
 
 
-def test_user_rules_1000_k1_vs_reference(user1000):
-    """configs[3]'s keywords and anchors do not fit K1's automaton: the long ones go to the
-    hashed prefilter (K1X).  K1 + K1X keyword bits and chunk events == k1_reference."""
+def _k1_vs_reference(sc, b, chunks=(64, 256)):
     import numpy as np
-    doc, sc = user1000
-    assert sc.info()["k1x_literals"] > 800
-    b = S.Batch.from_args(configs.mixed_batch(doc, 1 << 20, seed=65, plants_per_file=0.8))
-    for chunk in (64, 256):
+    for chunk in chunks:
         ctx = S.GpuContext(sc, 0, chunk_bytes=chunk, adapt_mib=0xFFFFFFFF)
         ctx.upload(b)
         ctx.kernels()
@@ -52,6 +47,46 @@ def test_user_rules_1000_k1_vs_reference(user1000):
         rkw, rev = sc.k1_reference(b, chunk)
         assert np.array_equal(kw, rkw)
         assert np.array_equal(ev, rev)
+
+
+@pytest.mark.parametrize("step", [None, "1", "2", "4"])
+def test_user_rules_1000_k1_vs_reference(step, knob):
+    """configs[3]'s keywords and anchors do not fit K1's automaton: the builtin rules' and
+    the short ones stay, the rest go to the hashed prefilter (K1X), which samples a window
+    every `step` bytes (None: the plan's choice).  K1 + K1X keyword bits and chunk events
+    == k1_reference."""
+    if step:
+        knob("x_step", step)
+    doc = configs.user_rules_doc(1000, seed=4)
+    sc = S.NewScanner(S.config_from_dict(doc))
+    assert sc.info()["k1x_literals"] > 800
+    _k1_vs_reference(sc, S.Batch.from_args(configs.mixed_batch(doc, 1 << 20, seed=65, plants_per_file=0.8)))
+
+
+@pytest.mark.parametrize("step", ["1", "2", "4"])
+def test_k1x_every_alignment(step, knob):
+    """K1X literals at every byte alignment, periodic literals (one 4-gram at several
+    offsets), overlapping occurrences, occurrences straddling file boundaries and ending at
+    the batch's last byte: keyword bits and events == k1_reference."""
+    knob("x_step", step)
+    doc = configs.user_rules_doc(1000, seed=4)
+    extra = ["aaaaaaaaq", "qzqzqzqzqz", "Mixed-Case-Key", "zzzzzzzz"]
+    for i, k in enumerate(extra):
+        doc["rules"].append({"id": "extra-%d" % i, "category": "user", "title": "extra", "severity": "LOW",
+                             "regex": r"(?i)%s(?P<secret>[0-9a-z]{8})" % k.lower().replace("-", r"\-"),
+                             "keywords": [k]})
+    sc = S.NewScanner(S.config_from_dict(doc))
+    files = []
+    for off in range(20):
+        for k in extra:
+            files.append(("f%d_%s" % (off, k), b"." * off + k.upper().encode() + b"0123abcd" + b"aaaa" * (off % 3)))
+    files.append(("periodic", b"aaaaaaaaaaaaaaaqzqzqzqzqzqzqzqzq" * 9 + b"zzzzzzzzzzzzzzzzzzzzz"))
+    # a literal split across two files, and one ending at the batch's last byte
+    files.append(("split_a", b"xxxxxxxxxxxxxMixed-Ca"))
+    files.append(("split_b", b"se-Key00000000 zzzz"))
+    files.append(("last", b"........................zzzzzzzz"))
+    b = S.Batch.from_args([S.ScanArgs(FilePath=n, Content=c) for n, c in files])
+    _k1_vs_reference(sc, b, chunks=(16, 64))
 
 
 def test_user_rules_1000_gpu_vs_oracle(user1000):

@@ -1,14 +1,20 @@
 #!/bin/bash
-# K1X words per lane per round (library variants x1, x8; default 4), user1000 kernel-only
-# timing, then the configs[3] GPU parity tests.  usage: tools/gpu_k1x.sh TAG
+# K1X (configs[3]) check: the user-rule GPU parity tests, then kernel-only timing and a
+# rocprofv3 kernel trace per K1X window step.  usage: tools/gpu_k1x.sh TAG [steps...]
 set -o pipefail
-out=gpurun_out/${1:-k1x}
+tag=${1:-k1x}; shift
+steps=${@:-0 4 2 1}
+out=gpurun_out/$tag
 mkdir -p $out
-for v in default x1 x8; do
-  if [ "$v" = default ]; then unset TSG_LIB_VARIANT; else export TSG_LIB_VARIANT=$v; fi
-  timeout -k 10 200 python -u tools/kab.py 1024 5 --rules user1000 > $out/kab_$v.json 2> $out/kab_$v.err || { tail -5 $out/kab_$v.err; exit 1; }
-  echo "$v $(cat $out/kab_$v.json)"
-done
-unset TSG_LIB_VARIANT
-timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -k "user1000 or k1x or configs" > $out/gpu_tests.log 2>&1 || { tail -20 $out/gpu_tests.log; exit 2; }
+cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
+echo "== tests" && timeout -k 10 600 python -u -m pytest tests/test_gpu_configs.py -m gpu -x -v --timeout 300 --timeout-method thread \
+  > $out/gpu_tests.log 2>&1 || { tail -30 $out/gpu_tests.log; exit 1; }
 tail -1 $out/gpu_tests.log
+for st in $steps; do
+  kn=""; [ "$st" != 0 ] && kn="--knob x_step=$st"
+  echo "== step $st" && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $out/s$st -o run -- \
+    python tools/kab.py 1024 5 --rules user1000 $kn > $out/s$st.out 2>&1 || { tail $out/s$st.out; exit 2; }
+  tail -1 $out/s$st.out
+  grep -E "k1_kernel|k1x" $out/s$st/run_kernel_stats.csv | cut -d, -f1-7
+done
+echo done

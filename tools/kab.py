@@ -3,7 +3,7 @@
 through the synchronous kernels hook; median K1 / gates / K2 HIP-event ms.  Run it once per
 library variant (TSG_LIB_VARIANT=<name>, tools/build_variants.sh).
 
-    python tools/kab.py [MiB] [reps] [--rules builtin|user1000|allow-exclude]
+    python tools/kab.py [MiB] [reps] [--rules builtin|user1000|allow-exclude] [--knob name=value]
 """
 import json
 import os
@@ -16,7 +16,11 @@ sys.path.insert(0, ROOT)
 
 def main():
     rules = sys.argv[sys.argv.index("--rules") + 1] if "--rules" in sys.argv else "builtin"
-    args = [a for a in sys.argv[1:] if not a.startswith("--") and a != rules]
+    knobs = [sys.argv[i + 1] for i, a in enumerate(sys.argv) if a == "--knob"]
+    args = [a for a in sys.argv[1:] if not a.startswith("--") and a != rules and a not in knobs]
+    from trivy_amd import _native as N
+    for kv in knobs:  # tsg_test_knob, before the rule set compiles
+        N.knob(*kv.split("=", 1))
     mib = int(args[0]) if args else 1024
     reps = int(args[1]) if len(args) > 1 else 7
     from bench import rule_set
@@ -35,7 +39,7 @@ def main():
     ctx.close()
     med = lambda k: statistics.median(r[k] for r in rows)  # noqa: E731
     nb = int(b.offsets[-1])
-    out = {"variant": os.environ.get("TSG_LIB_VARIANT", "default"), "bytes": nb, "rules": rules,
+    out = {"variant": os.environ.get("TSG_LIB_VARIANT", "default"), "bytes": nb, "rules": rules, "knobs": knobs,
            "k1_ms": round(med("k1_ms"), 4), "gate_ms": round(med("gate_ms"), 4),
            "k2_ms": round(med("k2_ms"), 4),
            "k1_GBps": round(nb / med("k1_ms") / 1e6, 1),

@@ -539,26 +539,30 @@ __global__ void __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(4, 8))
 }
 
 // ---------------------------------------------------------------- K1X
-// Literals K1's automaton has no room for (Plan::x_lits: the keywords and anchors of
-// >= 4 bytes of a large user rule set).  k1x_kernel slides a 4-byte window over the
-// batch, ASCII case folded, and tests the window's hash against an LDS bitmap of the
-// literals' prefixes (x_hash, 2^20 bits); each 16-byte word with a hit is listed
-// (one record per lane-word, a 16-bit mask of hit positions).  k1x_verify_kernel then
-// checks every listed position exactly against the literals with that 4-byte prefix
-// (an open-addressing table) and sets keyword bits (the whole literal inside the file
-// holding its last byte, K1's accept rule) and chunk event bits (chunk of the last
-// byte) with atomics.  A lane whose record does not fit the list verifies inline.
+// Literals K1's automaton has no room for (Plan::x_lits: keywords and anchors of a large
+// user rule set).  k1x_kernel samples a 4-byte window every STEP bytes of the batch (STEP =
+// Plan::x_step; 4: the word's aligned dwords, no byte shifts), ASCII case folded, and tests
+// its hash against an LDS bitmap (x_hash, 2^20 bits) holding, for every literal, its 4-grams
+// at offsets 0..STEP-1 -- every occurrence of a literal of >= STEP + 3 bytes covers exactly
+// one sampled window.  Each 16-byte word with a hit is listed (one record per lane-word, a
+// 16-bit mask of hit window positions).  k1x_verify_kernel then looks every listed window up
+// in an open-addressing table (4-gram -> {literal, offset}) and checks each candidate start
+// exactly; a match sets its keyword bit (the whole literal inside the file holding its last
+// byte, K1's accept rule) and chunk event bits (chunk of the last byte) with atomics.  A lane
+// whose record does not fit the list verifies inline.
 struct DevK1X {
   const uint32_t* bitmap;  // [2^kXBits / 32]
-  const uint4* slots;      // [mask + 1] {prefix, first literal, count, 0}; count 0 = empty
+  const uint4* slots;      // [mask + 1] {4-gram, first entry, count, 0}; count 0 = empty
   uint32_t mask;
-  const uint32_t* lits;    // literal indices of the slots, back to back
+  const uint32_t* lits;    // the slots' entries back to back: literal | offset of the 4-gram << 30
   const uint8_t* bytes;    // literal bytes, back to back
   const uint32_t* off;     // [n + 1]
   const int32_t* kwid;     // [n] keyword id or -1
   const uint32_t* ev;      // [n] event bits
   uint32_t kw_words;
+  uint32_t step;           // Plan::x_step: 1, 2 or 4
 };
+
 
 struct K1XArgs {
   const uint8_t* data;
@@ -586,26 +590,30 @@ __device__ __forceinline__ uint32_t x_hash_dev(uint32_t w) { return (w * 2654435
 
 __device__ __forceinline__ uint32_t x_low_byte(uint8_t c) { return (c >= 'A' && c <= 'Z') ? c + 32u : c; }
 
-// exact check of the literals starting at batch byte p (window w = its 4 lowercased bytes)
+// exact check of the literals whose 4-gram at some offset j starts at batch byte p (window
+// w = its 4 lowercased bytes): each candidate literal starts at p - j
 __device__ void k1x_verify_at(const DevK1X& x, const K1XArgs& A, uint64_t p, uint32_t w) {
   uint32_t h = (w * 0x85EBCA6Bu) & x.mask;
   for (;;) {
     const uint4 sl = x.slots[h];
-    if (sl.z == 0) return;  // no literal with this prefix
+    if (sl.z == 0) return;  // no literal with this 4-gram
     if (sl.x == w) {
-      for (uint32_t j = 0; j < sl.z; j++) {
-        const uint32_t i = x.lits[sl.y + j];
+      for (uint32_t e = 0; e < sl.z; e++) {
+        const uint32_t ent = x.lits[sl.y + e];
+        const uint32_t i = ent & 0x3FFFFFFFu, j = ent >> 30;
+        if (p < j) continue;
+        const uint64_t s = p - j;
         const uint32_t a = x.off[i], len = x.off[i + 1] - a;
-        if (p + len > A.total) continue;
-        uint32_t t = 4;
-        while (t < len && x_low_byte(A.data[p + t]) == x.bytes[a + t]) t++;
+        if (s + len > A.total) continue;
+        uint32_t t = 0;
+        while (t < len && x_low_byte(A.data[s + t]) == x.bytes[a + t]) t++;
         if (t < len) continue;
-        const uint64_t q = p + len - 1;
+        const uint64_t q = s + len - 1;
         if (x.ev[i]) atomicOr(&A.ev[q / A.chunk], x.ev[i]);
         const int32_t k = x.kwid[i];
         if (k >= 0) {
           const uint32_t f = file_of(A.cf, A.off, A.nfiles, q);
-          if (p >= A.off[f]) atomicOr(&A.kw[(size_t)f * x.kw_words + k / 32], 1u << (k % 32));
+          if (s >= A.off[f]) atomicOr(&A.kw[(size_t)f * x.kw_words + k / 32], 1u << (k % 32));
         }
       }
       return;
@@ -614,18 +622,23 @@ __device__ void k1x_verify_at(const DevK1X& x, const K1XArgs& A, uint64_t p, uin
   }
 }
 
-constexpr int kK1XBlock = 512;
+constexpr int kK1XBlock = 1024;
 #ifndef K1X_WORDS
 #define K1X_WORDS 4
 #endif
 constexpr int kXWords = K1X_WORDS;  // words per lane per round (k1x_kernel)
 
+// the window at byte k of a word (d: its dwords and the next word's first)
+__device__ __forceinline__ uint32_t k1x_window(const uint32_t (&d)[5], int k) {
+  return (k & 3) ? __builtin_amdgcn_alignbyte(d[k / 4 + 1], d[k / 4], k & 3) : d[k / 4];
+}
+
+template <int STEP>
 __device__ __forceinline__ uint32_t k1x_hits(const uint32_t* s_bm, const uint32_t (&d)[5]) {
   uint32_t hits = 0;
 #pragma unroll
-  for (int k = 0; k < 16; k++) {
-    const uint32_t w = (k & 3) ? __builtin_amdgcn_alignbyte(d[k / 4 + 1], d[k / 4], k & 3) : d[k / 4];
-    const uint32_t h = x_hash_dev(w);
+  for (int k = 0; k < 16; k += STEP) {
+    const uint32_t h = x_hash_dev(k1x_window(d, k));
     hits |= ((s_bm[h >> 5] >> (h & 31)) & 1u) << k;
   }
   return hits;
@@ -633,6 +646,7 @@ __device__ __forceinline__ uint32_t k1x_hits(const uint32_t* s_bm, const uint32_
 
 // Each block lists its hit records in its own slice of A.list (an LDS counter, no global
 // atomics); a record past the slice is verified inline.  A.count[block] = records kept.
+template <int STEP>
 __global__ void __launch_bounds__(kK1XBlock) k1x_kernel(DevK1X x, K1XArgs A) {
   extern __shared__ uint32_t s_bm[];  // 2^kXBits bits, then the block's record counter
   uint32_t* s_n = s_bm + (1u << kXBits) / 32;
@@ -655,7 +669,9 @@ __global__ void __launch_bounds__(kK1XBlock) k1x_kernel(DevK1X x, K1XArgs A) {
       const uint64_t w = w0 + (uint64_t)u * stride;
       // (the batch is padded with zero bytes past its end)
       v[u] = w < nwords ? *(const uint4*)(A.data + w * 16) : make_uint4(0, 0, 0, 0);
-      nx[u] = w < nwords ? *(const uint32_t*)(A.data + w * 16 + 16) : 0u;
+      // (STEP 4 never shifts a window into the next word)
+      if constexpr (STEP < 4) nx[u] = w < nwords ? *(const uint32_t*)(A.data + w * 16 + 16) : 0u;
+      else nx[u] = 0u;
     }
   };
   uint64_t wi = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -675,7 +691,7 @@ __global__ void __launch_bounds__(kK1XBlock) k1x_kernel(DevK1X x, K1XArgs A) {
       if (w >= nwords) break;
       const uint32_t d[5] = {x_lower4(cv[u].x), x_lower4(cv[u].y), x_lower4(cv[u].z), x_lower4(cv[u].w),
                              x_lower4(cn[u])};
-      uint32_t hits = k1x_hits(s_bm, d);
+      uint32_t hits = k1x_hits<STEP>(s_bm, d);
       // positions past the batch end never count (their window holds pad bytes)
       const uint64_t p0 = w * 16;
       if (p0 + 16 > A.total) hits &= (1u << (uint32_t)(A.total - p0)) - 1u;
@@ -686,8 +702,7 @@ __global__ void __launch_bounds__(kK1XBlock) k1x_kernel(DevK1X x, K1XArgs A) {
         } else {
           for (uint32_t t = hits; t; t &= t - 1) {
             const int k = __builtin_ctz(t);
-            const uint32_t wd = (k & 3) ? __builtin_amdgcn_alignbyte(d[k / 4 + 1], d[k / 4], k & 3) : d[k / 4];
-            k1x_verify_at(x, A, p0 + k, wd);
+            k1x_verify_at(x, A, p0 + k, k1x_window(d, k));
           }
         }
       }
@@ -697,19 +712,26 @@ __global__ void __launch_bounds__(kK1XBlock) k1x_kernel(DevK1X x, K1XArgs A) {
   if (threadIdx.x == 0) A.count[blockIdx.x] = min(*s_n, slice);
 }
 
+static const void* k1x_fn(uint32_t step) {
+  if (step == 4) return (const void*)k1x_kernel<4>;
+  if (step == 2) return (const void*)k1x_kernel<2>;
+  return (const void*)k1x_kernel<1>;
+}
+
+// one block per k1x_kernel block: its slice of the list
 __global__ void __launch_bounds__(kBlock) k1x_verify_kernel(DevK1X x, K1XArgs A, uint32_t nblocks) {
   const uint32_t slice = A.cap / nblocks;
-  const uint64_t n = (uint64_t)slice * nblocks;
-  for (uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (uint64_t)gridDim.x * blockDim.x) {
-    const uint32_t b = (uint32_t)(e / slice), j = (uint32_t)(e % slice);
-    if (j >= A.count[b]) continue;
-    const uint2 r = A.list[e];
-    const uint64_t p0 = (uint64_t)r.x * 16;
-    for (uint32_t t = r.y; t; t &= t - 1) {
-      const uint64_t p = p0 + __builtin_ctz(t);
-      const uint32_t w = x_low_byte(A.data[p]) | x_low_byte(A.data[p + 1]) << 8 | x_low_byte(A.data[p + 2]) << 16 |
-                         x_low_byte(A.data[p + 3]) << 24;
-      k1x_verify_at(x, A, p, w);
+  for (uint32_t b = blockIdx.x; b < nblocks; b += gridDim.x) {
+    const uint32_t n = A.count[b];
+    for (uint32_t j = threadIdx.x; j < n; j += blockDim.x) {
+      const uint2 r = A.list[(size_t)b * slice + j];
+      const uint64_t p0 = (uint64_t)r.x * 16;
+      for (uint32_t t = r.y; t; t &= t - 1) {
+        const uint64_t p = p0 + __builtin_ctz(t);
+        const uint32_t w = x_low_byte(A.data[p]) | x_low_byte(A.data[p + 1]) << 8 | x_low_byte(A.data[p + 2]) << 16 |
+                           x_low_byte(A.data[p + 3]) << 24;
+        k1x_verify_at(x, A, p, w);
+      }
     }
   }
 }
@@ -1745,24 +1767,29 @@ static int k1_tables(const Plan& p, const std::vector<uint8_t>& quiet, K1Host* h
   return TSG_OK;
 }
 
-// K1X tables: the prefix bitmap, the prefix -> literals table and the literals
+// K1X tables: the 4-gram bitmap, the 4-gram -> {literal, offset} table and the literals
 static int make_device_k1x(const Plan& p, DevK1X* out, std::vector<void*>* allocs) {
   *out = DevK1X{};
   out->kw_words = (uint32_t)p.kw_words;
+  out->step = (uint32_t)p.x_step;
   if (p.x_lits.empty()) return TSG_OK;
+  if (p.x_step != 1 && p.x_step != 2 && p.x_step != 4) return fail(TSG_ERR_INTERNAL, "K1X step not 1, 2 or 4");
   const size_t n = p.x_lits.size();
   std::vector<uint32_t> bitmap((1u << kXBits) / 32, 0);
   std::map<uint32_t, std::vector<uint32_t>> by4;
   std::vector<uint8_t> bytes;
   std::vector<uint32_t> off{0}, ev(n);
   std::vector<int32_t> kwid(n);
+  if (n >= (1u << 30)) return fail(TSG_ERR_INTERNAL, "too many K1X literals");
   for (size_t i = 0; i < n; i++) {
     const std::string& L = p.x_lits[i];
-    if (L.size() < 4) return fail(TSG_ERR_INTERNAL, "K1X literal shorter than 4 bytes");
-    const uint32_t w = x_prefix4((const uint8_t*)L.data());
-    const uint32_t h = x_hash(w);
-    bitmap[h >> 5] |= 1u << (h & 31);
-    by4[w].push_back((uint32_t)i);
+    if (L.size() < (size_t)p.x_step + 3) return fail(TSG_ERR_INTERNAL, "K1X literal shorter than its step + 3 bytes");
+    for (uint32_t j = 0; j < (uint32_t)p.x_step; j++) {  // an occurrence at s is sampled at s + j
+      const uint32_t w = x_prefix4((const uint8_t*)L.data() + j);
+      const uint32_t h = x_hash(w);
+      bitmap[h >> 5] |= 1u << (h & 31);
+      by4[w].push_back((uint32_t)i | j << 30);
+    }
     bytes.insert(bytes.end(), L.begin(), L.end());
     off.push_back((uint32_t)bytes.size());
     ev[i] = p.x_event[i];
@@ -2088,7 +2115,7 @@ int device_rules_create(int device, const Plan& p, uint32_t chunk, uint32_t ext_
   if ((rc = make_device_k1x(p, &r->k1x, &r->tables))) return rc;
   r->has_k1x = !p.x_lits.empty();
   if (r->has_k1x)  // the 128 KiB prefix bitmap is dynamic LDS
-    HIP_TRY(hipFuncSetAttribute((const void*)k1x_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+    HIP_TRY(hipFuncSetAttribute(k1x_fn(r->k1x.step), hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (1 << kXBits) / 8 + 16));
   HIP_TRY(hipMalloc((void**)&r->d_hits, sizeof(uint32_t) * r->k1.ns));
   const uint32_t G = (uint32_t)p.groups.size();
@@ -2333,9 +2360,9 @@ int enqueue_scan(DeviceRules* r, LaneState* l, const ScanInput& in, HostOut* out
                                                                    (uint64_t)r->cus));
     K1XArgs X{data, l->off, l->cf, total, C, F, l->kw, l->ev_bits, l->xlist, l->xcount,
               (uint32_t)std::min<size_t>(l->xlist_cap, 0xFFFFFFFFu)};
-    k1x_kernel<<<xg, kK1XBlock, (1u << kXBits) / 8 + 16, st>>>(r->k1x, X);
-    HIP_TRY(hipGetLastError());
-    k1x_verify_kernel<<<r->grid, kBlock, 0, st>>>(r->k1x, X, (uint32_t)xg);
+    void* xa[] = {(void*)&r->k1x, (void*)&X};
+    HIP_TRY(hipLaunchKernel(k1x_fn(r->k1x.step), dim3(xg), dim3(kK1XBlock), xa, (1u << kXBits) / 8 + 16, st));
+    k1x_verify_kernel<<<xg, kBlock, 0, st>>>(r->k1x, X, (uint32_t)xg);
     HIP_TRY(hipGetLastError());
   }
   HIP_TRY(hipEventRecord(out->ev[5], st));

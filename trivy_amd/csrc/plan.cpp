@@ -378,9 +378,8 @@ std::unique_ptr<Plan> build_plan(const Ruleset& rs, const PlanOptions& opt, std:
   for (size_t g = 0; g < p->groups.size(); g++) litg[g] = p->groups[g].events == (1u << kEvLit0);
   // keywords left out of K1 (table budget): a literal no ASCII text contains holds their id
   std::vector<char> kw_dropped(kws.size(), 0);
-  // hashed mode (K1X): keywords and anchors of >= 4 bytes leave the automaton
-  std::vector<char> kw_hashed(kws.size(), 0);
-  bool anchors_hashed = false;
+  // hashed mode (K1X): the keywords and anchors that leave the automaton
+  std::vector<char> kw_hashed(kws.size(), 0), anchor_hashed(R, 0);
   auto build_k1 = [&](bool with_anchors) -> bool {
     std::vector<std::string> lits = kws;
     for (size_t k = 0; k < lits.size(); k++)
@@ -405,7 +404,7 @@ std::unique_ptr<Plan> build_plan(const Ruleset& rs, const PlanOptions& opt, std:
       for (uint32_t r : g.rules) {
         p->rule_event[r] = bit;
         const std::string& s = anchor[r].lit;
-        if (anchors_hashed && s.size() >= 4) {
+        if (anchor_hashed[r]) {
           auto xi = xl.find(ascii_lower(s));
           if (xi == xl.end()) xl[ascii_lower(s)] = {-1, bit};
           else xi->second.second |= bit;
@@ -465,7 +464,7 @@ std::unique_ptr<Plan> build_plan(const Ruleset& rs, const PlanOptions& opt, std:
       if (!kw_dropped[k] && !kw_hashed[k]) add(kws[k]);
     if (with_anchors)
       for (size_t r = 0; r < R; r++)
-        if (!anchor[r].lit.empty() && !(anchors_hashed && anchor[r].lit.size() >= 4)) add(anchor[r].lit);
+        if (!anchor[r].lit.empty() && !anchor_hashed[r]) add(anchor[r].lit);
     size_t ncls = 1;
     for (int c = 0; c < 256; c++) ncls += bytes[c];
     return (pre.size() + 1) * ncls * 2;
@@ -476,15 +475,75 @@ std::unique_ptr<Plan> build_plan(const Ruleset& rs, const PlanOptions& opt, std:
   };
   bool k1_ok = (opt.anchors && try_k1(true)) || try_k1(false);
   if (!k1_ok && !knobs().no_k1x.load()) {
-    // Too many literal bytes for an LDS-resident automaton (large user rule sets): the
-    // keywords and anchors of >= 4 bytes go to the hashed prefilter (K1X), the short
-    // ones stay in the automaton.  Keyword bits stay exact, anchors keep their events.
-    for (int k = 0; k < p->fb_kw0; k++) kw_hashed[k] = kws[k].size() >= 4;
-    anchors_hashed = true;
-    k1_ok = (opt.anchors && try_k1(true)) || try_k1(false);
+    // Too many literal bytes for an LDS-resident automaton (large user rule sets).  K1X
+    // samples one 4-byte window every x_step bytes, so it takes literals of x_step + 3 bytes
+    // or more; the shorter ones stay in the automaton, and the others fill what is left of a
+    // packed table (k1_packed_fits) in rule order -- the builtin rules' first
+    // (scanner.go:302-311), whose keywords are the ones common in real text -- the rest are
+    // hashed.  Keyword bits stay exact, anchors keep their events.
+    // the widest step whose automaton fits the packed table, else the widest that builds
+    // (the x_step test knob forces one)
+    const int forced = knobs().x_step.load();
+    for (int attempt = 0; attempt < 6 && !k1_ok; attempt++) {
+      const int step = (attempt % 3 == 0) ? 4 : (attempt % 3 == 1) ? 2 : 1;
+      const bool need_packed = attempt < 3;
+      if (forced && step != forced) continue;
+      const size_t xmin = (size_t)step + 3;
+      std::set<std::string> pre;
+      bool bytes[256] = {false};
+      size_t nbytes = 0;
+      // table bytes with literal s added: rows x (classes padded to 2 mod 4) x 2, an upper
+      // bound of the exact automaton's (k1_estimate)
+      auto cost = [&](const std::string& s) {
+        const std::string l = ascii_lower(s);
+        size_t npre = 0, nb = 0;
+        bool seen[256] = {false};
+        for (size_t i = 1; i <= l.size(); i++) npre += pre.count(l.substr(0, i)) ? 0 : 1;
+        for (unsigned char ch : l) {
+          if (!bytes[ch] && !seen[ch]) nb++;
+          seen[ch] = true;
+        }
+        return (pre.size() + npre + 1) * (nbytes + nb + 1 + 3) * 2;
+      };
+      auto take = [&](const std::string& s) {
+        const std::string l = ascii_lower(s);
+        for (size_t i = 1; i <= l.size(); i++) pre.insert(l.substr(0, i));
+        for (unsigned char ch : l) {
+          if (!bytes[ch]) nbytes++;
+          bytes[ch] = true;
+        }
+      };
+      std::fill(kw_hashed.begin(), kw_hashed.end(), 0);
+      std::fill(anchor_hashed.begin(), anchor_hashed.end(), 0);
+      for (size_t k = 0; k < kws.size(); k++)
+        if (!kw_dropped[k] && kws[k].size() < xmin) take(kws[k]);
+      for (size_t r = 0; r < R; r++)
+        if (!anchor[r].lit.empty() && anchor[r].lit.size() < xmin) take(anchor[r].lit);
+      std::vector<char> kw_seen(kws.size(), 0);
+      auto place = [&](const std::string& s, char* hashed) {
+        if (s.size() < xmin) return;
+        if (cost(s) <= 65536) take(s);
+        else *hashed = 1;
+      };
+      for (size_t r = 0; r < R; r++) {
+        for (uint32_t k : p->rule_kws[r])
+          if ((int)k < p->fb_kw0 && !kw_dropped[k] && !kw_seen[k]) {
+            kw_seen[k] = 1;
+            place(kws[k], &kw_hashed[k]);
+          }
+        if (!anchor[r].lit.empty()) place(anchor[r].lit, &anchor_hashed[r]);
+      }
+      for (int k = 0; k < p->fb_kw0; k++)  // keywords no rule lists (none today)
+        if (!kw_seen[k] && !kw_dropped[k]) place(kws[k], &kw_hashed[k]);
+      k1_ok = (opt.anchors && try_k1(true)) || try_k1(false);
+      if (k1_ok && need_packed && !forced &&
+          (size_t)p->kw_dfa->nstates * p->kw_dfa->nclasses * 2 > 65536)
+        k1_ok = false;
+      if (k1_ok) p->x_step = step;
+    }
     if (!k1_ok) {
       std::fill(kw_hashed.begin(), kw_hashed.end(), 0);
-      anchors_hashed = false;
+      std::fill(anchor_hashed.begin(), anchor_hashed.end(), 0);
     }
   }
   if (!k1_ok) {

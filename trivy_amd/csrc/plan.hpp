@@ -59,6 +59,7 @@ struct Plan {
   std::vector<std::string> x_lits;     // ASCII-lowercased literal bytes
   std::vector<int32_t> x_kw;           // keyword id, or -1 (anchor only)
   std::vector<uint32_t> x_event;       // event bits (0: keyword only)
+  int x_step = 1;                      // K1X samples a 4-byte window every x_step bytes
   // run classes for kEvRunU / kEvRunD: byte -> membership bit 0 (U) / 1 (D)
   uint8_t run_cls[256] = {0};
   int run_k[2] = {32, 12};
