@@ -243,6 +243,9 @@ typedef struct tsg_stats {
    * coarse file map) and the H2D of the file offsets; aux_ms / sum_d2h_ms above are the
    * outputs kernel (results written into pinned, host-mapped memory) */
   double prep_ms, meta_ms, sum_prep_ms, sum_meta_ms;
+  /* K1X (large rule sets) in the last batch: 16-B words listed with a prefilter hit, and
+   * words verified inline because their block's list slice was full */
+  uint32_t k1x_records, k1x_inline;
 } tsg_stats;
 int tsg_ctx_get_stats(const tsg_ctx* ctx, tsg_stats* out);
 

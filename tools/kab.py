@@ -45,7 +45,8 @@ def main():
            "k1_GBps": round(nb / med("k1_ms") / 1e6, 1),
            "dev_GBps": round(nb / (med("k1_ms") + med("gate_ms") + med("k2_ms")) / 1e6, 1),
            "k2_items": rows[-1]["k2_items"], "k2_entries": rows[-1]["k2_launches"],
-           "candidates": rows[-1]["candidates"]}
+           "candidates": rows[-1]["candidates"], "k1x_records": rows[-1]["k1x_records"],
+           "k1x_inline": rows[-1]["k1x_inline"]}
     print(json.dumps(out), flush=True)
 
 

@@ -81,7 +81,8 @@ class Stats(C.Structure):
                 ("k2_tail_bytes", C.c_uint32), ("k2_tail_max", C.c_uint32),
                 ("k2_long_tails", C.c_uint32), ("k2_replays", C.c_uint32),
                 ("prep_ms", C.c_double), ("meta_ms", C.c_double),
-                ("sum_prep_ms", C.c_double), ("sum_meta_ms", C.c_double)]
+                ("sum_prep_ms", C.c_double), ("sum_meta_ms", C.c_double),
+                ("k1x_records", C.c_uint32), ("k1x_inline", C.c_uint32)]
 
 
 # (name, restype, argtypes) -- every symbol include/trivy_secret.h declares

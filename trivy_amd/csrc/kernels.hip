@@ -575,6 +575,7 @@ struct K1XArgs {
   uint2* list;      // {word index, hit mask}, one slice per k1x_kernel block
   uint32_t* count;  // [blocks] records in each slice
   uint32_t cap;     // records in all slices
+  uint32_t* stats;  // {records listed, words verified inline} (batch counts 13, 14)
 };
 
 __device__ __forceinline__ uint32_t x_lower4(uint32_t x) {
@@ -709,7 +710,12 @@ __global__ void __launch_bounds__(kK1XBlock) k1x_kernel(DevK1X x, K1XArgs A) {
     }
   }
   __syncthreads();
-  if (threadIdx.x == 0) A.count[blockIdx.x] = min(*s_n, slice);
+  if (threadIdx.x == 0) {
+    const uint32_t n = *s_n, kept = min(n, slice);
+    A.count[blockIdx.x] = kept;
+    atomicAdd(&A.stats[0], kept);
+    if (n > kept) atomicAdd(&A.stats[1], n - kept);
+  }
 }
 
 static const void* k1x_fn(uint32_t step) {
@@ -718,20 +724,20 @@ static const void* k1x_fn(uint32_t step) {
   return (const void*)k1x_kernel<1>;
 }
 
-// one block per k1x_kernel block: its slice of the list
+// kXVerifyParts blocks per k1x_kernel block, each a strided share of that block's slice
+constexpr uint32_t kXVerifyParts = 8;
 __global__ void __launch_bounds__(kBlock) k1x_verify_kernel(DevK1X x, K1XArgs A, uint32_t nblocks) {
   const uint32_t slice = A.cap / nblocks;
-  for (uint32_t b = blockIdx.x; b < nblocks; b += gridDim.x) {
-    const uint32_t n = A.count[b];
-    for (uint32_t j = threadIdx.x; j < n; j += blockDim.x) {
-      const uint2 r = A.list[(size_t)b * slice + j];
-      const uint64_t p0 = (uint64_t)r.x * 16;
-      for (uint32_t t = r.y; t; t &= t - 1) {
-        const uint64_t p = p0 + __builtin_ctz(t);
-        const uint32_t w = x_low_byte(A.data[p]) | x_low_byte(A.data[p + 1]) << 8 | x_low_byte(A.data[p + 2]) << 16 |
-                           x_low_byte(A.data[p + 3]) << 24;
-        k1x_verify_at(x, A, p, w);
-      }
+  const uint32_t b = blockIdx.x % nblocks, part = blockIdx.x / nblocks;
+  const uint32_t n = A.count[b];
+  for (uint32_t j = part * blockDim.x + threadIdx.x; j < n; j += kXVerifyParts * blockDim.x) {
+    const uint2 r = A.list[(size_t)b * slice + j];
+    const uint64_t p0 = (uint64_t)r.x * 16;
+    for (uint32_t t = r.y; t; t &= t - 1) {
+      const uint64_t p = p0 + __builtin_ctz(t);
+      const uint32_t w = x_low_byte(A.data[p]) | x_low_byte(A.data[p + 1]) << 8 | x_low_byte(A.data[p + 2]) << 16 |
+                         x_low_byte(A.data[p + 3]) << 24;
+      k1x_verify_at(x, A, p, w);
     }
   }
 }
@@ -2359,10 +2365,10 @@ int enqueue_scan(DeviceRules* r, LaneState* l, const ScanInput& in, HostOut* out
     const int xg = (int)std::max<uint64_t>(1, std::min<uint64_t>((total / 16 + kK1XBlock - 1) / kK1XBlock,
                                                                    (uint64_t)r->cus));
     K1XArgs X{data, l->off, l->cf, total, C, F, l->kw, l->ev_bits, l->xlist, l->xcount,
-              (uint32_t)std::min<size_t>(l->xlist_cap, 0xFFFFFFFFu)};
+              (uint32_t)std::min<size_t>(l->xlist_cap, 0xFFFFFFFFu), l->counts + 13};
     void* xa[] = {(void*)&r->k1x, (void*)&X};
     HIP_TRY(hipLaunchKernel(k1x_fn(r->k1x.step), dim3(xg), dim3(kK1XBlock), xa, (1u << kXBits) / 8 + 16, st));
-    k1x_verify_kernel<<<xg, kBlock, 0, st>>>(r->k1x, X, (uint32_t)xg);
+    k1x_verify_kernel<<<xg * kXVerifyParts, kBlock, 0, st>>>(r->k1x, X, (uint32_t)xg);
     HIP_TRY(hipGetLastError());
   }
   HIP_TRY(hipEventRecord(out->ev[5], st));
