@@ -542,19 +542,20 @@ __global__ void __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(4, 8))
 // Literals K1's automaton has no room for (Plan::x_lits: keywords and anchors of a large
 // user rule set).  k1x_kernel samples a 4-byte window every STEP bytes of the batch (STEP =
 // Plan::x_step; 4: the word's aligned dwords, no byte shifts), ASCII case folded, and tests
-// its hash against an LDS bitmap (x_hash, 2^20 bits) holding, for every literal, its 4-grams
-// at offsets 0..STEP-1 -- every occurrence of a literal of >= STEP + 3 bytes covers exactly
-// one sampled window.  Each 16-byte word with a hit is listed (one record per lane-word, a
+// its hash against a blocked Bloom filter in LDS (x_hash: one of 2^15 dwords, two bits in
+// it) holding, for every literal, its 4-grams at offsets j0..j0+STEP-1 (Plan::x_j0, windows
+// source text rarely holds) -- every occurrence of a literal covers exactly one sampled
+// window.  Each 16-byte word with a hit is listed (one record per lane-word, a
 // 16-bit mask of hit window positions).  k1x_verify_kernel then looks every listed window up
 // in an open-addressing table (4-gram -> {literal, offset}) and checks each candidate start
 // exactly; a match sets its keyword bit (the whole literal inside the file holding its last
 // byte, K1's accept rule) and chunk event bits (chunk of the last byte) with atomics.  A lane
 // whose record does not fit the list verifies inline.
 struct DevK1X {
-  const uint32_t* bitmap;  // [2^kXBits / 32]
+  const uint32_t* bitmap;  // [kXDwords] blocked Bloom filter
   const uint4* slots;      // [mask + 1] {4-gram, first entry, count, 0}; count 0 = empty
   uint32_t mask;
-  const uint32_t* lits;    // the slots' entries back to back: literal | offset of the 4-gram << 30
+  const uint32_t* lits;    // the slots' entries back to back: literal | offset of the 4-gram << 24
   const uint8_t* bytes;    // literal bytes, back to back
   const uint32_t* off;     // [n + 1]
   const int32_t* kwid;     // [n] keyword id or -1
@@ -587,7 +588,10 @@ __device__ __forceinline__ uint32_t x_lower4(uint32_t x) {
   return x | (up >> 2);
 }
 
-__device__ __forceinline__ uint32_t x_hash_dev(uint32_t w) { return (w * 2654435761u) >> (32 - kXBits); }
+
+// x_hash / x_bits of plan.hpp (the host builds the filter with those)
+__device__ __forceinline__ uint32_t x_hash_dev(uint32_t w) { return w * 2654435761u; }
+__device__ __forceinline__ uint32_t x_bits_dev(uint32_t h) { return 1u << ((h >> 12) & 31) | 1u << ((h >> 7) & 31); }
 
 __device__ __forceinline__ uint32_t x_low_byte(uint8_t c) { return (c >= 'A' && c <= 'Z') ? c + 32u : c; }
 
@@ -601,7 +605,7 @@ __device__ void k1x_verify_at(const DevK1X& x, const K1XArgs& A, uint64_t p, uin
     if (sl.x == w) {
       for (uint32_t e = 0; e < sl.z; e++) {
         const uint32_t ent = x.lits[sl.y + e];
-        const uint32_t i = ent & 0x3FFFFFFFu, j = ent >> 30;
+        const uint32_t i = ent & 0xFFFFFFu, j = ent >> 24;
         if (p < j) continue;
         const uint64_t s = p - j;
         const uint32_t a = x.off[i], len = x.off[i + 1] - a;
@@ -639,8 +643,8 @@ __device__ __forceinline__ uint32_t k1x_hits(const uint32_t* s_bm, const uint32_
   uint32_t hits = 0;
 #pragma unroll
   for (int k = 0; k < 16; k += STEP) {
-    const uint32_t h = x_hash_dev(k1x_window(d, k));
-    hits |= ((s_bm[h >> 5] >> (h & 31)) & 1u) << k;
+    const uint32_t h = x_hash_dev(k1x_window(d, k)), m = x_bits_dev(h);
+    hits |= (uint32_t)((s_bm[h >> (32 - kXDwordBits)] & m) == m) << k;
   }
   return hits;
 }
@@ -649,9 +653,9 @@ __device__ __forceinline__ uint32_t k1x_hits(const uint32_t* s_bm, const uint32_
 // atomics); a record past the slice is verified inline.  A.count[block] = records kept.
 template <int STEP>
 __global__ void __launch_bounds__(kK1XBlock) k1x_kernel(DevK1X x, K1XArgs A) {
-  extern __shared__ uint32_t s_bm[];  // 2^kXBits bits, then the block's record counter
-  uint32_t* s_n = s_bm + (1u << kXBits) / 32;
-  for (uint32_t i = threadIdx.x; i < (1u << kXBits) / 32; i += blockDim.x) s_bm[i] = x.bitmap[i];
+  extern __shared__ uint32_t s_bm[];  // the filter, then the block's record counter
+  uint32_t* s_n = s_bm + kXDwords;
+  for (uint32_t i = threadIdx.x; i < kXDwords; i += blockDim.x) s_bm[i] = x.bitmap[i];
   if (threadIdx.x == 0) *s_n = 0;
   __syncthreads();
   const uint32_t slice = A.cap / gridDim.x;
@@ -1781,20 +1785,22 @@ static int make_device_k1x(const Plan& p, DevK1X* out, std::vector<void*>* alloc
   if (p.x_lits.empty()) return TSG_OK;
   if (p.x_step != 1 && p.x_step != 2 && p.x_step != 4) return fail(TSG_ERR_INTERNAL, "K1X step not 1, 2 or 4");
   const size_t n = p.x_lits.size();
-  std::vector<uint32_t> bitmap((1u << kXBits) / 32, 0);
+  std::vector<uint32_t> bitmap(kXDwords, 0);
   std::map<uint32_t, std::vector<uint32_t>> by4;
   std::vector<uint8_t> bytes;
   std::vector<uint32_t> off{0}, ev(n);
   std::vector<int32_t> kwid(n);
-  if (n >= (1u << 30)) return fail(TSG_ERR_INTERNAL, "too many K1X literals");
+  if (n >= (1u << 24) || p.x_j0.size() != n) return fail(TSG_ERR_INTERNAL, "bad K1X literal table");
   for (size_t i = 0; i < n; i++) {
     const std::string& L = p.x_lits[i];
-    if (L.size() < (size_t)p.x_step + 3) return fail(TSG_ERR_INTERNAL, "K1X literal shorter than its step + 3 bytes");
-    for (uint32_t j = 0; j < (uint32_t)p.x_step; j++) {  // an occurrence at s is sampled at s + j
+    const uint32_t j0 = p.x_j0[i];
+    if (L.size() < j0 + (size_t)p.x_step + 3 || j0 + p.x_step > 256)
+      return fail(TSG_ERR_INTERNAL, "K1X literal shorter than its windows");
+    for (uint32_t j = j0; j < j0 + (uint32_t)p.x_step; j++) {  // an occurrence at s is sampled at one s + j
       const uint32_t w = x_prefix4((const uint8_t*)L.data() + j);
       const uint32_t h = x_hash(w);
-      bitmap[h >> 5] |= 1u << (h & 31);
-      by4[w].push_back((uint32_t)i | j << 30);
+      bitmap[x_dword(h)] |= x_bits(h);
+      by4[w].push_back((uint32_t)i | j << 24);
     }
     bytes.insert(bytes.end(), L.begin(), L.end());
     off.push_back((uint32_t)bytes.size());
@@ -2122,7 +2128,7 @@ int device_rules_create(int device, const Plan& p, uint32_t chunk, uint32_t ext_
   r->has_k1x = !p.x_lits.empty();
   if (r->has_k1x)  // the 128 KiB prefix bitmap is dynamic LDS
     HIP_TRY(hipFuncSetAttribute(k1x_fn(r->k1x.step), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (1 << kXBits) / 8 + 16));
+                                kXDwords * 4 + 16));
   HIP_TRY(hipMalloc((void**)&r->d_hits, sizeof(uint32_t) * r->k1.ns));
   const uint32_t G = (uint32_t)p.groups.size();
   if (G > 0x7FFF) return fail(TSG_ERR_INTERNAL, "more K2 groups than transition records can name");
@@ -2367,7 +2373,7 @@ int enqueue_scan(DeviceRules* r, LaneState* l, const ScanInput& in, HostOut* out
     K1XArgs X{data, l->off, l->cf, total, C, F, l->kw, l->ev_bits, l->xlist, l->xcount,
               (uint32_t)std::min<size_t>(l->xlist_cap, 0xFFFFFFFFu), l->counts + 13};
     void* xa[] = {(void*)&r->k1x, (void*)&X};
-    HIP_TRY(hipLaunchKernel(k1x_fn(r->k1x.step), dim3(xg), dim3(kK1XBlock), xa, (1u << kXBits) / 8 + 16, st));
+    HIP_TRY(hipLaunchKernel(k1x_fn(r->k1x.step), dim3(xg), dim3(kK1XBlock), xa, kXDwords * 4 + 16, st));
     k1x_verify_kernel<<<xg * kXVerifyParts, kBlock, 0, st>>>(r->k1x, X, (uint32_t)xg);
     HIP_TRY(hipGetLastError());
   }

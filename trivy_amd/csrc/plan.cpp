@@ -13,6 +13,7 @@
 #include <atomic>
 #include <map>
 #include <unordered_map>
+#include <unordered_set>
 #include <set>
 #include <thread>
 #include <x86intrin.h>
@@ -29,6 +30,38 @@ static bool is_ascii(const std::string& s) {
   for (unsigned char c : s)
     if (c >= 0x80) return false;
   return true;
+}
+
+// 4-byte strings frequent in source text (common4.inc): a K1X window on one of them costs a
+// verify record per occurrence
+static const std::unordered_set<uint32_t>& common4() {
+  static const std::unordered_set<uint32_t> set = [] {
+    static const char kCommon4[][5] = {
+#include "common4.inc"
+    };
+    std::unordered_set<uint32_t> s;
+    for (const auto& g : kCommon4) s.insert(x_prefix4((const uint8_t*)g));
+    return s;
+  }();
+  return set;
+}
+
+// K1X windows of a lowercased literal at step `step`: the first offset j0 whose windows
+// j0 .. j0 + step - 1 hold the fewest common 4-grams.  Returns that count (0: a quiet
+// literal), -1 when the literal is too short for the step.
+static int x_pick(const std::string& l, int step, uint32_t* j0) {
+  if (l.size() < (size_t)step + 3) return -1;
+  const size_t last = std::min(l.size() - 3 - (size_t)step, (size_t)256 - (size_t)step);
+  int best = -1;
+  for (size_t j = 0; j <= last && best != 0; j++) {
+    int c = 0;
+    for (size_t t = j; t < j + (size_t)step; t++) c += common4().count(x_prefix4((const uint8_t*)l.data() + t)) ? 1 : 0;
+    if (best < 0 || c < best) {
+      best = c;
+      *j0 = (uint32_t)j;
+    }
+  }
+  return best;
 }
 
 namespace {
@@ -444,6 +477,7 @@ std::unique_ptr<Plan> build_plan(const Ruleset& rs, const PlanOptions& opt, std:
     p->x_lits.clear();
     p->x_kw.clear();
     p->x_event.clear();
+    p->x_j0.clear();
     for (const auto& kv : xl) {
       p->x_lits.push_back(kv.first);
       p->x_kw.push_back(kv.second.first);
@@ -519,27 +553,41 @@ std::unique_ptr<Plan> build_plan(const Ruleset& rs, const PlanOptions& opt, std:
         if (!kw_dropped[k] && kws[k].size() < xmin) take(kws[k]);
       for (size_t r = 0; r < R; r++)
         if (!anchor[r].lit.empty() && anchor[r].lit.size() < xmin) take(anchor[r].lit);
-      std::vector<char> kw_seen(kws.size(), 0);
-      auto place = [&](const std::string& s, char* hashed) {
-        if (s.size() < xmin) return;
-        if (cost(s) <= 65536) take(s);
-        else *hashed = 1;
-      };
-      for (size_t r = 0; r < R; r++) {
-        for (uint32_t k : p->rule_kws[r])
-          if ((int)k < p->fb_kw0 && !kw_dropped[k] && !kw_seen[k]) {
-            kw_seen[k] = 1;
-            place(kws[k], &kw_hashed[k]);
-          }
-        if (!anchor[r].lit.empty()) place(anchor[r].lit, &anchor_hashed[r]);
+      // two passes in rule order: literals whose every K1X window choice holds a 4-gram
+      // common in text first, then the quiet ones
+      for (int pass = 0; pass < 2; pass++) {
+        std::vector<char> kw_seen(kws.size(), 0);
+        auto place = [&](const std::string& s, char* hashed) {
+          uint32_t j0 = 0;
+          const int c = x_pick(ascii_lower(s), step, &j0);
+          if (c < 0 || (pass == 0) != (c > 0)) return;  // too short (kept above), or the other pass
+          if (cost(s) <= 65536) take(s);
+          else *hashed = 1;
+        };
+        for (size_t r = 0; r < R; r++) {
+          for (uint32_t k : p->rule_kws[r])
+            if ((int)k < p->fb_kw0 && !kw_dropped[k] && !kw_seen[k]) {
+              kw_seen[k] = 1;
+              place(kws[k], &kw_hashed[k]);
+            }
+          if (!anchor[r].lit.empty()) place(anchor[r].lit, &anchor_hashed[r]);
+        }
+        for (int k = 0; k < p->fb_kw0; k++)  // keywords no rule lists (none today)
+          if (!kw_seen[k] && !kw_dropped[k]) place(kws[k], &kw_hashed[k]);
       }
-      for (int k = 0; k < p->fb_kw0; k++)  // keywords no rule lists (none today)
-        if (!kw_seen[k] && !kw_dropped[k]) place(kws[k], &kw_hashed[k]);
       k1_ok = (opt.anchors && try_k1(true)) || try_k1(false);
       if (k1_ok && need_packed && !forced &&
           (size_t)p->kw_dfa->nstates * p->kw_dfa->nclasses * 2 > 65536)
         k1_ok = false;
-      if (k1_ok) p->x_step = step;
+      if (k1_ok) {
+        p->x_step = step;
+        p->x_j0.assign(p->x_lits.size(), 0);
+        for (size_t i = 0; i < p->x_lits.size(); i++) {
+          uint32_t j0 = 0;
+          x_pick(p->x_lits[i], step, &j0);
+          p->x_j0[i] = (uint8_t)j0;
+        }
+      }
     }
     if (!k1_ok) {
       std::fill(kw_hashed.begin(), kw_hashed.end(), 0);

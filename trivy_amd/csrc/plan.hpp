@@ -60,6 +60,7 @@ struct Plan {
   std::vector<int32_t> x_kw;           // keyword id, or -1 (anchor only)
   std::vector<uint32_t> x_event;       // event bits (0: keyword only)
   int x_step = 1;                      // K1X samples a 4-byte window every x_step bytes
+  std::vector<uint8_t> x_j0;           // K1X windows of literal i: offsets x_j0[i] .. + x_step - 1
   // run classes for kEvRunU / kEvRunD: byte -> membership bit 0 (U) / 1 (D)
   uint8_t run_cls[256] = {0};
   int run_k[2] = {32, 12};
@@ -203,9 +204,13 @@ void k1x_reference(const Plan& plan, const BatchView& b, uint32_t chunk,
 inline uint32_t x_prefix4(const uint8_t* b) {
   return (uint32_t)b[0] | (uint32_t)b[1] << 8 | (uint32_t)b[2] << 16 | (uint32_t)b[3] << 24;
 }
-// K1X prefilter hash: bit of the 2^kXBits-bit LDS bitmap
-constexpr int kXBits = 20;
-inline uint32_t x_hash(uint32_t w) { return (w * 2654435761u) >> (32 - kXBits); }
+// K1X prefilter: a blocked Bloom filter of 2^kXDwordBits dwords (128 KiB of LDS).  A
+// window's hash picks one dword and two bits in it; the window passes when both are set.
+constexpr int kXDwordBits = 15;
+constexpr uint32_t kXDwords = 1u << kXDwordBits;
+inline uint32_t x_hash(uint32_t w) { return w * 2654435761u; }
+inline uint32_t x_dword(uint32_t h) { return h >> (32 - kXDwordBits); }
+inline uint32_t x_bits(uint32_t h) { return 1u << ((h >> 12) & 31) | 1u << ((h >> 7) & 31); }
 
 // Chunks of file f that K2 scans for group g (given the K1 output): chunk c of the file
 // is an item iff the group is gated for f and a chunk in [c, c + back] (inside f)
