@@ -554,7 +554,7 @@ __global__ void __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(4, 8))
 struct DevK1X {
   const uint32_t* bitmap;  // [kXDwords] blocked Bloom filter
   const uint4* slots;      // [mask + 1] {4-gram, first entry, count, 0}; count 0 = empty
-  uint32_t mask;
+  uint32_t mask, shift;    // open addressing from slot (4-gram * 0x85EBCA6B) >> shift
   const uint32_t* lits;    // the slots' entries back to back: literal | offset of the 4-gram << 24
   const uint8_t* bytes;    // literal bytes, back to back
   const uint32_t* off;     // [n + 1]
@@ -598,7 +598,8 @@ __device__ __forceinline__ uint32_t x_low_byte(uint8_t c) { return (c >= 'A' && 
 // exact check of the literals whose 4-gram at some offset j starts at batch byte p (window
 // w = its 4 lowercased bytes): each candidate literal starts at p - j
 __device__ void k1x_verify_at(const DevK1X& x, const K1XArgs& A, uint64_t p, uint32_t w) {
-  uint32_t h = (w * 0x85EBCA6Bu) & x.mask;
+  // (the product's top bits: its low bits see only the window's first bytes)
+  uint32_t h = (w * 0x85EBCA6Bu) >> x.shift;
   for (;;) {
     const uint4 sl = x.slots[h];
     if (sl.z == 0) return;  // no literal with this 4-gram
@@ -643,7 +644,7 @@ __device__ __forceinline__ uint32_t k1x_hits(const uint32_t* s_bm, const uint32_
   uint32_t hits = 0;
 #pragma unroll
   for (int k = 0; k < 16; k += STEP) {
-    const uint32_t h = x_hash_dev(k1x_window(d, k)), m = x_bits_dev(h);
+    const uint32_t h = x_hash_dev(k1x_window(d, k)), m = x_bits_dev(h);  // d: folded (x_fold)
     hits |= (uint32_t)((s_bm[h >> (32 - kXDwordBits)] & m) == m) << k;
   }
   return hits;
@@ -694,8 +695,10 @@ __global__ void __launch_bounds__(kK1XBlock) k1x_kernel(DevK1X x, K1XArgs A) {
     for (int u = 0; u < U; u++) {
       const uint64_t w = wi + (uint64_t)u * stride;
       if (w >= nwords) break;
-      const uint32_t d[5] = {x_lower4(cv[u].x), x_lower4(cv[u].y), x_lower4(cv[u].z), x_lower4(cv[u].w),
-                             x_lower4(cn[u])};
+      // the filter's keys are case folded by setting bit 5 of every byte (x_fold: exact for
+      // ASCII letters, a coarser fold elsewhere -- verification is exact)
+      const uint32_t d[5] = {cv[u].x | kXFold, cv[u].y | kXFold, cv[u].z | kXFold, cv[u].w | kXFold,
+                             cn[u] | kXFold};
       uint32_t hits = k1x_hits<STEP>(s_bm, d);
       // positions past the batch end never count (their window holds pad bytes)
       const uint64_t p0 = w * 16;
@@ -705,9 +708,11 @@ __global__ void __launch_bounds__(kK1XBlock) k1x_kernel(DevK1X x, K1XArgs A) {
         if (slot < slice) {
           list[slot] = make_uint2((uint32_t)w, hits);
         } else {
+          const uint32_t lw[5] = {x_lower4(cv[u].x), x_lower4(cv[u].y), x_lower4(cv[u].z), x_lower4(cv[u].w),
+                                  x_lower4(cn[u])};
           for (uint32_t t = hits; t; t &= t - 1) {
             const int k = __builtin_ctz(t);
-            k1x_verify_at(x, A, p0 + k, k1x_window(d, k));
+            k1x_verify_at(x, A, p0 + k, k1x_window(lw, k));
           }
         }
       }
@@ -1798,7 +1803,7 @@ static int make_device_k1x(const Plan& p, DevK1X* out, std::vector<void*>* alloc
       return fail(TSG_ERR_INTERNAL, "K1X literal shorter than its windows");
     for (uint32_t j = j0; j < j0 + (uint32_t)p.x_step; j++) {  // an occurrence at s is sampled at one s + j
       const uint32_t w = x_prefix4((const uint8_t*)L.data() + j);
-      const uint32_t h = x_hash(w);
+      const uint32_t h = x_hash(x_fold(w));
       bitmap[x_dword(h)] |= x_bits(h);
       by4[w].push_back((uint32_t)i | j << 24);
     }
@@ -1807,12 +1812,15 @@ static int make_device_k1x(const Plan& p, DevK1X* out, std::vector<void*>* alloc
     ev[i] = p.x_event[i];
     kwid[i] = p.x_kw[i];
   }
-  uint32_t nslots = 16;
-  while (nslots < 2 * by4.size()) nslots *= 2;
+  uint32_t nslots = 16, lg = 4;
+  while (nslots < 2 * by4.size()) {
+    nslots *= 2;
+    lg++;
+  }
   std::vector<uint4> slots(nslots, make_uint4(0, 0, 0, 0));
   std::vector<uint32_t> lits;
   for (const auto& kv : by4) {
-    uint32_t h = (kv.first * 0x85EBCA6Bu) & (nslots - 1);
+    uint32_t h = (kv.first * 0x85EBCA6Bu) >> (32 - lg);
     while (slots[h].z) h = (h + 1) & (nslots - 1);
     slots[h] = make_uint4(kv.first, (uint32_t)lits.size(), (uint32_t)kv.second.size(), 0);
     lits.insert(lits.end(), kv.second.begin(), kv.second.end());
@@ -1826,6 +1834,7 @@ static int make_device_k1x(const Plan& p, DevK1X* out, std::vector<void*>* alloc
   if ((rc = upload_vec(kwid, &out->kwid, allocs))) return rc;
   if ((rc = upload_vec(ev, &out->ev, allocs))) return rc;
   out->mask = nslots - 1;
+  out->shift = 32 - lg;
   return TSG_OK;
 }
 

@@ -208,6 +208,10 @@ inline uint32_t x_prefix4(const uint8_t* b) {
 // window's hash picks one dword and two bits in it; the window passes when both are set.
 constexpr int kXDwordBits = 15;
 constexpr uint32_t kXDwords = 1u << kXDwordBits;
+// Keys are folded windows: bit 5 of every byte set, so an ASCII letter and its capital agree
+// (one OR per dword on the device instead of a lowercase).
+constexpr uint32_t kXFold = 0x20202020u;
+inline uint32_t x_fold(uint32_t w) { return w | kXFold; }
 inline uint32_t x_hash(uint32_t w) { return w * 2654435761u; }
 inline uint32_t x_dword(uint32_t h) { return h >> (32 - kXDwordBits); }
 inline uint32_t x_bits(uint32_t h) { return 1u << ((h >> 12) & 31) | 1u << ((h >> 7) & 31); }
