@@ -84,6 +84,8 @@ void host_out_free(HostOut* o);
 int enqueue_scan(DeviceRules* d, LaneState* l, const ScanInput& in, HostOut* out);
 // after out->ev[kEvDone]: the HIP-event times of that batch's stages
 int batch_times(const HostOut* out, ScanTimes* t);
+// keyword bits of the lane's last batch, as K1 / K1X left them on the device (test hook)
+int lane_kw(LaneState* l, uint32_t* kw, size_t n);
 // K1 output of the lane's last batch (test hook): chunk events [nchunks]
 int lane_events(LaneState* l, uint32_t* ev, size_t n);
 // K2 per-entry trace of the lane's last batch (TSG_K2_TRACE; empty otherwise): per entry

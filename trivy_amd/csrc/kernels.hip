@@ -183,13 +183,16 @@ __global__ void __launch_bounds__(256) prep_kernel(PrepArgs A) {
 
 // ---------------------------------------------------------------- outputs to the host
 // One kernel writes a batch's outputs straight into pinned, host-mapped memory: the
-// candidate records (their count is only known on the device) and the small per-file /
-// per-group arrays (keyword bits, overflow, path and skip flags, counters).  It replaces
-// the candidate copy kernel and five runtime D2H copies.  Every range starts 16-B aligned
-// on both sides (host_out_alloc, hipMalloc).
-constexpr int kOutCopies = 5;
+// candidate records (their count is only known on the device), per-file flags (bit 0 the
+// overflow flag, bit 1 folding runes present: the fallback keywords' bits), the keyword
+// rows the host reads -- files with candidates or a flag, every file when the plan has
+// host-only rules or K2 skipped a group -- and the small arrays (counters, skipped groups).
+// It replaces the candidate copy kernel and five runtime D2H copies; the sparse rows cut
+// the PCIe writes of a 1 GiB batch from ~1.4 MB to ~0.2 MB.  Every range starts 16-B
+// aligned on both sides (host_out_alloc, hipMalloc).
+constexpr int kOutCopies = 4;
 struct OutArgs {
-  const uint32_t* count;  // device candidate count
+  const uint32_t* count;  // device counters (0 candidates, 7 groups skipped)
   uint32_t cand_cap;
   const uint8_t* cand;  // DevCand records
   uint8_t* cand_host;
@@ -197,6 +200,12 @@ struct OutArgs {
   uint8_t* dst[kOutCopies];
   uint64_t n[kOutCopies];
   uint32_t nc;
+  const uint32_t* kw;  // [F * W] device keyword bits
+  uint32_t* kw_host;
+  const uint8_t* ovf;  // [F] device overflow flags
+  uint8_t* flags_host;
+  uint32_t F, W, fb_lo, fb_hi;  // fallback keywords (folding runes): ids [fb_lo, fb_hi)
+  uint32_t all_rows;            // every keyword row (host-only rules)
 };
 
 __device__ __forceinline__ void copy_range(uint8_t* __restrict__ d, const uint8_t* __restrict__ s, uint64_t n,
@@ -208,8 +217,28 @@ __device__ __forceinline__ void copy_range(uint8_t* __restrict__ d, const uint8_
 
 __global__ void __launch_bounds__(256) outputs_kernel(OutArgs A) {
   const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x, nth = (uint64_t)gridDim.x * blockDim.x;
-  copy_range(A.cand_host, A.cand, (uint64_t)min(*A.count, A.cand_cap) * 12u, tid, nth);
+  const uint32_t ncand = min(A.count[0], A.cand_cap);
+  copy_range(A.cand_host, A.cand, (uint64_t)ncand * 12u, tid, nth);
   for (uint32_t c = 0; c < A.nc; c++) copy_range(A.dst[c], A.src[c], A.n[c], tid, nth);
+  const bool all = A.all_rows || A.count[7] != 0;
+  if (all) copy_range((uint8_t*)A.kw_host, (const uint8_t*)A.kw, (uint64_t)A.F * A.W * 4u, tid, nth);
+  for (uint64_t f = tid; f < A.F; f += nth) {
+    const uint32_t* row = A.kw + f * A.W;
+    uint32_t fold = 0;
+    for (uint32_t k = A.fb_lo; k < A.fb_hi; k++) fold |= (row[k / 32] >> (k % 32)) & 1u;
+    const uint8_t fl = (A.ovf[f] ? 1 : 0) | (fold ? 2 : 0);
+    A.flags_host[f] = fl;
+    if (fl && !all)
+      for (uint32_t w = 0; w < A.W; w++) A.kw_host[f * A.W + w] = row[w];
+  }
+  if (!all) {
+    const DevCand* cand = (const DevCand*)A.cand;
+    for (uint64_t i = tid; i < ncand; i += nth) {
+      const uint32_t f = cand[i].file;
+      if (f < A.F)
+        for (uint32_t w = 0; w < A.W; w++) A.kw_host[(size_t)f * A.W + w] = A.kw[(size_t)f * A.W + w];
+    }
+  }
 }
 
 // ---------------------------------------------------------------- K1
@@ -810,39 +839,48 @@ struct ItemArgs {
 // chunks whose K1 event word is not empty, compacted into `list`: each block takes a
 // contiguous range, counts it, reserves its output with ONE global atomic, then writes its
 // chunks in order (wave ballots + an LDS prefix over the block's waves)
+// One pass: each thread tests 8 consecutive chunks (two 16-B loads), the block scans the
+// counts and claims its output range with one atomic per 8 * kBlock chunks.  (Blocks'
+// ranges land in the list in claim order; its readers do not need it sorted.)
 __global__ void __launch_bounds__(kBlock) ev_compact_kernel(const uint32_t* __restrict__ ev, uint64_t nchunks,
                                                             uint32_t* __restrict__ list, uint32_t* __restrict__ count) {
   __shared__ uint32_t s_wave[kBlock / 64];
   __shared__ uint32_t s_base;
-  const uint64_t per = (nchunks + gridDim.x - 1) / gridDim.x;
-  const uint64_t c0 = (uint64_t)blockIdx.x * per, c1 = min(nchunks, c0 + per);
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  uint32_t n = 0;
-  for (uint64_t c = c0 + threadIdx.x; c < c1; c += blockDim.x) n += (ev[c] & ~kEvAlways) != 0;
-  for (int o = 32; o > 0; o >>= 1) n += __shfl_xor(n, o);
-  if (lane == 0) s_wave[wave] = n;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    uint32_t tot = 0;
-    for (uint32_t w = 0; w < kBlock / 64; w++) tot += s_wave[w];
-    s_base = tot ? atomicAdd(count, tot) : 0;
-  }
-  __syncthreads();
-  uint32_t at = s_base;
-  for (uint64_t cb = c0; cb < c1; cb += blockDim.x) {
-    const uint64_t c = cb + threadIdx.x;
-    const bool has = c < c1 && (ev[c] & ~kEvAlways) != 0;
-    const unsigned long long m = __ballot(has);
-    __syncthreads();  // s_wave reuse
-    if (lane == 0) s_wave[wave] = (uint32_t)__popcll(m);
-    __syncthreads();
-    uint32_t before = 0, tot = 0;
-    for (uint32_t w = 0; w < kBlock / 64; w++) {
-      before += w < wave ? s_wave[w] : 0;
-      tot += s_wave[w];
+  constexpr uint64_t kPer = 8ull * kBlock;
+  for (uint64_t c0 = (uint64_t)blockIdx.x * kPer; c0 < nchunks; c0 += (uint64_t)gridDim.x * kPer) {
+    const uint64_t c = c0 + (uint64_t)threadIdx.x * 8;
+    uint32_t v[8];
+    if (c + 8 <= nchunks) {
+      const uint4 a = *(const uint4*)(ev + c), b = *(const uint4*)(ev + c + 4);
+      v[0] = a.x, v[1] = a.y, v[2] = a.z, v[3] = a.w, v[4] = b.x, v[5] = b.y, v[6] = b.z, v[7] = b.w;
+    } else {
+#pragma unroll
+      for (int i = 0; i < 8; i++) v[i] = c + i < nchunks ? ev[c + i] : 0u;
     }
-    if (has) list[at + before + __popcll(m & ((1ull << lane) - 1))] = (uint32_t)c;
-    at += tot;
+    uint32_t has = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) has |= ((v[i] & ~kEvAlways) != 0 ? 1u : 0u) << i;
+    const uint32_t n = __popc(has);
+    // inclusive scan over the wave
+    uint32_t inc = n;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t t = __shfl_up(inc, o);
+      if (lane >= (uint32_t)o) inc += t;
+    }
+    if (lane == 63) s_wave[wave] = inc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      uint32_t tot = 0;
+      for (uint32_t w = 0; w < kBlock / 64; w++) tot += s_wave[w];
+      s_base = tot ? atomicAdd(count, tot) : 0;
+    }
+    __syncthreads();
+    uint32_t at = s_base + inc - n;
+    for (uint32_t w = 0; w < wave; w++) at += s_wave[w];
+    for (uint32_t t = has; t; t &= t - 1) list[at++] = (uint32_t)(c + __builtin_ctz(t));
+    __syncthreads();  // s_wave / s_base reuse
   }
 }
 
@@ -1895,6 +1933,7 @@ static int make_device_k1(const Plan& p, DevK1* out, std::vector<void*>* allocs,
 
 // ---------------------------------------------------------------- rule tables on a device
 struct DeviceRules {
+  uint32_t all_kw_rows = 0;  // the plan has host-only rules: the host reads every keyword row
   int device = 0;
   const Plan* plan = nullptr;
   uint32_t chunk = 256, ext_cap = 1u << 16, adapt_mib = 0;
@@ -2135,6 +2174,7 @@ int device_rules_create(int device, const Plan& p, uint32_t chunk, uint32_t ext_
   if ((rc = make_device_k1(p, &r->k1, &r->tables, &r->k1h))) return rc;
   if ((rc = make_device_k1x(p, &r->k1x, &r->tables))) return rc;
   r->has_k1x = !p.x_lits.empty();
+  for (uint8_t h : p.rule_hostonly) r->all_kw_rows |= h;
   if (r->has_k1x)  // the 128 KiB prefix bitmap is dynamic LDS
     HIP_TRY(hipFuncSetAttribute(k1x_fn(r->k1x.step), hipFuncAttributeMaxDynamicSharedMemorySize,
                                 kXDwords * 4 + 16));
@@ -2414,7 +2454,7 @@ int enqueue_scan(DeviceRules* r, LaneState* l, const ScanInput& in, HostOut* out
   if (work) {
     ggate_kernel<<<(F + 255) / 256, 256, 0, st>>>(l->kw, F, W, r->d_kwg, r->d_galw, r->GW, l->ggate);
     HIP_TRY(hipGetLastError());
-    const uint32_t cgrid = (uint32_t)std::min<uint64_t>((nchunks + kBlock - 1) / kBlock, (uint64_t)r->grid);
+    const uint32_t cgrid = (uint32_t)std::min<uint64_t>((nchunks + 8 * kBlock - 1) / (8 * kBlock), (uint64_t)r->grid);
     ev_compact_kernel<<<cgrid, kBlock, 0, st>>>(l->ev_bits, nchunks, l->evlist, l->counts + 1);
     HIP_TRY(hipGetLastError());
     const int igrid = r->grid;
@@ -2487,9 +2527,16 @@ int enqueue_scan(DeviceRules* r, LaneState* l, const ScanInput& in, HostOut* out
       }
     };
     copy(out->counts, l->counts, sizeof(uint32_t) * 16);
-    copy(out->kw, l->kw, sizeof(uint32_t) * (uint64_t)F * W);
-    copy(out->ovf, l->ovf, F);
     copy(out->gskip, l->gskip, G);
+    OA.kw = l->kw;
+    OA.kw_host = (uint32_t*)(out->blk_dev + ((uint8_t*)out->kw - out->blk));
+    OA.ovf = l->ovf;
+    OA.flags_host = out->blk_dev + (out->ovf - out->blk);
+    OA.F = F;
+    OA.W = W;
+    OA.fb_lo = (uint32_t)p.fb_kw0;
+    OA.fb_hi = (uint32_t)p.n_kw;
+    OA.all_rows = r->all_kw_rows;
     outputs_kernel<<<128, 256, 0, st>>>(OA);
     HIP_TRY(hipGetLastError());
   }
@@ -2521,6 +2568,13 @@ int lane_k2_trace(LaneState* l, std::vector<unsigned long long>* out) {
   const size_t n = std::min<size_t>((size_t)counts[2] * kTraceW, l->etrace_cap);
   out->resize(n);
   if (n) HIP_TRY(hipMemcpy(out->data(), l->etrace, n * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+  return TSG_OK;
+}
+
+int lane_kw(LaneState* l, uint32_t* kw, size_t n) {
+  HIP_TRY(hipSetDevice(l->d->device));
+  HIP_TRY(hipStreamSynchronize(l->st));
+  if (n) HIP_TRY(hipMemcpy(kw, l->kw, sizeof(uint32_t) * n, hipMemcpyDeviceToHost));
   return TSG_OK;
 }
 

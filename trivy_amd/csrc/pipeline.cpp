@@ -333,6 +333,7 @@ void run_job(tsg_ctx* c, std::shared_ptr<Batch> b, BatchView view, HostOut ho,
       kv.cand = ho.cand;
       kv.ncand = std::min<uint32_t>(ho.counts[0], ho.cand_cap);
       kv.overflow = ho.ovf;
+      kv.sparse_kw = true;  // outputs_kernel: flags and the keyword rows the host reads
       kv.kw_unknown = kwu ? kwu->data() : nullptr;
       kv.path_ok = nullptr;  // Global.AllowPath on the host (plan.cpp path_allowed)
       kv.group_skipped = skipped ? ho.gskip : nullptr;
@@ -764,8 +765,8 @@ int tsg_batch_kernels(tsg_ctx* c, uint32_t slot_id, uint32_t nfiles, uint32_t* k
       std::memcpy(b.counts, ho.counts, sizeof(b.counts));
       b.bytes = s.off[nfiles];
       update_stats(c, b);
-      if (kw) std::memcpy(kw, ho.kw, sizeof(uint32_t) * std::min(kw_len, W * nfiles));
-      if (ev) rc = lane_events(l, ev, ev_len);
+      if (kw) rc = lane_kw(l, kw, std::min(kw_len, W * nfiles));
+      if (ev && !rc) rc = lane_events(l, ev, ev_len);
       if (const char* tp = getenv("TSG_K2_TRACE")) {  // append the K2 entry trace (measurements)
         std::vector<unsigned long long> tr;
         if (!rc) rc = lane_k2_trace(l, &tr);

@@ -995,8 +995,10 @@ void resolve_batch(const Ruleset& rs, const Plan& plan, const BatchView& b,
     uint32_t cnt = 0;
     for (uint32_t f = (uint32_t)(bi * kBlk), fe = (uint32_t)std::min<size_t>(F, (bi + 1) * kBlk); f < fe; f++) {
       bool need = first[f] != first[f + 1] || b.offsets[f + 1] == b.offsets[f] ||
-                  (ko.overflow && ko.overflow[f]) || !hostonly.empty();
-      if (!need) {
+                  (ko.overflow && (ko.overflow[f] & 1)) || !hostonly.empty();
+      if (!need && ko.sparse_kw) {
+        need = (ko.overflow[f] & 2) != 0;
+      } else if (!need) {
         const uint32_t* kw = ko.kw + (size_t)f * plan.kw_words;
         for (int k = plan.fb_kw0; k < plan.n_kw && !need; k++) need = (kw[k / 32] >> (k % 32)) & 1;
       }
@@ -1091,7 +1093,7 @@ void resolve_batch(const Ruleset& rs, const Plan& plan, const BatchView& b,
       }
     };
     // kernel overflow: resolve every rule over the whole file
-    const bool ovf = ko.overflow && ko.overflow[f];
+    const bool ovf = ko.overflow && (ko.overflow[f] & 1);
     bool any_host = false;
     for (uint32_t r : hostonly)
       if (kw_state(r) != 0) any_host = true;
