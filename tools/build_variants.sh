@@ -1,5 +1,6 @@
 # Build measurement variants of libtrivy_secret.so: the same sources with other compile-time
-# settings (select one with TSG_LIB_VARIANT=<name>).  Every variant computes the same results.
+# settings (select one with TSG_LIB_VARIANT=<name>).  Every variant computes the same results
+# unless marked (wrong results): those only time a kernel's parts.
 #   usage: tools/build_variants.sh NAME...
 set -e
 cd "$(dirname "$0")/.."
@@ -23,5 +24,9 @@ for v in "$@"; do
     k2noinl) build $v -DK2_NOINL ;;      # K2: rare paths out of line
     x1) build $v -DK1X_WORDS=1 ;;        # K1X: words per lane per round
     x8) build $v -DK1X_WORDS=8 ;;
+    xnop) build $v -DXV_NOP ;;           # K1X verify: list reads only (wrong results)
+    xnocmp) build $v -DXV_NOCMP ;;       # K1X verify: no literal comparison (wrong results)
+    xdiag) build $v -DK1X_DIAG ;;        # K1X: verify counters in k2_long_tails (slot probes),
+                                         # k2_tail_bytes (entries examined), k2_tail_max (matches)
   esac
 done

@@ -46,7 +46,8 @@ def main():
            "dev_GBps": round(nb / (med("k1_ms") + med("gate_ms") + med("k2_ms")) / 1e6, 1),
            "k2_items": rows[-1]["k2_items"], "k2_entries": rows[-1]["k2_launches"],
            "candidates": rows[-1]["candidates"], "k1x_records": rows[-1]["k1x_records"],
-           "k1x_inline": rows[-1]["k1x_inline"]}
+           "k1x_inline": rows[-1]["k1x_inline"],
+           "diag": [rows[-1]["k2_tail_bytes"], rows[-1]["k2_tail_max"], rows[-1]["k2_long_tails"]]}
     print(json.dumps(out), flush=True)
 
 

@@ -591,7 +591,12 @@ struct DevK1X {
   const uint32_t* ev;      // [n] event bits
   uint32_t kw_words;
   uint32_t step;           // Plan::x_step: 1, 2 or 4
+  // slots, lits, off, kwid, ev and bytes are parts of one image (16-B aligned parts), which
+  // k1x_verify_kernel stages in LDS when it fits
+  const uint8_t* img;
+  uint32_t img_bytes;
 };
+constexpr uint32_t kXImgLds = 128 * 1024;  // verify: largest image staged in LDS
 
 
 struct K1XArgs {
@@ -605,7 +610,7 @@ struct K1XArgs {
   uint2* list;      // {word index, hit mask}, one slice per k1x_kernel block
   uint32_t* count;  // [blocks] records in each slice
   uint32_t cap;     // records in all slices
-  uint32_t* stats;  // {records listed, words verified inline} (batch counts 13, 14)
+  uint32_t* stats;  // {records listed, words verified inline} (batch counts 14, 15)
 };
 
 __device__ __forceinline__ uint32_t x_lower4(uint32_t x) {
@@ -626,13 +631,20 @@ __device__ __forceinline__ uint32_t x_low_byte(uint8_t c) { return (c >= 'A' && 
 
 // exact check of the literals whose 4-gram at some offset j starts at batch byte p (window
 // w = its 4 lowercased bytes): each candidate literal starts at p - j
+#ifdef K1X_DIAG  // measurement builds: slot probes, entries examined, literal matches
+#define K1X_DIAG_ADD(i, v) atomicAdd(&A.stats[(i)], (v))
+#else
+#define K1X_DIAG_ADD(i, v) ((void)0)
+#endif
 __device__ void k1x_verify_at(const DevK1X& x, const K1XArgs& A, uint64_t p, uint32_t w) {
   // (the product's top bits: its low bits see only the window's first bytes)
   uint32_t h = (w * 0x85EBCA6Bu) >> x.shift;
   for (;;) {
     const uint4 sl = x.slots[h];
+    K1X_DIAG_ADD(-4, 1u);
     if (sl.z == 0) return;  // no literal with this 4-gram
     if (sl.x == w) {
+      K1X_DIAG_ADD(-6, sl.z);
       for (uint32_t e = 0; e < sl.z; e++) {
         const uint32_t ent = x.lits[sl.y + e];
         const uint32_t i = ent & 0xFFFFFFu, j = ent >> 24;
@@ -641,8 +653,12 @@ __device__ void k1x_verify_at(const DevK1X& x, const K1XArgs& A, uint64_t p, uin
         const uint32_t a = x.off[i], len = x.off[i + 1] - a;
         if (s + len > A.total) continue;
         uint32_t t = 0;
+#ifdef XV_NOCMP  // measurement builds: no literal comparison (wrong results)
+        t = len;
+#endif
         while (t < len && x_low_byte(A.data[s + t]) == x.bytes[a + t]) t++;
         if (t < len) continue;
+        K1X_DIAG_ADD(-5, 1u);
         const uint64_t q = s + len - 1;
         if (x.ev[i]) atomicOr(&A.ev[q / A.chunk], x.ev[i]);
         const int32_t k = x.kwid[i];
@@ -762,20 +778,42 @@ static const void* k1x_fn(uint32_t step) {
   return (const void*)k1x_kernel<1>;
 }
 
-// kXVerifyParts blocks per k1x_kernel block, each a strided share of that block's slice
-constexpr uint32_t kXVerifyParts = 8;
-__global__ void __launch_bounds__(kBlock) k1x_verify_kernel(DevK1X x, K1XArgs A, uint32_t nblocks) {
-  const uint32_t slice = A.cap / nblocks;
-  const uint32_t b = blockIdx.x % nblocks, part = blockIdx.x / nblocks;
+// One block per k1x_kernel block, its slice of the list.  LDS: the table image is staged
+// first, so the lookups of a 4-gram that the text holds often (thousands of threads on the
+// same slot, entries and literal bytes) are LDS broadcasts instead of one L2 channel's
+// queue -- 10x on configs[3] (profiles/r04/xv).
+constexpr int kXVerifyBlock = 1024;
+template <bool LDS>
+__global__ void __launch_bounds__(kXVerifyBlock) k1x_verify_kernel(DevK1X x, K1XArgs A, uint32_t nblocks) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t x_img[];
+  const uint32_t b = blockIdx.x;
   const uint32_t n = A.count[b];
-  for (uint32_t j = part * blockDim.x + threadIdx.x; j < n; j += kXVerifyParts * blockDim.x) {
+  if (n == 0) return;
+  DevK1X y = x;
+  if constexpr (LDS) {
+    for (uint32_t i = threadIdx.x; i < x.img_bytes / 16; i += blockDim.x) ((uint4*)x_img)[i] = ((const uint4*)x.img)[i];
+    __syncthreads();
+    auto rebase = [&](auto* p) { return (decltype(p))(x_img + ((const uint8_t*)p - x.img)); };
+    y.slots = rebase(x.slots);
+    y.lits = rebase(x.lits);
+    y.off = rebase(x.off);
+    y.kwid = rebase(x.kwid);
+    y.ev = rebase(x.ev);
+    y.bytes = rebase(x.bytes);
+  }
+  const uint32_t slice = A.cap / nblocks;
+  for (uint32_t j = threadIdx.x; j < n; j += blockDim.x) {
     const uint2 r = A.list[(size_t)b * slice + j];
     const uint64_t p0 = (uint64_t)r.x * 16;
     for (uint32_t t = r.y; t; t &= t - 1) {
       const uint64_t p = p0 + __builtin_ctz(t);
       const uint32_t w = x_low_byte(A.data[p]) | x_low_byte(A.data[p + 1]) << 8 | x_low_byte(A.data[p + 2]) << 16 |
                          x_low_byte(A.data[p + 3]) << 24;
-      k1x_verify_at(x, A, p, w);
+#ifdef XV_NOP  // measurement builds: the verify kernel's fixed cost
+      if (w == 0x01020304u) A.stats[1] = 0;
+#else
+      k1x_verify_at(y, A, p, w);
+#endif
     }
   }
 }
@@ -839,28 +877,30 @@ struct ItemArgs {
 // chunks whose K1 event word is not empty, compacted into `list`: each block takes a
 // contiguous range, counts it, reserves its output with ONE global atomic, then writes its
 // chunks in order (wave ballots + an LDS prefix over the block's waves)
-// One pass: each thread tests 8 consecutive chunks (two 16-B loads), the block scans the
-// counts and claims its output range with one atomic per 8 * kBlock chunks.  (Blocks'
-// ranges land in the list in claim order; its readers do not need it sorted.)
+// One pass: each thread tests 32 consecutive chunks (eight 16-B loads in flight), the block
+// scans the counts and claims its output range with one atomic per 32 * kBlock chunks.
+// (Blocks' ranges land in the list in claim order; its readers do not need it sorted.)
+constexpr uint32_t kEvPer = 32;
 __global__ void __launch_bounds__(kBlock) ev_compact_kernel(const uint32_t* __restrict__ ev, uint64_t nchunks,
                                                             uint32_t* __restrict__ list, uint32_t* __restrict__ count) {
   __shared__ uint32_t s_wave[kBlock / 64];
   __shared__ uint32_t s_base;
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  constexpr uint64_t kPer = 8ull * kBlock;
+  constexpr uint64_t kPer = (uint64_t)kEvPer * kBlock;
   for (uint64_t c0 = (uint64_t)blockIdx.x * kPer; c0 < nchunks; c0 += (uint64_t)gridDim.x * kPer) {
-    const uint64_t c = c0 + (uint64_t)threadIdx.x * 8;
-    uint32_t v[8];
-    if (c + 8 <= nchunks) {
-      const uint4 a = *(const uint4*)(ev + c), b = *(const uint4*)(ev + c + 4);
-      v[0] = a.x, v[1] = a.y, v[2] = a.z, v[3] = a.w, v[4] = b.x, v[5] = b.y, v[6] = b.z, v[7] = b.w;
-    } else {
-#pragma unroll
-      for (int i = 0; i < 8; i++) v[i] = c + i < nchunks ? ev[c + i] : 0u;
-    }
+    const uint64_t c = c0 + (uint64_t)threadIdx.x * kEvPer;
     uint32_t has = 0;
+    if (c + kEvPer <= nchunks) {
+      uint4 v[kEvPer / 4];
 #pragma unroll
-    for (int i = 0; i < 8; i++) has |= ((v[i] & ~kEvAlways) != 0 ? 1u : 0u) << i;
+      for (uint32_t i = 0; i < kEvPer / 4; i++) v[i] = *(const uint4*)(ev + c + 4 * i);
+#pragma unroll
+      for (uint32_t i = 0; i < kEvPer / 4; i++)
+        has |= ((v[i].x & ~kEvAlways) != 0 ? 1u : 0u) << (4 * i) | ((v[i].y & ~kEvAlways) != 0 ? 2u : 0u) << (4 * i) |
+               ((v[i].z & ~kEvAlways) != 0 ? 4u : 0u) << (4 * i) | ((v[i].w & ~kEvAlways) != 0 ? 8u : 0u) << (4 * i);
+    } else {
+      for (uint32_t i = 0; i < kEvPer && c + i < nchunks; i++) has |= ((ev[c + i] & ~kEvAlways) != 0 ? 1u : 0u) << i;
+    }
     const uint32_t n = __popc(has);
     // inclusive scan over the wave
     uint32_t inc = n;
@@ -1865,12 +1905,31 @@ static int make_device_k1x(const Plan& p, DevK1X* out, std::vector<void*>* alloc
   }
   int rc;
   if ((rc = upload_vec(bitmap, &out->bitmap, allocs))) return rc;
-  if ((rc = upload_vec(slots, &out->slots, allocs))) return rc;
-  if ((rc = upload_vec(lits, &out->lits, allocs))) return rc;
-  if ((rc = upload_vec(bytes, &out->bytes, allocs))) return rc;
-  if ((rc = upload_vec(off, &out->off, allocs))) return rc;
-  if ((rc = upload_vec(kwid, &out->kwid, allocs))) return rc;
-  if ((rc = upload_vec(ev, &out->ev, allocs))) return rc;
+  // the verify tables as one image: slots | lits | off | kwid | ev | bytes
+  std::vector<uint8_t> img;
+  auto part = [&](const void* src, size_t n) {
+    const size_t at = img.size();
+    img.resize((at + n + 15) / 16 * 16, 0);
+    if (n) std::memcpy(img.data() + at, src, n);
+    return at;
+  };
+  const size_t o_slots = part(slots.data(), slots.size() * sizeof(uint4));
+  const size_t o_lits = part(lits.data(), lits.size() * 4);
+  const size_t o_off = part(off.data(), off.size() * 4);
+  const size_t o_kwid = part(kwid.data(), kwid.size() * 4);
+  const size_t o_ev = part(ev.data(), ev.size() * 4);
+  const size_t o_bytes = part(bytes.data(), bytes.size());
+  if (img.size() > 0xFFFFFFFFu) return fail(TSG_ERR_INTERNAL, "K1X tables too large");
+  const uint8_t* dimg = nullptr;
+  if ((rc = upload_vec(img, &dimg, allocs))) return rc;
+  out->img = dimg;
+  out->img_bytes = (uint32_t)img.size();
+  out->slots = (const uint4*)(dimg + o_slots);
+  out->lits = (const uint32_t*)(dimg + o_lits);
+  out->off = (const uint32_t*)(dimg + o_off);
+  out->kwid = (const int32_t*)(dimg + o_kwid);
+  out->ev = (const uint32_t*)(dimg + o_ev);
+  out->bytes = dimg + o_bytes;
   out->mask = nslots - 1;
   out->shift = 32 - lg;
   return TSG_OK;
@@ -2178,6 +2237,9 @@ int device_rules_create(int device, const Plan& p, uint32_t chunk, uint32_t ext_
   if (r->has_k1x)  // the 128 KiB prefix bitmap is dynamic LDS
     HIP_TRY(hipFuncSetAttribute(k1x_fn(r->k1x.step), hipFuncAttributeMaxDynamicSharedMemorySize,
                                 kXDwords * 4 + 16));
+  if (r->has_k1x && r->k1x.img_bytes <= kXImgLds)
+    HIP_TRY(hipFuncSetAttribute((const void*)k1x_verify_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                r->k1x.img_bytes));
   HIP_TRY(hipMalloc((void**)&r->d_hits, sizeof(uint32_t) * r->k1.ns));
   const uint32_t G = (uint32_t)p.groups.size();
   if (G > 0x7FFF) return fail(TSG_ERR_INTERNAL, "more K2 groups than transition records can name");
@@ -2263,6 +2325,9 @@ int lane_create(DeviceRules* d, LaneState** out) {
   l->d = d;
   HIP_TRY(hipStreamCreateWithFlags(&l->st, hipStreamNonBlocking));
   const uint32_t G = std::max<uint32_t>(1, (uint32_t)d->groups.size());
+  // per-batch counters: 0 candidates, 1 event chunks, 2 K2 entries, 3 dense entries, 5-7
+  // layout (5 items, 6 entries, 7 groups skipped), 8-11 K2 diagnostics,
+  // 12-13 K2 claim cursors (list, dense), 14-15 K1X (records listed, inline verified)
   HIP_TRY(hipMalloc((void**)&l->counts, sizeof(uint32_t) * 16));
   HIP_TRY(hipMalloc((void**)&l->gcount, sizeof(uint32_t) * G));
   HIP_TRY(hipMalloc((void**)&l->cursor, sizeof(uint32_t) * G));
@@ -2420,10 +2485,13 @@ int enqueue_scan(DeviceRules* r, LaneState* l, const ScanInput& in, HostOut* out
     const int xg = (int)std::max<uint64_t>(1, std::min<uint64_t>((total / 16 + kK1XBlock - 1) / kK1XBlock,
                                                                    (uint64_t)r->cus));
     K1XArgs X{data, l->off, l->cf, total, C, F, l->kw, l->ev_bits, l->xlist, l->xcount,
-              (uint32_t)std::min<size_t>(l->xlist_cap, 0xFFFFFFFFu), l->counts + 13};
+              (uint32_t)std::min<size_t>(l->xlist_cap, 0xFFFFFFFFu), l->counts + 14};
     void* xa[] = {(void*)&r->k1x, (void*)&X};
     HIP_TRY(hipLaunchKernel(k1x_fn(r->k1x.step), dim3(xg), dim3(kK1XBlock), xa, kXDwords * 4 + 16, st));
-    k1x_verify_kernel<<<xg * kXVerifyParts, kBlock, 0, st>>>(r->k1x, X, (uint32_t)xg);
+    if (r->k1x.img_bytes <= kXImgLds)
+      k1x_verify_kernel<true><<<xg, kXVerifyBlock, r->k1x.img_bytes, st>>>(r->k1x, X, (uint32_t)xg);
+    else
+      k1x_verify_kernel<false><<<xg, kXVerifyBlock, 0, st>>>(r->k1x, X, (uint32_t)xg);
     HIP_TRY(hipGetLastError());
   }
   HIP_TRY(hipEventRecord(out->ev[5], st));
@@ -2454,7 +2522,7 @@ int enqueue_scan(DeviceRules* r, LaneState* l, const ScanInput& in, HostOut* out
   if (work) {
     ggate_kernel<<<(F + 255) / 256, 256, 0, st>>>(l->kw, F, W, r->d_kwg, r->d_galw, r->GW, l->ggate);
     HIP_TRY(hipGetLastError());
-    const uint32_t cgrid = (uint32_t)std::min<uint64_t>((nchunks + 8 * kBlock - 1) / (8 * kBlock), (uint64_t)r->grid);
+    const uint32_t cgrid = (uint32_t)std::min<uint64_t>((nchunks + kEvPer * kBlock - 1) / (kEvPer * kBlock), (uint64_t)r->grid);
     ev_compact_kernel<<<cgrid, kBlock, 0, st>>>(l->ev_bits, nchunks, l->evlist, l->counts + 1);
     HIP_TRY(hipGetLastError());
     const int igrid = r->grid;

@@ -293,8 +293,8 @@ void update_stats(tsg_ctx* c, const Batch& b) {
   s.k2_tail_max = b.counts[9];
   s.k2_long_tails = b.counts[10];
   s.k2_replays = b.counts[11];
-  s.k1x_records = b.counts[13];
-  s.k1x_inline = b.counts[14];
+  s.k1x_records = b.counts[14];
+  s.k1x_inline = b.counts[15];
   s.k1_hot_states = c->dr ? device_rules_hot_states(c->dr) : 0;
   s.batches++;
   s.sum_bytes += b.bytes;
