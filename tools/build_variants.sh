@@ -26,6 +26,8 @@ for v in "$@"; do
     x8) build $v -DK1X_WORDS=8 ;;
     xnop) build $v -DXV_NOP ;;           # K1X verify: list reads only (wrong results)
     xnocmp) build $v -DXV_NOCMP ;;       # K1X verify: no literal comparison (wrong results)
+    xprobe) build $v -DXV_PROBE ;;       # K1X verify: slot probes only (wrong results)
+    xent) build $v -DXV_ENTRIES ;;       # K1X verify: entries, no comparison (wrong results)
     xdiag) build $v -DK1X_DIAG ;;        # K1X: verify counters in k2_long_tails (slot probes),
                                          # k2_tail_bytes (entries examined), k2_tail_max (matches)
   esac
