@@ -46,6 +46,36 @@ static const std::unordered_set<uint32_t>& common4() {
   return set;
 }
 
+// K1X windows of every literal of the plan: per literal the offset j0 whose windows hold
+// the fewest common 4-grams, then are shared by the fewest other literals (a window shared
+// by k literals costs k verifications per hit: 100 `begin_<name>` anchors all starting
+// "begi" made every "-----BEGIN" line of a batch check 100 literals).
+static void x_place_windows(Plan* p, int step) {
+  std::unordered_map<uint32_t, uint32_t> mult;
+  for (const auto& l : p->x_lits) {
+    std::unordered_set<uint32_t> mine;
+    for (size_t j = 0; j + 4 <= l.size(); j++) mine.insert(x_prefix4((const uint8_t*)l.data() + j));
+    for (uint32_t g : mine) mult[g]++;
+  }
+  p->x_j0.assign(p->x_lits.size(), 0);
+  for (size_t i = 0; i < p->x_lits.size(); i++) {
+    const std::string& l = p->x_lits[i];
+    const size_t last = std::min(l.size() - 3 - (size_t)step, (size_t)256 - (size_t)step);
+    uint64_t best = UINT64_MAX;
+    for (size_t j = 0; j <= last; j++) {
+      uint64_t c = 0;
+      for (size_t t = j; t < j + (size_t)step; t++) {
+        const uint32_t g = x_prefix4((const uint8_t*)l.data() + t);
+        c += (common4().count(g) ? 1000000u : 0u) + mult[g];
+      }
+      if (c < best) {
+        best = c;
+        p->x_j0[i] = (uint8_t)j;
+      }
+    }
+  }
+}
+
 // K1X windows of a lowercased literal at step `step`: the first offset j0 whose windows
 // j0 .. j0 + step - 1 hold the fewest common 4-grams.  Returns that count (0: a quiet
 // literal), -1 when the literal is too short for the step.
@@ -581,12 +611,7 @@ std::unique_ptr<Plan> build_plan(const Ruleset& rs, const PlanOptions& opt, std:
         k1_ok = false;
       if (k1_ok) {
         p->x_step = step;
-        p->x_j0.assign(p->x_lits.size(), 0);
-        for (size_t i = 0; i < p->x_lits.size(); i++) {
-          uint32_t j0 = 0;
-          x_pick(p->x_lits[i], step, &j0);
-          p->x_j0[i] = (uint8_t)j0;
-        }
+        x_place_windows(p, step);
       }
     }
     if (!k1_ok) {
