@@ -611,7 +611,7 @@ std::unique_ptr<Plan> build_plan(const Ruleset& rs, const PlanOptions& opt, std:
         k1_ok = false;
       if (k1_ok) {
         p->x_step = step;
-        x_place_windows(p, step);
+        x_place_windows(&*p, step);
       }
     }
     if (!k1_ok) {
