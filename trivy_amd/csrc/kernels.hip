@@ -896,6 +896,7 @@ struct ItemArgs {
   uint64_t nchunks;
   uint32_t F, G, GW, chunk, maxback;
   uint32_t* count;            // [G]
+  uint32_t* bcount;           // [gridDim.x * G] each count block's counts, for the emit pass
   const uint64_t* base;       // [G] item region of each group (emit pass), null: count pass
   uint32_t* cursor;           // [G]
   const uint8_t* listed;      // [G] 1 = list group (emit pass)
@@ -1018,27 +1019,24 @@ __global__ void __launch_bounds__(kBlock) items_count_kernel(ItemArgs A) {
   for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < nt; t += stride)
     gen_items(A, t, [&](uint32_t, uint32_t g, uint64_t lo, uint64_t hi) { atomicAdd(&s_count[g], (uint32_t)(hi - lo + 1)); });
   __syncthreads();
-  for (uint32_t g = threadIdx.x; g < A.G; g += blockDim.x)
+  for (uint32_t g = threadIdx.x; g < A.G; g += blockDim.x) {
+    A.bcount[(size_t)blockIdx.x * A.G + g] = s_count[g];
     if (s_count[g]) atomicAdd(&A.count[g], s_count[g]);
+  }
 }
 
-// emit pass: the block counts its items of listed groups again, reserves one range per
-// group with a single global atomic, then writes its items into it
+// emit pass (same grid as the count pass, so block b generates the items block b counted):
+// the block reserves one range per listed group with a single global atomic, then writes
+// its items into it
 __global__ void __launch_bounds__(kBlock) items_emit_kernel(ItemArgs A) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   uint32_t* s_count = (uint32_t*)smem;
   uint32_t* s_base = s_count + A.G;
-  for (uint32_t g = threadIdx.x; g < A.G; g += blockDim.x) s_count[g] = 0;
-  __syncthreads();
   const uint64_t nt = (uint64_t)*A.nev + A.F, stride = (uint64_t)gridDim.x * blockDim.x;
   const uint64_t t0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  for (uint64_t t = t0; t < nt; t += stride)
-    gen_items(A, t, [&](uint32_t, uint32_t g, uint64_t lo, uint64_t hi) {
-      if (A.listed[g] == kGroupList) atomicAdd(&s_count[g], (uint32_t)(hi - lo + 1));
-    });
-  __syncthreads();
   for (uint32_t g = threadIdx.x; g < A.G; g += blockDim.x) {
-    s_base[g] = s_count[g] ? (uint32_t)A.base[g] + atomicAdd(&A.cursor[g], s_count[g]) : 0;
+    const uint32_t n = A.listed[g] == kGroupList ? A.bcount[(size_t)blockIdx.x * A.G + g] : 0;
+    s_base[g] = n ? (uint32_t)A.base[g] + atomicAdd(&A.cursor[g], n) : 0;
     s_count[g] = 0;
   }
   __syncthreads();
@@ -1104,6 +1102,8 @@ constexpr uint32_t kEntryChunks = kStreams * kBlock;
 __global__ void __launch_bounds__(kLayoutBlock) layout_kernel(LayoutArgs A) {
   __shared__ unsigned long long s_wave64[kLayoutBlock / 64];
   __shared__ unsigned long long s_carry[5];  // items, entries, dense groups, skipped groups, dense entries
+  __shared__ uint4 s_grp[kLayoutBlock];  // per group of the tile: kind, first entry, entries, item base
+  __shared__ uint64_t s_cnt[kLayoutBlock];
   if (threadIdx.x < 5) s_carry[threadIdx.x] = 0;
   __syncthreads();
   for (uint32_t g0 = 0; g0 < A.G; g0 += blockDim.x) {
@@ -1131,22 +1131,31 @@ __global__ void __launch_bounds__(kLayoutBlock) layout_kernel(LayoutArgs A) {
     // (entries_cap covers every list entry the item capacity allows plus max_dense dense
     // groups, so the work list always fits)
     const uint64_t e0 = s_carry[1] + epre, d0 = s_carry[4] + dpre2;
+    const uint8_t k = !cnt ? kGroupNone : list ? kGroupList : dense ? kGroupDense : kGroupSkip;
     if (g < A.G) {
-      const uint8_t k = !cnt ? kGroupNone : list ? kGroupList : dense ? kGroupDense : kGroupSkip;
       A.kind[g] = k;
       A.gskip[g] = k == kGroupSkip ? 1 : 0;
       A.base[g] = s_carry[0] + ipre;
-      if (k == kGroupList)
-        for (uint64_t i = 0; i < nent; i++) {
-          const uint32_t first = (uint32_t)(i * kEntryItems);
-          A.entries[e0 + i] = make_uint4(g, (uint32_t)(s_carry[0] + ipre) + first,
-                                         (uint32_t)min<uint64_t>(kEntryItems, cnt - first), kGroupList);
+    }
+    s_grp[threadIdx.x] = make_uint4(k, (uint32_t)(k == kGroupDense ? d0 : e0),
+                                    (uint32_t)(k == kGroupDense ? ndent : nent), (uint32_t)(s_carry[0] + ipre));
+    s_cnt[threadIdx.x] = cnt;
+    __syncthreads();
+    // the work-list entries of this tile's groups, each group's by the whole block (a dense
+    // group has nchunks / kEntryChunks of them: thousands, one thread took 15 us)
+    for (uint32_t t = 0; t < kLayoutBlock && g0 + t < A.G; t++) {
+      const uint4 gi = s_grp[t];
+      if (gi.x == kGroupList)
+        for (uint32_t i = threadIdx.x; i < gi.z; i += blockDim.x) {
+          const uint32_t first = i * kEntryItems;
+          A.entries[gi.y + i] = make_uint4(g0 + t, gi.w + first, (uint32_t)min<uint64_t>(kEntryItems, s_cnt[t] - first),
+                                           kGroupList);
         }
-      else if (k == kGroupDense)
-        for (uint64_t i = 0; i < ndent; i++) {
-          const uint64_t first = i * kEntryChunks;
-          A.dentries[d0 + i] = make_uint4(g, (uint32_t)first,
-                                          (uint32_t)min<uint64_t>(kEntryChunks, A.nchunks - first), kGroupDense);
+      else if (gi.x == kGroupDense)
+        for (uint32_t i = threadIdx.x; i < gi.z; i += blockDim.x) {
+          const uint64_t first = (uint64_t)i * kEntryChunks;
+          A.dentries[gi.y + i] = make_uint4(g0 + t, (uint32_t)first,
+                                            (uint32_t)min<uint64_t>(kEntryChunks, A.nchunks - first), kGroupDense);
         }
     }
     __syncthreads();
@@ -2098,6 +2107,7 @@ struct LaneState {
   uint32_t cand_cap = 0;
   uint32_t* counts = nullptr;   // [16] 0 candidates, 1 event chunks, 2 K2 entries, ...
   uint32_t* gcount = nullptr;   // [G]
+  uint32_t* bcount = nullptr;   // [grid * G] items_count_kernel's per-block counts
   uint32_t* cursor = nullptr;   // [G]
   uint64_t* base = nullptr;     // [G]
   uint8_t* kind = nullptr;      // [G]
@@ -2110,7 +2120,7 @@ struct LaneState {
     (void)hipSetDevice(d->device);
     if (st) (void)hipStreamSynchronize(st);
     void* bufs[] = {data_alloc, meta, cf, ev_bits, xlist, xcount, evlist, kw, ggate, ovf,
-                    items, entries, dentries, cand, counts, gcount, cursor, base, kind, gskip, etrace};
+                    items, entries, dentries, cand, counts, gcount, bcount, cursor, base, kind, gskip, etrace};
     for (void* b : bufs) (void)hipFree(b);
     if (st) (void)hipStreamDestroy(st);
   }
@@ -2362,6 +2372,7 @@ int lane_create(DeviceRules* d, LaneState** out) {
   // 12-13 K2 claim cursors (list, dense), 14-15 K1X (records listed, inline verified)
   HIP_TRY(hipMalloc((void**)&l->counts, sizeof(uint32_t) * 16));
   HIP_TRY(hipMalloc((void**)&l->gcount, sizeof(uint32_t) * G));
+  HIP_TRY(hipMalloc((void**)&l->bcount, sizeof(uint32_t) * G * (size_t)d->grid));
   HIP_TRY(hipMalloc((void**)&l->cursor, sizeof(uint32_t) * G));
   HIP_TRY(hipMalloc((void**)&l->base, sizeof(uint64_t) * G));
   HIP_TRY(hipMalloc((void**)&l->kind, G));
@@ -2544,6 +2555,7 @@ int enqueue_scan(DeviceRules* r, LaneState* l, const ScanInput& in, HostOut* out
   IA.chunk = C;
   IA.maxback = r->maxback;
   IA.count = l->gcount;
+  IA.bcount = l->bcount;
   IA.cursor = l->cursor;
   IA.listed = l->kind;
   IA.evlist = l->evlist;
@@ -2557,7 +2569,7 @@ int enqueue_scan(DeviceRules* r, LaneState* l, const ScanInput& in, HostOut* out
     const uint32_t cgrid = (uint32_t)std::min<uint64_t>((nchunks + kEvPer * kBlock - 1) / (kEvPer * kBlock), (uint64_t)r->grid);
     ev_compact_kernel<<<cgrid, kBlock, 0, st>>>(l->ev_bits, nchunks, l->evlist, l->counts + 1);
     HIP_TRY(hipGetLastError());
-    const int igrid = r->grid;
+    const int igrid = r->grid;  // both items passes (bcount holds grid x G)
     hipLaunchKernelGGL(items_count_kernel, dim3(igrid), dim3(kBlock), G * sizeof(uint32_t) + 16, st, IA);
     HIP_TRY(hipGetLastError());
     LayoutArgs LA{l->gcount, G, nchunks, items_cap, max_dense, l->kind, l->base, l->entries, l->counts + 2,
