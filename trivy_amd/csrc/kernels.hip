@@ -1102,11 +1102,13 @@ constexpr uint32_t kEntryChunks = kStreams * kBlock;
 __global__ void __launch_bounds__(kLayoutBlock) layout_kernel(LayoutArgs A) {
   __shared__ unsigned long long s_wave64[kLayoutBlock / 64];
   __shared__ unsigned long long s_carry[5];  // items, entries, dense groups, skipped groups, dense entries
-  __shared__ uint4 s_grp[kLayoutBlock];  // per group of the tile: kind, first entry, entries, item base
-  __shared__ uint64_t s_cnt[kLayoutBlock];
+  __shared__ uint2 s_dense[kLayoutBlock];  // dense groups of the tile: group, first dense entry
+  __shared__ uint32_t s_ndense;
+  const uint32_t ndent_all = (uint32_t)((A.nchunks + kEntryChunks - 1) / kEntryChunks);
   if (threadIdx.x < 5) s_carry[threadIdx.x] = 0;
   __syncthreads();
   for (uint32_t g0 = 0; g0 < A.G; g0 += blockDim.x) {
+    if (threadIdx.x == 0) s_ndense = 0;
     const uint32_t g = g0 + threadIdx.x;
     const uint64_t cnt = g < A.G ? A.gcount[g] : 0;
     const bool dense_want = cnt * 2 > A.nchunks;
@@ -1137,26 +1139,23 @@ __global__ void __launch_bounds__(kLayoutBlock) layout_kernel(LayoutArgs A) {
       A.gskip[g] = k == kGroupSkip ? 1 : 0;
       A.base[g] = s_carry[0] + ipre;
     }
-    s_grp[threadIdx.x] = make_uint4(k, (uint32_t)(k == kGroupDense ? d0 : e0),
-                                    (uint32_t)(k == kGroupDense ? ndent : nent), (uint32_t)(s_carry[0] + ipre));
-    s_cnt[threadIdx.x] = cnt;
+    if (k == kGroupList)
+      for (uint64_t i = 0; i < nent; i++) {
+        const uint32_t first = (uint32_t)(i * kEntryItems);
+        A.entries[e0 + i] = make_uint4(g, (uint32_t)(s_carry[0] + ipre) + first,
+                                       (uint32_t)min<uint64_t>(kEntryItems, cnt - first), kGroupList);
+      }
+    if (k == kGroupDense) s_dense[atomicAdd(&s_ndense, 1u)] = make_uint2(g, (uint32_t)d0);
     __syncthreads();
-    // the work-list entries of this tile's groups, each group's by the whole block (a dense
-    // group has nchunks / kEntryChunks of them: thousands, one thread took 15 us)
-    for (uint32_t t = 0; t < kLayoutBlock && g0 + t < A.G; t++) {
-      const uint4 gi = s_grp[t];
-      if (gi.x == kGroupList)
-        for (uint32_t i = threadIdx.x; i < gi.z; i += blockDim.x) {
-          const uint32_t first = i * kEntryItems;
-          A.entries[gi.y + i] = make_uint4(g0 + t, gi.w + first, (uint32_t)min<uint64_t>(kEntryItems, s_cnt[t] - first),
-                                           kGroupList);
-        }
-      else if (gi.x == kGroupDense)
-        for (uint32_t i = threadIdx.x; i < gi.z; i += blockDim.x) {
-          const uint64_t first = (uint64_t)i * kEntryChunks;
-          A.dentries[gi.y + i] = make_uint4(g0 + t, (uint32_t)first,
-                                            (uint32_t)min<uint64_t>(kEntryChunks, A.nchunks - first), kGroupDense);
-        }
+    // a dense group's entries (nchunks / kEntryChunks of them: tens of thousands) are
+    // written by the whole block
+    for (uint32_t t = 0; t < s_ndense; t++) {
+      const uint2 dg = s_dense[t];
+      for (uint32_t i = threadIdx.x; i < ndent_all; i += blockDim.x) {
+        const uint64_t first = (uint64_t)i * kEntryChunks;
+        A.dentries[dg.y + i] = make_uint4(dg.x, (uint32_t)first,
+                                          (uint32_t)min<uint64_t>(kEntryChunks, A.nchunks - first), kGroupDense);
+      }
     }
     __syncthreads();
     if (threadIdx.x == 0) {
