@@ -358,7 +358,7 @@ def main():
                          "IsBinary passes them to Scan (configs[4]: 0.5)")
     ap.add_argument("--piece-mib", type=int, default=0,
                     help="e2e: piece floor of tsg_fs_scan / tsg_layer_scan (the 'piece_mib' test knob; "
-                         "0: the library's 160)")
+                         "0: the library's 16)")
     args = ap.parse_args()
     if args.e2e:
         return main_e2e(args)

@@ -294,7 +294,7 @@ const char* tsg_last_error(void);
  * TSG_PROF, TSG_PROF2, TSG_LAYER_PROF, TSG_K2_DIAG, TSG_K2_TRACE and TSG_DEBUG_RESOLVE only
  * add timings, counters or traces).  value NULL or "" resets the knob.
  *   "tar_range_kib"   sub-range floor of the parallel tar index walk (default 64 MiB)
- *   "piece_mib"       piece floor of tsg_layer_scan / tsg_fs_scan (default 160)
+ *   "piece_mib"       piece floor of tsg_layer_scan / tsg_fs_scan (default 16)
  *   "pike_only"       "1": the Go-regexp matcher uses the Pike VM alone (no backtracker)
  *   "no_k1x"          "1": a rule set too large for K1's automaton is not split onto K1X
  *   "x_step"          1, 2 or 4: the K1X window step of the next plans (default: the widest
