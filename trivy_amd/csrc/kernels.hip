@@ -858,11 +858,10 @@ __device__ __forceinline__ bool group_gated(const uint32_t* __restrict__ kwf, co
 // per file: bit g of ggate[f * GW + g / 64] = group g gated (Rule.MatchKeywords may pass):
 // the always-gated groups, ORed with the groups of every keyword bit the file has (a file
 // holds few keywords, so the cost is its set bits x GW, not groups x keyword words)
-__global__ void ggate_kernel(const uint32_t* __restrict__ kw, uint32_t F, uint32_t W,
-                             const unsigned long long* __restrict__ kwg,
-                             const unsigned long long* __restrict__ galw, uint32_t GW,
-                             unsigned long long* __restrict__ ggate) {
-  const uint32_t f = blockIdx.x * blockDim.x + threadIdx.x;
+__device__ __forceinline__ void ggate_file(uint32_t f, const uint32_t* __restrict__ kw, uint32_t F, uint32_t W,
+                                           const unsigned long long* __restrict__ kwg,
+                                           const unsigned long long* __restrict__ galw, uint32_t GW,
+                                           unsigned long long* __restrict__ ggate) {
   if (f >= F) return;
   const uint32_t* kwf = kw + (size_t)f * W;
   for (uint32_t w0 = 0; w0 < GW; w0 += 8) {
@@ -887,7 +886,7 @@ struct ItemArgs {
   const uint64_t* off;
   const uint32_t* cf;  // coarse file map (file_of)
   const uint32_t* ev;
-  const uint32_t* evlist;           // chunks with event bits (ev_compact_kernel)
+  const uint32_t* evlist;           // chunks with event bits (ev_compact_block)
   const uint32_t* nev;              // [1] length of evlist
   const unsigned long long* ggate;  // [F * GW]
   const unsigned long long* gofbit;  // [32 * GW] groups listening to event bit b; bit 31 = every chunk
@@ -903,20 +902,18 @@ struct ItemArgs {
   uint2* items;
 };
 
-// chunks whose K1 event word is not empty, compacted into `list`: each block takes a
-// contiguous range, counts it, reserves its output with ONE global atomic, then writes its
-// chunks in order (wave ballots + an LDS prefix over the block's waves)
-// One pass: each thread tests 32 consecutive chunks (eight 16-B loads in flight), the block
+// Chunks whose K1 event word is not empty, compacted into `list`.  One pass: each thread tests 32 consecutive chunks (eight 16-B loads in flight), the block
 // scans the counts and claims its output range with one atomic per 32 * kBlock chunks.
 // (Blocks' ranges land in the list in claim order; its readers do not need it sorted.)
 constexpr uint32_t kEvPer = 32;
-__global__ void __launch_bounds__(kBlock) ev_compact_kernel(const uint32_t* __restrict__ ev, uint64_t nchunks,
-                                                            uint32_t* __restrict__ list, uint32_t* __restrict__ count) {
+__device__ __forceinline__ void ev_compact_block(const uint32_t* __restrict__ ev, uint64_t nchunks,
+                                                 uint32_t* __restrict__ list, uint32_t* __restrict__ count,
+                                                 uint32_t bid, uint32_t nblocks) {
   __shared__ uint32_t s_wave[kBlock / 64];
   __shared__ uint32_t s_base;
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   constexpr uint64_t kPer = (uint64_t)kEvPer * kBlock;
-  for (uint64_t c0 = (uint64_t)blockIdx.x * kPer; c0 < nchunks; c0 += (uint64_t)gridDim.x * kPer) {
+  for (uint64_t c0 = (uint64_t)bid * kPer; c0 < nchunks; c0 += (uint64_t)nblocks * kPer) {
     const uint64_t c = c0 + (uint64_t)threadIdx.x * kEvPer;
     uint32_t has = 0;
     if (c + kEvPer <= nchunks) {
@@ -951,6 +948,27 @@ __global__ void __launch_bounds__(kBlock) ev_compact_kernel(const uint32_t* __re
     for (uint32_t t = has; t; t &= t - 1) list[at++] = (uint32_t)(c + __builtin_ctz(t));
     __syncthreads();  // s_wave / s_base reuse
   }
+}
+
+// The two passes that follow K1 and need nothing of each other, in one launch: blocks
+// [0, ev_blocks) compact the event chunks, the rest compute the files' group gates.
+struct GateArgs {
+  const uint32_t* ev;
+  uint64_t nchunks;
+  uint32_t* evlist;
+  uint32_t* nev;
+  uint32_t ev_blocks;
+  const uint32_t* kw;
+  uint32_t F, W, GW;
+  const unsigned long long* kwg;
+  const unsigned long long* galw;
+  unsigned long long* ggate;
+};
+__global__ void __launch_bounds__(kBlock) gates_kernel(GateArgs A) {
+  if (blockIdx.x < A.ev_blocks)
+    ev_compact_block(A.ev, A.nchunks, A.evlist, A.nev, blockIdx.x, A.ev_blocks);
+  else
+    ggate_file((blockIdx.x - A.ev_blocks) * blockDim.x + threadIdx.x, A.kw, A.F, A.W, A.kwg, A.galw, A.GW, A.ggate);
 }
 
 // Items of the K2 list: (file f, chunk c) for group g iff g is gated for f and a chunk in
@@ -2075,6 +2093,8 @@ struct DeviceRules {
 struct LaneState {
   DeviceRules* d = nullptr;
   hipStream_t st = nullptr;
+  hipStream_t st2 = nullptr;   // the dense K2 pass, beside the list pass
+  hipEvent_t fork = nullptr, join = nullptr;
   uint8_t* data_alloc = nullptr;  // kPad | batch | tail
   size_t data_cap = 0;
   uint8_t* meta = nullptr;        // the batch's file offsets (one H2D per batch)
@@ -2121,6 +2141,10 @@ struct LaneState {
     void* bufs[] = {data_alloc, meta, cf, ev_bits, xlist, xcount, evlist, kw, ggate, ovf,
                     items, entries, dentries, cand, counts, gcount, bcount, cursor, base, kind, gskip, etrace};
     for (void* b : bufs) (void)hipFree(b);
+    if (st2) (void)hipStreamSynchronize(st2);
+    if (fork) (void)hipEventDestroy(fork);
+    if (join) (void)hipEventDestroy(join);
+    if (st2) (void)hipStreamDestroy(st2);
     if (st) (void)hipStreamDestroy(st);
   }
 };
@@ -2365,6 +2389,9 @@ int lane_create(DeviceRules* d, LaneState** out) {
   auto l = std::make_unique<LaneState>();
   l->d = d;
   HIP_TRY(hipStreamCreateWithFlags(&l->st, hipStreamNonBlocking));
+  HIP_TRY(hipStreamCreateWithFlags(&l->st2, hipStreamNonBlocking));
+  HIP_TRY(hipEventCreateWithFlags(&l->fork, hipEventDisableTiming));
+  HIP_TRY(hipEventCreateWithFlags(&l->join, hipEventDisableTiming));
   const uint32_t G = std::max<uint32_t>(1, (uint32_t)d->groups.size());
   // per-batch counters: 0 candidates, 1 event chunks, 2 K2 entries, 3 dense entries, 5-7
   // layout (5 items, 6 entries, 7 groups skipped), 8-11 K2 diagnostics,
@@ -2563,10 +2590,9 @@ int enqueue_scan(DeviceRules* r, LaneState* l, const ScanInput& in, HostOut* out
   IA.items = l->items;
   const bool work = F && G && nchunks;
   if (work) {
-    ggate_kernel<<<(F + 255) / 256, 256, 0, st>>>(l->kw, F, W, r->d_kwg, r->d_galw, r->GW, l->ggate);
-    HIP_TRY(hipGetLastError());
     const uint32_t cgrid = (uint32_t)std::min<uint64_t>((nchunks + kEvPer * kBlock - 1) / (kEvPer * kBlock), (uint64_t)r->grid);
-    ev_compact_kernel<<<cgrid, kBlock, 0, st>>>(l->ev_bits, nchunks, l->evlist, l->counts + 1);
+    GateArgs GA{l->ev_bits, nchunks, l->evlist, l->counts + 1, cgrid, l->kw, F, W, r->GW, r->d_kwg, r->d_galw, l->ggate};
+    gates_kernel<<<cgrid + (F + kBlock - 1) / kBlock, kBlock, 0, st>>>(GA);
     HIP_TRY(hipGetLastError());
     const int igrid = r->grid;  // both items passes (bcount holds grid x G)
     hipLaunchKernelGGL(items_count_kernel, dim3(igrid), dim3(kBlock), G * sizeof(uint32_t) + 16, st, IA);
@@ -2613,11 +2639,17 @@ int enqueue_scan(DeviceRules* r, LaneState* l, const ScanInput& in, HostOut* out
     if (trace) HIP_TRY(hipMemsetAsync(l->etrace, 0, sizeof(unsigned long long) * entries_cap * kTraceW, st));
     A.etrace = trace ? l->etrace : nullptr;
     // one block per resident slot (the grids are persistent)
+    // the dense pass on the lane's second stream: its blocks take the CUs the list pass's
+    // last blocks leave idle, instead of starting after the whole list pass
+    HIP_TRY(hipEventRecord(l->fork, st));
+    HIP_TRY(hipStreamWaitEvent(l->st2, l->fork, 0));
     hipLaunchKernelGGL(k2_kernel, dim3(r->k2_grid), dim3(kBlock), r->max_lds, st, (const DevDFA*)r->d_groups, A);
     HIP_TRY(hipGetLastError());
-    hipLaunchKernelGGL(k2_dense_kernel, dim3(r->k2_dense_grid), dim3(kBlock), r->max_lds, st,
+    hipLaunchKernelGGL(k2_dense_kernel, dim3(r->k2_dense_grid), dim3(kBlock), r->max_lds, l->st2,
                        (const DevDFA*)r->d_groups, A);
     HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(l->join, l->st2));
+    HIP_TRY(hipStreamWaitEvent(st, l->join, 0));
   }
   HIP_TRY(hipEventRecord(out->ev[7], st));
   HIP_TRY(hipEventRecord(r->kernels_done, st));
