@@ -2093,8 +2093,6 @@ struct DeviceRules {
 struct LaneState {
   DeviceRules* d = nullptr;
   hipStream_t st = nullptr;
-  hipStream_t st2 = nullptr;   // the dense K2 pass, beside the list pass
-  hipEvent_t fork = nullptr, join = nullptr;
   uint8_t* data_alloc = nullptr;  // kPad | batch | tail
   size_t data_cap = 0;
   uint8_t* meta = nullptr;        // the batch's file offsets (one H2D per batch)
@@ -2141,10 +2139,6 @@ struct LaneState {
     void* bufs[] = {data_alloc, meta, cf, ev_bits, xlist, xcount, evlist, kw, ggate, ovf,
                     items, entries, dentries, cand, counts, gcount, bcount, cursor, base, kind, gskip, etrace};
     for (void* b : bufs) (void)hipFree(b);
-    if (st2) (void)hipStreamSynchronize(st2);
-    if (fork) (void)hipEventDestroy(fork);
-    if (join) (void)hipEventDestroy(join);
-    if (st2) (void)hipStreamDestroy(st2);
     if (st) (void)hipStreamDestroy(st);
   }
 };
@@ -2389,9 +2383,6 @@ int lane_create(DeviceRules* d, LaneState** out) {
   auto l = std::make_unique<LaneState>();
   l->d = d;
   HIP_TRY(hipStreamCreateWithFlags(&l->st, hipStreamNonBlocking));
-  HIP_TRY(hipStreamCreateWithFlags(&l->st2, hipStreamNonBlocking));
-  HIP_TRY(hipEventCreateWithFlags(&l->fork, hipEventDisableTiming));
-  HIP_TRY(hipEventCreateWithFlags(&l->join, hipEventDisableTiming));
   const uint32_t G = std::max<uint32_t>(1, (uint32_t)d->groups.size());
   // per-batch counters: 0 candidates, 1 event chunks, 2 K2 entries, 3 dense entries, 5-7
   // layout (5 items, 6 entries, 7 groups skipped), 8-11 K2 diagnostics,
@@ -2639,17 +2630,13 @@ int enqueue_scan(DeviceRules* r, LaneState* l, const ScanInput& in, HostOut* out
     if (trace) HIP_TRY(hipMemsetAsync(l->etrace, 0, sizeof(unsigned long long) * entries_cap * kTraceW, st));
     A.etrace = trace ? l->etrace : nullptr;
     // one block per resident slot (the grids are persistent)
-    // the dense pass on the lane's second stream: its blocks take the CUs the list pass's
-    // last blocks leave idle, instead of starting after the whole list pass
-    HIP_TRY(hipEventRecord(l->fork, st));
-    HIP_TRY(hipStreamWaitEvent(l->st2, l->fork, 0));
     hipLaunchKernelGGL(k2_kernel, dim3(r->k2_grid), dim3(kBlock), r->max_lds, st, (const DevDFA*)r->d_groups, A);
     HIP_TRY(hipGetLastError());
-    hipLaunchKernelGGL(k2_dense_kernel, dim3(r->k2_dense_grid), dim3(kBlock), r->max_lds, l->st2,
+    hipLaunchKernelGGL(k2_dense_kernel, dim3(r->k2_dense_grid), dim3(kBlock), r->max_lds, st,
                        (const DevDFA*)r->d_groups, A);
     HIP_TRY(hipGetLastError());
-    HIP_TRY(hipEventRecord(l->join, l->st2));
-    HIP_TRY(hipStreamWaitEvent(st, l->join, 0));
+    // (the dense pass on a second stream beside the list pass: K2 0.125 -> 0.152 ms per
+    // batch, the two grids slowed each other; profiles/r04/e)
   }
   HIP_TRY(hipEventRecord(out->ev[7], st));
   HIP_TRY(hipEventRecord(r->kernels_done, st));
