@@ -20,9 +20,9 @@ def user100():
 
 
 def test_user_rules_plan_degrades_not_fails(user100):
-    """183 rules: the K1 automaton would exceed its LDS budget; the keywords and anchors of
-    >= 4 bytes move to the hashed prefilter (K1X) instead of failing the rule-set compile
-    (the reference has no such limit), and no keyword becomes unknown."""
+    """183 rules: the K1 automaton would exceed its LDS budget; literals move to the hashed
+    prefilter (K1X) instead of failing the rule-set compile (the reference has no such
+    limit), and no keyword becomes unknown."""
     _, sc = user100
     info = sc.info()
     assert info["n_rules"] == 183 and info["kw_states"] > 0 and info["k1x_literals"] > 50
@@ -51,6 +51,25 @@ def test_k1x_reference_matches_bruteforce(user100):
             assert got == want, (f, k)
             hits += want
     assert hits > 20
+
+
+def test_k1x_split_per_step(knob):
+    """The x_step knob: 4 keeps every literal under 7 bytes in K1 (the largest automaton),
+    1 hashes down to 4 bytes; the default is the widest step whose K1 table is packed
+    (<= 64 KiB of u16 rows).  An unsupported step is an argument error."""
+    from trivy_amd import _native as N
+    doc = configs.user_rules_doc(1000, seed=4)
+    info = {}
+    for st in (None, "4", "2", "1"):
+        if st:
+            knob("x_step", st)
+        info[st] = S.NewScanner(S.config_from_dict(doc)).info()
+    assert info["4"]["kw_states"] > info["2"]["kw_states"] >= info["1"]["kw_states"]
+    assert info["4"]["k1x_literals"] < info["2"]["k1x_literals"] <= info["1"]["k1x_literals"]
+    assert info[None]["kw_states"] * info[None]["kw_classes"] * 2 <= 65536
+    assert info[None] == info["2"]
+    with pytest.raises(Exception):
+        N.knob("x_step", "3")
 
 
 @pytest.mark.parametrize("chunk", [64, 256])
