@@ -558,7 +558,8 @@ def main():
     if rank == 0 and not args.no_cpu_baseline:
         nt = args.host_threads or 16
         exact, opt, sub, exact_bytes = cpu_baselines(sc, batch0, args.cpu_mib << 20, nt)
-        line["cpu_baseline"], line["cpu_optimised"] = exact, opt
+        # (a one-GPU figure: reported at N=1; at N>1 the sample only checks the device)
+        line["cpu_baseline"], line["cpu_optimised"] = (exact, opt) if ngpus == 1 else (None, None)
         out = C.c_void_p()
         N.check(L.tsg_scan_batch(ctxs[0].handle, *sub.ptrs(), C.byref(out)))
         if _raw(out) != exact_bytes:
