@@ -58,7 +58,14 @@ struct ScanInput {
   uint64_t total;
   const char* paths;         // pinned host
   const uint64_t* poff;      // [nfiles + 1]
+  // the slot's whole pinned data buffer (data == room): enqueue_scan writes the zero tail
+  // and a copy of the offsets behind the batch there, so one H2D carries all three
+  uint8_t* room = nullptr;
+  uint64_t room_bytes = 0;
 };
+
+// pinned bytes a slot's data buffer keeps past its capacity for that tail and the offsets
+inline uint64_t slot_room_bytes(uint32_t files_cap) { return (128u << 10) + 8ull * ((uint64_t)files_cap + 1) + 64; }
 
 struct ScanTimes {  // HIP-event milliseconds of one batch on its lane
   float h2d = 0, meta = 0, wait = 0, prep = 0, k1 = 0, gates = 0, k2 = 0, out = 0;

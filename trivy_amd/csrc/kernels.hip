@@ -2459,11 +2459,18 @@ int enqueue_scan(DeviceRules* r, LaneState* l, const ScanInput& in, HostOut* out
   int rc;
   // ---- buffers (grown on demand; growing waits for the device)
   const size_t tail = (size_t)kK1Chains * kK1Seg * C + kPad;
-  if ((rc = ensure(&l->data_alloc, &l->data_cap, (size_t)total + kPad + tail))) return rc;
-  uint8_t* data = l->data_alloc + kPad;
   const size_t meta_bytes = sizeof(uint64_t) * ((size_t)F + 1);
-  if ((rc = ensure(&l->meta, &l->meta_cap, meta_bytes))) return rc;
-  l->off = (const uint64_t*)l->meta;
+  // one H2D when the slot has room behind the batch: [batch | zero tail | offsets]
+  const size_t o_off = ((size_t)total + tail + 15) & ~(size_t)15;
+  const bool one_copy = in.room == in.data && in.room_bytes >= o_off + meta_bytes;
+  if ((rc = ensure(&l->data_alloc, &l->data_cap, kPad + o_off + meta_bytes))) return rc;
+  uint8_t* data = l->data_alloc + kPad;
+  if (one_copy) {
+    l->off = (const uint64_t*)(data + o_off);
+  } else {
+    if ((rc = ensure(&l->meta, &l->meta_cap, meta_bytes))) return rc;
+    l->off = (const uint64_t*)l->meta;
+  }
   const uint64_t k1_item_chunks = (uint64_t)kK1Chains * kK1Seg;
   const uint64_t nchunks_pad = (nchunks + k1_item_chunks - 1) / k1_item_chunks * k1_item_chunks + 1;
   const uint64_t ncf = (total >> kCfShift) + 2;
@@ -2490,12 +2497,20 @@ int enqueue_scan(DeviceRules* r, LaneState* l, const ScanInput& in, HostOut* out
     HIP_TRY(hipMalloc((void**)&l->cand, sizeof(DevCand) * (size_t)out->cand_cap));
     l->cand_cap = out->cand_cap;
   }
-  // ---- H2D from the pinned slot: the batch, then its file offsets (two runtime copies; the
-  // paths stay on the host, where Global.AllowPath is settled per file, scanner.go:343-347)
+  // ---- H2D from the pinned slot: the batch, its zero tail and its file offsets in one
+  // runtime copy (the paths stay on the host, where Global.AllowPath is settled per file,
+  // scanner.go:343-347); a buffer without room behind the batch takes a second copy
   HIP_TRY(hipEventRecord(out->ev[0], st));
-  if (total) HIP_TRY(hipMemcpyAsync(data, in.data, total, hipMemcpyHostToDevice, st));
-  HIP_TRY(hipEventRecord(out->ev[1], st));
-  HIP_TRY(hipMemcpyAsync(l->meta, in.off, meta_bytes, hipMemcpyHostToDevice, st));
+  if (one_copy) {
+    std::memset(in.room + total, 0, o_off - total);
+    std::memcpy(in.room + o_off, in.off, meta_bytes);
+    HIP_TRY(hipMemcpyAsync(data, in.room, o_off + meta_bytes, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipEventRecord(out->ev[1], st));
+  } else {
+    if (total) HIP_TRY(hipMemcpyAsync(data, in.data, total, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipEventRecord(out->ev[1], st));
+    HIP_TRY(hipMemcpyAsync(l->meta, in.off, meta_bytes, hipMemcpyHostToDevice, st));
+  }
   HIP_TRY(hipEventRecord(out->ev[2], st));
   // the kernels of consecutive batches run one after the other (each has the whole chip;
   // their HIP-event times are the kernels' own), while this lane's H2D above overlapped
@@ -2517,7 +2532,7 @@ int enqueue_scan(DeviceRules* r, LaneState* l, const ScanInput& in, HostOut* out
       }
     };
     zero(l->data_alloc, kPad);
-    zero(data + total, tail);
+    if (!one_copy) zero(data + total, tail);
     zero(l->kw, sizeof(uint32_t) * (uint64_t)F * W);
     zero(l->ovf, F);
     zero(l->counts, sizeof(uint32_t) * 16);
@@ -2525,7 +2540,7 @@ int enqueue_scan(DeviceRules* r, LaneState* l, const ScanInput& in, HostOut* out
     zero(l->cursor, sizeof(uint32_t) * G);
     zero(l->gskip, G);
     zero(l->kind, G);
-    const uint64_t work = std::max<uint64_t>({PA.ncf, (uint64_t)F * W / 4, tail / 16, 1});
+    const uint64_t work = std::max<uint64_t>({PA.ncf, (uint64_t)F * W / 4, one_copy ? 1 : tail / 16, 1});
     const int pgrid = (int)std::min<uint64_t>((work + 255) / 256, (uint64_t)r->grid);
     prep_kernel<<<pgrid, 256, 0, st>>>(PA);
     HIP_TRY(hipGetLastError());

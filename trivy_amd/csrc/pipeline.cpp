@@ -171,7 +171,7 @@ int slot_reserve(tsg_ctx* c, Slot* s, uint64_t bytes, uint32_t files, uint64_t p
   s->data_cap = round_up(std::max<uint64_t>(bytes, 1), 1 << 20);
   s->files_cap = (uint32_t)std::min<uint64_t>(round_up(std::max<uint32_t>(files, 1), 4096), 0xFFFFFFF0u);
   s->paths_cap = round_up(std::max<uint64_t>(pbytes, 1), 1 << 16);
-  s->data = (uint8_t*)host_alloc(pinned, s->data_cap + 16);
+  s->data = (uint8_t*)host_alloc(pinned, s->data_cap + slot_room_bytes(s->files_cap));
   s->off = (uint64_t*)host_alloc(pinned, sizeof(uint64_t) * ((size_t)s->files_cap + 1));
   s->paths = (char*)host_alloc(pinned, s->paths_cap + 16);
   s->poff = (uint64_t*)host_alloc(pinned, sizeof(uint64_t) * ((size_t)s->files_cap + 1));
@@ -412,7 +412,8 @@ int submit_locked(tsg_ctx* c, uint32_t sid, uint32_t nfiles, bool keep_result,
   if (!c->emulate) {
     if ((rc = out_take(c, nfiles, &b->out))) return rc;
     LaneState* l = c->lanes[c->seq++ % c->lanes.size()];
-    ScanInput in{s.data, s.off, nfiles, s.off[nfiles], s.paths, s.poff};
+    ScanInput in{s.data, s.off, nfiles, s.off[nfiles], s.paths, s.poff, s.data,
+                 s.data_cap + slot_room_bytes(s.files_cap)};
     if ((rc = enqueue_scan(c->dr, l, in, &c->outs[b->out]))) {
       c->out_busy[b->out] = 0;
       return rc;
@@ -752,7 +753,8 @@ int tsg_batch_kernels(tsg_ctx* c, uint32_t slot_id, uint32_t nfiles, uint32_t* k
     int oi;
     if ((rc = out_take(c, nfiles, &oi))) return rc;
     LaneState* l = c->lanes[c->seq++ % c->lanes.size()];
-    ScanInput in{s.data, s.off, nfiles, s.off[nfiles], s.paths, s.poff};
+    ScanInput in{s.data, s.off, nfiles, s.off[nfiles], s.paths, s.poff, s.data,
+                 s.data_cap + slot_room_bytes(s.files_cap)};
     if ((rc = enqueue_scan(c->dr, l, in, &c->outs[oi]))) {
       c->out_busy[oi] = 0;
       return rc;
