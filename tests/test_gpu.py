@@ -48,9 +48,11 @@ def test_reference_cases_one_batch(in_dir):
         assert canon_secret(g) == c["want"], c["name"]
 
 
-@pytest.mark.parametrize("chunk", [16, 64, 256, 1024])
+@pytest.mark.parametrize("chunk", [16, 64, 256, 1024, 131072])
 def test_corpus_vs_emulation(builtin, chunk):
-    """Device kernels == the CPU emulation of the same algorithm, incl. candidates."""
+    """Device kernels == the CPU emulation of the same algorithm, incl. candidates.  (128 KiB
+    chunks need a zero tail longer than a slot's room behind its data: the batch and its
+    offsets then cross in two copies, enqueue_scan's other path.)"""
     batch, _ = corpus.make_corpus(4 << 20, seed=21 + chunk, plants_per_mib=50)
     ctx = S.GpuContext(builtin, 0, chunk_bytes=chunk)
     ctx.upload(batch)
