@@ -1,6 +1,7 @@
 # Build measurement variants of libtrivy_secret.so: the same sources with other compile-time
-# settings (select one with TSG_LIB_VARIANT=<name>).  Every variant computes the same results
-# unless marked (wrong results): those only time a kernel's parts.
+# settings (select one with TSG_LIB_VARIANT=<name>).  Every variant computes the same results.
+# (Round 4's K1X verify bisection used part-timing builds that computed wrong results; they
+# are not kept in the product source: profiles/r04/xv/ holds their timings.)
 #   usage: tools/build_variants.sh NAME...
 set -e
 cd "$(dirname "$0")/.."
@@ -24,10 +25,6 @@ for v in "$@"; do
     k2noinl) build $v -DK2_NOINL ;;      # K2: rare paths out of line
     x1) build $v -DK1X_WORDS=1 ;;        # K1X: words per lane per round
     x8) build $v -DK1X_WORDS=8 ;;
-    xnop) build $v -DXV_NOP ;;           # K1X verify: list reads only (wrong results)
-    xnocmp) build $v -DXV_NOCMP ;;       # K1X verify: no literal comparison (wrong results)
-    xprobe) build $v -DXV_PROBE ;;       # K1X verify: slot probes only (wrong results)
-    xent) build $v -DXV_ENTRIES ;;       # K1X verify: entries, no comparison (wrong results)
     xdiag) build $v -DK1X_DIAG ;;        # K1X: verify counters in k2_long_tails (slot probes),
                                          # k2_tail_bytes (entries examined), k2_tail_max (matches)
   esac

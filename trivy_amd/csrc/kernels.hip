@@ -646,10 +646,6 @@ __device__ void k1x_verify_at(const DevK1X& x, const K1XArgs& A, uint64_t p, uin
     if (sl.z == 0) return;  // no literal with this 4-gram
     if (sl.x == w) {
       K1X_DIAG_ADD(-6, sl.z);
-#ifdef XV_PROBE  // measurement builds: slot probes only (wrong results)
-      if (sl.y == 0xFFFFFFFFu) A.stats[1] = 0;
-      return;
-#endif
       for (uint32_t e = 0; e < sl.z; e++) {
         const uint32_t ent = x.lits[sl.y + e];
         const uint32_t i = ent & 0xFFFFFFu, j = ent >> 24;
@@ -657,10 +653,6 @@ __device__ void k1x_verify_at(const DevK1X& x, const K1XArgs& A, uint64_t p, uin
         const uint64_t s = p - j;
         const uint32_t a = x.off[i], len = x.len[i];
         if (s + len > A.total) continue;
-#ifdef XV_ENTRIES  // measurement builds: entries without the comparison (wrong results)
-        if (len == 0xFFFFu) A.stats[1] = 0;
-        continue;
-#endif
         // compare 32 bytes per round from aligned dword loads issued together (a byte loop
         // of dependent loads cost 0.19 ms per GiB on configs[3]); the batch has a zero tail
         const uint32_t* lw = (const uint32_t*)(x.bytes + a);  // 4-aligned, zero padded
@@ -681,9 +673,6 @@ __device__ void k1x_verify_at(const DevK1X& x, const K1XArgs& A, uint64_t p, uin
             }
           }
         }
-#ifdef XV_NOCMP  // measurement builds: no literal comparison (wrong results)
-        eq = true;
-#endif
         if (!eq) continue;
         K1X_DIAG_ADD(-5, 1u);
         const uint64_t q = s + len - 1;
@@ -837,11 +826,7 @@ __global__ void __launch_bounds__(kXVerifyBlock) k1x_verify_kernel(DevK1X x, K1X
       const uint64_t p = p0 + __builtin_ctz(t);
       const uint32_t w = x_low_byte(A.data[p]) | x_low_byte(A.data[p + 1]) << 8 | x_low_byte(A.data[p + 2]) << 16 |
                          x_low_byte(A.data[p + 3]) << 24;
-#ifdef XV_NOP  // measurement builds: the verify kernel's fixed cost
-      if (w == 0x01020304u) A.stats[1] = 0;
-#else
       k1x_verify_at(y, A, p, w);
-#endif
     }
   }
 }
