@@ -2372,12 +2372,21 @@ int device_rules_create(int device, const Plan& p, uint32_t chunk, uint32_t ext_
   {  // the LDS split: worth a second launch when one more block per CU fits and at least
      // half of the groups' tables stage in that smaller LDS size
     const int occ_max = r->k2_grid / std::max(r->cus, 1);
-    const uint32_t lds_cu = (uint32_t)prop.maxSharedMemoryPerMultiProcessor;
-    uint32_t small = lds_cu / (uint32_t)(occ_max + 1);
-    small = small > 1024 ? (small - 1024) & ~255u : 0;  // room for the kernel's static LDS
+    // the largest LDS size (256-B steps) at which one more block per CU is resident
+    uint32_t lo = 0, hi = r->max_lds / 256;  // in 256-B units: lo fits, hi does not
     int occ_small = 0;
-    if (small >= 16 && small < r->max_lds)
-      HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ_small, (const void*)k2_kernel, kBlock, small));
+    auto blocks = [&](uint32_t units, int* b) {
+      return hipOccupancyMaxActiveBlocksPerMultiprocessor(b, (const void*)k2_kernel, kBlock, units * 256);
+    };
+    while (hi - lo > 1) {
+      const uint32_t mid = (lo + hi) / 2;
+      int b = 0;
+      HIP_TRY(blocks(mid, &b));
+      if (b > occ_max) lo = mid;
+      else hi = mid;
+    }
+    const uint32_t small = lo * 256;
+    if (small) HIP_TRY(blocks(lo, &occ_small));
     std::vector<uint8_t> gbig(std::max<uint32_t>(G, 1), 0);
     uint32_t nsmall = 0;
     for (uint32_t g = 0; g < G; g++) {
