@@ -1071,9 +1071,6 @@ struct LayoutArgs {
   uint64_t* base;     // [G] first item of a list group
   uint4* entries;     // K2 work list of list groups: {group, first item, n, kGroupList}
   uint32_t* nentries;
-  const uint8_t* gbig;   // [G] or null: 1 = the group's tables need the large-LDS K2 launch
-  uint4* entries_big;    // ... of those groups
-  uint32_t* nentries_big;
   uint4* dentries;    // ... of dense groups: {group, first chunk, n, kGroupDense}
   uint32_t* ndentries;
   uint8_t* gskip;     // [G] (to the host)
@@ -1107,11 +1104,11 @@ constexpr uint32_t kEntryChunks = kStreams * kBlock;
 
 __global__ void __launch_bounds__(kLayoutBlock) layout_kernel(LayoutArgs A) {
   __shared__ unsigned long long s_wave64[kLayoutBlock / 64];
-  __shared__ unsigned long long s_carry[6];  // items, entries, dense groups, skipped groups, dense entries, big entries
+  __shared__ unsigned long long s_carry[5];  // items, entries, dense groups, skipped groups, dense entries
   __shared__ uint2 s_dense[kLayoutBlock];  // dense groups of the tile: group, first dense entry
   __shared__ uint32_t s_ndense;
   const uint32_t ndent_all = (uint32_t)((A.nchunks + kEntryChunks - 1) / kEntryChunks);
-  if (threadIdx.x < 6) s_carry[threadIdx.x] = 0;
+  if (threadIdx.x < 5) s_carry[threadIdx.x] = 0;
   __syncthreads();
   for (uint32_t g0 = 0; g0 < A.G; g0 += blockDim.x) {
     if (threadIdx.x == 0) s_ndense = 0;
@@ -1130,18 +1127,15 @@ __global__ void __launch_bounds__(kLayoutBlock) layout_kernel(LayoutArgs A) {
     // range stays unused: the regions keep group order)
     const uint64_t nent = list ? (cnt + kEntryItems - 1) / kEntryItems : 0;
     const uint64_t ndent = dense ? (A.nchunks + kEntryChunks - 1) / kEntryChunks : 0;
-    unsigned long long epre, dpre2, bpre;
-    const bool big = A.gbig && g < A.G && A.gbig[g];
-    const unsigned long long etot = block_exclusive_scan<unsigned long long>(big ? 0 : nent, &epre, s_wave64);
-    const unsigned long long btot = block_exclusive_scan<unsigned long long>(big ? nent : 0, &bpre, s_wave64);
+    unsigned long long epre, dpre2;
+    const unsigned long long etot = block_exclusive_scan<unsigned long long>(nent, &epre, s_wave64);
     const unsigned long long dtot2 = block_exclusive_scan<unsigned long long>(ndent, &dpre2, s_wave64);
     const bool skip = cnt && !list && !dense;
     unsigned long long spre;
     const unsigned long long stot = block_exclusive_scan<unsigned long long>(skip ? 1 : 0, &spre, s_wave64);
     // (entries_cap covers every list entry the item capacity allows plus max_dense dense
     // groups, so the work list always fits)
-    const uint64_t e0 = big ? s_carry[5] + bpre : s_carry[1] + epre, d0 = s_carry[4] + dpre2;
-    uint4* const ents = big ? A.entries_big : A.entries;
+    const uint64_t e0 = s_carry[1] + epre, d0 = s_carry[4] + dpre2;
     const uint8_t k = !cnt ? kGroupNone : list ? kGroupList : dense ? kGroupDense : kGroupSkip;
     if (g < A.G) {
       A.kind[g] = k;
@@ -1151,8 +1145,8 @@ __global__ void __launch_bounds__(kLayoutBlock) layout_kernel(LayoutArgs A) {
     if (k == kGroupList)
       for (uint64_t i = 0; i < nent; i++) {
         const uint32_t first = (uint32_t)(i * kEntryItems);
-        ents[e0 + i] = make_uint4(g, (uint32_t)(s_carry[0] + ipre) + first,
-                                  (uint32_t)min<uint64_t>(kEntryItems, cnt - first), kGroupList);
+        A.entries[e0 + i] = make_uint4(g, (uint32_t)(s_carry[0] + ipre) + first,
+                                       (uint32_t)min<uint64_t>(kEntryItems, cnt - first), kGroupList);
       }
     if (k == kGroupDense) s_dense[atomicAdd(&s_ndense, 1u)] = make_uint2(g, (uint32_t)d0);
     __syncthreads();
@@ -1173,16 +1167,14 @@ __global__ void __launch_bounds__(kLayoutBlock) layout_kernel(LayoutArgs A) {
       s_carry[2] += dtot;
       s_carry[3] += stot;
       s_carry[4] += dtot2;
-      s_carry[5] += btot;
     }
     __syncthreads();
   }
   if (threadIdx.x == 0) {
     *A.nentries = (uint32_t)s_carry[1];
-    if (A.nentries_big) *A.nentries_big = (uint32_t)s_carry[5];
     *A.ndentries = (uint32_t)s_carry[4];
     A.stats[1] = (uint32_t)min<unsigned long long>(s_carry[0], 0xFFFFFFFFull);
-    A.stats[2] = (uint32_t)(s_carry[1] + s_carry[5]);
+    A.stats[2] = (uint32_t)s_carry[1];
     A.stats[3] = (uint32_t)s_carry[3];
   }
 }
@@ -2050,11 +2042,6 @@ struct DeviceRules {
   int grid = 0;          // 8 blocks per CU
   int cus = 0;
   int k2_grid = 0, k2_dense_grid = 0;  // resident blocks of the persistent K2 kernels
-  // K2 list pass split by LDS: groups whose staged tables fit small_lds run in a launch
-  // with more resident blocks (k2_grid_small), the others (gbig) at max_lds; 0: one launch
-  uint32_t small_lds = 0;
-  int k2_grid_small = 0;
-  const uint8_t* d_gbig = nullptr;
   hipEvent_t kernels_done = nullptr;   // end of the kernels of the last enqueued batch
   bool kernels_done_valid = false;
   std::vector<void*> tables;
@@ -2116,8 +2103,6 @@ struct LaneState {
   size_t items_cap = 0;
   uint4* entries = nullptr;
   size_t entries_cap = 0;
-  uint4* entries_big = nullptr;  // the large-LDS groups' list entries (DeviceRules::small_lds)
-  size_t entries_big_cap = 0;
   uint4* dentries = nullptr;
   size_t dentries_cap = 0;
   DevCand* cand = nullptr;
@@ -2137,7 +2122,7 @@ struct LaneState {
     (void)hipSetDevice(d->device);
     if (st) (void)hipStreamSynchronize(st);
     void* bufs[] = {data_alloc, meta, cf, ev_bits, xlist, xcount, evlist, kw, ggate, ovf,
-                    items, entries, entries_big, dentries, cand, counts, gcount, bcount, cursor, base, kind, gskip, etrace};
+                    items, entries, dentries, cand, counts, gcount, bcount, cursor, base, kind, gskip, etrace};
     for (void* b : bufs) (void)hipFree(b);
     if (st) (void)hipStreamDestroy(st);
   }
@@ -2369,38 +2354,6 @@ int device_rules_create(int device, const Plan& p, uint32_t chunk, uint32_t ext_
   r->k2_grid = r->cus * std::max(occ, 1);
   HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void*)k2_dense_kernel, kBlock, r->max_lds));
   r->k2_dense_grid = r->cus * std::max(occ, 1);
-  {  // the LDS split: worth a second launch when one more block per CU fits and at least
-     // half of the groups' tables stage in that smaller LDS size
-    const int occ_max = r->k2_grid / std::max(r->cus, 1);
-    // the largest LDS size (256-B steps) at which one more block per CU is resident
-    uint32_t lo = 0, hi = r->max_lds / 256;  // in 256-B units: lo fits, hi does not
-    int occ_small = 0;
-    auto blocks = [&](uint32_t units, int* b) {
-      return hipOccupancyMaxActiveBlocksPerMultiprocessor(b, (const void*)k2_kernel, kBlock, units * 256);
-    };
-    while (hi - lo > 1) {
-      const uint32_t mid = (lo + hi) / 2;
-      int b = 0;
-      HIP_TRY(blocks(mid, &b));
-      if (b > occ_max) lo = mid;
-      else hi = mid;
-    }
-    const uint32_t small = lo * 256;
-    if (small) HIP_TRY(blocks(lo, &occ_small));
-    std::vector<uint8_t> gbig(std::max<uint32_t>(G, 1), 0);
-    uint32_t nsmall = 0;
-    for (uint32_t g = 0; g < G; g++) {
-      gbig[g] = r->groups[g].lds_bytes > small ? 1 : 0;
-      nsmall += gbig[g] ? 0 : 1;
-    }
-    if (occ_small > occ_max && 2 * nsmall >= G) {
-      r->small_lds = small;
-      r->k2_grid_small = r->cus * occ_small;
-      const uint8_t* cgb = nullptr;
-      if ((rc = upload_vec(gbig, &cgb, &r->tables))) return rc;
-      r->d_gbig = cgb;
-    }
-  }
   *out = r.release();
   return TSG_OK;
 }
@@ -2418,9 +2371,8 @@ int lane_create(DeviceRules* d, LaneState** out) {
   const uint32_t G = std::max<uint32_t>(1, (uint32_t)d->groups.size());
   // per-batch counters: 0 candidates, 1 event chunks, 2 K2 entries, 3 dense entries, 5-7
   // layout (5 items, 6 entries, 7 groups skipped), 8-11 K2 diagnostics,
-  // 12-13 K2 claim cursors (list, dense), 14-15 K1X (records listed, inline verified); on the
-  // device only: 16 the large-LDS list's claim cursor, 17 its entries
-  HIP_TRY(hipMalloc((void**)&l->counts, sizeof(uint32_t) * 32));
+  // 12-13 K2 claim cursors (list, dense), 14-15 K1X (records listed, inline verified)
+  HIP_TRY(hipMalloc((void**)&l->counts, sizeof(uint32_t) * 16));
   HIP_TRY(hipMalloc((void**)&l->gcount, sizeof(uint32_t) * G));
   HIP_TRY(hipMalloc((void**)&l->bcount, sizeof(uint32_t) * G * (size_t)d->grid));
   HIP_TRY(hipMalloc((void**)&l->cursor, sizeof(uint32_t) * G));
@@ -2524,7 +2476,6 @@ int enqueue_scan(DeviceRules* r, LaneState* l, const ScanInput& in, HostOut* out
   const uint64_t dentries_cap = (uint64_t)max_dense * ((nchunks + kEntryChunks - 1) / kEntryChunks + 1);
   if ((rc = ensure(&l->items, &l->items_cap, (size_t)items_cap))) return rc;
   if ((rc = ensure(&l->entries, &l->entries_cap, (size_t)entries_cap))) return rc;
-  if (r->small_lds && (rc = ensure(&l->entries_big, &l->entries_big_cap, (size_t)entries_cap))) return rc;
   if ((rc = ensure(&l->dentries, &l->dentries_cap, (size_t)dentries_cap))) return rc;
   if (!l->cand || l->cand_cap < out->cand_cap) {
     if (l->cand) HIP_TRY(hipFree(l->cand));
@@ -2569,7 +2520,7 @@ int enqueue_scan(DeviceRules* r, LaneState* l, const ScanInput& in, HostOut* out
     if (!one_copy) zero(data + total, tail);
     zero(l->kw, sizeof(uint32_t) * (uint64_t)F * W);
     zero(l->ovf, F);
-    zero(l->counts, sizeof(uint32_t) * 32);
+    zero(l->counts, sizeof(uint32_t) * 16);
     zero(l->gcount, sizeof(uint32_t) * G);
     zero(l->cursor, sizeof(uint32_t) * G);
     zero(l->gskip, G);
@@ -2638,8 +2589,7 @@ int enqueue_scan(DeviceRules* r, LaneState* l, const ScanInput& in, HostOut* out
     hipLaunchKernelGGL(items_count_kernel, dim3(igrid), dim3(kBlock), G * sizeof(uint32_t) + 16, st, IA);
     HIP_TRY(hipGetLastError());
     LayoutArgs LA{l->gcount, G, nchunks, items_cap, max_dense, l->kind, l->base, l->entries, l->counts + 2,
-                  r->small_lds ? r->d_gbig : nullptr, r->small_lds ? l->entries_big : nullptr,
-                  r->small_lds ? l->counts + 17 : nullptr, l->dentries, l->counts + 3, l->gskip, l->counts + 4};
+                  l->dentries, l->counts + 3, l->gskip, l->counts + 4};
     hipLaunchKernelGGL(layout_kernel, dim3(1), dim3(kLayoutBlock), 0, st, LA);
     HIP_TRY(hipGetLastError());
     hipLaunchKernelGGL(items_emit_kernel, dim3(igrid), dim3(kBlock), 2 * G * sizeof(uint32_t) + 16, st, IA);
@@ -2679,21 +2629,8 @@ int enqueue_scan(DeviceRules* r, LaneState* l, const ScanInput& in, HostOut* out
     if (trace && (rc = ensure(&l->etrace, &l->etrace_cap, (size_t)entries_cap * kTraceW))) return rc;
     if (trace) HIP_TRY(hipMemsetAsync(l->etrace, 0, sizeof(unsigned long long) * entries_cap * kTraceW, st));
     A.etrace = trace ? l->etrace : nullptr;
-    // one block per resident slot (the grids are persistent); with the LDS split, the groups
-    // whose tables fit small_lds first at more blocks per CU, then the others
-    if (r->small_lds) {
-      hipLaunchKernelGGL(k2_kernel, dim3(r->k2_grid_small), dim3(kBlock), r->small_lds, st,
-                         (const DevDFA*)r->d_groups, A);
-      HIP_TRY(hipGetLastError());
-      K2Args B = A;
-      B.entries = l->entries_big;
-      B.nentries = l->counts + 17;
-      B.claim = l->counts + 16;
-      B.etrace = nullptr;
-      hipLaunchKernelGGL(k2_kernel, dim3(r->k2_grid), dim3(kBlock), r->max_lds, st, (const DevDFA*)r->d_groups, B);
-    } else {
-      hipLaunchKernelGGL(k2_kernel, dim3(r->k2_grid), dim3(kBlock), r->max_lds, st, (const DevDFA*)r->d_groups, A);
-    }
+    // one block per resident slot (the grids are persistent)
+    hipLaunchKernelGGL(k2_kernel, dim3(r->k2_grid), dim3(kBlock), r->max_lds, st, (const DevDFA*)r->d_groups, A);
     HIP_TRY(hipGetLastError());
     hipLaunchKernelGGL(k2_dense_kernel, dim3(r->k2_dense_grid), dim3(kBlock), r->max_lds, st,
                        (const DevDFA*)r->d_groups, A);
