@@ -23,6 +23,7 @@ for v in "$@"; do
     ns4) build $v -DK1_CHAINS=4 ;;
     k2ctr) build $v -DK2_TRACE_CTR ;;    # K2: per-entry counters (TSG_K2_TRACE)
     k2noinl) build $v -DK2_NOINL ;;      # K2: rare paths out of line
+    k2w4) build $v -DK2_W=4 ;;           # K2: at least 4 waves per SIMD (<= 128 VGPRs, 38 spilled)
     x1) build $v -DK1X_WORDS=1 ;;        # K1X: words per lane per round
     x8) build $v -DK1X_WORDS=8 ;;
     xdiag) build $v -DK1X_DIAG ;;        # K1X: verify counters in k2_long_tails (slot probes),
