@@ -122,3 +122,23 @@ def test_allow_exclude_binary_gpu_vs_exact():
     want = sc.ScanBatch(b, nthreads=16)
     assert sc.ScanBatch(b, device=0) == want
     assert sum(len(x["Findings"] or []) for x in want) > 5
+
+
+def test_hostonly_rule_gpu_vs_exact():
+    """A rule no DFA fits (3,000 12-letter words in one alternation: no counted repetition
+    to relax, one top-level atom) is resolved on the host over every file, so the outputs
+    kernel hands back every file's keyword row (its sparse form covers only files with
+    candidates or flags).  Device == exact CPU path, with the word planted in some files."""
+    import numpy as np
+    rng = np.random.default_rng(7)
+    words = ["".join(rng.choice(list("abcdefghijklmnopqrstuvwxyz"), size=12)) for _ in range(3000)]
+    doc = {"rules": [{"id": "many-words", "category": "custom", "title": "many words", "severity": "LOW",
+                      "regex": "(?P<secret>(?:" + "|".join(words) + "))"}]}
+    sc = S.NewScanner(S.config_from_dict(doc))
+    assert sc.info()["n_hostonly"] == 1
+    args = configs.mixed_batch(doc, 1 << 20, seed=66, plants_per_file=0.3)
+    args += [S.ScanArgs("w/%d.txt" % i, ("x = %s\n" % words[i * 7]).encode()) for i in range(40)]
+    b = S.Batch.from_args(args)
+    want = sc.ScanBatch(b, nthreads=16)
+    assert sc.ScanBatch(b, device=0) == want
+    assert sum(1 for x in want if any(f["RuleID"] == "many-words" for f in x["Findings"] or [])) >= 40
