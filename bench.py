@@ -379,6 +379,9 @@ def main():
         if vis < max(devices) + 1:
             raise SystemExit("bench: --gpus %d needs device %d, but this process sees %d GPU(s); "
                              "refusing to run on fewer" % (args.gpus, max(devices), vis))
+        if world > 1:  # the barrier's torch.cuda.synchronize() on this rank's GPU, not GPU 0
+            import torch
+            torch.cuda.set_device(local)
     from trivy_amd import corpus
     from trivy_amd import secret as S
     from trivy_amd import _native as N
