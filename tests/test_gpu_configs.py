@@ -142,3 +142,22 @@ def test_hostonly_rule_gpu_vs_exact():
     want = sc.ScanBatch(b, nthreads=16)
     assert sc.ScanBatch(b, device=0) == want
     assert sum(1 for x in want if any(f["RuleID"] == "many-words" for f in x["Findings"] or [])) >= 40
+
+
+def test_k1x_list_overflow_inline_verify():
+    """Every 16-byte word of a 2 MiB batch holds a K1X literal (a periodic one, repeated):
+    the blocks' list slices overflow and the rest of the hits are verified inline in
+    k1x_kernel.  Keyword bits and events == k1_reference; the inline path ran."""
+    doc = configs.user_rules_doc(1000, seed=4)
+    doc["rules"].append({"id": "periodic", "category": "user", "title": "periodic", "severity": "LOW",
+                         "regex": r"qzqzqzqzqz(?P<secret>[0-9]{4})", "keywords": ["qzqzqzqzqz"]})
+    sc = S.NewScanner(S.config_from_dict(doc))
+    files = [S.ScanArgs("p/%d.txt" % i, b"qz" * (16 << 10) + b"0123\n") for i in range(64)]
+    b = S.Batch.from_args(files)
+    _k1_vs_reference(sc, b, chunks=(256,))
+    ctx = S.GpuContext(sc, 0, chunk_bytes=256, adapt_mib=0xFFFFFFFF)
+    ctx.upload(b)
+    ctx.kernels()
+    st = ctx.stats()
+    ctx.close()
+    assert st["k1x_inline"] > 0 and st["k1x_records"] > 0
