@@ -344,6 +344,10 @@ def main():
                          "blobs (configs[4])")
     ap.add_argument("--emulate", action="store_true",
                     help="tests only: emulated contexts (the kernels' algorithm on the CPU), no GPU")
+    ap.add_argument("--rehearse-shared-gpu", action="store_true",
+                    help="rehearsal only (not a measurement): under torchrun, rank r drives GPU "
+                         "r %% visible, so the multi-rank path runs on a box with fewer GPUs; "
+                         "the line is marked \"rehearsal\"")
     ap.add_argument("--e2e", choices=["fs", "layer"], default=None,
                     help="end-to-end ingest + scan instead of the configs[1] line: 'fs' = a "
                          "seeded source tree on disk (configs[0] shape, --e2e-mib), 'layer' = a "
@@ -376,6 +380,9 @@ def main():
     ngpus = world if world > 1 else args.gpus
     if not args.emulate:
         vis = _visible_gpus()
+        if args.rehearse_shared_gpu and world > 1 and vis > 0:
+            local = local % vis
+            devices = [local]
         if vis < max(devices) + 1:
             raise SystemExit("bench: --gpus %d needs device %d, but this process sees %d GPU(s); "
                              "refusing to run on fewer" % (args.gpus, max(devices), vis))
@@ -549,6 +556,8 @@ def main():
                      "gen_s": round(gen_s, 2), "pack_into_pinned_s": round(pack_s, 2),
                      "rule_compile_s": round(compile_s, 2)},
     }
+    if args.rehearse_shared_gpu:
+        line["rehearsal"] = "ranks share GPUs (--rehearse-shared-gpu): not a measurement"
     log("timed %d steps: %.3f s" % (args.steps, dt))
     # every step of every device must have produced the same findings as its warmup steps
     # (the timed loop reads every result)
