@@ -524,6 +524,7 @@ void find_location(int64_t start, int64_t end, const Censored& c, int64_t start_
   for (int64_t i = start_line; i > code_start; i--) ls = c.prev_nl(ls - 1) + 1;
   bool found_first = false;
   f->lines.clear();
+  f->lines.reserve((size_t)(end_line + 2 - code_start));
   for (int64_t i = code_start; i < end_line + 2; i++) {
     const int64_t le = c.next_nl(ls);
     bool cause = i >= start_line && i <= end_line;
