@@ -246,6 +246,9 @@ typedef struct tsg_stats {
   /* K1X (large rule sets) in the last batch: 16-B words listed with a prefilter hit, and
    * words verified inline because their block's list slice was full */
   uint32_t k1x_records, k1x_inline;
+  /* K1F (the filter-and-verify K1) in the last batch: 16-B words listed with a filter hit,
+   * and literal occurrences its verification confirmed */
+  uint32_t k1f_listed, k1f_arrivals;
 } tsg_stats;
 int tsg_ctx_get_stats(const tsg_ctx* ctx, tsg_stats* out);
 
@@ -303,6 +306,8 @@ const char* tsg_last_error(void);
  *                     kernel does (tsg_scan_batch_emulated, TSG_CTX_EMULATE contexts)
  *   "emu_kw_unknown"  comma-separated keywords the emulated K1 leaves to the host, as
  *                     after its adaptation (tsg_scan_batch_emulated)
+ *   "k1_automaton"    "1": contexts created next run K1 as the LDS automaton instead of the
+ *                     filter-and-verify K1F (k1f.hpp)
  * Returns TSG_ERR_ARG for an unknown name. */
 int tsg_test_knob(const char* name, const char* value);
 
@@ -338,6 +343,15 @@ int tsg_emulate_k1(const tsg_ruleset* rs, const uint8_t* data, const uint64_t* o
                    uint32_t nfiles, uint32_t chunk, uint32_t* kw, size_t kw_len, uint32_t* ev,
                    size_t ev_len);
 
+/* K1F (the filter-and-verify K1, k1f.hpp) emulated on the CPU with the device's tables and
+ * bit logic: keyword bits and chunk events in tsg_emulate_k1's layout; the literals listed
+ * in quiet_ids are left out of the filter (the adaptation's hot literals).  stats (or NULL):
+ * {flagged word groups, verified literal occurrences, records in the filter, 0}.
+ * TSG_ERR_CONFIG when K1F does not apply to the rule set (the automaton K1 runs then). */
+int tsg_emulate_k1f(const tsg_ruleset* rs, const uint8_t* data, const uint64_t* offsets,
+                    uint32_t nfiles, uint32_t chunk, const uint32_t* quiet_ids, uint32_t nquiet,
+                    uint32_t* kw, size_t kw_len, uint32_t* ev, size_t ev_len, uint64_t* stats);
+
 /* Plan introspection: per rule group id (-1 host-only), relaxation (-1 exact), max len. */
 int tsg_ruleset_rule_plan(const tsg_ruleset* rs, uint32_t rule, int32_t* group, int32_t* relax,
                           int64_t* max_len);
@@ -347,6 +361,12 @@ int tsg_ruleset_rule_plan(const tsg_ruleset* rs, uint32_t rule, int32_t* group, 
  * and a description of the anchor. */
 int tsg_ruleset_rule_anchor(const tsg_ruleset* rs, uint32_t rule, uint32_t* event, int64_t* evdist,
                             char* desc, size_t desc_len);
+
+/* Plan introspection: K1 literal i (0 <= i < n; ids below tsg_ruleset_info.n_keywords are
+ * keywords, the rest anchor literals): its bytes (min(len, cap) copied), length and event
+ * bits.  TSG_ERR_ARG once i >= n. */
+int tsg_ruleset_k1_literal(const tsg_ruleset* rs, uint32_t i, uint8_t* buf, uint32_t cap,
+                           uint32_t* len, uint32_t* event);
 
 /* Emulate K1+K2 on the CPU with the GPU algorithm and resolve (tests). */
 int tsg_scan_batch_emulated(const tsg_ruleset* rs, const uint8_t* data, const uint64_t* offsets,

@@ -79,11 +79,15 @@ def _small_files_batch(seed):
     return S.Batch.from_args(args)
 
 
+@pytest.mark.parametrize("k1", ["k1f", "automaton"])
 @pytest.mark.parametrize("chunk", [16, 48, 256, 1024])
-def test_k1_matches_reference(builtin, chunk):
-    """K1 keyword bits and chunk events are exactly the reference semantics."""
+def test_k1_matches_reference(builtin, chunk, k1, knob):
+    """K1 keyword bits and chunk events are exactly the reference semantics (K1F, the
+    default, and the automaton K1 it replaces)."""
     import numpy as np
     batch = _small_files_batch(chunk)
+    if k1 == "automaton":
+        knob("k1_automaton", 1)
     ctx = S.GpuContext(builtin, 0, chunk_bytes=chunk, adapt_mib=0xFFFFFFFF)
     ctx.upload(batch)
     ctx.kernels()
@@ -93,6 +97,41 @@ def test_k1_matches_reference(builtin, chunk):
     assert np.array_equal(kw, rkw)
     assert np.array_equal(ev, rev)
     assert (ev & 1).any() and (ev >> 2).any()
+
+
+@pytest.mark.parametrize("chunk", [16, 48, 256, 131072])
+def test_k1f_edges_match_reference(builtin, chunk):
+    """K1F on the K1 edge batch (literals at file and batch edges and split across files,
+    runs at every offset, case, CR, high bytes, tiny files): == k1_reference."""
+    import numpy as np
+    batch = corpus.k1_edge_batch(builtin.k1_literals(), 7 + chunk % 5)
+    ctx = S.GpuContext(builtin, 0, chunk_bytes=chunk, adapt_mib=0xFFFFFFFF)
+    ctx.upload(batch)
+    ctx.kernels()
+    kw, ev = ctx.k1_output(chunk)
+    ctx.close()
+    rkw, rev = builtin.k1_reference(batch, chunk)
+    assert np.array_equal(kw, rkw)
+    assert np.array_equal(ev, rev)
+
+
+@pytest.mark.parametrize("size", [1, 15, 16, 17, 1023, 1024, 1025, 64 * 1024 + 3, 3 << 20])
+def test_k1f_batch_sizes(builtin, size):
+    """K1F's tiles, wave ranges and look-behind carries at batch sizes around a tile and at
+    many tiles per wave: == k1_reference (one file, then the same bytes as many files)."""
+    import numpy as np
+    big, _ = corpus.make_corpus(max(size, 4096) + 4096, seed=size % 1000, plants_per_mib=500)
+    data = bytes(big.data[:size])
+    for batch in (S.Batch.from_args([S.ScanArgs("a.txt", data)]),
+                  S.Batch.from_args([S.ScanArgs("p/%d" % i, data[i * 777:(i + 1) * 777])
+                                     for i in range((size + 776) // 777)])):
+        ctx = S.GpuContext(builtin, 0, chunk_bytes=256, adapt_mib=0xFFFFFFFF)
+        ctx.upload(batch)
+        ctx.kernels()
+        kw, ev = ctx.k1_output(256)
+        ctx.close()
+        rkw, rev = builtin.k1_reference(batch, 256)
+        assert np.array_equal(kw, rkw) and np.array_equal(ev, rev)
 
 
 def test_k1_adaptation_exact(builtin):

@@ -82,7 +82,8 @@ class Stats(C.Structure):
                 ("k2_long_tails", C.c_uint32), ("k2_replays", C.c_uint32),
                 ("prep_ms", C.c_double), ("meta_ms", C.c_double),
                 ("sum_prep_ms", C.c_double), ("sum_meta_ms", C.c_double),
-                ("k1x_records", C.c_uint32), ("k1x_inline", C.c_uint32)]
+                ("k1x_records", C.c_uint32), ("k1x_inline", C.c_uint32),
+                ("k1f_listed", C.c_uint32), ("k1f_arrivals", C.c_uint32)]
 
 
 # (name, restype, argtypes) -- every symbol include/trivy_secret.h declares
@@ -185,6 +186,11 @@ SIGNATURES = [
     ("tsg_go_sort_perm", C.c_int, [_P, _U64P, _I64P, C.c_uint32, C.POINTER(C.c_uint32)]),
     ("tsg_ruleset_rule_anchor", C.c_int, [_P, C.c_uint32, C.POINTER(C.c_uint32),
                                           C.POINTER(C.c_int64), C.c_char_p, C.c_size_t]),
+    ("tsg_emulate_k1f", C.c_int, [_P, _P, _U64P, C.c_uint32, C.c_uint32, C.POINTER(C.c_uint32),
+                                  C.c_uint32, C.POINTER(C.c_uint32), C.c_size_t,
+                                  C.POINTER(C.c_uint32), C.c_size_t, C.POINTER(C.c_uint64)]),
+    ("tsg_ruleset_k1_literal", C.c_int, [_P, C.c_uint32, C.c_char_p, C.c_uint32,
+                                         C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]),
 ]
 
 _lib = None

@@ -7,6 +7,7 @@
 #include <thread>
 
 #include "internal.hpp"
+#include "k1f.hpp"
 
 namespace tsg {
 
@@ -290,6 +291,41 @@ int tsg_emulate_k1(const tsg_ruleset* rs, const uint8_t* data, const uint64_t* o
   }
 }
 
+int tsg_emulate_k1f(const tsg_ruleset* rs, const uint8_t* data, const uint64_t* offsets,
+                    uint32_t nfiles, uint32_t chunk, const uint32_t* quiet_ids, uint32_t nquiet,
+                    uint32_t* kw, size_t kw_len, uint32_t* ev, size_t ev_len, uint64_t* stats) {
+  if (!rs || !offsets || chunk == 0 || (nquiet && !quiet_ids)) return fail(TSG_ERR_ARG, "bad argument");
+  try {
+    const Plan& p = *rs->plan;
+    std::vector<uint8_t> quiet(p.n_lit, 0);
+    for (uint32_t i = 0; i < nquiet; i++) {
+      if (quiet_ids[i] >= (uint32_t)p.n_lit) return fail(TSG_ERR_ARG, "no such K1 literal");
+      quiet[quiet_ids[i]] = 1;
+    }
+    K1FTables t;
+    std::string why;
+    if (!k1f_build(p, quiet, &t, &why)) return fail(TSG_ERR_CONFIG, "K1F does not apply: " + why);
+    std::vector<uint64_t> poff(nfiles + 1, 0);
+    BatchView b{data, offsets, nfiles, "", poff.data()};
+    std::vector<uint32_t> k, e;
+    uint64_t st[2];
+    k1f_emulate(p, t, b, chunk, &k, &e, st);
+    if (kw) std::memcpy(kw, k.data(), sizeof(uint32_t) * std::min(kw_len, k.size()));
+    if (ev) std::memcpy(ev, e.data(), sizeof(uint32_t) * std::min(ev_len, e.size()));
+    if (stats) {
+      stats[0] = st[0];
+      stats[1] = st[1];
+      stats[2] = t.nlit;
+      stats[3] = 0;
+    }
+    return TSG_OK;
+  } catch (const std::bad_alloc&) {
+    return fail(TSG_ERR_NOMEM, "out of memory");
+  } catch (const std::exception& ex) {
+    return fail(TSG_ERR_INTERNAL, ex.what());
+  }
+}
+
 int tsg_ruleset_rule_plan(const tsg_ruleset* rs, uint32_t rule, int32_t* group, int32_t* relax,
                           int64_t* max_len) {
   if (!rs || rule >= rs->rs.rules.size()) return fail(TSG_ERR_ARG, "bad argument");
@@ -307,6 +343,18 @@ int tsg_ruleset_rule_anchor(const tsg_ruleset* rs, uint32_t rule, uint32_t* even
   if (event) *event = p.rule_event[rule];
   if (evdist) *evdist = p.rule_evdist[rule];
   copy_err(p.rule_anchor[rule], desc, desc_len);
+  return TSG_OK;
+}
+
+int tsg_ruleset_k1_literal(const tsg_ruleset* rs, uint32_t i, uint8_t* buf, uint32_t cap,
+                           uint32_t* len, uint32_t* event) {
+  if (!rs || (!buf && cap)) return fail(TSG_ERR_ARG, "bad argument");
+  const Plan& p = *rs->plan;
+  if (i >= p.k1_lits.size()) return fail(TSG_ERR_ARG, "no such K1 literal");
+  const std::string& s = p.k1_lits[i];
+  if (buf) std::memcpy(buf, s.data(), std::min<size_t>(cap, s.size()));
+  if (len) *len = (uint32_t)s.size();
+  if (event) *event = p.lit_event[i];
   return TSG_OK;
 }
 

@@ -35,9 +35,9 @@ struct HostOut {
   uint8_t* gskip = nullptr;     // [groups] 1 = K2 skipped the group (item capacity)
   Candidate* cand = nullptr;    // [cand_cap] host-mapped: K2 candidates copied out
   Candidate* cand_dev = nullptr;  // device address of `cand`
-  uint32_t* counts = nullptr;   // [16] 0 candidates, 1 event chunks, 2 K2 list entries,
+  uint32_t* counts = nullptr;   // [32] 0 candidates, 1 event chunks, 2 K2 list entries,
                                 // 3 dense entries, 5 items, 6 entries, 7 skipped groups,
-                                // 8-11 K2 diagnostics (TSG_K2_DIAG)
+                                // 8-11 K2 diagnostics (TSG_K2_DIAG), 14-15 K1X, 16-17 K1F
   uint32_t files_cap = 0, cand_cap = 0, groups = 0, kw_words = 0;
   // stage boundaries of the batch on its lane's stream: data H2D | offsets H2D | wait for
   // the previous batch's kernels | prep | K1 | gates | K2 | outputs; ev[kEvDone] completes

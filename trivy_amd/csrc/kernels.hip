@@ -35,6 +35,7 @@
 
 #include "device.hpp"
 #include "internal.hpp"
+#include "k1f.hpp"
 
 namespace tsg {
 
@@ -66,6 +67,7 @@ constexpr __host__ __device__ int k1_threads(int ldsk) { return ldsk == 156 ? 10
 // lane reads its own bank) when the automaton leaves room for it; else 256 words
 constexpr uint32_t kK1RepBytes = 256 * 32 * 4;
 constexpr int kBlock = 256;
+constexpr int kCounts = 32;  // per-batch device counters (lane_create)
 constexpr int kPad = 256;     // zero bytes before and after the batch in HBM (>= K1 warm-up)
 constexpr int kMaxBack = 16;  // event windows up to this many chunks; larger -> whole file
 
@@ -565,6 +567,221 @@ __global__ void __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(4, 8))
   const uint64_t ib = (uint64_t)A.item_step * NS * A.seg * A.chunk;
   for (uint64_t it0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) & ~3ull; it0 < A.nitems; it0 += stride)
     L.template item_quad<NS>(it0, ib, q);
+}
+
+// ---------------------------------------------------------------- K1F
+// The filter-and-verify K1 (k1f.hpp): every wave streams a contiguous range of 1 KiB tiles,
+// lane l taking the 16-byte word at tile + 16 l (one coalesced 16-B load per lane).  Per
+// byte: the address of its entry from the byte in place (v_perm), one ds_read_b128 of the
+// entry (replicated per 16 lanes: conflict-free whatever the text), and per window end R(q)
+// = and3 + and.  Nothing waits on the previous byte.  The three look-behind bytes of lane l's
+// windows come from lane l-1 as partial ANDs (DPP wave_shr), lane 0's from the previous
+// tile's lane 63 (readlane); the run flags of words l-1 and l-2 likewise.  A word whose
+// windows name a bucket is listed in a per-wave LDS ring (word offset, groups of four window
+// ends, bucket union); 64 listed words are verified together, one per lane, against the
+// bucket's literal records (window compare, then the whole literal), and a match sets its
+// event bits (its last byte's chunk) and keyword bit (the file holding that byte, when the
+// literal starts inside it) with atomics.  Run events are ORed per chunk over the lanes of
+// the chunk (ballots) and written with one atomic per chunk; prep zeroes the events.
+constexpr uint32_t kFQueue = 128;                          // ring entries per wave
+constexpr uint32_t kFEntBytes = 256 * 256;                 // 256 entries x 16 replicas x 16 B
+constexpr uint32_t kFQueueOff = kFEntBytes;
+constexpr uint32_t kFImgOff = kFQueueOff + 16 * kFQueue * 8;
+constexpr uint32_t kFLds = kFImgOff + kFImgMax;            // 96 KiB: one 1024-thread block per CU
+constexpr int kFThreads = 1024;
+
+struct DevK1F {
+  const uint4* ent;    // [256] entries d_0..d_3
+  const uint8_t* img;  // verification image (k1f.hpp)
+  uint32_t img_bytes, kw_words, nlit;
+};
+
+struct K1FArgs {
+  const uint8_t* data;
+  const uint64_t* off;
+  const uint32_t* cf;  // coarse file map (file_of)
+  uint32_t total, chunk, nfiles, ntiles;
+  uint32_t* kw;
+  uint32_t* ev;     // zeroed by prep; ORed into
+  uint32_t* hits;   // [nlit] verified arrivals per record (sampling pass) or null
+  uint32_t* stats;  // [2] listed words, verified arrivals
+};
+
+// lane i <- lane i - 1, lane 0 <- old (DPP wave_shr:1, out-of-range source keeps old)
+__device__ __forceinline__ uint32_t f_shr1(uint32_t v, uint32_t old) {
+  return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)v, 0x138, 0xF, 0xF, false);
+}
+
+__device__ __forceinline__ uint32_t f_load4u(const uint8_t* data, uint32_t a) {  // bytes a..a+3
+  const uint32_t* p = (const uint32_t*)(data + (a & ~3u));
+  return __builtin_amdgcn_alignbyte(p[1], p[0], a & 3u);
+}
+
+struct FCarry {  // the previous tile's lane 63 (window partials, run flags) and lane 62 (flags)
+  uint32_t a, b, c, m63, m62;
+};
+
+struct K1FLane {
+  const DevK1F& d;
+  const K1FArgs& A;
+  const uint8_t* smem;
+  uint32_t lane, lane16;
+
+  // One tile: the lane's 16 bytes v at batch byte pos.  Returns the run events of the word
+  // (kEvRunU / kEvRunD) and the OR of its windows by groups of four (g[i]: ends 4i..4i+3).
+  __device__ __forceinline__ uint32_t tile(uint4 v, FCarry& cy, uint32_t (&g)[4]) const {
+    uint4 e[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+      const uint32_t w = k < 4 ? v.x : k < 8 ? v.y : k < 12 ? v.z : v.w;
+      e[k] = *(const uint4*)(smem + __builtin_amdgcn_perm(w, lane16, 0x0C0C0000u | ((4u + (uint32_t)(k & 3)) << 8)));
+    }
+    const uint32_t ao = k1f_and3(e[13].x, e[14].y, e[15].z), bo = e[14].x & e[15].y, co = e[15].x;
+    const uint32_t ai = f_shr1(ao, cy.a), bi = f_shr1(bo, cy.b), ci = f_shr1(co, cy.c);
+    cy.a = __builtin_amdgcn_readlane(ao, 63);
+    cy.b = __builtin_amdgcn_readlane(bo, 63);
+    cy.c = __builtin_amdgcn_readlane(co, 63);
+    uint32_t r[16];
+    r[0] = ai & e[0].w;
+    r[1] = k1f_and3(bi, e[0].z, e[1].w);
+    r[2] = k1f_and3(ci, e[0].y, e[1].z) & e[2].w;
+#pragma unroll
+    for (int k = 3; k < 16; k++) r[k] = k1f_and3(e[k - 3].x, e[k - 2].y, e[k - 1].z) & e[k].w;
+#pragma unroll
+    for (int i = 0; i < 4; i++) g[i] = k1f_or3(r[4 * i], r[4 * i + 1], r[4 * i + 2]) | r[4 * i + 3];
+    const uint32_t m = k1f_flags(r[3], r[7], r[11], r[15]);
+    const uint32_t m1 = f_shr1(m, cy.m63), m2 = f_shr1(m1, cy.m62);
+    cy.m63 = __builtin_amdgcn_readlane(m, 63);
+    cy.m62 = __builtin_amdgcn_readlane(m, 62);
+    return k1f_runs(m, m1, m2);
+  }
+
+  // a verified occurrence of record i starting at s, ending at e (< total)
+  __device__ __forceinline__ void report(const K1FLit& L, uint32_t i, uint32_t s, uint32_t e, uint32_t& narr) const {
+    narr++;
+    if (A.hits) atomicAdd(&A.hits[i], 1u);
+    if (L.ev) atomicOr(&A.ev[e / A.chunk], L.ev);
+    if (L.kw >= 0) {
+      const uint32_t f = file_of(A.cf, A.off, A.nfiles, e);
+      if (s >= A.off[f]) atomicOr(&A.kw[(size_t)f * d.kw_words + (uint32_t)L.kw / 32], 1u << ((uint32_t)L.kw % 32));
+    }
+  }
+
+  // the listed word at P: every window end of the groups in gm, against the buckets in bu
+  __device__ void verify(uint32_t P, uint32_t gm, uint32_t bu, uint32_t& narr) const {
+    const uint16_t* bstart = (const uint16_t*)(smem + kFImgOff);
+    const K1FLit* recs = (const K1FLit*)(smem + kFImgOff + kFImgLits);
+    const uint32_t* dw = (const uint32_t*)(A.data + P) - 1;  // bytes P-4 .. P+19 (kPad before the batch)
+    uint32_t w[6];
+#pragma unroll
+    for (int i = 0; i < 6; i++) w[i] = dw[i];
+    for (uint32_t k = 0; k < 16; k++) {
+      if (!((gm >> (k >> 2)) & 1)) continue;
+      const uint32_t o = k + 1;  // window bytes P+k-3 .. P+k = offsets o .. o+3 of w
+      const uint32_t lo = o < 4 ? w[0] : o < 8 ? w[1] : o < 12 ? w[2] : o < 16 ? w[3] : w[4];
+      const uint32_t hi = o < 4 ? w[1] : o < 8 ? w[2] : o < 12 ? w[3] : o < 16 ? w[4] : w[5];
+      const uint32_t win = __builtin_amdgcn_alignbyte(hi, lo, o & 3u);
+      uint32_t bm = bu;
+#pragma unroll
+      for (int j = 0; j < 4; j++)
+        bm &= *(const uint32_t*)(smem + ((((win >> (8 * j)) & 0xFFu) << 8) | lane16) + 4 * j);
+      bm &= 0xFFFFu;
+      if (!bm) continue;
+      const uint32_t q = P + k, wl = k1f_lower4(win);
+      for (; bm; bm &= bm - 1) {
+        const uint32_t b = __builtin_ctz(bm);
+        for (uint32_t i = bstart[b]; i < bstart[b + 1]; i++) {
+          const K1FLit L = recs[i];
+          if ((wl & L.wmask) != L.wkey || q < L.wend) continue;
+          const uint32_t s = q - L.wend, e = s + L.len - 1;
+          if (e >= A.total) continue;
+          bool eq = true;
+          for (uint32_t t = 0; t < L.len && eq; t += 4) {
+            const uint32_t dv = k1f_lower4(f_load4u(A.data, s + t));
+            const uint32_t lv = *(const uint32_t*)(smem + kFImgOff + L.boff + t);
+            const uint32_t mk = L.len - t >= 4 ? ~0u : (1u << (8 * (L.len - t))) - 1u;
+            eq = ((dv ^ lv) & mk) == 0;
+          }
+          if (eq) report(L, i, s, e, narr);
+        }
+      }
+    }
+  }
+};
+
+__global__ void __launch_bounds__(kFThreads) k1f_kernel(DevK1F d, K1FArgs A) {
+  __shared__ __attribute__((aligned(16))) uint8_t smem[kFLds];
+  for (uint32_t i = threadIdx.x; i < 256u * 16u; i += blockDim.x) ((uint4*)smem)[i] = d.ent[i >> 4];
+  for (uint32_t i = threadIdx.x; i < d.img_bytes / 16; i += blockDim.x)
+    ((uint4*)(smem + kFImgOff))[i] = ((const uint4*)d.img)[i];
+  __syncthreads();
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6, wpb = blockDim.x >> 6;
+  const uint32_t gw = blockIdx.x * wpb + wave, nw = gridDim.x * wpb;
+  const uint32_t t0 = (uint32_t)((uint64_t)gw * A.ntiles / nw), t1 = (uint32_t)((uint64_t)(gw + 1) * A.ntiles / nw);
+  if (t0 >= t1) return;  // (no block barrier below)
+  const K1FLane L{d, A, smem, lane, (lane & 15u) << 4};
+  uint2* ring = (uint2*)(smem + kFQueueOff) + wave * kFQueue;
+  uint32_t qh = 0, qn = 0, nlisted = 0, narr = 0;
+  auto drain = [&](uint32_t n) __attribute__((always_inline)) {
+    __builtin_amdgcn_wave_barrier();
+    if (lane < n) {
+      const uint2 x = ring[(qh + lane) & (kFQueue - 1)];
+      L.verify(x.x, x.y & 0xFu, x.y >> 16, narr);
+    }
+    __builtin_amdgcn_wave_barrier();
+    qh = (qh + n) & (kFQueue - 1);
+    qn -= n;
+  };
+  FCarry cy{0, 0, 0, 0, 0};
+  uint32_t g[4];
+  {  // warm-up: the tile before t0 (zero bytes before the batch) gives the carries
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (t0 > 0) v = *(const uint4*)(A.data + (size_t)(t0 - 1) * kFTile + 16u * lane);
+    (void)L.tile(v, cy, g);
+  }
+  const uint4* base = (const uint4*)A.data + lane;
+  uint4 p0 = base[(size_t)t0 * 64], p1 = base[(size_t)min(t0 + 1, t1 - 1) * 64];
+  for (uint32_t t = t0; t < t1; t++) {
+    const uint4 v = p0;
+    p0 = p1;
+    p1 = base[(size_t)min(t + 2, t1 - 1) * 64];
+    const uint32_t pos = t * kFTile + 16u * lane;
+    const uint32_t rb = L.tile(v, cy, g);
+    // run events: one atomic per chunk (the leader lane of each chunk in the tile)
+    const uint64_t bu = __ballot(rb & 1u), bd = __ballot(rb & 2u);
+    if (bu | bd) {
+      const uint32_t c = pos / A.chunk;
+      const bool lead = lane == 0 || pos - c * A.chunk < 16u;
+      const uint64_t ld = __ballot(lead);
+      if (lead) {
+        const uint64_t above = ld & (~0ull << lane << 1);
+        const uint64_t gm = (above ? (above & (~above + 1)) - 1 : ~0ull) & (~0ull << lane);
+        const uint32_t bits = ((bu & gm) ? kEvRunU : 0u) | ((bd & gm) ? kEvRunD : 0u);
+        if (bits) atomicOr(&A.ev[c], bits);
+      }
+    }
+    // listed words
+    const uint32_t un = k1f_or3(g[0], g[1], g[2]) | g[3];
+    const uint32_t bun = un & 0xFFFFu;
+    const uint64_t hb = __ballot(bun != 0);
+    if (hb) {
+      const uint32_t n = (uint32_t)__popcll(hb);
+      if (bun) {
+        const uint32_t slot = __builtin_amdgcn_mbcnt_hi((uint32_t)(hb >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)hb, 0u));
+        const uint32_t gm = ((g[0] & 0xFFFFu) ? 1u : 0u) | ((g[1] & 0xFFFFu) ? 2u : 0u) | ((g[2] & 0xFFFFu) ? 4u : 0u) |
+                            ((g[3] & 0xFFFFu) ? 8u : 0u);
+        ring[(qh + qn + slot) & (kFQueue - 1)] = make_uint2(pos, gm | bun << 16);
+      }
+      qn += n;
+      nlisted += n;
+      if (qn >= 64) drain(64);
+    }
+  }
+  if (qn) drain(qn);
+  if (A.stats) {
+    if (lane == 0) atomicAdd(&A.stats[0], nlisted);
+    if (narr) atomicAdd(&A.stats[1], narr);
+  }
 }
 
 // ---------------------------------------------------------------- K1X
@@ -2049,6 +2266,10 @@ struct DeviceRules {
   K1Host k1h;
   DevK1X k1x{};
   bool has_k1x = false;
+  bool use_k1f = false;  // K1 is the filter-and-verify K1F (k1f.hpp), else the automaton
+  DevK1F k1f{};
+  K1FTables k1ft;        // host copy (the adaptation rebuilds it)
+  uint32_t* d_fhits = nullptr;  // [n_lit] K1F sampling counters
   uint32_t* d_hits = nullptr;
   bool adapted = false;
   uint32_t hot_states = 0;
@@ -2071,6 +2292,7 @@ struct DeviceRules {
     if (kernels_done) (void)hipEventDestroy(kernels_done);
     for (auto* p : tables) (void)hipFree(p);
     (void)hipFree(d_hits);
+    (void)hipFree(d_fhits);
   }
 };
 
@@ -2188,10 +2410,11 @@ static int launch_k1(DeviceRules* r, const K1Args& A, hipStream_t st) {
 // anchor events fire everywhere.  Results are unchanged; K1 stops paying per-occurrence
 // accepts for words like "key" that occur in most files anyway.  The device is idle
 // while the shared tables change (every lane is synchronized first).
+static int apply_unknown(DeviceRules* r, const std::shared_ptr<std::vector<uint8_t>>& kw_unknown, uint32_t ev_hot);
 static int adapt_k1(DeviceRules* r, LaneState* l, uint64_t total, uint32_t nfiles, uint64_t nchunks, uint64_t k1_items) {
   const Plan& p = *r->plan;
   HIP_TRY(hipDeviceSynchronize());
-  const uint32_t ns = r->k1.ns, W = r->k1.kw_words, mw = r->k1.mw, G = (uint32_t)r->groups.size();
+  const uint32_t ns = r->k1.ns, W = r->k1.kw_words, mw = r->k1.mw;
   const uint64_t step = std::max<uint64_t>(1, k1_items / 16384);
   const uint64_t nsamp = (k1_items + step - 1) / step;
   HIP_TRY(hipMemsetAsync(r->d_hits, 0, sizeof(uint32_t) * ns, l->st));
@@ -2234,7 +2457,14 @@ static int adapt_k1(DeviceRules* r, LaneState* l, uint64_t total, uint32_t nfile
   if ((rc = k1_tables(p, hot, &r->k1h, &r->k1.start, &r->k1.acc_row))) return rc;
   HIP_TRY(hipMemcpy((void*)r->k1.tab, r->k1h.tab.data(), r->k1h.tab.size() * sizeof(uint16_t), hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy((void*)r->k1.accs, r->k1h.accs.data(), r->k1h.accs.size() * sizeof(uint16_t), hipMemcpyHostToDevice));
-  // gates of groups with an unknown keyword open; events of hot anchor literals fire everywhere
+  return apply_unknown(r, kw_unknown, ev_hot);
+}
+
+// After an adaptation: the gates of groups with an unknown keyword open, and the events of
+// hot anchor literals fire everywhere.
+static int apply_unknown(DeviceRules* r, const std::shared_ptr<std::vector<uint8_t>>& kw_unknown, uint32_t ev_hot) {
+  const Plan& p = *r->plan;
+  const uint32_t G = (uint32_t)r->groups.size();
   std::vector<uint32_t> galways = r->h_galways, gevents = r->h_gevents;
   std::vector<unsigned long long> gofbit = r->h_gofbit;
   for (uint32_t g = 0; g < G; g++) {
@@ -2260,6 +2490,80 @@ static int adapt_k1(DeviceRules* r, LaneState* l, uint64_t total, uint32_t nfile
   return TSG_OK;
 }
 
+// K1F's tables (r->k1ft) into their fixed device buffers
+static int upload_k1f(DeviceRules* r) {
+  const K1FTables& t = r->k1ft;
+  if (t.ent.size() != 256 * 4 || t.img.size() > kFImgMax || t.img.size() % 16)
+    return fail(TSG_ERR_INTERNAL, "bad K1F tables");
+  HIP_TRY(hipMemcpy((void*)r->k1f.ent, t.ent.data(), 256 * 16, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy((void*)r->k1f.img, t.img.data(), t.img.size(), hipMemcpyHostToDevice));
+  r->k1f.img_bytes = (uint32_t)t.img.size();
+  r->k1f.nlit = t.nlit;
+  return TSG_OK;
+}
+
+// one K1F launch over the first ntiles tiles of the batch
+static int launch_k1f(DeviceRules* r, const K1FArgs& A, hipStream_t st) {
+  const uint32_t wpb = kFThreads / 64;
+  const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>((A.ntiles + wpb - 1) / wpb, (uint64_t)r->cus));
+  k1f_kernel<<<grid, kFThreads, 0, st>>>(r->k1f, A);
+  HIP_TRY(hipGetLastError());
+  return TSG_OK;
+}
+
+// K1F adaptation (once per device, on the first large batch), the counterpart of adapt_k1:
+// a sampling launch over the first 64 MiB counts the verified arrivals of every literal;
+// the most frequent leave the filter until the rest arrive at most once per 4 KiB.  Their
+// keywords become unknown (the host checks them exactly) and their events fire everywhere,
+// so results are unchanged; K1F stops verifying words like "key" that most files hold.
+static int adapt_k1f(DeviceRules* r, LaneState* l, const K1FArgs& A0) {
+  const Plan& p = *r->plan;
+  HIP_TRY(hipDeviceSynchronize());
+  const uint32_t nrec = r->k1ft.nlit;
+  HIP_TRY(hipMemsetAsync(r->d_fhits, 0, sizeof(uint32_t) * std::max<uint32_t>(1, nrec), l->st));
+  K1FArgs A = A0;
+  A.ntiles = std::min<uint32_t>(A0.ntiles, (64u << 20) / kFTile);
+  A.hits = r->d_fhits;
+  A.stats = nullptr;
+  int rc;
+  if ((rc = launch_k1f(r, A, l->st))) return rc;
+  std::vector<uint32_t> hits(std::max<uint32_t>(1, nrec));
+  HIP_TRY(hipMemcpyAsync(hits.data(), r->d_fhits, sizeof(uint32_t) * hits.size(), hipMemcpyDeviceToHost, l->st));
+  HIP_TRY(hipStreamSynchronize(l->st));
+  r->adapted = true;
+  const uint64_t sample_bytes = std::min<uint64_t>((uint64_t)A.ntiles * kFTile, A.total);
+  const K1FLit* recs = (const K1FLit*)(r->k1ft.img.data() + kFImgLits);
+  std::vector<uint32_t> order;
+  uint64_t tot = 0;
+  for (uint32_t i = 0; i < nrec; i++)
+    if (hits[i]) {
+      tot += hits[i];
+      order.push_back(i);
+    }
+  std::sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return hits[a] > hits[b]; });
+  const uint64_t budget = sample_bytes / 4096;  // reporting budget: one arrival per 4 KiB
+  std::vector<uint8_t> quiet(p.n_lit, 0);
+  auto kw_unknown = std::make_shared<std::vector<uint8_t>>(p.n_kw, 0);
+  uint32_t ev_hot = 0, nhot = 0;
+  for (uint32_t i : order) {
+    if (tot <= budget) break;
+    const uint32_t id = recs[i].id;
+    if ((int)id >= p.fb_kw0 && (int)id < p.n_kw) continue;  // folding runes stay exact
+    quiet[id] = 1;
+    nhot++;
+    tot -= hits[i];
+    if ((int)id < p.n_kw) (*kw_unknown)[id] = 1;
+    ev_hot |= p.lit_event[id];
+  }
+  r->hot_states = nhot;
+  if (!nhot) return TSG_OK;
+  K1FTables t;
+  if (!k1f_build(p, quiet, &t, nullptr)) return fail(TSG_ERR_INTERNAL, "K1F tables without the hot literals");
+  r->k1ft = std::move(t);
+  if ((rc = upload_k1f(r))) return rc;
+  return apply_unknown(r, kw_unknown, ev_hot);
+}
+
 int device_rules_create(int device, const Plan& p, uint32_t chunk, uint32_t ext_cap, uint32_t adapt_mib,
                         DeviceRules** out) {
   int ndev = 0;
@@ -2277,6 +2581,21 @@ int device_rules_create(int device, const Plan& p, uint32_t chunk, uint32_t ext_
   if ((rc = make_device_k1(p, &r->k1, &r->tables, &r->k1h))) return rc;
   if ((rc = make_device_k1x(p, &r->k1x, &r->tables))) return rc;
   r->has_k1x = !p.x_lits.empty();
+  if (!knobs().k1_automaton.load() && k1f_build(p, {}, &r->k1ft, nullptr)) {
+    // fixed-size device tables: the adaptation rewrites them in place
+    void* ent = nullptr;
+    void* img = nullptr;
+    HIP_TRY(hipMalloc(&ent, 256 * 16));
+    r->tables.push_back(ent);
+    HIP_TRY(hipMalloc(&img, kFImgMax));
+    r->tables.push_back(img);
+    r->k1f.ent = (const uint4*)ent;
+    r->k1f.img = (const uint8_t*)img;
+    r->k1f.kw_words = (uint32_t)p.kw_words;
+    if ((rc = upload_k1f(r.get()))) return rc;
+    HIP_TRY(hipMalloc((void**)&r->d_fhits, sizeof(uint32_t) * std::max(1, p.n_lit)));
+    r->use_k1f = true;
+  }
   for (uint8_t h : p.rule_hostonly) r->all_kw_rows |= h;
   if (r->has_k1x)  // the 128 KiB prefix bitmap is dynamic LDS
     HIP_TRY(hipFuncSetAttribute(k1x_fn(r->k1x.step), hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -2371,8 +2690,9 @@ int lane_create(DeviceRules* d, LaneState** out) {
   const uint32_t G = std::max<uint32_t>(1, (uint32_t)d->groups.size());
   // per-batch counters: 0 candidates, 1 event chunks, 2 K2 entries, 3 dense entries, 5-7
   // layout (5 items, 6 entries, 7 groups skipped), 8-11 K2 diagnostics,
-  // 12-13 K2 claim cursors (list, dense), 14-15 K1X (records listed, inline verified)
-  HIP_TRY(hipMalloc((void**)&l->counts, sizeof(uint32_t) * 16));
+  // 12-13 K2 claim cursors (list, dense), 14-15 K1X (records listed, inline verified),
+  // 16-17 K1F (words listed, literal occurrences verified)
+  HIP_TRY(hipMalloc((void**)&l->counts, sizeof(uint32_t) * kCounts));
   HIP_TRY(hipMalloc((void**)&l->gcount, sizeof(uint32_t) * G));
   HIP_TRY(hipMalloc((void**)&l->bcount, sizeof(uint32_t) * G * (size_t)d->grid));
   HIP_TRY(hipMalloc((void**)&l->cursor, sizeof(uint32_t) * G));
@@ -2441,9 +2761,12 @@ int enqueue_scan(DeviceRules* r, LaneState* l, const ScanInput& in, HostOut* out
   if (total / C >= (1ull << 32) - 2) return fail(TSG_ERR_ARG, "batch too large for u32 chunk ids");
   const uint64_t nchunks = (total + C - 1) / C;
   l->nchunks = nchunks;
+  // K1F addresses the batch with 32-bit offsets (and its tiles past the end)
+  const bool k1f = r->use_k1f && total + (1u << 16) < (1ull << 32);
   int rc;
   // ---- buffers (grown on demand; growing waits for the device)
-  const size_t tail = (size_t)kK1Chains * kK1Seg * C + kPad;
+  // (K1F reads whole 1 KiB tiles: at least 4 KiB of zero tail)
+  const size_t tail = std::max<size_t>((size_t)kK1Chains * kK1Seg * C + kPad, 4096);
   const size_t meta_bytes = sizeof(uint64_t) * ((size_t)F + 1);
   // one H2D when the slot has room behind the batch: [batch | zero tail | offsets]
   const size_t o_off = ((size_t)total + tail + 15) & ~(size_t)15;
@@ -2520,12 +2843,13 @@ int enqueue_scan(DeviceRules* r, LaneState* l, const ScanInput& in, HostOut* out
     if (!one_copy) zero(data + total, tail);
     zero(l->kw, sizeof(uint32_t) * (uint64_t)F * W);
     zero(l->ovf, F);
-    zero(l->counts, sizeof(uint32_t) * 16);
+    zero(l->counts, sizeof(uint32_t) * kCounts);
+    if (k1f) zero(l->ev_bits, sizeof(uint32_t) * nchunks_pad);  // K1F ORs events in
     zero(l->gcount, sizeof(uint32_t) * G);
     zero(l->cursor, sizeof(uint32_t) * G);
     zero(l->gskip, G);
     zero(l->kind, G);
-    const uint64_t work = std::max<uint64_t>({PA.ncf, (uint64_t)F * W / 4, one_copy ? 1 : tail / 16, 1});
+    const uint64_t work = std::max<uint64_t>({PA.ncf, (uint64_t)F * W / 4, one_copy ? 1 : tail / 16, k1f ? nchunks_pad / 4 : 1, 1});
     const int pgrid = (int)std::min<uint64_t>((work + 255) / 256, (uint64_t)r->grid);
     prep_kernel<<<pgrid, 256, 0, st>>>(PA);
     HIP_TRY(hipGetLastError());
@@ -2535,9 +2859,15 @@ int enqueue_scan(DeviceRules* r, LaneState* l, const ScanInput& in, HostOut* out
   // ---- K1
   const uint64_t k1_items = (nchunks + k1_item_chunks - 1) / k1_item_chunks;
   const uint64_t adapt_bytes = r->adapt_mib == 0xFFFFFFFFu ? ~0ull : (uint64_t)(r->adapt_mib ? r->adapt_mib : 16) << 20;
-  if (!r->adapted && k1_items >= 64 && total >= adapt_bytes)
+  if (k1f) {
+    K1FArgs A{data, l->off, l->cf, (uint32_t)total, C, F, (uint32_t)((total + kFTile - 1) / kFTile),
+              l->kw, l->ev_bits, nullptr, l->counts + 16};
+    if (!r->adapted && total >= adapt_bytes && (rc = adapt_k1f(r, l, A))) return rc;
+    if (total && (rc = launch_k1f(r, A, st))) return rc;
+  } else if (!r->adapted && k1_items >= 64 && total >= adapt_bytes) {
     if ((rc = adapt_k1(r, l, total, F, nchunks, k1_items))) return rc;
-  if (k1_items) {
+  }
+  if (!k1f && k1_items) {
     K1Args A{data, l->off, l->cf, total, nchunks, k1_items, 1, C, F, l->kw, l->ev_bits, nullptr, (uint32_t)kK1Seg};
     if ((rc = launch_k1(r, A, st))) return rc;
   }
@@ -2656,7 +2986,7 @@ int enqueue_scan(DeviceRules* r, LaneState* l, const ScanInput& in, HostOut* out
         OA.n[OA.nc++] = n;
       }
     };
-    copy(out->counts, l->counts, sizeof(uint32_t) * 16);
+    copy(out->counts, l->counts, sizeof(uint32_t) * kCounts);
     copy(out->gskip, l->gskip, G);
     OA.kw = l->kw;
     OA.kw_host = (uint32_t*)(out->blk_dev + ((uint8_t*)out->kw - out->blk));

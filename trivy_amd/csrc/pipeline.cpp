@@ -81,7 +81,7 @@ struct Batch {
   std::unique_ptr<tsg_result> res;
   BatchResult br;
   ScanTimes t;
-  uint32_t counts[16] = {};
+  uint32_t counts[32] = {};
   double resolve_ms = 0;
   uint64_t files_found = 0;
 };
@@ -295,6 +295,8 @@ void update_stats(tsg_ctx* c, const Batch& b) {
   s.k2_replays = b.counts[11];
   s.k1x_records = b.counts[14];
   s.k1x_inline = b.counts[15];
+  s.k1f_listed = b.counts[16];
+  s.k1f_arrivals = b.counts[17];
   s.k1_hot_states = c->dr ? device_rules_hot_states(c->dr) : 0;
   s.batches++;
   s.sum_bytes += b.bytes;

@@ -495,6 +495,7 @@ std::unique_ptr<Plan> build_plan(const Ruleset& rs, const PlanOptions& opt, std:
     if ((size_t)d->nstates * d->nclasses * 2 > (size_t)opt.max_kw_table_bytes) return false;
     p->n_lit = (int)lits.size();
     p->lit_event = lit_event;
+    p->k1_lits = lits;
     p->kw_mask_events.assign(d->masks.size(), 0);
     for (size_t m = 0; m < d->masks.size(); m++)
       for (int id = 0; id < p->n_lit; id++)

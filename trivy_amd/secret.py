@@ -295,6 +295,32 @@ class Scanner:
                                        ev.ctypes.data_as(u32p), ev.size))
         return kw.reshape(batch.nfiles, W), ev
 
+    def k1_literals(self):
+        """K1's literals as (bytes, event bits); ids below n_keywords are keywords."""
+        out = []
+        buf = C.create_string_buffer(1 << 16)
+        n, ev = C.c_uint32(), C.c_uint32()
+        while N.lib().tsg_ruleset_k1_literal(self._h, len(out), buf, len(buf), C.byref(n), C.byref(ev)) == 0:
+            out.append((buf.raw[:n.value], ev.value))
+        return out
+
+    def k1f_emulate(self, batch, chunk, quiet=()):
+        """K1F's algorithm on the CPU (k1f.hpp): (keyword bits, chunk events, stats)."""
+        import numpy as np
+        W = (self.info()["n_keywords"] + 31) // 32
+        kw = np.zeros(batch.nfiles * W, dtype=np.uint32)
+        ev = np.zeros((int(batch.offsets[-1]) + chunk - 1) // chunk, dtype=np.uint32)
+        q = np.array(list(quiet) or [0], dtype=np.uint32)
+        st = np.zeros(4, dtype=np.uint64)
+        u32p = C.POINTER(C.c_uint32)
+        N.check(N.lib().tsg_emulate_k1f(self.handle, C.c_void_p(batch.data.ctypes.data),
+                                        batch.offsets.ctypes.data_as(C.POINTER(C.c_uint64)),
+                                        batch.nfiles, chunk, q.ctypes.data_as(u32p), len(quiet),
+                                        kw.ctypes.data_as(u32p), kw.size, ev.ctypes.data_as(u32p),
+                                        ev.size, st.ctypes.data_as(C.POINTER(C.c_uint64))))
+        return kw.reshape(batch.nfiles, W), ev, {"groups": int(st[0]), "arrivals": int(st[1]),
+                                                 "records": int(st[2])}
+
     def AllowPath(self, path):
         b = _b(path)
         rc = N.lib().tsg_ruleset_allow_path(self._h, b, len(b))
