@@ -190,8 +190,11 @@ int tsg_slot_acquire(tsg_ctx* ctx, uint64_t data_bytes, uint32_t nfiles, uint64_
                      tsg_slot_view* out);
 /* Submit the slot's first nfiles files: the device part runs asynchronously, the host
  * resolution follows it on the resolver pool.  *ticket names this submission for
- * tsg_batch_collect.  The slot may be submitted again (same bytes) at once (submissions
- * only read it) and must not be written until its submissions are collected. */
+ * tsg_batch_collect.  The slot may be submitted again (same bytes) at once, also with a
+ * different nfiles: a submission reads the slot and never writes the bytes the caller can
+ * reach (only a slot the library filled itself -- tsg_batch_upload -- submitted whole and
+ * with nothing else in flight carries its zero tail and offsets in the room behind data_cap).
+ * The slot must not be written until its submissions are collected. */
 int tsg_slot_submit(tsg_ctx* ctx, uint32_t slot_id, uint32_t nfiles, uint64_t* ticket);
 /* Give the slot back to the context (it is reused once its submissions are done). */
 int tsg_slot_release(tsg_ctx* ctx, uint32_t slot_id);

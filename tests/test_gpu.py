@@ -316,6 +316,34 @@ def test_zero_copy_slots_gpu(builtin):
     ctx.close()
 
 
+def test_slot_prefix_then_whole_gpu(builtin):
+    """A slot submitted as a prefix of its files and then whole, both in flight at once: each
+    submission reads only its files and never writes the caller's bytes past them (ADVICE r4:
+    the single-H2D path once zeroed the files after a prefix).  Each result == the exact path
+    over the same files; the slot's bytes are unchanged afterwards."""
+    import numpy as np
+    b, _ = corpus.make_corpus(8 << 20, seed=46, plants_per_mib=60)
+    ctx = S.GpuContext(builtin, 0)
+    tot, pb = int(b.offsets[-1]), int(b.path_offsets[-1])
+    sid, data, offs, paths, poffs = ctx.acquire_slot(tot, b.nfiles, pb)
+    data[:tot] = b.data[:tot]
+    offs[:b.nfiles + 1] = b.offsets
+    paths[:pb] = b.paths[:pb]
+    poffs[:b.nfiles + 1] = b.path_offsets
+    before = data[:tot].copy()
+    half = b.nfiles // 2
+    prefix = S.Batch(b.data[:int(b.offsets[half])], b.offsets[:half + 1].copy(),
+                     b.paths[:int(b.path_offsets[half])], b.path_offsets[:half + 1].copy())
+    t1 = ctx.submit_slot(sid, half, paths_of=prefix)
+    t2 = ctx.submit_slot(sid, b.nfiles, paths_of=b)
+    got1, got2 = ctx.collect(t1), ctx.collect(t2)
+    assert np.array_equal(data[:tot], before)
+    ctx.release_slot(sid)
+    ctx.close()
+    assert got1 == builtin.ScanBatch(prefix, nthreads=16)
+    assert got2 == builtin.ScanBatch(b, nthreads=16)
+
+
 def test_queue_concurrent_callers_gpu(builtin):
     """tsg_queue on the device: 16 threads share one context; per-file results equal
     Scanner.Scan (analyzer.go:419-443)."""

@@ -12,6 +12,7 @@ import os
 import numpy as np
 import pytest
 
+from tests.conftest import ROOT
 from tests.test_walker import layer_bytes
 from trivy_amd import analyzer as A
 from trivy_amd import configs
@@ -257,3 +258,39 @@ def test_fs_scan_drops_binary_across_pieces(tmp_path, scanner, seed):
     assert walked == ref.walked == 120
     assert 40 < len(paths) < 100
     ctx.close()
+
+
+_EMFILE_CHILD = r"""
+import os, sys, errno
+sys.path.insert(0, sys.argv[2])
+from trivy_amd import secret as S, walker as W, _native as N
+sc = S.NewScanner(None)
+held = []
+try:  # take every descriptor but one: the walk's directory gets it, no file open can succeed
+    while True:
+        held.append(os.open("/dev/null", os.O_RDONLY))
+except OSError as e:
+    assert e.errno == errno.EMFILE
+os.close(held.pop())
+try:
+    W.NativeFS(sc, sys.argv[1])
+    print("PACKED")
+except N.NativeError as e:
+    print("ERROR", e)
+"""
+
+
+def test_fs_pack_open_error_fails_scan(tmp_path):
+    """A file the walk listed but cannot open for a reason other than permissions (here a
+    descriptor table that stays full past open_at_retry's wait) fails the scan like the
+    reference's "unable to open" (analyzer.go:411-416) instead of silently dropping the file
+    (ADVICE r4).  Run in a child process with a low descriptor limit."""
+    import subprocess
+    import sys
+    root = tmp_path / "t"
+    (root / "d").mkdir(parents=True)
+    for i in range(3):
+        (root / "d" / ("f%d.txt" % i)).write_text("token = %d\n" % i)
+    prog = "import resource; resource.setrlimit(resource.RLIMIT_NOFILE, (64, 64))\n" + _EMFILE_CHILD
+    r = subprocess.run([sys.executable, "-c", prog, str(root), ROOT], capture_output=True, text=True, timeout=120)
+    assert "ERROR" in r.stdout and "unable to open" in r.stdout, r.stdout + r.stderr

@@ -186,9 +186,11 @@ __global__ void __launch_bounds__(256) prep_kernel(PrepArgs A) {
 // ---------------------------------------------------------------- outputs to the host
 // One kernel writes a batch's outputs straight into pinned, host-mapped memory: the
 // candidate records (their count is only known on the device), per-file flags (bit 0 the
-// overflow flag, bit 1 folding runes present: the fallback keywords' bits), the keyword
-// rows the host reads -- files with candidates or a flag, every file when the plan has
-// host-only rules or K2 skipped a group -- and the small arrays (counters, skipped groups).
+// overflow flag, bit 1 folding runes present: the fallback keywords' bits, bit 2 the
+// file's keyword row was written), the keyword rows the host reads -- files with
+// candidates (K2's hascand) or a flag, every file when the plan has host-only rules or K2
+// skipped a group; each row once -- and the small arrays (counters, skipped groups).  The
+// host reads a keyword row only with bit 2 set (plan.cpp resolve_batch checks it).
 // It replaces the candidate copy kernel and five runtime D2H copies; the sparse rows cut
 // the PCIe writes of a 1 GiB batch from ~1.4 MB to ~0.2 MB.  Every range starts 16-B
 // aligned on both sides (host_out_alloc, hipMalloc).
@@ -205,6 +207,7 @@ struct OutArgs {
   const uint32_t* kw;  // [F * W] device keyword bits
   uint32_t* kw_host;
   const uint8_t* ovf;  // [F] device overflow flags
+  const uint8_t* hascand;  // [F] device: the file has a candidate record
   uint8_t* flags_host;
   uint32_t F, W, fb_lo, fb_hi;  // fallback keywords (folding runes): ids [fb_lo, fb_hi)
   uint32_t all_rows;            // every keyword row (host-only rules)
@@ -229,17 +232,10 @@ __global__ void __launch_bounds__(256) outputs_kernel(OutArgs A) {
     uint32_t fold = 0;
     for (uint32_t k = A.fb_lo; k < A.fb_hi; k++) fold |= (row[k / 32] >> (k % 32)) & 1u;
     const uint8_t fl = (A.ovf[f] ? 1 : 0) | (fold ? 2 : 0);
-    A.flags_host[f] = fl;
-    if (fl && !all)
+    const bool put = all || fl || A.hascand[f];
+    A.flags_host[f] = fl | (put ? 4 : 0);
+    if (put && !all)
       for (uint32_t w = 0; w < A.W; w++) A.kw_host[f * A.W + w] = row[w];
-  }
-  if (!all) {
-    const DevCand* cand = (const DevCand*)A.cand;
-    for (uint64_t i = tid; i < ncand; i += nth) {
-      const uint32_t f = cand[i].file;
-      if (f < A.F)
-        for (uint32_t w = 0; w < A.W; w++) A.kw_host[(size_t)f * A.W + w] = A.kw[(size_t)f * A.W + w];
-    }
   }
 }
 
@@ -1416,6 +1412,7 @@ struct K2Args {
   uint32_t* cand_count;
   uint32_t cand_cap;
   uint8_t* ovf;
+  uint8_t* hascand;  // [nfiles] 1: the file has a candidate record (outputs_kernel's rows)
   uint32_t* diag;  // null, or [4]: tail bytes, longest tail, tails over 4 KiB, word replays
   uint32_t* claim;  // [2] next list / dense entry (zeroed per batch)
   uint32_t word_recs;  // accepting words as one kCandWord record each (groups < 2^14)
@@ -1454,6 +1451,7 @@ __device__ __forceinline__ void emit_cand(const K2Args& A, uint32_t file, uint32
     A.ovf[file] = 1;  // (also a file of 4 GiB or more: its 32-bit end offsets would wrap)
     if (idx < A.cand_cap) A.cand[idx] = DevCand{file, rule, 0};
   }
+  A.hascand[file] = 1;
 }
 
 #ifdef K2_NOINL  // the rare paths out of line (their registers do not add to the hot loop's)
@@ -1507,6 +1505,7 @@ struct Lane {
       A.ovf[file] = 1;
       if (idx < A.cand_cap) A.cand[idx] = DevCand{file, rule, 0};
     }
+    A.hascand[file] = 1;
   }
   // A word with an accept, again from registers (bytes lo..hi-1 of v, batch position wb):
   // its accepting transitions are counted, reserved with one atomic and written as
@@ -2321,6 +2320,8 @@ struct LaneState {
   size_t ggate_cap = 0;
   uint8_t* ovf = nullptr;
   size_t ovf_cap = 0;
+  uint8_t* hascand = nullptr;
+  size_t hascand_cap = 0;
   uint2* items = nullptr;
   size_t items_cap = 0;
   uint4* entries = nullptr;
@@ -2343,7 +2344,7 @@ struct LaneState {
     if (!d) return;
     (void)hipSetDevice(d->device);
     if (st) (void)hipStreamSynchronize(st);
-    void* bufs[] = {data_alloc, meta, cf, ev_bits, xlist, xcount, evlist, kw, ggate, ovf,
+    void* bufs[] = {data_alloc, meta, cf, ev_bits, xlist, xcount, evlist, kw, ggate, ovf, hascand,
                     items, entries, dentries, cand, counts, gcount, bcount, cursor, base, kind, gskip, etrace};
     for (void* b : bufs) (void)hipFree(b);
     if (st) (void)hipStreamDestroy(st);
@@ -2791,6 +2792,7 @@ int enqueue_scan(DeviceRules* r, LaneState* l, const ScanInput& in, HostOut* out
   if ((rc = ensure(&l->kw, &l->kw_cap, (size_t)F * W + 1))) return rc;
   if ((rc = ensure(&l->ggate, &l->ggate_cap, (size_t)F * r->GW + 1))) return rc;
   if ((rc = ensure(&l->ovf, &l->ovf_cap, (size_t)F + 1))) return rc;
+  if ((rc = ensure(&l->hascand, &l->hascand_cap, (size_t)F + 1))) return rc;
   // item capacity: twice the batch's chunks (the builtin rules list ~11 % of them); over
   // it, groups are skipped (kGroupSkip) and resolved on the host, never dropped
   const uint64_t items_cap = std::max<uint64_t>(2 * nchunks, 1u << 16);
@@ -2843,6 +2845,7 @@ int enqueue_scan(DeviceRules* r, LaneState* l, const ScanInput& in, HostOut* out
     if (!one_copy) zero(data + total, tail);
     zero(l->kw, sizeof(uint32_t) * (uint64_t)F * W);
     zero(l->ovf, F);
+    zero(l->hascand, F);
     zero(l->counts, sizeof(uint32_t) * kCounts);
     if (k1f) zero(l->ev_bits, sizeof(uint32_t) * nchunks_pad);  // K1F ORs events in
     zero(l->gcount, sizeof(uint32_t) * G);
@@ -2951,6 +2954,7 @@ int enqueue_scan(DeviceRules* r, LaneState* l, const ScanInput& in, HostOut* out
     A.cand_count = l->counts;
     A.cand_cap = out->cand_cap;
     A.ovf = l->ovf;
+    A.hascand = l->hascand;
     static const bool diag = getenv("TSG_K2_DIAG") != nullptr;
     A.diag = diag ? l->counts + 8 : nullptr;
     A.claim = l->counts + 12;
@@ -2991,6 +2995,7 @@ int enqueue_scan(DeviceRules* r, LaneState* l, const ScanInput& in, HostOut* out
     OA.kw = l->kw;
     OA.kw_host = (uint32_t*)(out->blk_dev + ((uint8_t*)out->kw - out->blk));
     OA.ovf = l->ovf;
+    OA.hascand = l->hascand;
     OA.flags_host = out->blk_dev + (out->ovf - out->blk);
     OA.F = F;
     OA.W = W;

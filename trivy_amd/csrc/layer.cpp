@@ -20,6 +20,8 @@
 #include <memory>
 #include <vector>
 #include <thread>
+#include <atomic>
+#include <mutex>
 
 #include <cerrno>
 #include <dirent.h>
@@ -43,6 +45,23 @@ int open_at_retry(int dfd, const char* path, int flags) {
     std::this_thread::sleep_for(std::chrono::microseconds(500));
   }
 }
+
+// A failed open of a file the walk listed (analyzer.go:411-416): a permission error skips the
+// file, and so does a file gone or replaced since the listing (ENOENT, ELOOP under
+// O_NOFOLLOW, ENOTDIR), which the walk would not have listed; any other error -- a descriptor
+// table still full after open_at_retry's wait included -- fails the scan ("unable to open").
+// Thread-safe: the parallel readers record the first such error.
+struct OpenErr {
+  std::mutex m;
+  std::atomic<bool> set{false};
+  std::string msg;
+  void add(int e, const std::string& path) {
+    if (e == EACCES || e == EPERM || e == ENOENT || e == ELOOP || e == ENOTDIR) return;
+    std::lock_guard<std::mutex> g(m);
+    if (!set) msg = "unable to open " + path + ": " + strerror(e);
+    set = true;
+  }
+};
 }  // namespace
 }  // namespace tsg
 
@@ -1207,6 +1226,7 @@ int fs_collect(const tsg_ruleset* rs, const char* root, const char* const* skip_
     uint32_t walked = 0;
     // a regular file at `path` (name relative to the open directory dfd, or dfd < 0): the
     // walk's file callback, its Required gate and its head; true if walked
+    OpenErr oe;
     auto visit_file = [&](int dfd, const char* name, const std::string& path, std::unique_ptr<FsFile>* keep) {
       if (contains(g.skip_files, trim_left_slash(path))) return false;
       std::string fp;
@@ -1230,7 +1250,10 @@ int fs_collect(const tsg_ruleset* rs, const char* root, const char* const* skip_
         return true;
       }
       const int fd = open_at_retry(dfd, dfd >= 0 ? name : path.c_str(), O_RDONLY | O_NOFOLLOW | O_CLOEXEC);
-      if (fd < 0) return true;  // analyzer.go:411-413: a permission error skips the file
+      if (fd < 0) {  // analyzer.go:411-416 (OpenErr)
+        oe.add(errno, path);
+        return true;
+      }
       struct stat fs2;
       if (fstat(fd, &fs2) != 0 || !S_ISREG(fs2.st_mode)) {  // (replaced since the listing)
         close(fd);
@@ -1255,6 +1278,7 @@ int fs_collect(const tsg_ruleset* rs, const char* root, const char* const* skip_
       } else if (lstat(r0.c_str(), &s0) == 0 && S_ISREG(s0.st_mode)) {  // fs.go:37-38
         std::unique_ptr<FsFile> f;
         walked += visit_file(-1, nullptr, r0, &f);
+        if (oe.set) return fail(TSG_ERR_ARG, oe.msg);
         if (f) files.push_back(std::move(f));
       }
     }
@@ -1320,6 +1344,10 @@ int fs_collect(const tsg_ruleset* rs, const char* root, const char* const* skip_
           wk[k] = visit_file(dirfd(v.d), ents[k].name->c_str(), clean(level[l0 + ents[k].dir] + "/" + *ents[k].name),
                              &got[k]);
         }, 8);
+        if (oe.set) {
+          for (auto& v : dirs) if (v.d) closedir(v.d);
+          return fail(TSG_ERR_ARG, oe.msg);
+        }
         for (size_t k = 0; k < ents.size(); k++) {
           walked += wk[k];
           if (got[k]) files.push_back(std::move(got[k]));
@@ -1364,12 +1392,13 @@ std::vector<size_t> fs_layout(const std::vector<std::unique_ptr<FsFile>>& files,
 }
 
 // file f's bytes at dst: a small file from its head, a large one read in place
-uint64_t fs_fill(FsFile& f, uint8_t* dst) {
+uint64_t fs_fill(FsFile& f, uint8_t* dst, OpenErr* oe) {
   if (f.size <= kSmall) {
     if (f.got) std::memcpy(dst, f.head.data(), f.got);
     return f.got;
   }
   const int fd = open_at_retry(-1, f.full.c_str(), O_RDONLY | O_CLOEXEC);
+  if (fd < 0) oe->add(errno, f.full);
   const uint64_t r = fd < 0 ? 0 : read_upto(fd, dst, f.got);
   if (fd >= 0) close(fd);
   return r;
@@ -1391,7 +1420,9 @@ int fs_pack(const tsg_ruleset* rs, const char* root, const char* const* skip_fil
     const std::vector<size_t> kept = fs_layout(files, L.get());
     uint8_t* const dst = sink.reserve(L.get(), L->offsets.back(), (uint32_t)kept.size(), L->paths.size());
     std::vector<uint64_t> got(kept.size());
-    pool_for(kept.size(), 16, [&](size_t k) { got[k] = fs_fill(*files[kept[k]], dst + L->offsets[k]); }, 4);
+    OpenErr oe;
+    pool_for(kept.size(), 16, [&](size_t k) { got[k] = fs_fill(*files[kept[k]], dst + L->offsets[k], &oe); }, 4);
+    if (oe.set) return fail(TSG_ERR_ARG, oe.msg);
     // a large file that shrank between the walk and its read: close the gaps (rare)
     bool short_read = false;
     for (size_t k = 0; k < kept.size(); k++) short_read |= got[k] != L->offsets[k + 1] - L->offsets[k];
@@ -1446,15 +1477,20 @@ extern "C" int tsg_fs_pack_shard(const tsg_ruleset* rs, const char* root, const 
     // read this rank's files whole (in parallel), then IsBinary on what was read
     std::vector<std::vector<uint8_t>> body(mine.size());
     std::vector<uint8_t> keep(mine.size(), 0);
+    tsg::OpenErr oe;
     tsg::pool_for(mine.size(), 16, [&](size_t k) {
       const tsg::FsFile& f = *files[mine[k]];
       const int fd = tsg::open_at_retry(-1, f.full.c_str(), O_RDONLY | O_NOFOLLOW | O_CLOEXEC);
-      if (fd < 0) return;  // analyzer.go:411-413: a permission error skips the file
+      if (fd < 0) {  // analyzer.go:411-416 (OpenErr)
+        oe.add(errno, f.full);
+        return;
+      }
       body[k].resize(f.size);
       body[k].resize(tsg::read_upto(fd, body[k].data(), f.size));
       close(fd);
       keep[k] = !tsg::is_binary(body[k].data(), (int64_t)body[k].size());
     }, 4);
+    if (oe.set) return tsg::fail(TSG_ERR_ARG, oe.msg);
     auto L = std::make_unique<tsg_layer>();
     L->walked = walked;
     uint64_t total = 0;
@@ -1519,10 +1555,12 @@ extern "C" int tsg_fs_scan(tsg_ctx* ctx, const char* root, const char* const* sk
     // every listed file read straight into its place in a piece; an unreadable or binary
     // one is scanned along (its bytes are there already) and dropped from the results
     std::vector<uint8_t> drop(kept.size(), 0);
+    tsg::OpenErr oe;
     rc = tsg::scan_in_pieces(ctx, L.get(), [&](size_t k, uint8_t* dst) -> uint64_t {
       const tsg::FsFile& f = *files[kept[k]];
       const int fd = tsg::open_at_retry(-1, f.full.c_str(), O_RDONLY | O_NOFOLLOW | O_CLOEXEC);
-      if (fd < 0) {  // analyzer.go:411-413: a permission error skips the file
+      if (fd < 0) {  // analyzer.go:411-416 (OpenErr)
+        oe.add(errno, f.full);
         drop[k] = 1;
         return 0;
       }
@@ -1532,6 +1570,11 @@ extern "C" int tsg_fs_scan(tsg_ctx* ctx, const char* root, const char* const* sk
       return r;
     }, out, &drop);
     if (rc) return rc;
+    if (oe.set) {
+      tsg_result_free(*out);
+      *out = nullptr;
+      return tsg::fail(TSG_ERR_ARG, oe.msg);
+    }
     const auto t3 = now();
     // the listing (one heap block per file) is freed behind the return
     try {

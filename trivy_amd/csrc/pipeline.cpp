@@ -60,8 +60,20 @@ struct Slot {
   int inflight = 0;  // submissions whose host job has not finished
   int owner = kFree;
   std::thread::id holder;  // thread that took it (kCaller / kUpload)
-  uint32_t nfiles = 0;
+  // files the library itself wrote into the slot (upload, queue); kUnknownFill when the
+  // caller writes it (tsg_slot_acquire).  Only a submission of exactly those files, with no
+  // other submission of the slot in flight, may use the slot's bytes past its batch for the
+  // zero tail and the offsets (enqueue_scan's single H2D): nothing the caller owns is there.
+  uint32_t filled = 0;
 };
+constexpr uint32_t kUnknownFill = 0xFFFFFFFFu;
+
+// ScanInput of a submission of the slot's first nfiles files (lock held)
+ScanInput slot_input(const Slot& s, uint32_t nfiles) {
+  const bool room = s.inflight == 0 && s.filled == nfiles;
+  return ScanInput{s.data, s.off, nfiles, s.off[nfiles], s.paths, s.poff, room ? s.data : nullptr,
+                   room ? s.data_cap + slot_room_bytes(s.files_cap) : 0};
+}
 
 // One submission of a slot.
 struct Batch {
@@ -211,6 +223,7 @@ int slot_take(tsg_ctx* c, std::unique_lock<std::mutex>& lk, int owner, uint64_t 
       int rc = slot_reserve(c, c->slots[pick].get(), bytes, files, pbytes);
       if (rc) return rc;
       c->slots[pick]->owner = owner;
+      c->slots[pick]->filled = kUnknownFill;
       c->slots[pick]->holder = std::this_thread::get_id();
       *id = (uint32_t)pick;
       return TSG_OK;
@@ -414,8 +427,7 @@ int submit_locked(tsg_ctx* c, uint32_t sid, uint32_t nfiles, bool keep_result,
   if (!c->emulate) {
     if ((rc = out_take(c, nfiles, &b->out))) return rc;
     LaneState* l = c->lanes[c->seq++ % c->lanes.size()];
-    ScanInput in{s.data, s.off, nfiles, s.off[nfiles], s.paths, s.poff, s.data,
-                 s.data_cap + slot_room_bytes(s.files_cap)};
+    const ScanInput in = slot_input(s, nfiles);
     if ((rc = enqueue_scan(c->dr, l, in, &c->outs[b->out]))) {
       c->out_busy[b->out] = 0;
       return rc;
@@ -530,6 +542,7 @@ void q_submit(tsg_queue* q, std::shared_ptr<OpenBatch> ob) {
   };
   {
     std::lock_guard<std::mutex> g(q->c->m);
+    q->c->slots[ob->slot]->filled = ob->nfiles;  // the queue wrote exactly these files
     rc = submit_locked(q->c, ob->slot, ob->nfiles, true, ready, &b);
     q->c->slots[ob->slot]->owner = kFree;  // free once its job is done
     q->c->cv.notify_all();
@@ -675,7 +688,7 @@ int upload_into_slot(tsg_ctx* c, int owner, const uint8_t* data, const uint64_t*
   std::memcpy(s.off, offsets, sizeof(uint64_t) * ((size_t)nfiles + 1));
   if (pbytes) std::memcpy(s.paths, paths, pbytes);
   std::memcpy(s.poff, path_offsets, sizeof(uint64_t) * ((size_t)nfiles + 1));
-  s.nfiles = nfiles;
+  s.filled = nfiles;
   return TSG_OK;
 }
 }  // namespace
@@ -755,8 +768,7 @@ int tsg_batch_kernels(tsg_ctx* c, uint32_t slot_id, uint32_t nfiles, uint32_t* k
     int oi;
     if ((rc = out_take(c, nfiles, &oi))) return rc;
     LaneState* l = c->lanes[c->seq++ % c->lanes.size()];
-    ScanInput in{s.data, s.off, nfiles, s.off[nfiles], s.paths, s.poff, s.data,
-                 s.data_cap + slot_room_bytes(s.files_cap)};
+    const ScanInput in = slot_input(s, nfiles);
     if ((rc = enqueue_scan(c->dr, l, in, &c->outs[oi]))) {
       c->out_busy[oi] = 0;
       return rc;

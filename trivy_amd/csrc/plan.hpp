@@ -136,9 +136,10 @@ struct KernelOutputView {
   const Candidate* cand = nullptr;
   size_t ncand = 0;
   const uint8_t* overflow = nullptr;    // [nfiles] or null: bit 0 = resolve the whole file exactly
-  // overflow bit 1 = folding runes present (their keyword bits set), and `kw` holds only the
-  // rows of files with candidates or a flag set (the device's outputs kernel); otherwise
-  // `kw` is whole and folding runes are read from it
+  // overflow bit 1 = folding runes present (their keyword bits set), bit 2 = the file's
+  // keyword row is written, and `kw` holds only those rows (files with candidates or a flag
+  // set: the device's outputs kernel); otherwise `kw` is whole and folding runes are read
+  // from it
   bool sparse_kw = false;
   const uint8_t* kw_unknown = nullptr;  // [n_kw] or null: keyword bits K1 no longer reports
   const uint8_t* path_ok = nullptr;     // [nfiles] or null: Global.AllowPath from the device
