@@ -115,14 +115,12 @@ K1F_HD inline uint32_t k1f_or3(uint32_t a, uint32_t b, uint32_t c) {
 // the run flags of one 16-byte word from the windows ending at its bytes 3, 7, 11, 15:
 // bit k = U(byte k), bit 16 + k = D(byte k)
 K1F_HD inline uint32_t k1f_flags(uint32_t r3, uint32_t r7, uint32_t r11, uint32_t r15) {
-  // byte i of x = [U(4i..4i+3) | D(4i..4i+3) << 4] (byte 2 of each window's R)
-  const uint32_t x = k1f_perm(r7, r3, 0x0C0C0602u) | k1f_perm(r15, r11, 0x06020C0Cu);
-  uint32_t u = x & 0x0F0F0F0Fu, d = (x >> 4) & 0x0F0F0F0Fu;
-  u = (u | (u >> 4)) & 0x00FF00FFu;
-  d = (d | (d >> 4)) & 0x00FF00FFu;
-  u = (u | (u >> 8)) & 0x0000FFFFu;
-  d = (d | (d >> 8)) & 0x0000FFFFu;
-  return u | d << 16;
+  // byte 2 of the window ending at 4i+3 is [U(4i..4i+3) | D(4i..4i+3) << 4]; gathered in the
+  // order i = 0, 2, 1, 3 the nibbles read (low first) u0 d0 u2 d2 u1 d1 u3 d3, and one delta
+  // swap at distance 12 (d0 <-> u1, d2 <-> u3) leaves u0 u1 u2 u3 d0 d1 d2 d3
+  const uint32_t x = k1f_perm(r11, r3, 0x0C0C0602u) | k1f_perm(r15, r7, 0x06020C0Cu);
+  const uint32_t t = ((x >> 12) ^ x) & 0x0000F0F0u;
+  return x ^ t ^ (t << 12);
 }
 
 K1F_HD inline uint32_t k1f_ctz(uint32_t x) {

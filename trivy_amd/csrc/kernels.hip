@@ -607,14 +607,20 @@ struct K1FArgs {
 __device__ __forceinline__ uint32_t f_shr1(uint32_t v, uint32_t old) {
   return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)v, 0x138, 0xF, 0xF, false);
 }
+// lane i <- lane i - 1, lane 0 <- lane 63 (DPP wave_ror:1)
+__device__ __forceinline__ uint32_t f_ror1(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x13C, 0xF, 0xF, false);
+}
+// lane l <- lane l - 1 of this tile, lane 0 <- lane 63 of the previous tile
+__device__ __forceinline__ uint32_t f_prev(uint32_t cur, uint32_t prev) { return f_shr1(cur, f_ror1(prev)); }
 
 __device__ __forceinline__ uint32_t f_load4u(const uint8_t* data, uint32_t a) {  // bytes a..a+3
   const uint32_t* p = (const uint32_t*)(data + (a & ~3u));
   return __builtin_amdgcn_alignbyte(p[1], p[0], a & 3u);
 }
 
-struct FCarry {  // the previous tile's lane 63 (window partials, run flags) and lane 62 (flags)
-  uint32_t a, b, c, m63, m62;
+struct FCarry {  // the previous tile's per-lane window partials and run flags (f_prev)
+  uint32_t a, b, c, m, m1;
 };
 
 struct K1FLane {
@@ -633,10 +639,10 @@ struct K1FLane {
       e[k] = *(const uint4*)(smem + __builtin_amdgcn_perm(w, lane16, 0x0C0C0000u | ((4u + (uint32_t)(k & 3)) << 8)));
     }
     const uint32_t ao = k1f_and3(e[13].x, e[14].y, e[15].z), bo = e[14].x & e[15].y, co = e[15].x;
-    const uint32_t ai = f_shr1(ao, cy.a), bi = f_shr1(bo, cy.b), ci = f_shr1(co, cy.c);
-    cy.a = __builtin_amdgcn_readlane(ao, 63);
-    cy.b = __builtin_amdgcn_readlane(bo, 63);
-    cy.c = __builtin_amdgcn_readlane(co, 63);
+    const uint32_t ai = f_prev(ao, cy.a), bi = f_prev(bo, cy.b), ci = f_prev(co, cy.c);
+    cy.a = ao;
+    cy.b = bo;
+    cy.c = co;
     uint32_t r[16];
     r[0] = ai & e[0].w;
     r[1] = k1f_and3(bi, e[0].z, e[1].w);
@@ -646,9 +652,9 @@ struct K1FLane {
 #pragma unroll
     for (int i = 0; i < 4; i++) g[i] = k1f_or3(r[4 * i], r[4 * i + 1], r[4 * i + 2]) | r[4 * i + 3];
     const uint32_t m = k1f_flags(r[3], r[7], r[11], r[15]);
-    const uint32_t m1 = f_shr1(m, cy.m63), m2 = f_shr1(m1, cy.m62);
-    cy.m63 = __builtin_amdgcn_readlane(m, 63);
-    cy.m62 = __builtin_amdgcn_readlane(m, 62);
+    const uint32_t m1 = f_prev(m, cy.m), m2 = f_prev(m1, cy.m1);
+    cy.m = m;
+    cy.m1 = m1;
     return k1f_runs(m, m1, m2);
   }
 
@@ -728,24 +734,22 @@ __global__ void __launch_bounds__(kFThreads) k1f_kernel(DevK1F d, K1FArgs A) {
     qh = (qh + n) & (kFQueue - 1);
     qn -= n;
   };
-  FCarry cy{0, 0, 0, 0, 0};
+  FCarry cy{0, 0, 0, 0, 0};  // (the warm-up tile's own inputs do not reach its outputs)
   uint32_t g[4];
   {  // warm-up: the tile before t0 (zero bytes before the batch) gives the carries
     uint4 v = make_uint4(0, 0, 0, 0);
     if (t0 > 0) v = *(const uint4*)(A.data + (size_t)(t0 - 1) * kFTile + 16u * lane);
     (void)L.tile(v, cy, g);
   }
-  const uint4* base = (const uint4*)A.data + lane;
-  uint4 p0 = base[(size_t)t0 * 64], p1 = base[(size_t)min(t0 + 1, t1 - 1) * 64];
-  for (uint32_t t = t0; t < t1; t++) {
-    const uint4 v = p0;
-    p0 = p1;
-    p1 = base[(size_t)min(t + 2, t1 - 1) * 64];
+  // the tiles of the range, two per iteration with two loads in flight (the batch has a zero
+  // tail of 4 KiB: loads past the last tile stay inside it)
+  const uint8_t* base = A.data + 16u * lane;
+  auto body = [&](uint4 v, uint32_t t) __attribute__((always_inline)) {
     const uint32_t pos = t * kFTile + 16u * lane;
     const uint32_t rb = L.tile(v, cy, g);
     // run events: one atomic per chunk (the leader lane of each chunk in the tile)
     const uint64_t bu = __ballot(rb & 1u), bd = __ballot(rb & 2u);
-    if (bu | bd) {
+    if (__builtin_expect(bu | bd, 0)) {
       const uint32_t c = pos / A.chunk;
       const bool lead = lane == 0 || pos - c * A.chunk < 16u;
       const uint64_t ld = __ballot(lead);
@@ -760,7 +764,7 @@ __global__ void __launch_bounds__(kFThreads) k1f_kernel(DevK1F d, K1FArgs A) {
     const uint32_t un = k1f_or3(g[0], g[1], g[2]) | g[3];
     const uint32_t bun = un & 0xFFFFu;
     const uint64_t hb = __ballot(bun != 0);
-    if (hb) {
+    if (__builtin_expect(hb != 0, 0)) {
       const uint32_t n = (uint32_t)__popcll(hb);
       if (bun) {
         const uint32_t slot = __builtin_amdgcn_mbcnt_hi((uint32_t)(hb >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)hb, 0u));
@@ -772,7 +776,18 @@ __global__ void __launch_bounds__(kFThreads) k1f_kernel(DevK1F d, K1FArgs A) {
       nlisted += n;
       if (qn >= 64) drain(64);
     }
+  };
+  uint4 p0 = *(const uint4*)(base + t0 * kFTile), p1 = *(const uint4*)(base + (t0 + 1) * kFTile);
+  uint32_t t = t0;
+  for (; t + 1 < t1; t += 2) {
+    const uint4 v0 = p0;
+    p0 = *(const uint4*)(base + (t + 2) * kFTile);
+    body(v0, t);
+    const uint4 v1 = p1;
+    p1 = *(const uint4*)(base + (t + 3) * kFTile);
+    body(v1, t + 1);
   }
+  if (t < t1) body(p0, t);
   if (qn) drain(qn);
   if (A.stats) {
     if (lane == 0) atomicAdd(&A.stats[0], nlisted);
