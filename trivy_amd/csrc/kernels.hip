@@ -156,7 +156,7 @@ __device__ __forceinline__ uint32_t file_of(const uint32_t* __restrict__ cf, con
 // One kernel replaces the per-batch runtime fills: it zeroes the lane's output and counter
 // buffers and the zero tail after the batch (K1's chains read past its end), and builds the
 // coarse file map.  (Each fill was a runtime kernel of its own, ~7 us each, 16 per batch.)
-constexpr int kPrepZeros = 10;
+constexpr int kPrepZeros = 16;
 struct PrepArgs {
   const uint64_t* off;
   uint32_t nfiles;
@@ -2850,11 +2850,15 @@ int enqueue_scan(DeviceRules* r, LaneState* l, const ScanInput& in, HostOut* out
     PA.nfiles = F;
     PA.ncf = F ? ncf : 0;
     PA.cf = l->cf;
+    bool too_many = false;
     auto zero = [&](void* ptr, uint64_t n) {
-      if (n) {
-        PA.zp[PA.nz] = (uint8_t*)ptr;
-        PA.zn[PA.nz++] = n;
+      if (!n) return;
+      if (PA.nz == (uint32_t)kPrepZeros) {
+        too_many = true;
+        return;
       }
+      PA.zp[PA.nz] = (uint8_t*)ptr;
+      PA.zn[PA.nz++] = n;
     };
     zero(l->data_alloc, kPad);
     if (!one_copy) zero(data + total, tail);
@@ -2867,6 +2871,7 @@ int enqueue_scan(DeviceRules* r, LaneState* l, const ScanInput& in, HostOut* out
     zero(l->cursor, sizeof(uint32_t) * G);
     zero(l->gskip, G);
     zero(l->kind, G);
+    if (too_many) return fail(TSG_ERR_INTERNAL, "more zero fills than the prep kernel takes");
     const uint64_t work = std::max<uint64_t>({PA.ncf, (uint64_t)F * W / 4, one_copy ? 1 : tail / 16, k1f ? nchunks_pad / 4 : 1, 1});
     const int pgrid = (int)std::min<uint64_t>((work + 255) / 256, (uint64_t)r->grid);
     prep_kernel<<<pgrid, 256, 0, st>>>(PA);
