@@ -579,11 +579,12 @@ __global__ void __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(4, 8))
 // event bits (its last byte's chunk) and keyword bit (the file holding that byte, when the
 // literal starts inside it) with atomics.  Run events are ORed per chunk over the lanes of
 // the chunk (ballots) and written with one atomic per chunk; prep zeroes the events.
-constexpr uint32_t kFQueue = 128;                          // ring entries per wave
+constexpr uint32_t kFQueue = 512;                          // ring entries per wave
 constexpr uint32_t kFEntBytes = 256 * 256;                 // 256 entries x 16 replicas x 16 B
 constexpr uint32_t kFQueueOff = kFEntBytes;
 constexpr uint32_t kFImgOff = kFQueueOff + 16 * kFQueue * 8;
-constexpr uint32_t kFLds = kFImgOff + kFImgMax;            // 96 KiB: one 1024-thread block per CU
+constexpr uint32_t kFLds = kFImgOff + kFImgMax;            // 144 KiB: one 1024-thread block per CU
+constexpr uint32_t kFDepth = 4;                            // tiles in flight per wave
 constexpr int kFThreads = 1024;
 
 struct DevK1F {
@@ -741,8 +742,10 @@ __global__ void __launch_bounds__(kFThreads) k1f_kernel(DevK1F d, K1FArgs A) {
     if (t0 > 0) v = *(const uint4*)(A.data + (size_t)(t0 - 1) * kFTile + 16u * lane);
     (void)L.tile(v, cy, g);
   }
-  // the tiles of the range, two per iteration with two loads in flight (the batch has a zero
-  // tail of 4 KiB: loads past the last tile stay inside it)
+  // the tiles of the range, kFDepth loads in flight: memory latency, not the ALUs, bounds a
+  // wave with fewer (2 in flight: 0.436 ms per 0.98 GB, profiles/r05/k1f_b).  Listed words
+  // are verified after every kFDepth tiles (the ring holds what they can list).  The batch
+  // has a zero tail of 8 KiB: loads past the last tile stay inside it.
   const uint8_t* base = A.data + 16u * lane;
   auto body = [&](uint4 v, uint32_t t) __attribute__((always_inline)) {
     const uint32_t pos = t * kFTile + 16u * lane;
@@ -774,20 +777,25 @@ __global__ void __launch_bounds__(kFThreads) k1f_kernel(DevK1F d, K1FArgs A) {
       }
       qn += n;
       nlisted += n;
-      if (qn >= 64) drain(64);
     }
   };
-  uint4 p0 = *(const uint4*)(base + t0 * kFTile), p1 = *(const uint4*)(base + (t0 + 1) * kFTile);
+  uint4 p[kFDepth];
+#pragma unroll
+  for (uint32_t k = 0; k < kFDepth; k++) p[k] = *(const uint4*)(base + (t0 + k) * kFTile);
   uint32_t t = t0;
-  for (; t + 1 < t1; t += 2) {
-    const uint4 v0 = p0;
-    p0 = *(const uint4*)(base + (t + 2) * kFTile);
-    body(v0, t);
-    const uint4 v1 = p1;
-    p1 = *(const uint4*)(base + (t + 3) * kFTile);
-    body(v1, t + 1);
+  for (; t + kFDepth <= t1; t += kFDepth) {
+#pragma unroll
+    for (uint32_t k = 0; k < kFDepth; k++) {
+      const uint4 v = p[k];
+      p[k] = *(const uint4*)(base + (t + kFDepth + k) * kFTile);
+      body(v, t + k);
+    }
+    while (qn >= 64) drain(64);
   }
-  if (t < t1) body(p0, t);
+#pragma unroll
+  for (uint32_t k = 0; k < kFDepth - 1; k++)
+    if (t + k < t1) body(p[k], t + k);
+  while (qn >= 64) drain(64);
   if (qn) drain(qn);
   if (A.stats) {
     if (lane == 0) atomicAdd(&A.stats[0], nlisted);
@@ -2528,7 +2536,7 @@ static int launch_k1f(DeviceRules* r, const K1FArgs& A, hipStream_t st) {
 }
 
 // K1F adaptation (once per device, on the first large batch), the counterpart of adapt_k1:
-// a sampling launch over the first 64 MiB counts the verified arrivals of every literal;
+// a sampling launch over the first 16 MiB counts the verified arrivals of every literal;
 // the most frequent leave the filter until the rest arrive at most once per 4 KiB.  Their
 // keywords become unknown (the host checks them exactly) and their events fire everywhere,
 // so results are unchanged; K1F stops verifying words like "key" that most files hold.
@@ -2538,7 +2546,7 @@ static int adapt_k1f(DeviceRules* r, LaneState* l, const K1FArgs& A0) {
   const uint32_t nrec = r->k1ft.nlit;
   HIP_TRY(hipMemsetAsync(r->d_fhits, 0, sizeof(uint32_t) * std::max<uint32_t>(1, nrec), l->st));
   K1FArgs A = A0;
-  A.ntiles = std::min<uint32_t>(A0.ntiles, (64u << 20) / kFTile);
+  A.ntiles = std::min<uint32_t>(A0.ntiles, (16u << 20) / kFTile);
   A.hits = r->d_fhits;
   A.stats = nullptr;
   int rc;
@@ -2781,8 +2789,8 @@ int enqueue_scan(DeviceRules* r, LaneState* l, const ScanInput& in, HostOut* out
   const bool k1f = r->use_k1f && total + (1u << 16) < (1ull << 32);
   int rc;
   // ---- buffers (grown on demand; growing waits for the device)
-  // (K1F reads whole 1 KiB tiles: at least 4 KiB of zero tail)
-  const size_t tail = std::max<size_t>((size_t)kK1Chains * kK1Seg * C + kPad, 4096);
+  // (K1F reads whole 1 KiB tiles, kFDepth past its last: at least 8 KiB of zero tail)
+  const size_t tail = std::max<size_t>((size_t)kK1Chains * kK1Seg * C + kPad, 8192);
   const size_t meta_bytes = sizeof(uint64_t) * ((size_t)F + 1);
   // one H2D when the slot has room behind the batch: [batch | zero tail | offsets]
   const size_t o_off = ((size_t)total + tail + 15) & ~(size_t)15;
