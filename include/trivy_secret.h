@@ -348,12 +348,15 @@ int tsg_emulate_k1(const tsg_ruleset* rs, const uint8_t* data, const uint64_t* o
 
 /* K1F (the filter-and-verify K1, k1f.hpp) emulated on the CPU with the device's tables and
  * bit logic: keyword bits and chunk events in tsg_emulate_k1's layout; the literals listed
- * in quiet_ids are left out of the filter (the adaptation's hot literals).  stats (or NULL):
- * {flagged word groups, verified literal occurrences, records in the filter, 0}.
- * TSG_ERR_CONFIG when K1F does not apply to the rule set (the automaton K1 runs then). */
+ * in quiet_ids are left out of the filter (the adaptation's hot literals), and with
+ * sample_kib > 0 the filter is priced on the batch's first sample_kib KiB (as the
+ * adaptation prices it on a sample of its batch).  stats (or NULL): {flagged word groups,
+ * verified literal occurrences, records in the filter, 0}.  TSG_ERR_CONFIG when K1F does
+ * not apply to the rule set (the automaton K1 runs then). */
 int tsg_emulate_k1f(const tsg_ruleset* rs, const uint8_t* data, const uint64_t* offsets,
                     uint32_t nfiles, uint32_t chunk, const uint32_t* quiet_ids, uint32_t nquiet,
-                    uint32_t* kw, size_t kw_len, uint32_t* ev, size_t ev_len, uint64_t* stats);
+                    uint32_t sample_kib, uint32_t* kw, size_t kw_len, uint32_t* ev, size_t ev_len,
+                    uint64_t* stats);
 
 /* Plan introspection: per rule group id (-1 host-only), relaxation (-1 exact), max len. */
 int tsg_ruleset_rule_plan(const tsg_ruleset* rs, uint32_t rule, int32_t* group, int32_t* relax,

@@ -100,3 +100,30 @@ def test_k1f_applies_or_declines_per_config():
             continue
         assert np.array_equal(kw, fk)
         assert np.array_equal(ev, fe)
+
+
+def test_sample_priced_filter(builtin):
+    """The adaptation's rebuild prices windows and buckets by their counts in a sample of
+    the data: same bits as k1_reference (for the literals it keeps), and far fewer words
+    listed for verification than the text-model buckets on the same corpus."""
+    lits = builtin.k1_literals()
+    hot = [b"sk", b"lob", b"key", b"live_", b"account", b"sg.", b"linear", b"pk.", b"-----"]
+    quiet = [i for i, (s, _) in enumerate(lits) if s in hot]
+    batch, _ = corpus.make_corpus(8 << 20, seed=13, plants_per_mib=20)
+    kw, ev = builtin.k1_reference(batch, 256)
+    fk0, fe0, st0 = builtin.k1f_emulate(batch, 256, quiet)
+    fk, fe, st = builtin.k1f_emulate(batch, 256, quiet, sample_kib=1024)
+    assert np.array_equal(fk, fk0) and np.array_equal(fe, fe0)
+    assert np.all((fk & ~kw) == 0) and np.all((fe & ~ev) == 0)
+    assert st["arrivals"] == st0["arrivals"]
+    assert st["groups"] * 5 < st0["groups"]
+
+
+@pytest.mark.parametrize("chunk", [16, 256])
+def test_sample_priced_filter_edges(builtin, chunk):
+    """Sample-priced buckets (sampled from the edge batch itself) keep the exact semantics."""
+    batch = corpus.k1_edge_batch(builtin.k1_literals(), 21)
+    kw, ev = builtin.k1_reference(batch, chunk)
+    fk, fe, _ = builtin.k1f_emulate(batch, chunk, sample_kib=64)
+    assert np.array_equal(kw, fk)
+    assert np.array_equal(ev, fe)

@@ -187,7 +187,7 @@ SIGNATURES = [
     ("tsg_ruleset_rule_anchor", C.c_int, [_P, C.c_uint32, C.POINTER(C.c_uint32),
                                           C.POINTER(C.c_int64), C.c_char_p, C.c_size_t]),
     ("tsg_emulate_k1f", C.c_int, [_P, _P, _U64P, C.c_uint32, C.c_uint32, C.POINTER(C.c_uint32),
-                                  C.c_uint32, C.POINTER(C.c_uint32), C.c_size_t,
+                                  C.c_uint32, C.c_uint32, C.POINTER(C.c_uint32), C.c_size_t,
                                   C.POINTER(C.c_uint32), C.c_size_t, C.POINTER(C.c_uint64)]),
     ("tsg_ruleset_k1_literal", C.c_int, [_P, C.c_uint32, C.c_char_p, C.c_uint32,
                                          C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]),

@@ -293,7 +293,8 @@ int tsg_emulate_k1(const tsg_ruleset* rs, const uint8_t* data, const uint64_t* o
 
 int tsg_emulate_k1f(const tsg_ruleset* rs, const uint8_t* data, const uint64_t* offsets,
                     uint32_t nfiles, uint32_t chunk, const uint32_t* quiet_ids, uint32_t nquiet,
-                    uint32_t* kw, size_t kw_len, uint32_t* ev, size_t ev_len, uint64_t* stats) {
+                    uint32_t sample_kib, uint32_t* kw, size_t kw_len, uint32_t* ev, size_t ev_len,
+                    uint64_t* stats) {
   if (!rs || !offsets || chunk == 0 || (nquiet && !quiet_ids)) return fail(TSG_ERR_ARG, "bad argument");
   try {
     const Plan& p = *rs->plan;
@@ -304,7 +305,8 @@ int tsg_emulate_k1f(const tsg_ruleset* rs, const uint8_t* data, const uint64_t* 
     }
     K1FTables t;
     std::string why;
-    if (!k1f_build(p, quiet, &t, &why)) return fail(TSG_ERR_CONFIG, "K1F does not apply: " + why);
+    const size_t smp = std::min<uint64_t>((uint64_t)sample_kib << 10, offsets[nfiles]);
+    if (!k1f_build(p, quiet, &t, &why, smp ? data : nullptr, smp)) return fail(TSG_ERR_CONFIG, "K1F does not apply: " + why);
     std::vector<uint64_t> poff(nfiles + 1, 0);
     BatchView b{data, offsets, nfiles, "", poff.data()};
     std::vector<uint32_t> k, e;

@@ -5,6 +5,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstring>
+#include <memory>
 
 namespace tsg {
 
@@ -84,6 +85,73 @@ double win_cost(const Win& w) {
   return s;
 }
 
+// Exact n-gram counts of a sample of the data (ASCII lowercased): what a bucket's position
+// sets accept there, for the adaptation's rebuild.  A window's "any" positions are always a
+// prefix (a short literal's window ends at its last byte), so a bucket with a of them is
+// priced by the (4 - a)-grams of its other positions.
+struct Grams {
+  // open addressing, u32 key -> count (count 0 = empty)
+  struct Map {
+    std::vector<uint32_t> key, cnt;
+    uint32_t mask = 0;
+    void init(size_t n) {
+      size_t cap = 1024;
+      while (cap < 2 * n) cap *= 2;
+      key.assign(cap, 0);
+      cnt.assign(cap, 0);
+      mask = (uint32_t)cap - 1;
+    }
+    uint32_t slot(uint32_t k) const {
+      uint32_t h = (k * 0x9E3779B1u) & mask;
+      while (cnt[h] && key[h] != k) h = (h + 1) & mask;
+      return h;
+    }
+    void add(uint32_t k) {
+      const uint32_t h = slot(k);
+      key[h] = k;
+      cnt[h]++;
+    }
+    uint32_t get(uint32_t k) const { return cnt[slot(k)]; }
+  };
+  std::vector<uint32_t> h1, h2;  // [256], [65536]
+  Map h3, h4;
+  uint64_t n = 0;
+  Grams(const uint8_t* d, size_t len) : h1(256, 0), h2(65536, 0) {
+    std::vector<uint8_t> l(len);
+    for (size_t i = 0; i < len; i++) l[i] = fold(d[i]);
+    n = len;
+    h3.init(len);
+    h4.init(len);
+    for (size_t i = 0; i < len; i++) {
+      h1[l[i]]++;
+      if (i >= 1) h2[l[i - 1] | l[i] << 8]++;
+      if (i >= 2) h3.add(l[i - 2] | l[i - 1] << 8 | (uint32_t)l[i] << 16);
+      if (i >= 3) h4.add(l[i - 3] | l[i - 2] << 8 | (uint32_t)l[i - 1] << 16 | (uint32_t)l[i] << 24);
+    }
+  }
+  // windows of the sample that the position sets accept; < 0 when there are too many
+  // combinations to enumerate
+  double count(const Win& w) const {
+    int a = 0;
+    while (a < 4 && w.s[a].empty()) a++;
+    if (a == 4) return (double)n;
+    double combos = 1;
+    for (int j = a; j < 4; j++) combos *= (double)w.s[j].size();
+    if (combos > 65536) return -1;
+    double tot = 0;
+    uint32_t idx[4] = {0, 0, 0, 0};
+    for (;;) {
+      uint32_t key = 0;
+      for (int j = a; j < 4; j++) key |= (uint32_t)w.s[j][idx[j]] << (8 * (j - a));
+      tot += a == 0 ? h4.get(key) : a == 1 ? h3.get(key) : a == 2 ? h2[key] : h1[key];
+      int j = 3;
+      while (j >= a && ++idx[j] == w.s[j].size()) idx[j--] = 0;
+      if (j < a) break;
+    }
+    return tot;
+  }
+};
+
 Win lit_window(const std::string& l, int j0) {
   Win w;
   for (int j = 0; j < 4; j++)
@@ -93,7 +161,8 @@ Win lit_window(const std::string& l, int j0) {
 
 }  // namespace
 
-bool k1f_build(const Plan& p, const std::vector<uint8_t>& quiet, K1FTables* t, std::string* why) {
+bool k1f_build(const Plan& p, const std::vector<uint8_t>& quiet, K1FTables* t, std::string* why,
+               const uint8_t* sample, size_t sample_len) {
   auto no = [&](const char* r) {
     if (why) *why = r;
     return false;
@@ -108,7 +177,18 @@ bool k1f_build(const Plan& p, const std::vector<uint8_t>& quiet, K1FTables* t, s
     if (quiet.empty() || !quiet[i]) act.push_back(i);
   }
   if (act.size() > 400) return no("more than 400 literals");
-  // each literal's window: the cheapest under the text model
+  // The price of a bucket: its expected windows per byte under the text model, or with a
+  // sample of the data its exact count there plus a tenth of the model's expectation (which
+  // orders the windows the sample never holds)
+  std::unique_ptr<Grams> grams;
+  if (sample && sample_len >= 4096) grams = std::make_unique<Grams>(sample, sample_len);
+  auto win_price = [&](const Win& w) {
+    const double m = win_cost(w);
+    if (!grams) return m;
+    const double c = grams->count(w);
+    return (c < 0 ? m * (double)grams->n : c) + 0.1 * m * (double)grams->n;
+  };
+  // each literal's window: the cheapest
   t->j0.assign(n, 0);
   t->bucket_of.assign(n, -1);
   std::vector<Win> win(act.size());
@@ -116,9 +196,9 @@ bool k1f_build(const Plan& p, const std::vector<uint8_t>& quiet, K1FTables* t, s
     const std::string& l = p.k1_lits[act[a]];
     const int len = (int)l.size();
     int best = len < 4 ? len - 4 : 0;
-    double bc = win_cost(lit_window(l, best));
+    double bc = win_price(lit_window(l, best));
     for (int j0 = best + 1; len >= 4 && j0 <= len - 4; j0++) {
-      const double c = win_cost(lit_window(l, j0));
+      const double c = win_price(lit_window(l, j0));
       if (c < bc) {
         bc = c;
         best = j0;
@@ -134,13 +214,14 @@ bool k1f_build(const Plan& p, const std::vector<uint8_t>& quiet, K1FTables* t, s
   for (size_t a = 0; a < act.size(); a++) {
     grp.push_back({(int)a});
     gw.push_back(win[a]);
-    gc.push_back(win_cost(win[a]));
+    gc.push_back(win_price(win[a]));
   }
   const size_t G0 = grp.size();
   std::vector<double> pc(G0 * G0, 0);  // merge cost of (x, y), x < y, by slot
-  auto pair_cost = [&](size_t x, size_t y) { return win_cost(win_union(gw[x], gw[y])) - gc[x] - gc[y]; };
-  for (size_t x = 0; x < G0; x++)
+  auto pair_cost = [&](size_t x, size_t y) { return win_price(win_union(gw[x], gw[y])) - gc[x] - gc[y]; };
+  pool_for(G0, 16, [&](size_t x) {
     for (size_t y = x + 1; y < G0; y++) pc[x * G0 + y] = pair_cost(x, y);
+  }, 1);
   std::vector<char> alive(G0, 1);
   size_t ngroups = G0;
   while (ngroups > (size_t)kFBuckets) {
@@ -159,11 +240,12 @@ bool k1f_build(const Plan& p, const std::vector<uint8_t>& quiet, K1FTables* t, s
     }
     grp[bx].insert(grp[bx].end(), grp[by].begin(), grp[by].end());
     gw[bx] = win_union(gw[bx], gw[by]);
-    gc[bx] = win_cost(gw[bx]);
+    gc[bx] = win_price(gw[bx]);
     alive[by] = 0;
     ngroups--;
-    for (size_t z = 0; z < G0; z++)
+    pool_for(G0, 16, [&](size_t z) {
       if (alive[z] && z != bx) pc[std::min(z, bx) * G0 + std::max(z, bx)] = pair_cost(std::min(z, bx), std::max(z, bx));
+    }, 8);
   }
   std::vector<std::vector<int>> buckets;  // literal slots (into act) per bucket
   for (size_t x = 0; x < G0; x++)

@@ -71,9 +71,12 @@ struct K1FTables {
 };
 
 // Builds the filter for the plan's K1 literals (Plan::k1_lits) except those flagged in
-// `quiet` ([n_lit], the adaptation's hot literals; empty = none).  False (with the reason)
-// when K1F does not apply to the plan; the automaton K1 runs then.
-bool k1f_build(const Plan& p, const std::vector<uint8_t>& quiet, K1FTables* t, std::string* why);
+// `quiet` ([n_lit], the adaptation's hot literals; empty = none).  The windows and buckets
+// are priced with a Markov model of source text (bigram.inc), or -- given a sample of the
+// data (the adaptation's first batch) -- by their exact counts in it.  False (with the
+// reason) when K1F does not apply to the plan; the automaton K1 runs then.
+bool k1f_build(const Plan& p, const std::vector<uint8_t>& quiet, K1FTables* t, std::string* why,
+               const uint8_t* sample = nullptr, size_t sample_len = 0);
 
 // CPU emulation of k1f_kernel's algorithm (filter, run flags, verification) with the same
 // tables and bit logic; tests compare it with k1_reference.  hits ([nlit] or null) counts

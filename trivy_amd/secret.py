@@ -304,8 +304,9 @@ class Scanner:
             out.append((buf.raw[:n.value], ev.value))
         return out
 
-    def k1f_emulate(self, batch, chunk, quiet=()):
-        """K1F's algorithm on the CPU (k1f.hpp): (keyword bits, chunk events, stats)."""
+    def k1f_emulate(self, batch, chunk, quiet=(), sample_kib=0):
+        """K1F's algorithm on the CPU (k1f.hpp): (keyword bits, chunk events, stats); with
+        sample_kib the filter is priced on the batch's first sample_kib KiB."""
         import numpy as np
         W = (self.info()["n_keywords"] + 31) // 32
         kw = np.zeros(batch.nfiles * W, dtype=np.uint32)
@@ -316,7 +317,7 @@ class Scanner:
         N.check(N.lib().tsg_emulate_k1f(self.handle, C.c_void_p(batch.data.ctypes.data),
                                         batch.offsets.ctypes.data_as(C.POINTER(C.c_uint64)),
                                         batch.nfiles, chunk, q.ctypes.data_as(u32p), len(quiet),
-                                        kw.ctypes.data_as(u32p), kw.size, ev.ctypes.data_as(u32p),
+                                        sample_kib, kw.ctypes.data_as(u32p), kw.size, ev.ctypes.data_as(u32p),
                                         ev.size, st.ctypes.data_as(C.POINTER(C.c_uint64))))
         return kw.reshape(batch.nfiles, W), ev, {"groups": int(st[0]), "arrivals": int(st[1]),
                                                  "records": int(st[2])}
