@@ -584,7 +584,10 @@ constexpr uint32_t kFEntBytes = 256 * 256;                 // 256 entries x 16 r
 constexpr uint32_t kFQueueOff = kFEntBytes;
 constexpr uint32_t kFImgOff = kFQueueOff + 16 * kFQueue * 8;
 constexpr uint32_t kFLds = kFImgOff + kFImgMax;            // 144 KiB: one 1024-thread block per CU
-constexpr uint32_t kFDepth = 4;                            // tiles in flight per wave
+#ifndef K1F_DEPTH
+#define K1F_DEPTH 4
+#endif
+constexpr uint32_t kFDepth = K1F_DEPTH;                    // tiles in flight per wave
 constexpr int kFThreads = 1024;
 
 struct DevK1F {
@@ -601,7 +604,9 @@ struct K1FArgs {
   uint32_t* kw;
   uint32_t* ev;     // zeroed by prep; ORed into
   uint32_t* hits;   // [nlit] verified arrivals per record (sampling pass) or null
-  uint32_t* stats;  // [2] listed words, verified arrivals
+  uint32_t* stats;  // [3] listed words, verified arrivals, list length (zeroed by prep)
+  uint2* list;      // listed words for k1v_kernel: {word offset, groups | buckets << 16}
+  uint32_t list_cap;
 };
 
 // lane i <- lane i - 1, lane 0 <- old (DPP wave_shr:1, out-of-range source keeps old)
@@ -659,6 +664,18 @@ struct K1FLane {
     return k1f_runs(m, m1, m2);
   }
 
+};
+
+// Verification of listed words (k1v_kernel; inline in k1f_kernel when the list is full):
+// the LDS image of the literal records and the byte entries, either replicated per 16 lanes
+// (k1f_kernel's table: entry of byte b at b << 8 | lane16) or plain (entry at b << 4).
+struct K1FVerify {
+  const DevK1F& d;
+  const K1FArgs& A;
+  const uint8_t* img;  // the verification image in LDS
+  const uint8_t* ent;  // the entries in LDS
+  uint32_t eshift, lane16;
+
   // a verified occurrence of record i starting at s, ending at e (< total)
   __device__ __forceinline__ void report(const K1FLit& L, uint32_t i, uint32_t s, uint32_t e, uint32_t& narr) const {
     narr++;
@@ -672,8 +689,8 @@ struct K1FLane {
 
   // the listed word at P: every window end of the groups in gm, against the buckets in bu
   __device__ void verify(uint32_t P, uint32_t gm, uint32_t bu, uint32_t& narr) const {
-    const uint16_t* bstart = (const uint16_t*)(smem + kFImgOff);
-    const K1FLit* recs = (const K1FLit*)(smem + kFImgOff + kFImgLits);
+    const uint16_t* bstart = (const uint16_t*)img;
+    const K1FLit* recs = (const K1FLit*)(img + kFImgLits);
     const uint32_t* dw = (const uint32_t*)(A.data + P) - 1;  // bytes P-4 .. P+19 (kPad before the batch)
     uint32_t w[6];
 #pragma unroll
@@ -687,7 +704,7 @@ struct K1FLane {
       uint32_t bm = bu;
 #pragma unroll
       for (int j = 0; j < 4; j++)
-        bm &= *(const uint32_t*)(smem + ((((win >> (8 * j)) & 0xFFu) << 8) | lane16) + 4 * j);
+        bm &= *(const uint32_t*)(ent + ((((win >> (8 * j)) & 0xFFu) << eshift) | lane16) + 4 * j);
       bm &= 0xFFFFu;
       if (!bm) continue;
       const uint32_t q = P + k, wl = k1f_lower4(win);
@@ -701,7 +718,7 @@ struct K1FLane {
           bool eq = true;
           for (uint32_t t = 0; t < L.len && eq; t += 4) {
             const uint32_t dv = k1f_lower4(f_load4u(A.data, s + t));
-            const uint32_t lv = *(const uint32_t*)(smem + kFImgOff + L.boff + t);
+            const uint32_t lv = *(const uint32_t*)(img + L.boff + t);
             const uint32_t mk = L.len - t >= 4 ? ~0u : (1u << (8 * (L.len - t))) - 1u;
             eq = ((dv ^ lv) & mk) == 0;
           }
@@ -725,11 +742,22 @@ __global__ void __launch_bounds__(kFThreads) k1f_kernel(DevK1F d, K1FArgs A) {
   const K1FLane L{d, A, smem, lane, (lane & 15u) << 4};
   uint2* ring = (uint2*)(smem + kFQueueOff) + wave * kFQueue;
   uint32_t qh = 0, qn = 0, nlisted = 0, narr = 0;
+  // n (<= 64) listed words from the ring to the global list for k1v_kernel; when the list is
+  // full, their slots are marked void and the wave verifies them itself
   auto drain = [&](uint32_t n) __attribute__((always_inline)) {
     __builtin_amdgcn_wave_barrier();
+    uint32_t at = 0;
+    if (lane == 0) at = atomicAdd(&A.stats[2], n);
+    at = __builtin_amdgcn_readfirstlane(__shfl(at, 0));
     if (lane < n) {
       const uint2 x = ring[(qh + lane) & (kFQueue - 1)];
-      L.verify(x.x, x.y & 0xFu, x.y >> 16, narr);
+      if (at + n <= A.list_cap) {
+        A.list[at + lane] = x;
+      } else {
+        if (at + lane < A.list_cap) A.list[at + lane] = make_uint2(~0u, 0u);
+        const K1FVerify V{d, A, smem + kFImgOff, smem, 8, (lane & 15u) << 4};
+        V.verify(x.x, x.y & 0xFu, x.y >> 16, narr);
+      }
     }
     __builtin_amdgcn_wave_barrier();
     qh = (qh + n) & (kFQueue - 1);
@@ -742,10 +770,10 @@ __global__ void __launch_bounds__(kFThreads) k1f_kernel(DevK1F d, K1FArgs A) {
     if (t0 > 0) v = *(const uint4*)(A.data + (size_t)(t0 - 1) * kFTile + 16u * lane);
     (void)L.tile(v, cy, g);
   }
-  // the tiles of the range, kFDepth loads in flight: memory latency, not the ALUs, bounds a
-  // wave with fewer (2 in flight: 0.436 ms per 0.98 GB, profiles/r05/k1f_b).  Listed words
-  // are verified after every kFDepth tiles (the ring holds what they can list).  The batch
-  // has a zero tail of 8 KiB: loads past the last tile stay inside it.
+  // the tiles of the range, kFDepth loads in flight (memory latency bounds a wave with fewer:
+  // profiles/r05/kv2).  Listed words go to the global list after every kFDepth tiles (the
+  // ring holds what they can list).  The batch has a zero tail of 8 KiB: loads past the last
+  // tile stay inside it.
   const uint8_t* base = A.data + 16u * lane;
   auto body = [&](uint4 v, uint32_t t) __attribute__((always_inline)) {
     const uint32_t pos = t * kFTile + 16u * lane;
@@ -797,10 +825,28 @@ __global__ void __launch_bounds__(kFThreads) k1f_kernel(DevK1F d, K1FArgs A) {
     if (t + k < t1) body(p[k], t + k);
   while (qn >= 64) drain(64);
   if (qn) drain(qn);
-  if (A.stats) {
-    if (lane == 0) atomicAdd(&A.stats[0], nlisted);
-    if (narr) atomicAdd(&A.stats[1], narr);
+  if (lane == 0) atomicAdd(&A.stats[0], nlisted);
+  if (narr) atomicAdd(&A.stats[1], narr);
+}
+
+// The listed words of a K1F launch, verified one per lane (K1FVerify) by a grid of the
+// resident blocks: apart from K1F's streaming loop, where a wave verifying its words would
+// stall its loads behind the verification's dependent reads (profiles/r05/kv2).
+constexpr int kFVThreads = 256;
+__global__ void __launch_bounds__(kFVThreads) k1v_kernel(DevK1F d, K1FArgs A) {
+  __shared__ __attribute__((aligned(16))) uint8_t s_img[kFImgMax];
+  __shared__ __attribute__((aligned(16))) uint4 s_ent[256];
+  for (uint32_t i = threadIdx.x; i < 256u; i += blockDim.x) s_ent[i] = d.ent[i];
+  for (uint32_t i = threadIdx.x; i < d.img_bytes / 16; i += blockDim.x) ((uint4*)s_img)[i] = ((const uint4*)d.img)[i];
+  __syncthreads();
+  const uint32_t n = min(A.stats[2], A.list_cap);
+  const K1FVerify V{d, A, s_img, (const uint8_t*)s_ent, 4, 0};
+  uint32_t narr = 0;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const uint2 x = A.list[i];
+    if (x.x != ~0u) V.verify(x.x, x.y & 0xFu, x.y >> 16, narr);
   }
+  if (narr) atomicAdd(&A.stats[1], narr);
 }
 
 // ---------------------------------------------------------------- K1X
@@ -2345,6 +2391,8 @@ struct LaneState {
   size_t ovf_cap = 0;
   uint8_t* hascand = nullptr;
   size_t hascand_cap = 0;
+  uint2* flist = nullptr;  // K1F's listed words (k1v_kernel)
+  size_t flist_cap = 0;
   uint2* items = nullptr;
   size_t items_cap = 0;
   uint4* entries = nullptr;
@@ -2367,7 +2415,7 @@ struct LaneState {
     if (!d) return;
     (void)hipSetDevice(d->device);
     if (st) (void)hipStreamSynchronize(st);
-    void* bufs[] = {data_alloc, meta, cf, ev_bits, xlist, xcount, evlist, kw, ggate, ovf, hascand,
+    void* bufs[] = {data_alloc, meta, cf, ev_bits, xlist, xcount, evlist, kw, ggate, ovf, hascand, flist,
                     items, entries, dentries, cand, counts, gcount, bcount, cursor, base, kind, gskip, etrace};
     for (void* b : bufs) (void)hipFree(b);
     if (st) (void)hipStreamDestroy(st);
@@ -2532,6 +2580,8 @@ static int launch_k1f(DeviceRules* r, const K1FArgs& A, hipStream_t st) {
   const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>((A.ntiles + wpb - 1) / wpb, (uint64_t)r->cus));
   k1f_kernel<<<grid, kFThreads, 0, st>>>(r->k1f, A);
   HIP_TRY(hipGetLastError());
+  k1v_kernel<<<r->cus * 2, kFVThreads, 0, st>>>(r->k1f, A);
+  HIP_TRY(hipGetLastError());
   return TSG_OK;
 }
 
@@ -2551,7 +2601,7 @@ static int adapt_k1f(DeviceRules* r, LaneState* l, const K1FArgs& A0, const uint
   K1FArgs A = A0;
   A.ntiles = std::min<uint32_t>(A0.ntiles, (16u << 20) / kFTile);
   A.hits = r->d_fhits;
-  A.stats = nullptr;
+  A.stats = l->counts + 24;  // (the batch's own counters stay those of its real launch)
   int rc;
   if ((rc = launch_k1f(r, A, l->st))) return rc;
   std::vector<uint32_t> hits(std::max<uint32_t>(1, nrec));
@@ -2728,7 +2778,8 @@ int lane_create(DeviceRules* d, LaneState** out) {
   // per-batch counters: 0 candidates, 1 event chunks, 2 K2 entries, 3 dense entries, 5-7
   // layout (5 items, 6 entries, 7 groups skipped), 8-11 K2 diagnostics,
   // 12-13 K2 claim cursors (list, dense), 14-15 K1X (records listed, inline verified),
-  // 16-17 K1F (words listed, literal occurrences verified)
+  // 16-18 K1F (words listed, literal occurrences verified, list length), 24-26 the same of
+  // the adaptation's sampling launch
   HIP_TRY(hipMalloc((void**)&l->counts, sizeof(uint32_t) * kCounts));
   HIP_TRY(hipMalloc((void**)&l->gcount, sizeof(uint32_t) * G));
   HIP_TRY(hipMalloc((void**)&l->bcount, sizeof(uint32_t) * G * (size_t)d->grid));
@@ -2829,6 +2880,9 @@ int enqueue_scan(DeviceRules* r, LaneState* l, const ScanInput& in, HostOut* out
   if ((rc = ensure(&l->ggate, &l->ggate_cap, (size_t)F * r->GW + 1))) return rc;
   if ((rc = ensure(&l->ovf, &l->ovf_cap, (size_t)F + 1))) return rc;
   if ((rc = ensure(&l->hascand, &l->hascand_cap, (size_t)F + 1))) return rc;
+  // K1F's list of words to verify: 1 M entries, or one per KiB of a larger batch (the
+  // adapted filter lists ~0.03 per KiB; past the capacity K1F verifies inline)
+  if (r->use_k1f && (rc = ensure(&l->flist, &l->flist_cap, std::max<size_t>(1u << 20, (size_t)(total >> 10))))) return rc;
   // item capacity: twice the batch's chunks (the builtin rules list ~11 % of them); over
   // it, groups are skipped (kGroupSkip) and resolved on the host, never dropped
   const uint64_t items_cap = std::max<uint64_t>(2 * nchunks, 1u << 16);
@@ -2905,7 +2959,8 @@ int enqueue_scan(DeviceRules* r, LaneState* l, const ScanInput& in, HostOut* out
   const uint64_t adapt_bytes = r->adapt_mib == 0xFFFFFFFFu ? ~0ull : (uint64_t)(r->adapt_mib ? r->adapt_mib : 16) << 20;
   if (k1f) {
     K1FArgs A{data, l->off, l->cf, (uint32_t)total, C, F, (uint32_t)((total + kFTile - 1) / kFTile),
-              l->kw, l->ev_bits, nullptr, l->counts + 16};
+              l->kw, l->ev_bits, nullptr, l->counts + 16, l->flist, (uint32_t)std::min<size_t>(l->flist_cap, 0xFFFFFFFFu)};
+    if (knobs().k1f_list_cap.load() > 0) A.list_cap = (uint32_t)std::min<int64_t>(A.list_cap, knobs().k1f_list_cap.load());
     if (!r->adapted && total >= adapt_bytes && (rc = adapt_k1f(r, l, A, in.data))) return rc;
     if (total && (rc = launch_k1f(r, A, st))) return rc;
   } else if (!r->adapted && k1_items >= 64 && total >= adapt_bytes) {
