@@ -97,6 +97,32 @@ def cpu_model():
     return "unknown"
 
 
+def cpu_share():
+    """The CPUs this process may use: the affinity mask, the cgroup's CPU quota (cpu.max) and
+    the harness's thread budget (OMP_NUM_THREADS; 16 per GPU on the GPU box, where nproc
+    counts the whole machine).  Returns (threads, details)."""
+    det = {"nproc": os.cpu_count()}
+    n = os.cpu_count() or 1
+    try:
+        det["affinity"] = len(os.sched_getaffinity(0))
+        n = min(n, det["affinity"])
+    except (AttributeError, OSError):
+        pass
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            det["cgroup_quota_cpus"] = round(int(q) / int(per), 2)
+            n = min(n, max(1, int(int(q) / int(per))))
+    except (OSError, ValueError):
+        pass
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    if omp.isdigit() and int(omp) > 0:
+        det["omp_num_threads"] = int(omp)
+        n = min(n, int(omp))
+    det["threads_used"] = n
+    return n, det
+
+
 def _sub_batch(batch, max_bytes):
     from trivy_amd.secret import Batch
     nf = 0
@@ -122,8 +148,9 @@ def cpu_baselines(sc, batch, max_bytes, nthreads):
     dt = time.perf_counter() - t0
     exact_bytes = _raw(out)
     model = cpu_model()
+    _, share = cpu_share()
     exact = {"value": round(nb / dt / 1e9, 4), "unit": "GB/s", "cores": nthreads, "kind": "port",
-             "cpu": model,
+             "cpu": model, "cpu_share": share,
              "sample": "first %d files (%.0f MB) of the same corpus; exact CPU path of "
                        "libtrivy_secret.so (tsg_scan_cpu_batch: per-rule bytes.ToLower keyword "
                        "gate + Go-semantics regexp, scanner.go:341-416 restated), %.1f s"
@@ -568,7 +595,7 @@ def main():
                       "files_with_findings_per_step": sum(r.step_findings[0][0] for r in runs),
                       "steps_checked": len(runs[0].step_findings)}
     if rank == 0 and not args.no_cpu_baseline:
-        nt = args.host_threads or 16
+        nt = args.host_threads or cpu_share()[0]
         exact, opt, sub, exact_bytes = cpu_baselines(sc, batch0, args.cpu_mib << 20, nt)
         # (a one-GPU figure: reported at N=1; at N>1 the sample only checks the device)
         line["cpu_baseline"], line["cpu_optimised"] = (exact, opt) if ngpus == 1 else (None, None)
@@ -677,7 +704,7 @@ def main_e2e(args):
         summ0, raw0 = step(check=True)
     out = C.c_void_p()
     t0 = time.perf_counter()
-    N.check(L.tsg_scan_cpu_batch(sc.handle, *ref.batch.ptrs(), args.host_threads or 16, C.byref(out)))
+    N.check(L.tsg_scan_cpu_batch(sc.handle, *ref.batch.ptrs(), args.host_threads or cpu_share()[0], C.byref(out)))
     cpu_s = time.perf_counter() - t0
     if raw0 != _raw(out):
         raise SystemExit("bench --e2e: device results differ from the exact CPU path")
@@ -718,7 +745,8 @@ def main_e2e(args):
                             "scan_ms": round((c - b) * 1e3, 2),
                             "scan_GBps_of_scanned": round(scanned / (c - b) / 1e9, 3)},
             "cpu_baseline": {"value": round(scanned / cpu_s / 1e9, 4), "unit": "GB/s of scanned bytes",
-                             "cores": args.host_threads or 16, "kind": "port",
+                             "cores": args.host_threads or cpu_share()[0], "kind": "port",
+                             "cpu_share": cpu_share()[1],
                              "sample": "the whole packed input; exact CPU path (tsg_scan_cpu_batch)"},
             "gen_s": round(gen_s, 2),
             "checks": {"step1_eq_exact_cpu": True, "findings_per_step": summ0[1],
