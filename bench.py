@@ -584,7 +584,14 @@ def main():
                      "rule_compile_s": round(compile_s, 2)},
     }
     if args.rehearse_shared_gpu:
-        line["rehearsal"] = "ranks share GPUs (--rehearse-shared-gpu): not a measurement"
+        # ranks share GPUs: the line cannot claim more GPUs than it used, nor a multi-GPU rate
+        distinct = min(world, _visible_gpus()) if not args.emulate else 1
+        line["rehearsal"] = {"note": "ranks share GPUs (--rehearse-shared-gpu): not a measurement",
+                             "ranks": world, "distinct_gpus": distinct}
+        line["n_gpus"] = distinct
+        line["value"] = None
+        line["vs_baseline"] = None
+        line["roofline"]["aggregate"] = None
     log("timed %d steps: %.3f s" % (args.steps, dt))
     # every step of every device must have produced the same findings as its warmup steps
     # (the timed loop reads every result)

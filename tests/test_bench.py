@@ -82,3 +82,49 @@ def test_e2e_fs_configs4_mix_emulated():
     assert "with a text head" in line["data"] and line["config"]["findings"] > 0
     # the dropped half is read (input bytes) but not scanned
     assert line["config"]["scanned_bytes"] < 0.9 * line["config"]["input_bytes"]
+
+
+def test_eight_devices_one_process_emulated():
+    """N = 8 in one process, as a single trivy process binds a node (tsg_multi over 8
+    emulated devices; image.go:210-234's per-layer goroutines and gather): every device gets
+    its share, its own slots and lanes at the run's depth, and the resolver pool sized for
+    eight devices; the sample check and the per-step findings check pass."""
+    line = _line(_run(["--gpus", "8", "--emulate", "--gb", "0.004", "--batch-mib", "1", "--steps", "2",
+                       "--warmup", "1", "--depth", "4", "--cpu-mib", "1"], timeout=600))
+    assert line["n_gpus"] == 8
+    assert line["config"]["devices"] == list(range(8))
+    per = line["kernels"]["per_device"]
+    assert [p["device"] for p in per] == list(range(8)) and all(p["batches"] > 0 for p in per)
+    assert line["config"]["job_bytes"] == 8 * line["config"]["bytes_per_gpu"]
+    assert line["roofline"]["aggregate"]["gpus"] == 8
+    assert line["checks"]["sample_device_eq_exact_cpu"] is True
+
+
+def test_torchrun_eight_ranks_emulated():
+    """The driver's N = 8 form on the CPU: torchrun, eight ranks over gloo, one emulated
+    device each; barrier + max-over-ranks timing, rank 0's line alone."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "8",
+           "--master-addr", "127.0.0.1", "--master-port", "29641", os.path.join(ROOT, "bench.py"),
+           "--gpus", "8", "--emulate", "--no-cpu-baseline", "--gb", "0.004", "--batch-mib", "1",
+           "--steps", "2", "--warmup", "1"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [x for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 8 and "torchrun" in line["config"]["parallelism"]
+    assert line["config"]["job_bytes"] == 8 * line["config"]["bytes_per_gpu"]
+    assert line["roofline"]["aggregate"]["gpus"] == 8
+
+
+def test_rehearsal_line_claims_no_more_gpus_than_used():
+    """--rehearse-shared-gpu (ranks sharing GPUs): the line reports the distinct GPUs it used
+    and no throughput value or aggregate roofline, so it cannot read as a multi-GPU run."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", "29651", os.path.join(ROOT, "bench.py"),
+           "--gpus", "2", "--emulate", "--rehearse-shared-gpu", "--no-cpu-baseline"] + SMALL
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=400, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][0])
+    assert line["n_gpus"] == 1 and line["value"] is None
+    assert line["rehearsal"]["ranks"] == 2 and line["roofline"]["aggregate"] is None
