@@ -311,8 +311,6 @@ const char* tsg_last_error(void);
  *                     after its adaptation (tsg_scan_batch_emulated)
  *   "k1_automaton"    "1": contexts created next run K1 as the LDS automaton instead of the
  *                     filter-and-verify K1F (k1f.hpp)
- *   "k1f_list_cap"    entries of K1F's list of words to verify (default 1 M or one per KiB;
- *                     past it K1F verifies inline)
  * Returns TSG_ERR_ARG for an unknown name. */
 int tsg_test_knob(const char* name, const char* value);
 

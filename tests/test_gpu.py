@@ -134,24 +134,6 @@ def test_k1f_batch_sizes(builtin, size):
         assert np.array_equal(kw, rkw) and np.array_equal(ev, rev)
 
 
-@pytest.mark.parametrize("cap", [1, 64, 100])
-def test_k1f_list_overflow_verifies_inline(builtin, cap, knob):
-    """K1F's list of words to verify held to `cap` entries (the "k1f_list_cap" knob): past it
-    the waves verify their words inline; keyword bits and events stay == k1_reference."""
-    import numpy as np
-    knob("k1f_list_cap", cap)
-    batch, _ = corpus.make_corpus(1 << 20, seed=50 + cap, plants_per_mib=300)
-    ctx = S.GpuContext(builtin, 0, chunk_bytes=256, adapt_mib=0xFFFFFFFF)
-    ctx.upload(batch)
-    ctx.kernels()
-    kw, ev = ctx.k1_output(256)
-    st = ctx.stats()
-    ctx.close()
-    rkw, rev = builtin.k1_reference(batch, 256)
-    assert np.array_equal(kw, rkw) and np.array_equal(ev, rev)
-    assert st["k1f_listed"] > cap
-
-
 def test_k1_adaptation_exact(builtin):
     """Frequent literals dropped from K1 after sampling: same findings as the exact CPU path."""
     batch, _ = corpus.make_corpus(8 << 20, seed=31, plants_per_mib=40)

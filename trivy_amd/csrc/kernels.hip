@@ -579,10 +579,10 @@ __global__ void __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(4, 8))
 // event bits (its last byte's chunk) and keyword bit (the file holding that byte, when the
 // literal starts inside it) with atomics.  Run events are ORed per chunk over the lanes of
 // the chunk (ballots) and written with one atomic per chunk; prep zeroes the events.
-constexpr uint32_t kFQueue = 512;                          // ring entries per wave
+constexpr uint32_t kFQueue = 128;                          // ring entries (32 B) per wave
 constexpr uint32_t kFEntBytes = 256 * 256;                 // 256 entries x 16 replicas x 16 B
 constexpr uint32_t kFQueueOff = kFEntBytes;
-constexpr uint32_t kFImgOff = kFQueueOff + 16 * kFQueue * 8;
+constexpr uint32_t kFImgOff = kFQueueOff + 16 * kFQueue * 32;
 constexpr uint32_t kFLds = kFImgOff + kFImgMax;            // 144 KiB: one 1024-thread block per CU
 #ifndef K1F_DEPTH
 #define K1F_DEPTH 4
@@ -604,9 +604,7 @@ struct K1FArgs {
   uint32_t* kw;
   uint32_t* ev;     // zeroed by prep; ORed into
   uint32_t* hits;   // [nlit] verified arrivals per record (sampling pass) or null
-  uint32_t* stats;  // [3] listed words, verified arrivals, list length (zeroed by prep)
-  uint2* list;      // listed words for k1v_kernel: {word offset, groups | buckets << 16}
-  uint32_t list_cap;
+  uint32_t* stats;  // [2] listed words, verified arrivals (zeroed by prep)
 };
 
 // lane i <- lane i - 1, lane 0 <- old (DPP wave_shr:1, out-of-range source keeps old)
@@ -666,7 +664,7 @@ struct K1FLane {
 
 };
 
-// Verification of listed words (k1v_kernel; inline in k1f_kernel when the list is full):
+// Verification of listed words (k1f_kernel drains its ring 64 words at a time):
 // the LDS image of the literal records and the byte entries, either replicated per 16 lanes
 // (k1f_kernel's table: entry of byte b at b << 8 | lane16) or plain (entry at b << 4).
 struct K1FVerify {
@@ -687,14 +685,12 @@ struct K1FVerify {
     }
   }
 
-  // the listed word at P: every window end of the groups in gm, against the buckets in bu
-  __device__ void verify(uint32_t P, uint32_t gm, uint32_t bu, uint32_t& narr) const {
+  // The listed word at P with its bytes P-4 .. P+15 as captured at listing (w[0..4]): every
+  // window end of the groups in gm, against the buckets in bu.  Only a window that equals a
+  // literal's reads the batch again, for the part of the literal outside the captured bytes.
+  __device__ void verify(uint32_t P, uint32_t gm, uint32_t bu, const uint32_t (&w)[6], uint32_t& narr) const {
     const uint16_t* bstart = (const uint16_t*)img;
     const K1FLit* recs = (const K1FLit*)(img + kFImgLits);
-    const uint32_t* dw = (const uint32_t*)(A.data + P) - 1;  // bytes P-4 .. P+19 (kPad before the batch)
-    uint32_t w[6];
-#pragma unroll
-    for (int i = 0; i < 6; i++) w[i] = dw[i];
     for (uint32_t k = 0; k < 16; k++) {
       if (!((gm >> (k >> 2)) & 1)) continue;
       const uint32_t o = k + 1;  // window bytes P+k-3 .. P+k = offsets o .. o+3 of w
@@ -717,7 +713,16 @@ struct K1FVerify {
           if (e >= A.total) continue;
           bool eq = true;
           for (uint32_t t = 0; t < L.len && eq; t += 4) {
-            const uint32_t dv = k1f_lower4(f_load4u(A.data, s + t));
+            const uint32_t a = s + t, o2 = a + 4 - P;  // captured: offsets o2 .. o2+3 of w
+            uint32_t raw;
+            if (a + 4 <= P + 16 && a + 4 >= P) {
+              const uint32_t lo2 = o2 < 4 ? w[0] : o2 < 8 ? w[1] : o2 < 12 ? w[2] : o2 < 16 ? w[3] : w[4];
+              const uint32_t hi2 = o2 < 4 ? w[1] : o2 < 8 ? w[2] : o2 < 12 ? w[3] : o2 < 16 ? w[4] : w[5];
+              raw = __builtin_amdgcn_alignbyte(hi2, lo2, o2 & 3u);
+            } else {
+              raw = f_load4u(A.data, a);
+            }
+            const uint32_t dv = k1f_lower4(raw);
             const uint32_t lv = *(const uint32_t*)(img + L.boff + t);
             const uint32_t mk = L.len - t >= 4 ? ~0u : (1u << (8 * (L.len - t))) - 1u;
             eq = ((dv ^ lv) & mk) == 0;
@@ -740,40 +745,35 @@ __global__ void __launch_bounds__(kFThreads) k1f_kernel(DevK1F d, K1FArgs A) {
   const uint32_t t0 = (uint32_t)((uint64_t)gw * A.ntiles / nw), t1 = (uint32_t)((uint64_t)(gw + 1) * A.ntiles / nw);
   if (t0 >= t1) return;  // (no block barrier below)
   const K1FLane L{d, A, smem, lane, (lane & 15u) << 4};
-  uint2* ring = (uint2*)(smem + kFQueueOff) + wave * kFQueue;
+  uint4* ring = (uint4*)(smem + kFQueueOff) + 2 * wave * kFQueue;  // 2 x uint4 per entry
   uint32_t qh = 0, qn = 0, nlisted = 0, narr = 0;
-  // n (<= 64) listed words from the ring to the global list for k1v_kernel; when the list is
-  // full, their slots are marked void and the wave verifies them itself
+  // n (<= 64) listed words verified, one per lane, from their captured bytes
   auto drain = [&](uint32_t n) __attribute__((always_inline)) {
     __builtin_amdgcn_wave_barrier();
-    uint32_t at = 0;
-    if (lane == 0) at = atomicAdd(&A.stats[2], n);
-    at = __builtin_amdgcn_readfirstlane(__shfl(at, 0));
     if (lane < n) {
-      const uint2 x = ring[(qh + lane) & (kFQueue - 1)];
-      if (at + n <= A.list_cap) {
-        A.list[at + lane] = x;
-      } else {
-        if (at + lane < A.list_cap) A.list[at + lane] = make_uint2(~0u, 0u);
-        const K1FVerify V{d, A, smem + kFImgOff, smem, 8, (lane & 15u) << 4};
-        V.verify(x.x, x.y & 0xFu, x.y >> 16, narr);
-      }
+      const uint32_t i = (qh + lane) & (kFQueue - 1);
+      const uint4 x = ring[2 * i], y = ring[2 * i + 1];
+      const uint32_t w[6] = {x.z, x.w, y.x, y.y, y.z, 0u};
+      const K1FVerify V{d, A, smem + kFImgOff, smem, 8, (lane & 15u) << 4};
+      V.verify(x.x, x.y & 0xFu, x.y >> 16, w, narr);
     }
     __builtin_amdgcn_wave_barrier();
     qh = (qh + n) & (kFQueue - 1);
     qn -= n;
   };
   FCarry cy{0, 0, 0, 0, 0};  // (the warm-up tile's own inputs do not reach its outputs)
-  uint32_t g[4];
+  uint32_t g[4], vw = 0;     // vw: the previous tile's last dword per lane (captured bytes)
   {  // warm-up: the tile before t0 (zero bytes before the batch) gives the carries
     uint4 v = make_uint4(0, 0, 0, 0);
     if (t0 > 0) v = *(const uint4*)(A.data + (size_t)(t0 - 1) * kFTile + 16u * lane);
     (void)L.tile(v, cy, g);
+    vw = v.w;
   }
   // the tiles of the range, kFDepth loads in flight (memory latency bounds a wave with fewer:
-  // profiles/r05/kv2).  Listed words go to the global list after every kFDepth tiles (the
-  // ring holds what they can list).  The batch has a zero tail of 8 KiB: loads past the last
-  // tile stay inside it.
+  // profiles/r05/kv2).  A listed word enters the ring with its 20 bytes (the 4 before it
+  // from the previous lane), so its verification reads LDS, not the batch; 64 listed words
+  // are verified together.  The batch has a zero tail of 8 KiB: loads past the last tile
+  // stay inside it.
   const uint8_t* base = A.data + 16u * lane;
   auto body = [&](uint4 v, uint32_t t) __attribute__((always_inline)) {
     const uint32_t pos = t * kFTile + 16u * lane;
@@ -797,15 +797,20 @@ __global__ void __launch_bounds__(kFThreads) k1f_kernel(DevK1F d, K1FArgs A) {
     const uint64_t hb = __ballot(bun != 0);
     if (__builtin_expect(hb != 0, 0)) {
       const uint32_t n = (uint32_t)__popcll(hb);
+      const uint32_t wprev = f_prev(v.w, vw);  // bytes pos-4 .. pos-1 (all lanes: DPP)
       if (bun) {
         const uint32_t slot = __builtin_amdgcn_mbcnt_hi((uint32_t)(hb >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)hb, 0u));
         const uint32_t gm = ((g[0] & 0xFFFFu) ? 1u : 0u) | ((g[1] & 0xFFFFu) ? 2u : 0u) | ((g[2] & 0xFFFFu) ? 4u : 0u) |
                             ((g[3] & 0xFFFFu) ? 8u : 0u);
-        ring[(qh + qn + slot) & (kFQueue - 1)] = make_uint2(pos, gm | bun << 16);
+        const uint32_t i = (qh + qn + slot) & (kFQueue - 1);
+        ring[2 * i] = make_uint4(pos, gm | bun << 16, wprev, v.x);
+        ring[2 * i + 1] = make_uint4(v.y, v.z, v.w, 0u);
       }
       qn += n;
       nlisted += n;
+      if (qn >= 64) drain(64);
     }
+    vw = v.w;
   };
   uint4 p[kFDepth];
 #pragma unroll
@@ -818,34 +823,12 @@ __global__ void __launch_bounds__(kFThreads) k1f_kernel(DevK1F d, K1FArgs A) {
       p[k] = *(const uint4*)(base + (t + kFDepth + k) * kFTile);
       body(v, t + k);
     }
-    while (qn >= 64) drain(64);
   }
 #pragma unroll
   for (uint32_t k = 0; k < kFDepth - 1; k++)
     if (t + k < t1) body(p[k], t + k);
-  while (qn >= 64) drain(64);
   if (qn) drain(qn);
   if (lane == 0) atomicAdd(&A.stats[0], nlisted);
-  if (narr) atomicAdd(&A.stats[1], narr);
-}
-
-// The listed words of a K1F launch, verified one per lane (K1FVerify) by a grid of the
-// resident blocks: apart from K1F's streaming loop, where a wave verifying its words would
-// stall its loads behind the verification's dependent reads (profiles/r05/kv2).
-constexpr int kFVThreads = 256;
-__global__ void __launch_bounds__(kFVThreads) k1v_kernel(DevK1F d, K1FArgs A) {
-  __shared__ __attribute__((aligned(16))) uint8_t s_img[kFImgMax];
-  __shared__ __attribute__((aligned(16))) uint4 s_ent[256];
-  for (uint32_t i = threadIdx.x; i < 256u; i += blockDim.x) s_ent[i] = d.ent[i];
-  for (uint32_t i = threadIdx.x; i < d.img_bytes / 16; i += blockDim.x) ((uint4*)s_img)[i] = ((const uint4*)d.img)[i];
-  __syncthreads();
-  const uint32_t n = min(A.stats[2], A.list_cap);
-  const K1FVerify V{d, A, s_img, (const uint8_t*)s_ent, 4, 0};
-  uint32_t narr = 0;
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-    const uint2 x = A.list[i];
-    if (x.x != ~0u) V.verify(x.x, x.y & 0xFu, x.y >> 16, narr);
-  }
   if (narr) atomicAdd(&A.stats[1], narr);
 }
 
@@ -2391,8 +2374,6 @@ struct LaneState {
   size_t ovf_cap = 0;
   uint8_t* hascand = nullptr;
   size_t hascand_cap = 0;
-  uint2* flist = nullptr;  // K1F's listed words (k1v_kernel)
-  size_t flist_cap = 0;
   uint2* items = nullptr;
   size_t items_cap = 0;
   uint4* entries = nullptr;
@@ -2415,7 +2396,7 @@ struct LaneState {
     if (!d) return;
     (void)hipSetDevice(d->device);
     if (st) (void)hipStreamSynchronize(st);
-    void* bufs[] = {data_alloc, meta, cf, ev_bits, xlist, xcount, evlist, kw, ggate, ovf, hascand, flist,
+    void* bufs[] = {data_alloc, meta, cf, ev_bits, xlist, xcount, evlist, kw, ggate, ovf, hascand,
                     items, entries, dentries, cand, counts, gcount, bcount, cursor, base, kind, gskip, etrace};
     for (void* b : bufs) (void)hipFree(b);
     if (st) (void)hipStreamDestroy(st);
@@ -2579,8 +2560,6 @@ static int launch_k1f(DeviceRules* r, const K1FArgs& A, hipStream_t st) {
   const uint32_t wpb = kFThreads / 64;
   const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>((A.ntiles + wpb - 1) / wpb, (uint64_t)r->cus));
   k1f_kernel<<<grid, kFThreads, 0, st>>>(r->k1f, A);
-  HIP_TRY(hipGetLastError());
-  k1v_kernel<<<r->cus * 2, kFVThreads, 0, st>>>(r->k1f, A);
   HIP_TRY(hipGetLastError());
   return TSG_OK;
 }
@@ -2778,8 +2757,8 @@ int lane_create(DeviceRules* d, LaneState** out) {
   // per-batch counters: 0 candidates, 1 event chunks, 2 K2 entries, 3 dense entries, 5-7
   // layout (5 items, 6 entries, 7 groups skipped), 8-11 K2 diagnostics,
   // 12-13 K2 claim cursors (list, dense), 14-15 K1X (records listed, inline verified),
-  // 16-18 K1F (words listed, literal occurrences verified, list length), 24-26 the same of
-  // the adaptation's sampling launch
+  // 16-17 K1F (words listed, literal occurrences verified), 24-25 the same of the
+  // adaptation's sampling launch
   HIP_TRY(hipMalloc((void**)&l->counts, sizeof(uint32_t) * kCounts));
   HIP_TRY(hipMalloc((void**)&l->gcount, sizeof(uint32_t) * G));
   HIP_TRY(hipMalloc((void**)&l->bcount, sizeof(uint32_t) * G * (size_t)d->grid));
@@ -2880,9 +2859,6 @@ int enqueue_scan(DeviceRules* r, LaneState* l, const ScanInput& in, HostOut* out
   if ((rc = ensure(&l->ggate, &l->ggate_cap, (size_t)F * r->GW + 1))) return rc;
   if ((rc = ensure(&l->ovf, &l->ovf_cap, (size_t)F + 1))) return rc;
   if ((rc = ensure(&l->hascand, &l->hascand_cap, (size_t)F + 1))) return rc;
-  // K1F's list of words to verify: 1 M entries, or one per KiB of a larger batch (the
-  // adapted filter lists ~0.03 per KiB; past the capacity K1F verifies inline)
-  if (r->use_k1f && (rc = ensure(&l->flist, &l->flist_cap, std::max<size_t>(1u << 20, (size_t)(total >> 10))))) return rc;
   // item capacity: twice the batch's chunks (the builtin rules list ~11 % of them); over
   // it, groups are skipped (kGroupSkip) and resolved on the host, never dropped
   const uint64_t items_cap = std::max<uint64_t>(2 * nchunks, 1u << 16);
@@ -2959,8 +2935,7 @@ int enqueue_scan(DeviceRules* r, LaneState* l, const ScanInput& in, HostOut* out
   const uint64_t adapt_bytes = r->adapt_mib == 0xFFFFFFFFu ? ~0ull : (uint64_t)(r->adapt_mib ? r->adapt_mib : 16) << 20;
   if (k1f) {
     K1FArgs A{data, l->off, l->cf, (uint32_t)total, C, F, (uint32_t)((total + kFTile - 1) / kFTile),
-              l->kw, l->ev_bits, nullptr, l->counts + 16, l->flist, (uint32_t)std::min<size_t>(l->flist_cap, 0xFFFFFFFFu)};
-    if (knobs().k1f_list_cap.load() > 0) A.list_cap = (uint32_t)std::min<int64_t>(A.list_cap, knobs().k1f_list_cap.load());
+              l->kw, l->ev_bits, nullptr, l->counts + 16};
     if (!r->adapted && total >= adapt_bytes && (rc = adapt_k1f(r, l, A, in.data))) return rc;
     if (total && (rc = launch_k1f(r, A, st))) return rc;
   } else if (!r->adapted && k1_items >= 64 && total >= adapt_bytes) {

@@ -36,7 +36,6 @@ extern "C" int tsg_test_knob(const char* name, const char* value) {
   else if (!strcmp(name, "no_k1x")) k.no_k1x = x;
   else if (!strcmp(name, "emu_wordrec")) k.emu_wordrec = x;
   else if (!strcmp(name, "k1_automaton")) k.k1_automaton = x;
-  else if (!strcmp(name, "k1f_list_cap")) k.k1f_list_cap = x;
   else if (!strcmp(name, "x_step")) {
     if (x != 0 && x != 1 && x != 2 && x != 4) return fail(TSG_ERR_ARG, "x_step must be 0, 1, 2 or 4");
     k.x_step = x;
