@@ -582,13 +582,16 @@ __global__ void __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(4, 8))
 constexpr uint32_t kFQueue = 128;                          // ring entries (32 B) per wave
 constexpr uint32_t kFEntBytes = 256 * 256;                 // 256 entries x 16 replicas x 16 B
 constexpr uint32_t kFQueueOff = kFEntBytes;
-constexpr uint32_t kFImgOff = kFQueueOff + 16 * kFQueue * 32;
-constexpr uint32_t kFLds = kFImgOff + kFImgMax;            // 144 KiB: one 1024-thread block per CU
+#ifndef K1F_THREADS
+#define K1F_THREADS 1024
+#endif
+constexpr int kFThreads = K1F_THREADS;                     // one block per CU
+constexpr uint32_t kFImgOff = kFQueueOff + (kFThreads / 64) * kFQueue * 32;
+constexpr uint32_t kFLds = kFImgOff + kFImgMax;            // 144 KiB at 1024 threads
 #ifndef K1F_DEPTH
 #define K1F_DEPTH 4
 #endif
 constexpr uint32_t kFDepth = K1F_DEPTH;                    // tiles in flight per wave
-constexpr int kFThreads = 1024;
 
 struct DevK1F {
   const uint4* ent;    // [256] entries d_0..d_3
@@ -635,24 +638,51 @@ struct K1FLane {
 
   // One tile: the lane's 16 bytes v at batch byte pos.  Returns the run events of the word
   // (kEvRunU / kEvRunD) and the OR of its windows by groups of four (g[i]: ends 4i..4i+3).
+  __device__ __forceinline__ uint4 entry(uint32_t w, int k) const {  // byte k (0..3) of dword w
+    return *(const uint4*)(smem + __builtin_amdgcn_perm(w, lane16, 0x0C0C0000u | ((4u + (uint32_t)k) << 8)));
+  }
+  // One tile: the lane's 16 bytes v.  Returns the run events of the word (kEvRunU /
+  // kEvRunD) and the OR of its windows by groups of four (g[i]: window ends 4i..4i+3).  In
+  // three phases (bytes 13-15, 0-7, 8-12) so that at most 8 entries are live: the registers
+  // left over hold more tiles in flight (kFDepth).
   __device__ __forceinline__ uint32_t tile(uint4 v, FCarry& cy, uint32_t (&g)[4]) const {
-    uint4 e[16];
-#pragma unroll
-    for (int k = 0; k < 16; k++) {
-      const uint32_t w = k < 4 ? v.x : k < 8 ? v.y : k < 12 ? v.z : v.w;
-      e[k] = *(const uint4*)(smem + __builtin_amdgcn_perm(w, lane16, 0x0C0C0000u | ((4u + (uint32_t)(k & 3)) << 8)));
-    }
-    const uint32_t ao = k1f_and3(e[13].x, e[14].y, e[15].z), bo = e[14].x & e[15].y, co = e[15].x;
+    // bytes 13..15: the partial windows lane l+1 needs
+    const uint4 e13 = entry(v.w, 1), e14 = entry(v.w, 2), e15 = entry(v.w, 3);
+    const uint32_t ao = k1f_and3(e13.x, e14.y, e15.z), bo = e14.x & e15.y, co = e15.x;
     const uint32_t ai = f_prev(ao, cy.a), bi = f_prev(bo, cy.b), ci = f_prev(co, cy.c);
     cy.a = ao;
     cy.b = bo;
     cy.c = co;
     uint32_t r[16];
-    r[0] = ai & e[0].w;
-    r[1] = k1f_and3(bi, e[0].z, e[1].w);
-    r[2] = k1f_and3(ci, e[0].y, e[1].z) & e[2].w;
+    __builtin_amdgcn_sched_barrier(0);
+    {  // bytes 0..7
+      uint4 e[8];
 #pragma unroll
-    for (int k = 3; k < 16; k++) r[k] = k1f_and3(e[k - 3].x, e[k - 2].y, e[k - 1].z) & e[k].w;
+      for (int k = 0; k < 8; k++) e[k] = entry(k < 4 ? v.x : v.y, k & 3);
+      r[0] = ai & e[0].w;
+      r[1] = k1f_and3(bi, e[0].z, e[1].w);
+      r[2] = k1f_and3(ci, e[0].y, e[1].z) & e[2].w;
+#pragma unroll
+      for (int k = 3; k < 8; k++) r[k] = k1f_and3(e[k - 3].x, e[k - 2].y, e[k - 1].z) & e[k].w;
+      // partial windows ending at 8, 9, 10
+      r[8] = k1f_and3(e[5].x, e[6].y, e[7].z);
+      r[9] = e[6].x & e[7].y;
+      r[10] = e[7].x;
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    {  // bytes 8..12 (13..15 from above)
+      uint4 e[8];
+#pragma unroll
+      for (int k = 0; k < 5; k++) e[k] = entry(k < 4 ? v.z : v.w, k & 3);
+      e[5] = e13;
+      e[6] = e14;
+      e[7] = e15;
+      r[8] &= e[0].w;
+      r[9] = k1f_and3(r[9], e[0].z, e[1].w);
+      r[10] = k1f_and3(r[10], e[0].y, e[1].z) & e[2].w;
+#pragma unroll
+      for (int k = 3; k < 8; k++) r[8 + k] = k1f_and3(e[k - 3].x, e[k - 2].y, e[k - 1].z) & e[k].w;
+    }
 #pragma unroll
     for (int i = 0; i < 4; i++) g[i] = k1f_or3(r[4 * i], r[4 * i + 1], r[4 * i + 2]) | r[4 * i + 3];
     const uint32_t m = k1f_flags(r[3], r[7], r[11], r[15]);
@@ -661,7 +691,6 @@ struct K1FLane {
     cy.m1 = m1;
     return k1f_runs(m, m1, m2);
   }
-
 };
 
 // Verification of listed words (k1f_kernel drains its ring 64 words at a time):
