@@ -578,7 +578,11 @@ __global__ void __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(4, 8))
 // bucket's literal records (window compare, then the whole literal), and a match sets its
 // event bits (its last byte's chunk) and keyword bit (the file holding that byte, when the
 // literal starts inside it) with atomics.  Run events are ORed per chunk over the lanes of
-// the chunk (ballots) and written with one atomic per chunk; prep zeroes the events.
+// the chunk (ballots) and written with one atomic per chunk; prep zeroes the events.  The
+// block's part of the coarse file map sits in LDS, so a keyword arrival away from file
+// starts sets its bit without a global load, and a literal inside the captured bytes is
+// compared without one: the verification of the last words of the range (which nothing
+// overlaps) costs LDS latency, not HBM round trips under full streaming load.
 constexpr uint32_t kFQueue = 128;                          // ring entries (32 B) per wave
 constexpr uint32_t kFEntBytes = 256 * 256;                 // 256 entries x 16 replicas x 16 B
 constexpr uint32_t kFQueueOff = kFEntBytes;
@@ -587,7 +591,10 @@ constexpr uint32_t kFQueueOff = kFEntBytes;
 #endif
 constexpr int kFThreads = K1F_THREADS;                     // one block per CU
 constexpr uint32_t kFImgOff = kFQueueOff + (kFThreads / 64) * kFQueue * 32;
-constexpr uint32_t kFLds = kFImgOff + kFImgMax;            // 144 KiB at 1024 threads
+constexpr uint32_t kFCfOff = kFImgOff + kFImgMax;
+constexpr uint32_t kFCfMax = 512;                          // coarse file map entries in LDS
+constexpr uint32_t kFStOff = kFCfOff + 4 * kFCfMax;        // block counters (listed, arrivals, waves done)
+constexpr uint32_t kFLds = kFStOff + 16;                   // 146 KiB at 1024 threads
 #ifndef K1F_DEPTH
 #define K1F_DEPTH 4
 #endif
@@ -603,7 +610,7 @@ struct K1FArgs {
   const uint8_t* data;
   const uint64_t* off;
   const uint32_t* cf;  // coarse file map (file_of)
-  uint32_t total, chunk, nfiles, ntiles;
+  uint32_t total, chunk, nfiles, ntiles, ncf;  // ncf: entries of cf
   uint32_t* kw;
   uint32_t* ev;     // zeroed by prep; ORed into
   uint32_t* hits;   // [nlit] verified arrivals per record (sampling pass) or null
@@ -696,12 +703,22 @@ struct K1FLane {
 // Verification of listed words (k1f_kernel drains its ring 64 words at a time):
 // the LDS image of the literal records and the byte entries, either replicated per 16 lanes
 // (k1f_kernel's table: entry of byte b at b << 8 | lane16) or plain (entry at b << 4).
+// bytes o .. o+3 (o <= 19) of the captured bytes w
+__device__ __forceinline__ uint32_t f_wat(const uint32_t (&w)[6], uint32_t o) {
+  const uint32_t i = o >> 2;
+  const uint32_t lo = i == 0 ? w[0] : i == 1 ? w[1] : i == 2 ? w[2] : i == 3 ? w[3] : w[4];
+  const uint32_t hi = i == 0 ? w[1] : i == 1 ? w[2] : i == 2 ? w[3] : i == 3 ? w[4] : w[5];
+  return __builtin_amdgcn_alignbyte(hi, lo, o & 3u);
+}
+
 struct K1FVerify {
   const DevK1F& d;
   const K1FArgs& A;
   const uint8_t* img;  // the verification image in LDS
   const uint8_t* ent;  // the entries in LDS
   uint32_t eshift, lane16;
+  const uint32_t* lcf;  // cf[kc0 .. kc0 + ncl) in LDS
+  uint32_t kc0, ncl;
 
   // a verified occurrence of record i starting at s, ending at e (< total)
   __device__ __forceinline__ void report(const K1FLit& L, uint32_t i, uint32_t s, uint32_t e, uint32_t& narr) const {
@@ -709,8 +726,19 @@ struct K1FVerify {
     if (A.hits) atomicAdd(&A.hits[i], 1u);
     if (L.ev) atomicOr(&A.ev[e / A.chunk], L.ev);
     if (L.kw >= 0) {
-      const uint32_t f = file_of(A.cf, A.off, A.nfiles, e);
-      if (s >= A.off[f]) atomicOr(&A.kw[(size_t)f * d.kw_words + (uint32_t)L.kw / 32], 1u << ((uint32_t)L.kw % 32));
+      // the same file holds the first bytes of the coarse blocks of s and past e's: no file
+      // starts in (s, e], the literal lies inside the file holding e
+      const uint32_t ks = (s >> kCfShift) - kc0, ke = (e >> kCfShift) + 1 - kc0;
+      uint32_t f;
+      bool in;
+      if (ks < ncl && ke < ncl && lcf[ks] == lcf[ke]) {
+        f = lcf[ks];
+        in = true;
+      } else {
+        f = file_of(A.cf, A.off, A.nfiles, e);
+        in = s >= A.off[f];
+      }
+      if (in) atomicOr(&A.kw[(size_t)f * d.kw_words + (uint32_t)L.kw / 32], 1u << ((uint32_t)L.kw % 32));
     }
   }
 
@@ -722,10 +750,7 @@ struct K1FVerify {
     const K1FLit* recs = (const K1FLit*)(img + kFImgLits);
     for (uint32_t k = 0; k < 16; k++) {
       if (!((gm >> (k >> 2)) & 1)) continue;
-      const uint32_t o = k + 1;  // window bytes P+k-3 .. P+k = offsets o .. o+3 of w
-      const uint32_t lo = o < 4 ? w[0] : o < 8 ? w[1] : o < 12 ? w[2] : o < 16 ? w[3] : w[4];
-      const uint32_t hi = o < 4 ? w[1] : o < 8 ? w[2] : o < 12 ? w[3] : o < 16 ? w[4] : w[5];
-      const uint32_t win = __builtin_amdgcn_alignbyte(hi, lo, o & 3u);
+      const uint32_t win = f_wat(w, k + 1);  // window bytes P+k-3 .. P+k
       uint32_t bm = bu;
 #pragma unroll
       for (int j = 0; j < 4; j++)
@@ -741,20 +766,38 @@ struct K1FVerify {
           const uint32_t s = q - L.wend, e = s + L.len - 1;
           if (e >= A.total) continue;
           bool eq = true;
-          for (uint32_t t = 0; t < L.len && eq; t += 4) {
-            const uint32_t a = s + t, o2 = a + 4 - P;  // captured: offsets o2 .. o2+3 of w
-            uint32_t raw;
-            if (a + 4 <= P + 16 && a + 4 >= P) {
-              const uint32_t lo2 = o2 < 4 ? w[0] : o2 < 8 ? w[1] : o2 < 12 ? w[2] : o2 < 16 ? w[3] : w[4];
-              const uint32_t hi2 = o2 < 4 ? w[1] : o2 < 8 ? w[2] : o2 < 12 ? w[3] : o2 < 16 ? w[4] : w[5];
-              raw = __builtin_amdgcn_alignbyte(hi2, lo2, o2 & 3u);
-            } else {
-              raw = f_load4u(A.data, a);
+          if (s + 4 >= P && e < P + 16) {  // inside the captured bytes
+            const uint32_t os = s + 4 - P;
+#pragma unroll
+            for (uint32_t tt = 0; tt < 20; tt += 4) {
+              if (tt < L.len) {
+                const uint32_t dv = k1f_lower4(f_wat(w, os + tt));
+                const uint32_t lv = *(const uint32_t*)(img + L.boff + tt);
+                const uint32_t mk = L.len - tt >= 4 ? ~0u : (1u << (8 * (L.len - tt))) - 1u;
+                eq = eq && ((dv ^ lv) & mk) == 0;
+              }
             }
-            const uint32_t dv = k1f_lower4(raw);
-            const uint32_t lv = *(const uint32_t*)(img + L.boff + t);
-            const uint32_t mk = L.len - t >= 4 ? ~0u : (1u << (8 * (L.len - t))) - 1u;
-            eq = ((dv ^ lv) & mk) == 0;
+            if (eq) report(L, i, s, e, narr);
+            continue;
+          }
+          // the whole literal, 32 bytes per round from aligned dword loads issued together
+          // (one dependent load per dword cost a round trip each: profiles/r05/ab3)
+          const uint32_t* dw = (const uint32_t*)(A.data + (s & ~3u));
+          const uint32_t sh = s & 3u;
+          for (uint32_t t = 0; t < L.len && eq; t += 32) {
+            uint32_t dd[9];
+#pragma unroll
+            for (int u = 0; u < 9; u++) dd[u] = t + 4 * u < L.len + 4 ? dw[t / 4 + u] : 0u;
+#pragma unroll
+            for (int u = 0; u < 8; u++) {
+              const uint32_t tt = t + 4 * u;
+              if (tt < L.len) {
+                const uint32_t dv = k1f_lower4(__builtin_amdgcn_alignbyte(dd[u + 1], dd[u], sh));
+                const uint32_t lv = *(const uint32_t*)(img + L.boff + tt);
+                const uint32_t mk = L.len - tt >= 4 ? ~0u : (1u << (8 * (L.len - tt))) - 1u;
+                eq = eq && ((dv ^ lv) & mk) == 0;
+              }
+            }
           }
           if (eq) report(L, i, s, e, narr);
         }
@@ -768,9 +811,19 @@ __global__ void __launch_bounds__(kFThreads) k1f_kernel(DevK1F d, K1FArgs A) {
   for (uint32_t i = threadIdx.x; i < 256u * 16u; i += blockDim.x) ((uint4*)smem)[i] = d.ent[i >> 4];
   for (uint32_t i = threadIdx.x; i < d.img_bytes / 16; i += blockDim.x)
     ((uint4*)(smem + kFImgOff))[i] = ((const uint4*)d.img)[i];
-  __syncthreads();
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6, wpb = blockDim.x >> 6;
   const uint32_t gw = blockIdx.x * wpb + wave, nw = gridDim.x * wpb;
+  // the coarse file map around the block's bytes (literals reach 4 KiB either side)
+  const uint64_t bb0 = (uint64_t)blockIdx.x * wpb * A.ntiles / nw * kFTile;
+  const uint64_t bb1 = (uint64_t)(blockIdx.x + 1) * wpb * A.ntiles / nw * kFTile;
+  const uint32_t kc0 = (uint32_t)((bb0 > 4096 ? bb0 - 4096 : 0) >> kCfShift);
+  const uint64_t kc1 = min<uint64_t>(A.ncf, ((bb1 + 4096) >> kCfShift) + 2);
+  const uint32_t ncl = kc1 > kc0 ? (uint32_t)min<uint64_t>(kc1 - kc0, kFCfMax) : 0u;
+  uint32_t* lcf = (uint32_t*)(smem + kFCfOff);
+  for (uint32_t i = threadIdx.x; i < ncl; i += blockDim.x) lcf[i] = A.cf[kc0 + i];
+  uint32_t* bst = (uint32_t*)(smem + kFStOff);
+  if (threadIdx.x < 3) bst[threadIdx.x] = 0;
+  __syncthreads();
   const uint32_t t0 = (uint32_t)((uint64_t)gw * A.ntiles / nw), t1 = (uint32_t)((uint64_t)(gw + 1) * A.ntiles / nw);
   if (t0 >= t1) return;  // (no block barrier below)
   const K1FLane L{d, A, smem, lane, (lane & 15u) << 4};
@@ -783,7 +836,7 @@ __global__ void __launch_bounds__(kFThreads) k1f_kernel(DevK1F d, K1FArgs A) {
       const uint32_t i = (qh + lane) & (kFQueue - 1);
       const uint4 x = ring[2 * i], y = ring[2 * i + 1];
       const uint32_t w[6] = {x.z, x.w, y.x, y.y, y.z, 0u};
-      const K1FVerify V{d, A, smem + kFImgOff, smem, 8, (lane & 15u) << 4};
+      const K1FVerify V{d, A, smem + kFImgOff, smem, 8, (lane & 15u) << 4, lcf, kc0, ncl};
       V.verify(x.x, x.y & 0xFu, x.y >> 16, w, narr);
     }
     __builtin_amdgcn_wave_barrier();
@@ -846,6 +899,10 @@ __global__ void __launch_bounds__(kFThreads) k1f_kernel(DevK1F d, K1FArgs A) {
   for (uint32_t k = 0; k < kFDepth; k++) p[k] = *(const uint4*)(base + (t0 + k) * kFTile);
   uint32_t t = t0;
   for (; t + kFDepth <= t1; t += kFDepth) {
+    // the words listed so far are verified before the range's last tiles, while their loads
+    // are in flight: a verification at the very end (a literal read back, a file lookup)
+    // would extend the kernel by its latency (profiles/r05/ab3)
+    if (t + 2 * kFDepth > t1 && qn) drain(qn);
 #pragma unroll
     for (uint32_t k = 0; k < kFDepth; k++) {
       const uint4 v = p[k];
@@ -857,8 +914,26 @@ __global__ void __launch_bounds__(kFThreads) k1f_kernel(DevK1F d, K1FArgs A) {
   for (uint32_t k = 0; k < kFDepth - 1; k++)
     if (t + k < t1) body(p[k], t + k);
   if (qn) drain(qn);
-  if (lane == 0) atomicAdd(&A.stats[0], nlisted);
-  if (narr) atomicAdd(&A.stats[1], narr);
+  // the counters: per wave, per block in LDS, one global atomic per block (a same-address
+  // atomic from every lane or wave at the end of the kernel serialised into its tail:
+  // 20 us per launch, profiles/r05/ab6)
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) narr += __shfl_xor(narr, o);
+  if (lane == 0) {
+    uint32_t nact = 0;  // the block's waves with tiles
+    for (uint32_t w = 0; w < wpb; w++) {
+      const uint32_t g0 = blockIdx.x * wpb + w;
+      nact += (uint64_t)g0 * A.ntiles / nw < (uint64_t)(g0 + 1) * A.ntiles / nw ? 1u : 0u;
+    }
+    atomicAdd(&bst[0], nlisted);
+    atomicAdd(&bst[1], narr);
+    __threadfence_block();
+    if (atomicAdd(&bst[2], 1u) == nact - 1) {
+      const uint32_t bl = atomicAdd(&bst[0], 0u), ba = atomicAdd(&bst[1], 0u);
+      if (bl) atomicAdd(&A.stats[0], bl);
+      if (ba) atomicAdd(&A.stats[1], ba);
+    }
+  }
 }
 
 // ---------------------------------------------------------------- K1X
@@ -2963,7 +3038,7 @@ int enqueue_scan(DeviceRules* r, LaneState* l, const ScanInput& in, HostOut* out
   const uint64_t k1_items = (nchunks + k1_item_chunks - 1) / k1_item_chunks;
   const uint64_t adapt_bytes = r->adapt_mib == 0xFFFFFFFFu ? ~0ull : (uint64_t)(r->adapt_mib ? r->adapt_mib : 16) << 20;
   if (k1f) {
-    K1FArgs A{data, l->off, l->cf, (uint32_t)total, C, F, (uint32_t)((total + kFTile - 1) / kFTile),
+    K1FArgs A{data, l->off, l->cf, (uint32_t)total, C, F, (uint32_t)((total + kFTile - 1) / kFTile), F ? (uint32_t)ncf : 0u,
               l->kw, l->ev_bits, nullptr, l->counts + 16};
     if (!r->adapted && total >= adapt_bytes && (rc = adapt_k1f(r, l, A, in.data))) return rc;
     if (total && (rc = launch_k1f(r, A, st))) return rc;
