@@ -252,6 +252,8 @@ typedef struct tsg_stats {
   /* K1F (the filter-and-verify K1) in the last batch: 16-B words listed with a filter hit,
    * and literal occurrences its verification confirmed */
   uint32_t k1f_listed, k1f_arrivals;
+  /* chunks of the last batch whose K1 event word is not empty (the item passes' units) */
+  uint32_t event_chunks;
 } tsg_stats;
 int tsg_ctx_get_stats(const tsg_ctx* ctx, tsg_stats* out);
 

@@ -47,7 +47,7 @@ def main():
            "k2_items": rows[-1]["k2_items"], "k2_entries": rows[-1]["k2_launches"],
            "candidates": rows[-1]["candidates"], "k1x_records": rows[-1]["k1x_records"],
            "k1x_inline": rows[-1]["k1x_inline"],
-           "k1f_listed": rows[-1]["k1f_listed"], "k1f_arrivals": rows[-1]["k1f_arrivals"],
+           "k1f_listed": rows[-1]["k1f_listed"], "event_chunks": rows[-1]["event_chunks"], "k1f_arrivals": rows[-1]["k1f_arrivals"],
            "k1_hot": rows[-1]["k1_hot_states"],
            "diag": [rows[-1]["k2_tail_bytes"], rows[-1]["k2_tail_max"], rows[-1]["k2_long_tails"]]}
     print(json.dumps(out), flush=True)

@@ -39,9 +39,9 @@ struct HostOut {
                                 // 3 dense entries, 5 items, 6 entries, 7 skipped groups,
                                 // 8-11 K2 diagnostics (TSG_K2_DIAG), 14-15 K1X, 16-17 K1F
   uint32_t files_cap = 0, cand_cap = 0, groups = 0, kw_words = 0;
-  // stage boundaries of the batch on its lane's stream: data H2D | offsets H2D | wait for
-  // the previous batch's kernels | prep | K1 | gates | K2 | outputs; ev[kEvDone] completes
-  // the batch
+  // stage boundaries of the batch on its lane's stream: data H2D | offsets H2D | prep |
+  // wait for the previous batch's kernels | K1 | gates | K2 | outputs; ev[kEvDone]
+  // completes the batch
   hipEvent_t ev[9] = {};
 };
 

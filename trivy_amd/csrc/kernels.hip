@@ -69,6 +69,9 @@ constexpr uint32_t kK1RepBytes = 256 * 32 * 4;
 constexpr int kBlock = 256;
 constexpr int kCounts = 32;  // per-batch device counters (lane_create)
 constexpr int kPad = 256;     // zero bytes before and after the batch in HBM (>= K1 warm-up)
+#ifndef ITEMS_BPC
+#define ITEMS_BPC 8  // item passes: blocks per CU
+#endif
 constexpr int kMaxBack = 16;  // event windows up to this many chunks; larger -> whole file
 
 // ---------------------------------------------------------------- device tables
@@ -633,6 +636,17 @@ __device__ __forceinline__ uint32_t f_load4u(const uint8_t* data, uint32_t a) { 
   return __builtin_amdgcn_alignbyte(p[1], p[0], a & 3u);
 }
 
+// a lane's 16 bytes of a tile (K1F_NT: non-temporal, the batch is read once)
+typedef uint32_t f_u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint4 f_tile_load(const uint8_t* p) {
+#if defined(K1F_NT)
+  const f_u32x4 v = __builtin_nontemporal_load((const f_u32x4*)p);
+  return make_uint4(v.x, v.y, v.z, v.w);
+#else
+  return *(const uint4*)p;
+#endif
+}
+
 struct FCarry {  // the previous tile's per-lane window partials and run flags (f_prev)
   uint32_t a, b, c, m, m1;
 };
@@ -896,7 +910,7 @@ __global__ void __launch_bounds__(kFThreads) k1f_kernel(DevK1F d, K1FArgs A) {
   };
   uint4 p[kFDepth];
 #pragma unroll
-  for (uint32_t k = 0; k < kFDepth; k++) p[k] = *(const uint4*)(base + (t0 + k) * kFTile);
+  for (uint32_t k = 0; k < kFDepth; k++) p[k] = f_tile_load(base + (t0 + k) * kFTile);
   uint32_t t = t0;
   for (; t + kFDepth <= t1; t += kFDepth) {
     // the words listed so far are verified before the range's last tiles, while their loads
@@ -906,7 +920,7 @@ __global__ void __launch_bounds__(kFThreads) k1f_kernel(DevK1F d, K1FArgs A) {
 #pragma unroll
     for (uint32_t k = 0; k < kFDepth; k++) {
       const uint4 v = p[k];
-      p[k] = *(const uint4*)(base + (t + kFDepth + k) * kFTile);
+      p[k] = f_tile_load(base + (t + kFDepth + k) * kFTile);
       body(v, t + k);
     }
   }
@@ -1250,9 +1264,7 @@ struct ItemArgs {
   uint32_t F, G, GW, chunk, maxback;
   uint32_t* count;            // [G]
   uint32_t* bcount;           // [gridDim.x * G] each count block's counts, for the emit pass
-  const uint64_t* base;       // [G] item region of each group (emit pass), null: count pass
   uint32_t* cursor;           // [G]
-  const uint8_t* listed;      // [G] 1 = list group (emit pass)
   uint2* items;
 };
 
@@ -1332,35 +1344,78 @@ __global__ void __launch_bounds__(kBlock) gates_kernel(GateArgs A) {
 // item comes from the first event chunk at or after it, exactly once.  Threads
 // [0, nev) take event chunks, [nev, nev + F) take the files of every-chunk groups.
 // visit(f, g, c_lo, c_hi): items c_lo..c_hi.
+// the group tables gen_items reads per candidate, staged in the item passes' LDS
+static inline size_t item_lds_host(uint32_t G, uint32_t GW) { return 256 * (size_t)GW + 8 * (size_t)G; }
+struct ItemLds {
+  const unsigned long long* gofbit;  // [32 * GW]
+  const uint32_t* gback;             // [G]
+  const uint32_t* gevents;           // [G]
+};
+__device__ __forceinline__ uint32_t item_lds_bytes(uint32_t G, uint32_t GW) { return 256 * GW + 8 * G; }
+// copies the tables to smem (8-aligned); the caller's __syncthreads() publishes them
+__device__ __forceinline__ ItemLds item_lds_load(const ItemArgs& A, uint8_t* smem) {
+  unsigned long long* gofbit = (unsigned long long*)smem;
+  uint32_t* gback = (uint32_t*)(gofbit + 32 * A.GW);
+  uint32_t* gevents = gback + A.G;
+  for (uint32_t i = threadIdx.x; i < 32 * A.GW; i += blockDim.x) gofbit[i] = A.gofbit[i];
+  for (uint32_t i = threadIdx.x; i < A.G; i += blockDim.x) {
+    gback[i] = A.gback[i];
+    gevents[i] = A.gevents[i];
+  }
+  return ItemLds{gofbit, gback, gevents};
+}
+
 template <class V>
-__device__ __forceinline__ void gen_items(const ItemArgs& A, uint64_t t, V visit) {
+__device__ __forceinline__ void gen_items(const ItemArgs& A, const ItemLds& T, uint64_t t, V visit) {
   const uint32_t nev = *A.nev;
   const uint32_t C = A.chunk;
   if (t < nev) {
     const uint64_t e = A.evlist[t];
     const uint32_t evb = A.ev[e] & ~kEvAlways;
     const uint64_t ce = (e + 1) * C;
+    // the event words of the kMaxBack chunks before e, loaded together (a dependent load per
+    // chunk of the back scan cost a round trip each)
+    // (five 16-B loads from the aligned base below e - 16: one wide request per lane each)
+    uint32_t pw[kMaxBack];
+    if (e >= (uint64_t)kMaxBack) {
+      const uint64_t b0 = (e - kMaxBack) & ~3ull;
+      const uint32_t sh = (uint32_t)(e - kMaxBack - b0);  // 0..3
+      uint32_t x[20];
+#pragma unroll
+      for (int j = 0; j < 5; j++) {
+        const uint4 q = *(const uint4*)(A.ev + b0 + 4 * j);
+        x[4 * j] = q.x;
+        x[4 * j + 1] = q.y;
+        x[4 * j + 2] = q.z;
+        x[4 * j + 3] = q.w;
+      }
+#pragma unroll
+      for (int i = 0; i < kMaxBack; i++) {  // ev[e - 1 - i] = x[sh + 15 - i]
+        const int k = kMaxBack - 1 - i;
+        pw[i] = sh == 0 ? x[k] : sh == 1 ? x[k + 1] : sh == 2 ? x[k + 2] : x[k + 3];
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < kMaxBack; i++) pw[i] = e > (uint64_t)i ? A.ev[e - 1 - i] : 0u;
+    }
     for (uint32_t f = file_of(A.cf, A.off, A.F, e * C); f < A.F && A.off[f] < ce; f++) {
       const uint64_t fs = A.off[f], fe = A.off[f + 1];
       if (fe == fs) continue;
       const uint64_t fc0 = fs / C;
       for (uint32_t w = 0; w < A.GW; w++) {
         unsigned long long cand = 0;
-        for (uint32_t bits = evb; bits; bits &= bits - 1) cand |= A.gofbit[__builtin_ctz(bits) * A.GW + w];
-        cand &= A.ggate[(size_t)f * A.GW + w] & ~A.gofbit[31 * A.GW + w];
+        for (uint32_t bits = evb; bits; bits &= bits - 1) cand |= T.gofbit[__builtin_ctz(bits) * A.GW + w];
+        cand &= A.ggate[(size_t)f * A.GW + w] & ~T.gofbit[31 * A.GW + w];
         while (cand) {
           const uint32_t g = w * 64 + __builtin_ctzll(cand);
           cand &= cand - 1;
-          const uint32_t back = A.gback[g];
-          uint64_t lo = e > fc0 + back ? e - back : fc0;
-          for (uint64_t q = e; q > lo;) {
-            q--;
-            if (A.ev[q] & A.gevents[g]) {
-              lo = q + 1;
-              break;
-            }
-          }
-          visit(f, g, lo, e);
+          const uint32_t back = T.gback[g], gev = T.gevents[g];  // back <= kMaxBack here
+          const uint64_t lo0 = e > fc0 + back ? e - back : fc0;
+          const uint32_t lim = (uint32_t)(e - lo0);  // chunks e-1 .. lo0
+          uint32_t m = 0;  // bit i: chunk e-1-i carries one of g's events
+#pragma unroll
+          for (int i = 0; i < kMaxBack; i++) m |= ((pw[i] & gev) != 0 && (uint32_t)i < lim ? 1u : 0u) << i;
+          visit(f, g, m ? e - __builtin_ctz(m) : lo0, e);
         }
       }
     }
@@ -1369,7 +1424,7 @@ __device__ __forceinline__ void gen_items(const ItemArgs& A, uint64_t t, V visit
     const uint64_t fs = A.off[f], fe = A.off[f + 1];
     if (fe == fs) return;
     for (uint32_t w = 0; w < A.GW; w++) {
-      unsigned long long cand = A.ggate[(size_t)f * A.GW + w] & A.gofbit[31 * A.GW + w];
+      unsigned long long cand = A.ggate[(size_t)f * A.GW + w] & T.gofbit[31 * A.GW + w];
       while (cand) {
         const uint32_t g = w * 64 + __builtin_ctzll(cand);
         cand &= cand - 1;
@@ -1384,12 +1439,13 @@ __device__ __forceinline__ void gen_items(const ItemArgs& A, uint64_t t, V visit
 // count pass: items per group (block totals in LDS, one global atomic per group and block)
 __global__ void __launch_bounds__(kBlock) items_count_kernel(ItemArgs A) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  uint32_t* s_count = (uint32_t*)smem;
+  const ItemLds T = item_lds_load(A, smem);
+  uint32_t* s_count = (uint32_t*)(smem + item_lds_bytes(A.G, A.GW));
   for (uint32_t g = threadIdx.x; g < A.G; g += blockDim.x) s_count[g] = 0;
   __syncthreads();
   const uint64_t nt = (uint64_t)*A.nev + A.F, stride = (uint64_t)gridDim.x * blockDim.x;
   for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < nt; t += stride)
-    gen_items(A, t, [&](uint32_t, uint32_t g, uint64_t lo, uint64_t hi) { atomicAdd(&s_count[g], (uint32_t)(hi - lo + 1)); });
+    gen_items(A, T, t, [&](uint32_t, uint32_t g, uint64_t lo, uint64_t hi) { atomicAdd(&s_count[g], (uint32_t)(hi - lo + 1)); });
   __syncthreads();
   for (uint32_t g = threadIdx.x; g < A.G; g += blockDim.x) {
     A.bcount[(size_t)blockIdx.x * A.G + g] = s_count[g];
@@ -1397,47 +1453,24 @@ __global__ void __launch_bounds__(kBlock) items_count_kernel(ItemArgs A) {
   }
 }
 
-// emit pass (same grid as the count pass, so block b generates the items block b counted):
-// the block reserves one range per listed group with a single global atomic, then writes
-// its items into it
-__global__ void __launch_bounds__(kBlock) items_emit_kernel(ItemArgs A) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  uint32_t* s_count = (uint32_t*)smem;
-  uint32_t* s_base = s_count + A.G;
-  const uint64_t nt = (uint64_t)*A.nev + A.F, stride = (uint64_t)gridDim.x * blockDim.x;
-  const uint64_t t0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  for (uint32_t g = threadIdx.x; g < A.G; g += blockDim.x) {
-    const uint32_t n = A.listed[g] == kGroupList ? A.bcount[(size_t)blockIdx.x * A.G + g] : 0;
-    s_base[g] = n ? (uint32_t)A.base[g] + atomicAdd(&A.cursor[g], n) : 0;
-    s_count[g] = 0;
-  }
-  __syncthreads();
-  for (uint64_t t = t0; t < nt; t += stride)
-    gen_items(A, t, [&](uint32_t f, uint32_t g, uint64_t lo, uint64_t hi) {
-      if (A.listed[g] != kGroupList) return;
-      const uint32_t n = (uint32_t)(hi - lo + 1);
-      uint32_t at = s_base[g] + atomicAdd(&s_count[g], n);
-      for (uint64_t c = lo; c <= hi; c++) A.items[at++] = make_uint2(f, (uint32_t)c);
-    });
-}
-
 // ---------------------------------------------------------------- device-side item layout
-// One block decides, from the item counts, how K2 covers each group and writes K2's work
-// list, so the host never reads the counts back:
+// Every block of the emit pass decides, from the item counts, how K2 covers each group (the
+// same decision in every block: the counts are final when the pass starts), so neither the
+// host nor a one-block launch stands between the two item passes:
 //   list   (kGroupList)  its items go to a region of the item array; K2 entries of up to
 //                        kEntryItems items
 //   dense  (kGroupDense) its items cover more than half the batch: K2 entries of
 //                        kEntryChunks consecutive chunks of the whole batch, gated per file
 //   skip   (kGroupSkip)  over the item capacity or the dense budget: K2 does not scan it
 //                        and the host resolves its rules like rules without a GPU program
-// Groups are taken in id order, so the outcome is deterministic.
+// Groups are taken in id order, so the outcome is deterministic.  K2's work list is written
+// by all blocks (a list group's entries by block g mod grid, a dense group's sliced over the
+// grid), the counters and skip flags by block 0.
 struct LayoutArgs {
   const uint32_t* gcount;  // [G]
   uint32_t G;
   uint64_t nchunks, items_cap;
   uint32_t max_dense;
-  uint8_t* kind;      // [G]
-  uint64_t* base;     // [G] first item of a list group
   uint4* entries;     // K2 work list of list groups: {group, first item, n, kGroupList}
   uint32_t* nentries;
   uint4* dentries;    // ... of dense groups: {group, first chunk, n, kGroupDense}
@@ -1446,7 +1479,7 @@ struct LayoutArgs {
   uint32_t* stats;    // [1] items listed, [2] entries, [3] skipped groups
 };
 
-// exclusive prefix sum of v over the block (blockDim.x = kLayoutBlock); returns the total
+// exclusive prefix sum of v over the block; returns the total
 template <class T>
 __device__ T block_exclusive_scan(T v, T* out, T* s_wave) {
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
@@ -1467,14 +1500,14 @@ __device__ T block_exclusive_scan(T v, T* out, T* s_wave) {
   return total;
 }
 
-constexpr int kLayoutBlock = 1024;
 constexpr uint32_t kEntryItems = 2 * kBlock;    // two chains per lane
 constexpr uint32_t kEntryChunks = kStreams * kBlock;
 
-__global__ void __launch_bounds__(kLayoutBlock) layout_kernel(LayoutArgs A) {
-  __shared__ unsigned long long s_wave64[kLayoutBlock / 64];
+// the layout into s_kind / s_gbase ([G] in LDS) and K2's work list (see above)
+__device__ void layout_block(const LayoutArgs& A, uint8_t* s_kind, uint32_t* s_gbase) {
+  __shared__ unsigned long long s_wave64[kBlock / 64];
   __shared__ unsigned long long s_carry[5];  // items, entries, dense groups, skipped groups, dense entries
-  __shared__ uint2 s_dense[kLayoutBlock];  // dense groups of the tile: group, first dense entry
+  __shared__ uint2 s_dense[kBlock];  // dense groups of the tile: group, first dense entry
   __shared__ uint32_t s_ndense;
   const uint32_t ndent_all = (uint32_t)((A.nchunks + kEntryChunks - 1) / kEntryChunks);
   if (threadIdx.x < 5) s_carry[threadIdx.x] = 0;
@@ -1495,7 +1528,7 @@ __global__ void __launch_bounds__(kLayoutBlock) layout_kernel(LayoutArgs A) {
     // items of groups that fit are placed at their prefix position (a skipped group's
     // range stays unused: the regions keep group order)
     const uint64_t nent = list ? (cnt + kEntryItems - 1) / kEntryItems : 0;
-    const uint64_t ndent = dense ? (A.nchunks + kEntryChunks - 1) / kEntryChunks : 0;
+    const uint64_t ndent = dense ? ndent_all : 0;
     unsigned long long epre, dpre2;
     const unsigned long long etot = block_exclusive_scan<unsigned long long>(nent, &epre, s_wave64);
     const unsigned long long dtot2 = block_exclusive_scan<unsigned long long>(ndent, &dpre2, s_wave64);
@@ -1507,11 +1540,11 @@ __global__ void __launch_bounds__(kLayoutBlock) layout_kernel(LayoutArgs A) {
     const uint64_t e0 = s_carry[1] + epre, d0 = s_carry[4] + dpre2;
     const uint8_t k = !cnt ? kGroupNone : list ? kGroupList : dense ? kGroupDense : kGroupSkip;
     if (g < A.G) {
-      A.kind[g] = k;
-      A.gskip[g] = k == kGroupSkip ? 1 : 0;
-      A.base[g] = s_carry[0] + ipre;
+      s_kind[g] = k;
+      s_gbase[g] = (uint32_t)(s_carry[0] + ipre);
+      if (blockIdx.x == 0) A.gskip[g] = k == kGroupSkip ? 1 : 0;
     }
-    if (k == kGroupList)
+    if (k == kGroupList && g % gridDim.x == blockIdx.x)
       for (uint64_t i = 0; i < nent; i++) {
         const uint32_t first = (uint32_t)(i * kEntryItems);
         A.entries[e0 + i] = make_uint4(g, (uint32_t)(s_carry[0] + ipre) + first,
@@ -1519,11 +1552,10 @@ __global__ void __launch_bounds__(kLayoutBlock) layout_kernel(LayoutArgs A) {
       }
     if (k == kGroupDense) s_dense[atomicAdd(&s_ndense, 1u)] = make_uint2(g, (uint32_t)d0);
     __syncthreads();
-    // a dense group's entries (nchunks / kEntryChunks of them: tens of thousands) are
-    // written by the whole block
+    // a dense group's entries (nchunks / kEntryChunks of them: thousands) over the grid
     for (uint32_t t = 0; t < s_ndense; t++) {
       const uint2 dg = s_dense[t];
-      for (uint32_t i = threadIdx.x; i < ndent_all; i += blockDim.x) {
+      for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < ndent_all; i += gridDim.x * blockDim.x) {
         const uint64_t first = (uint64_t)i * kEntryChunks;
         A.dentries[dg.y + i] = make_uint4(dg.x, (uint32_t)first,
                                           (uint32_t)min<uint64_t>(kEntryChunks, A.nchunks - first), kGroupDense);
@@ -1539,13 +1571,41 @@ __global__ void __launch_bounds__(kLayoutBlock) layout_kernel(LayoutArgs A) {
     }
     __syncthreads();
   }
-  if (threadIdx.x == 0) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
     *A.nentries = (uint32_t)s_carry[1];
     *A.ndentries = (uint32_t)s_carry[4];
     A.stats[1] = (uint32_t)min<unsigned long long>(s_carry[0], 0xFFFFFFFFull);
     A.stats[2] = (uint32_t)s_carry[1];
     A.stats[3] = (uint32_t)s_carry[3];
   }
+}
+
+// emit pass (same grid as the count pass, so block b generates the items block b counted):
+// the layout (above), then the block reserves one range per listed group with a single
+// global atomic and writes its items into it
+__global__ void __launch_bounds__(kBlock) items_emit_kernel(ItemArgs A, LayoutArgs LA) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const ItemLds T = item_lds_load(A, smem);  // (published by layout_block's barriers)
+  uint32_t* s_count = (uint32_t*)(smem + item_lds_bytes(A.G, A.GW));
+  uint32_t* s_base = s_count + A.G;
+  uint32_t* s_gbase = s_base + A.G;
+  uint8_t* s_kind = (uint8_t*)(s_gbase + A.G);
+  layout_block(LA, s_kind, s_gbase);
+  const uint64_t nt = (uint64_t)*A.nev + A.F, stride = (uint64_t)gridDim.x * blockDim.x;
+  const uint64_t t0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (uint32_t g = threadIdx.x; g < A.G; g += blockDim.x) {
+    const uint32_t n = s_kind[g] == kGroupList ? A.bcount[(size_t)blockIdx.x * A.G + g] : 0;
+    s_base[g] = n ? s_gbase[g] + atomicAdd(&A.cursor[g], n) : 0;
+    s_count[g] = 0;
+  }
+  __syncthreads();
+  for (uint64_t t = t0; t < nt; t += stride)
+    gen_items(A, T, t, [&](uint32_t f, uint32_t g, uint64_t lo, uint64_t hi) {
+      if (s_kind[g] != kGroupList) return;
+      const uint32_t n = (uint32_t)(hi - lo + 1);
+      uint32_t at = s_base[g] + atomicAdd(&s_count[g], n);
+      for (uint64_t c = lo; c <= hi; c++) A.items[at++] = make_uint2(f, (uint32_t)c);
+    });
 }
 
 // ---------------------------------------------------------------- K2
@@ -2490,8 +2550,6 @@ struct LaneState {
   uint32_t* gcount = nullptr;   // [G]
   uint32_t* bcount = nullptr;   // [grid * G] items_count_kernel's per-block counts
   uint32_t* cursor = nullptr;   // [G]
-  uint64_t* base = nullptr;     // [G]
-  uint8_t* kind = nullptr;      // [G]
   uint8_t* gskip = nullptr;     // [G]
   unsigned long long* etrace = nullptr;  // [entries_cap * kTraceW] K2 entry trace (TSG_K2_TRACE)
   size_t etrace_cap = 0;
@@ -2501,7 +2559,7 @@ struct LaneState {
     (void)hipSetDevice(d->device);
     if (st) (void)hipStreamSynchronize(st);
     void* bufs[] = {data_alloc, meta, cf, ev_bits, xlist, xcount, evlist, kw, ggate, ovf, hascand,
-                    items, entries, dentries, cand, counts, gcount, bcount, cursor, base, kind, gskip, etrace};
+                    items, entries, dentries, cand, counts, gcount, bcount, cursor, gskip, etrace};
     for (void* b : bufs) (void)hipFree(b);
     if (st) (void)hipStreamDestroy(st);
   }
@@ -2796,6 +2854,14 @@ int device_rules_create(int device, const Plan& p, uint32_t chunk, uint32_t ext_
       if (((gp.events >> b) & 1) || back > (uint32_t)kMaxBack) gofbit[b * r->GW + g / 64] |= 1ull << (g % 64);
   }
   r->max_lds = std::max<uint32_t>(r->max_lds, 16);
+  {  // the item passes' LDS: group tables (item_lds_bytes), counts, ranges, bases, kinds
+    const size_t emit_lds = item_lds_host(G, r->GW) + 13 * (size_t)G + 16;
+    if (emit_lds > 160 * 1024) return fail(TSG_ERR_INTERNAL, "too many rule groups for the item passes");
+    if (emit_lds > 64 * 1024) {
+      HIP_TRY(hipFuncSetAttribute((const void*)items_emit_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)emit_lds));
+      HIP_TRY(hipFuncSetAttribute((const void*)items_count_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)emit_lds));
+    }
+  }
   if (r->max_lds > 64 * 1024) {
     HIP_TRY(hipFuncSetAttribute((const void*)k2_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)r->max_lds));
     HIP_TRY(hipFuncSetAttribute((const void*)k2_dense_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -2867,8 +2933,6 @@ int lane_create(DeviceRules* d, LaneState** out) {
   HIP_TRY(hipMalloc((void**)&l->gcount, sizeof(uint32_t) * G));
   HIP_TRY(hipMalloc((void**)&l->bcount, sizeof(uint32_t) * G * (size_t)d->grid));
   HIP_TRY(hipMalloc((void**)&l->cursor, sizeof(uint32_t) * G));
-  HIP_TRY(hipMalloc((void**)&l->base, sizeof(uint64_t) * G));
-  HIP_TRY(hipMalloc((void**)&l->kind, G));
   HIP_TRY(hipMalloc((void**)&l->gskip, G));
   *out = l.release();
   return TSG_OK;
@@ -2954,7 +3018,7 @@ int enqueue_scan(DeviceRules* r, LaneState* l, const ScanInput& in, HostOut* out
   const uint64_t nchunks_pad = (nchunks + k1_item_chunks - 1) / k1_item_chunks * k1_item_chunks + 1;
   const uint64_t ncf = (total >> kCfShift) + 2;
   if ((rc = ensure(&l->cf, &l->cf_cap, (size_t)ncf))) return rc;
-  if ((rc = ensure(&l->ev_bits, &l->ev_cap, (size_t)nchunks_pad))) return rc;
+  if ((rc = ensure(&l->ev_bits, &l->ev_cap, (size_t)nchunks_pad + 4))) return rc;
   // K1X hit records: one per 256 bytes (a lane-word with a hit past that verifies inline)
   if (r->has_k1x && (rc = ensure(&l->xlist, &l->xlist_cap, (size_t)(total / 256 + 65536)))) return rc;
   if (r->has_k1x && (rc = ensure(&l->xcount, &l->xcount_cap, (size_t)std::max(r->cus, 1)))) return rc;
@@ -2992,12 +3056,6 @@ int enqueue_scan(DeviceRules* r, LaneState* l, const ScanInput& in, HostOut* out
     HIP_TRY(hipMemcpyAsync(l->meta, in.off, meta_bytes, hipMemcpyHostToDevice, st));
   }
   HIP_TRY(hipEventRecord(out->ev[2], st));
-  // the kernels of consecutive batches run one after the other (each has the whole chip;
-  // their HIP-event times are the kernels' own), while this lane's H2D above overlapped
-  // the previous batch's kernels on the other lane
-  if (r->kernels_done_valid) HIP_TRY(hipStreamWaitEvent(st, r->kernels_done, 0));
-  HIP_TRY(hipEventRecord(out->ev[3], st));
-
   // ---- prep: zero fills and the coarse file map, one kernel
   {
     PrepArgs PA{};
@@ -3025,13 +3083,18 @@ int enqueue_scan(DeviceRules* r, LaneState* l, const ScanInput& in, HostOut* out
     zero(l->gcount, sizeof(uint32_t) * G);
     zero(l->cursor, sizeof(uint32_t) * G);
     zero(l->gskip, G);
-    zero(l->kind, G);
     if (too_many) return fail(TSG_ERR_INTERNAL, "more zero fills than the prep kernel takes");
     const uint64_t work = std::max<uint64_t>({PA.ncf, (uint64_t)F * W / 4, one_copy ? 1 : tail / 16, k1f ? nchunks_pad / 4 : 1, 1});
     const int pgrid = (int)std::min<uint64_t>((work + 255) / 256, (uint64_t)r->grid);
     prep_kernel<<<pgrid, 256, 0, st>>>(PA);
     HIP_TRY(hipGetLastError());
   }
+  // the kernels of consecutive batches run one after the other (each has the whole chip;
+  // their HIP-event times are the kernels' own), while this lane's H2D and prep above
+  // overlapped the previous batch's kernels on the other lane (prep touches this lane's
+  // buffers only: off the critical path, 17 us per batch with its event)
+  HIP_TRY(hipEventRecord(out->ev[3], st));
+  if (r->kernels_done_valid) HIP_TRY(hipStreamWaitEvent(st, r->kernels_done, 0));
   HIP_TRY(hipEventRecord(out->ev[4], st));
 
   // ---- K1
@@ -3082,10 +3145,8 @@ int enqueue_scan(DeviceRules* r, LaneState* l, const ScanInput& in, HostOut* out
   IA.count = l->gcount;
   IA.bcount = l->bcount;
   IA.cursor = l->cursor;
-  IA.listed = l->kind;
   IA.evlist = l->evlist;
   IA.nev = l->counts + 1;
-  IA.base = l->base;
   IA.items = l->items;
   const bool work = F && G && nchunks;
   if (work) {
@@ -3093,14 +3154,14 @@ int enqueue_scan(DeviceRules* r, LaneState* l, const ScanInput& in, HostOut* out
     GateArgs GA{l->ev_bits, nchunks, l->evlist, l->counts + 1, cgrid, l->kw, F, W, r->GW, r->d_kwg, r->d_galw, l->ggate};
     gates_kernel<<<cgrid + (F + kBlock - 1) / kBlock, kBlock, 0, st>>>(GA);
     HIP_TRY(hipGetLastError());
-    const int igrid = r->grid;  // both items passes (bcount holds grid x G)
-    hipLaunchKernelGGL(items_count_kernel, dim3(igrid), dim3(kBlock), G * sizeof(uint32_t) + 16, st, IA);
+    // both items passes (bcount holds grid x G); ITEMS_BPC blocks per CU
+    const int igrid = std::min(r->grid, r->cus * ITEMS_BPC);
+    const size_t ilds = item_lds_host(G, r->GW);
+    hipLaunchKernelGGL(items_count_kernel, dim3(igrid), dim3(kBlock), ilds + G * sizeof(uint32_t) + 16, st, IA);
     HIP_TRY(hipGetLastError());
-    LayoutArgs LA{l->gcount, G, nchunks, items_cap, max_dense, l->kind, l->base, l->entries, l->counts + 2,
+    LayoutArgs LA{l->gcount, G, nchunks, items_cap, max_dense, l->entries, l->counts + 2,
                   l->dentries, l->counts + 3, l->gskip, l->counts + 4};
-    hipLaunchKernelGGL(layout_kernel, dim3(1), dim3(kLayoutBlock), 0, st, LA);
-    HIP_TRY(hipGetLastError());
-    hipLaunchKernelGGL(items_emit_kernel, dim3(igrid), dim3(kBlock), 2 * G * sizeof(uint32_t) + 16, st, IA);
+    hipLaunchKernelGGL(items_emit_kernel, dim3(igrid), dim3(kBlock), ilds + 3 * G * sizeof(uint32_t) + G + 16, st, IA, LA);
     HIP_TRY(hipGetLastError());
   }
   HIP_TRY(hipEventRecord(out->ev[6], st));
@@ -3189,8 +3250,8 @@ int batch_times(const HostOut* o, ScanTimes* t) {
   for (int k = 0; k < kEvDone; k++) HIP_TRY(hipEventElapsedTime(&x[k], o->ev[k], o->ev[k + 1]));
   t->h2d = x[0];
   t->meta = x[1];
-  t->wait = x[2];
-  t->prep = x[3];
+  t->prep = x[2];  // (prep runs before the wait on the other lane's kernels)
+  t->wait = x[3];
   t->k1 = x[4];
   t->gates = x[5];
   t->k2 = x[6];
