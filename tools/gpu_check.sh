@@ -14,4 +14,11 @@ for v in default "$@"; do
   timeout -k 10 240 python -u tools/kab.py 1024 7 > $out/kab_$v.json 2> $out/kab_$v.err || { echo "fail $v"; tail $out/kab_$v.err; exit 2; }
   echo $v $(python -c "import json; d=json.load(open('$out/kab_$v.json')); print(d['k1_ms'], d['k1_GBps'], d['gate_ms'], d['k2_ms'], d['dev_GBps'], d['k1f_listed'], d['k1f_arrivals'])")
 done
+if [ -n "$KAB_RULES" ]; then
+  for r in $KAB_RULES; do
+    unset TSG_LIB_VARIANT
+    timeout -k 10 240 python -u tools/kab.py 1024 5 --rules $r > $out/kab_default_$r.json 2> $out/kab_$r.err || { echo "fail $r"; tail $out/kab_$r.err; exit 3; }
+    echo $r $(python -c "import json; d=json.load(open('$out/kab_default_$r.json')); print(d['k1_ms'], d['gate_ms'], d['k2_ms'], d['dev_GBps'])")
+  done
+fi
 echo done

@@ -88,6 +88,15 @@ def report(out):
     rep["us_per_item"] = {k: round(float(np.percentile(dur / np.maximum(n, 1), p)), 3)
                           for k, p in (("p50", 50), ("p90", 90), ("max", 100))}
     rep["busy_us_per_xcc"] = {int(x): round(float(dur[xcc == x].sum()), 1) for x in np.unique(xcc)}
+    if "--phases" in sys.argv:  # K2_TRACE_PHASE builds: thread 0's stamps in words 4..7
+        ph = t[:, 4:8].astype(np.int64)
+        ok = (ph > 0).all(axis=1)
+        marks = np.column_stack([st, ph, en])[ok]
+        names = ["claim..staged", "staged..setup", "setup..loop", "loop..tails", "tails..next claim"]
+        rep["phases_us_p50"] = {nm: round(float(np.median(us(marks[:, i + 1] - marks[:, i]))), 2)
+                                for i, nm in enumerate(names)}
+        rep["phases_us_mean"] = {nm: round(float(np.mean(us(marks[:, i + 1] - marks[:, i]))), 2)
+                                 for i, nm in enumerate(names)}
     print(json.dumps(rep, indent=1))
     return rep
 

@@ -155,6 +155,30 @@ __device__ __forceinline__ uint32_t file_of(const uint32_t* __restrict__ cf, con
   return bsearch_file(off, cf[k], min(nfiles, cf[k + 1] + 1), p);
 }
 
+// nbytes of src (16-B aligned, readable to the next multiple of 16: upload_vec pads) into
+// LDS at dst (16-B aligned), eight 16-B loads in flight per thread: a block restages a DFA
+// of up to 48 KB in two memory round trips.  (One dword per thread and iteration, each load
+// waited on before the next, cost ~50 us per restage: most of a K2 list entry's time,
+// profiles/r05/k2t1.)
+__device__ __forceinline__ void stage16(uint8_t* dst, const void* src, uint32_t nbytes) {
+  const uint32_t n = (nbytes + 15) / 16;
+  const uint4* s = (const uint4*)src;
+  uint4* d = (uint4*)dst;
+  for (uint32_t i0 = threadIdx.x; i0 < n; i0 += 8 * blockDim.x) {
+    uint4 v[8];
+#pragma unroll
+    for (uint32_t k = 0; k < 8; k++) {
+      const uint32_t i = i0 + k * blockDim.x;
+      v[k] = i < n ? s[i] : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < 8; k++) {
+      const uint32_t i = i0 + k * blockDim.x;
+      if (i < n) d[i] = v[k];
+    }
+  }
+}
+
 // ---------------------------------------------------------------- per-batch preparation
 // One kernel replaces the per-batch runtime fills: it zeroes the lane's output and counter
 // buffers and the zero tail after the batch (K1's chains read past its end), and builds the
@@ -413,7 +437,7 @@ struct K1Lane {
       s0[i] = c[i].s;
       top[i] = 0;
     }
-#pragma unroll(K1_UNROLL)
+#pragma unroll K1_UNROLL
     for (int k = 0; k < 16; k++)
 #pragma unroll
       for (int i = 0; i < NS; i++) {
@@ -822,9 +846,24 @@ struct K1FVerify {
 
 __global__ void __launch_bounds__(kFThreads) k1f_kernel(DevK1F d, K1FArgs A) {
   __shared__ __attribute__((aligned(16))) uint8_t smem[kFLds];
-  for (uint32_t i = threadIdx.x; i < 256u * 16u; i += blockDim.x) ((uint4*)smem)[i] = d.ent[i >> 4];
-  for (uint32_t i = threadIdx.x; i < d.img_bytes / 16; i += blockDim.x)
-    ((uint4*)(smem + kFImgOff))[i] = ((const uint4*)d.img)[i];
+  {  // the entries (replicated) and the image, every load issued before the stores
+    constexpr uint32_t kRep = 256u * 16u / kFThreads, kImg = kFImgMax / 16 / kFThreads;
+    uint4 e[kRep], m[kImg];
+#pragma unroll
+    for (uint32_t k = 0; k < kRep; k++) e[k] = d.ent[(threadIdx.x + k * kFThreads) >> 4];
+#pragma unroll
+    for (uint32_t k = 0; k < kImg; k++) {
+      const uint32_t i = threadIdx.x + k * kFThreads;
+      m[k] = i < d.img_bytes / 16 ? ((const uint4*)d.img)[i] : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < kRep; k++) ((uint4*)smem)[threadIdx.x + k * kFThreads] = e[k];
+#pragma unroll
+    for (uint32_t k = 0; k < kImg; k++) {
+      const uint32_t i = threadIdx.x + k * kFThreads;
+      if (i < d.img_bytes / 16) ((uint4*)(smem + kFImgOff))[i] = m[k];
+    }
+  }
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6, wpb = blockDim.x >> 6;
   const uint32_t gw = blockIdx.x * wpb + wave, nw = gridDim.x * wpb;
   // the coarse file map around the block's bytes (literals reach 4 KiB either side)
@@ -1098,9 +1137,9 @@ __device__ __forceinline__ uint32_t k1x_hits(const uint32_t* s_bm, const uint32_
 // atomics); a record past the slice is verified inline.  A.count[block] = records kept.
 template <int STEP>
 __global__ void __launch_bounds__(kK1XBlock) k1x_kernel(DevK1X x, K1XArgs A) {
-  extern __shared__ uint32_t s_bm[];  // the filter, then the block's record counter
+  extern __shared__ __attribute__((aligned(16))) uint32_t s_bm[];  // the filter, then the block's record counter
   uint32_t* s_n = s_bm + kXDwords;
-  for (uint32_t i = threadIdx.x; i < kXDwords; i += blockDim.x) s_bm[i] = x.bitmap[i];
+  stage16((uint8_t*)s_bm, x.bitmap, kXDwords * 4);
   if (threadIdx.x == 0) *s_n = 0;
   __syncthreads();
   const uint32_t slice = A.cap / gridDim.x;
@@ -1190,7 +1229,7 @@ __global__ void __launch_bounds__(kXVerifyBlock) k1x_verify_kernel(DevK1X x, K1X
   if (n == 0) return;
   DevK1X y = x;
   if constexpr (LDS) {
-    for (uint32_t i = threadIdx.x; i < x.img_bytes / 16; i += blockDim.x) ((uint4*)x_img)[i] = ((const uint4*)x.img)[i];
+    stage16(x_img, x.img, x.img_bytes / 16 * 16);
     __syncthreads();
     auto rebase = [&](auto* p) { return (decltype(p))(x_img + ((const uint8_t*)p - x.img)); };
     y.slots = rebase(x.slots);
@@ -1644,6 +1683,12 @@ __shared__ unsigned long long* s_ectr;
 #else
 #define K2_CTR(k, op, v) ((void)0)
 #endif
+#ifdef K2_TRACE_PHASE  // measurement builds: wall-clock stamps of thread 0 in words 4..7
+__shared__ unsigned long long* s_tph;
+#define K2_PHASE(k) (s_tph && threadIdx.x == 0 ? (void)(s_tph[k] = wall_clock64()) : (void)0)
+#else
+#define K2_PHASE(k) ((void)0)
+#endif
 
 // Candidate emission, wave-aggregated: the lanes that reach an accept together reserve
 // their records with ONE atomic (ballot, popcount prefix, broadcast of the base).  A record
@@ -1905,33 +1950,27 @@ struct Lane {
 };
 
 __device__ __forceinline__ void stage_dfa(const DevDFA& d, uint8_t* smem) {
-  uint16_t* s_tab = (uint16_t*)smem;
-  const uint32_t* src = (const uint32_t*)d.tab;
-  uint32_t* dst = (uint32_t*)s_tab;
-  for (uint32_t i = threadIdx.x; i < (d.ns * d.nc + 1) / 2; i += blockDim.x) dst[i] = src[i];
-  uint8_t* s_cls = smem + d.o_cls;
-  for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) s_cls[i] = d.cls[i];
-  uint8_t* s_dead = smem + d.o_dead;
-  for (uint32_t i = threadIdx.x; i < d.ns; i += blockDim.x) s_dead[i] = d.dead[i];
+  stage16(smem, d.tab, (d.ns * d.nc + 1) / 2 * 4);
+  stage16(smem + d.o_cls, d.cls, 256);
+  stage16(smem + d.o_dead, d.dead, d.ns);
   if (d.state_acc) {
-    uint16_t* s_accs = (uint16_t*)(smem + d.o_accs);
-    uint64_t* s_masks = (uint64_t*)(smem + d.o_masks);
-    for (uint32_t i = threadIdx.x; i < d.ns; i += blockDim.x) s_accs[i] = d.acc_state[i];
-    for (uint32_t i = threadIdx.x; i < d.nmasks * d.mw; i += blockDim.x) s_masks[i] = d.masks[i];
+    stage16(smem + d.o_accs, d.acc_state, d.ns * 2);
+    stage16(smem + d.o_masks, d.masks, d.nmasks * d.mw * 8);
   }
   __syncthreads();
 }
 
 // One list entry: up to kEntryItems (file, chunk) items of group d, in rounds of two per
-// lane stepped as two interleaved DFA chains.  Items are whole chunks of the batch stream (aligned to
-// the chunk size, a multiple of 64), so the loads are quad-transposed like K1's: the four
-// lanes of a quad fetch 64 contiguous bytes of one lane's chunk per instruction.  Bytes of
-// a chunk outside the item's file are stepped as no-ops (the file's first byte starts
-// from the start state of its context, its end stops the chain).
+// lane stepped as two interleaved DFA chains.  Items are whole chunks of the batch stream
+// (aligned to the chunk size, a multiple of 64).  Bytes of a chunk outside the item's file
+// are stepped as no-ops (the file's first byte starts from the start state of its
+// context, its end stops the chain).
+// A chain keeps 32-bit fields only (the chunk index, not a 64-bit base; the file start is
+// reloaded on the rare accept), so the hot loop fits 128 VGPRs: 4 waves per SIMD.
 struct K2Item {
   uint32_t s, file;
   uint32_t lo, hi;  // the chunk's bytes inside its file: [base + lo, base + hi)
-  uint64_t fs, base;
+  uint32_t chunk;   // base = chunk * C
 };
 
 __device__ __forceinline__ void k2_list_pair(const DevDFA& d, const K2Args& A, const uint16_t* s_tab,
@@ -1950,8 +1989,6 @@ __device__ __forceinline__ void k2_list_pair(const DevDFA& d, const K2Args& A, c
                                              const uint8_t* s_cls, const uint16_t* s_accs,
                                              const uint64_t* s_masks, uint32_t g, uint32_t first, uint32_t n) {
   const uint32_t C = A.chunk;
-  const uint32_t lane = threadIdx.x & 63, q = lane & 3;
-  const bool b0 = q & 1, b1 = (q >> 1) & 1;
   K2Item it[2];
   bool live[2];
 #pragma unroll
@@ -1960,31 +1997,23 @@ __device__ __forceinline__ void k2_list_pair(const DevDFA& d, const K2Args& A, c
     live[i] = k < n;
     const uint2 item = A.items[first + (live[i] ? k : 0)];
     it[i].file = item.x;
-    it[i].fs = A.off[item.x];
-    const uint64_t fe = A.off[item.x + 1];
-    it[i].base = (uint64_t)item.y * C;
-    const uint64_t a = max(it[i].fs, it[i].base);
-    it[i].lo = (uint32_t)(a - it[i].base);
-    it[i].hi = live[i] ? (uint32_t)(min(fe, it[i].base + C) - it[i].base) : it[i].lo;  // a ghost steps nothing
-    it[i].s = a == it[i].fs ? d.start[0] : d.start[ctx_of(A.data[a - 1])];
+    it[i].chunk = item.y;
+    const uint64_t fs = A.off[item.x], fe = A.off[item.x + 1];
+    const uint64_t base = (uint64_t)item.y * C;
+    const uint64_t a = max(fs, base);
+    it[i].lo = (uint32_t)(a - base);
+    it[i].hi = live[i] ? (uint32_t)(min(fe, base + C) - base) : it[i].lo;  // a ghost steps nothing
+    it[i].s = a == fs ? d.start[0] : d.start[ctx_of(A.data[a - 1])];
   }
-  // word q of quad lane t's chunk, for each chain
-  const uint8_t* src[2][4];
-#pragma unroll
-  for (int i = 0; i < 2; i++)
-#pragma unroll
-    for (int t = 0; t < 4; t++) {
-      const uint64_t bt = __shfl((unsigned long long)it[i].base, (int)((lane & ~3u) + t));
-      src[i][t] = A.data + bt + 16u * q;
-    }
   Lane L{d, A, s_tab, s_cls, s_accs, s_masks, 0, 0, g};
   if (C & 127) {  // chunk sizes that are not whole 128-byte lines (tests): lane by lane
 #pragma unroll
     for (int i = 0; i < 2; i++)
       if (live[i]) {
+        const uint64_t base = (uint64_t)it[i].chunk * C;
         L.file = it[i].file;
-        L.fs = it[i].fs;
-        L.piece(A.off[it[i].file + 1], it[i].base + it[i].lo, it[i].base + it[i].hi);
+        L.fs = A.off[it[i].file];
+        L.piece(A.off[it[i].file + 1], base + it[i].lo, base + it[i].hi);
       }
     return;
   }
@@ -1992,7 +2021,6 @@ __device__ __forceinline__ void k2_list_pair(const DevDFA& d, const K2Args& A, c
   auto word = [&](K2Item& c, uint32_t o, const uint4 v) __attribute__((always_inline)) {
     const int32_t lo = min(16, max(0, (int32_t)c.lo - (int32_t)o));
     const int32_t hi = min(16, max(0, (int32_t)c.hi - (int32_t)o));
-    const uint64_t wb = c.base + o;
     const uint32_t mask = ((1u << hi) - 1u) & ~((1u << lo) - 1u);
     uint32_t s = c.s, any = 0;
     const uint32_t s0 = s;
@@ -2007,44 +2035,44 @@ __device__ __forceinline__ void k2_list_pair(const DevDFA& d, const K2Args& A, c
       if (A.diag) atomicAdd(&A.diag[3], 1u);
       K2_CTR(0, atomicAdd, 1);
       L.file = c.file;
-      L.fs = c.fs;
-      L.accept_word(s0, v, lo, hi, wb);
+      L.fs = A.off[c.file];
+      L.accept_word(s0, v, lo, hi, (uint64_t)c.chunk * C + o);
     }
     c.s = s;
   };
-  // two 64-byte blocks of both chains in registers (x: chain 0, y: chain 1; 0: current,
-  // 1: next), named individually so they stay in VGPRs
-  uint4 x0[4], y0[4];
-#define K2_LOAD(X, Y, J)                                                        \
-  _Pragma("unroll") for (int t = 0; t < 4; t++) {                              \
-    X[t] = *(const uint4*)(src[0][t] + (J));                                     \
-    Y[t] = *(const uint4*)(src[1][t] + (J));                                     \
-  }
-#define K2_BLOCK(X, Y, J)                                                       \
-  quad_transpose4(X, b0, b1);                                                   \
-  quad_transpose4(Y, b0, b1);                                                   \
-  _Pragma("unroll") for (int w = 0; w < 4; w++) {                              \
-    word(it[0], (uint32_t)(J) + 16u * w, X[w]);                                 \
-    word(it[1], (uint32_t)(J) + 16u * w, Y[w]);                                 \
-  }
-  K2_LOAD(x0, y0, 0)
-  // one 64-B block per chain, stepped in place, then reloaded (160 VGPRs: 3 waves/SIMD)
-  for (uint64_t j = 0; j < C; j += 64) {
-    K2_BLOCK(x0, y0, j)
-    if (j + 64 < C) {
-      K2_LOAD(x0, y0, j + 64)
+  K2_PHASE(1);
+  // Each lane loads its own chains' 16-byte words, two words ahead of the one it steps
+  // (six words in registers): the first word of a 128-B line comes from HBM, the next seven
+  // from L2, and a load's latency hides behind two words of stepping.  (The quad-transposed
+  // 64-B blocks loaded once per block and waited on at once exposed a memory round trip
+  // every 64 bytes: profiles/r05/sq1, 51 us per 512-item entry.)
+  const uint8_t* p0 = A.data + (uint64_t)it[0].chunk * C;
+  const uint8_t* p1 = A.data + (uint64_t)it[1].chunk * C;
+  uint4 a0 = *(const uint4*)p0, a1 = *(const uint4*)(p0 + 16);
+  uint4 c0 = *(const uint4*)p1, c1 = *(const uint4*)(p1 + 16);
+  for (uint32_t o = 0; o < C; o += 16) {
+    uint4 a2 = make_uint4(0, 0, 0, 0), c2 = make_uint4(0, 0, 0, 0);
+    if (o + 32 < C) {
+      a2 = *(const uint4*)(p0 + o + 32);
+      c2 = *(const uint4*)(p1 + o + 32);
     }
+    word(it[0], o, a0);
+    word(it[1], o, c0);
+    a0 = a1;
+    a1 = a2;
+    c0 = c1;
+    c1 = c2;
   }
-#undef K2_LOAD
-#undef K2_BLOCK
+  K2_PHASE(2);
   // matches that started in the chunk and run past it (inside the file): follow them
 #pragma unroll
   for (int i = 0; i < 2; i++)
     if (live[i]) {
       L.file = it[i].file;
-      L.fs = it[i].fs;
-      L.tail(it[i].s, A.off[it[i].file + 1], it[i].base + it[i].hi);
+      L.fs = A.off[it[i].file];
+      L.tail(it[i].s, A.off[it[i].file + 1], (uint64_t)it[i].chunk * C + it[i].hi);
     }
+  K2_PHASE(3);
 }
 
 // One dense entry: chunks [first, first + n) of the batch, kStreams consecutive chunks per
@@ -2100,6 +2128,9 @@ __device__ __forceinline__ void k2_run(const DevDFA* __restrict__ dfas, const K2
 #ifdef K2_TRACE_CTR
   if (threadIdx.x == 0) s_ectr = nullptr;
 #endif
+#ifdef K2_TRACE_PHASE
+  if (threadIdx.x == 0) s_tph = nullptr;
+#endif
   for (;;) {
     if (threadIdx.x == 0) s_e = atomicAdd(claim, 1u);
     __syncthreads();
@@ -2117,9 +2148,12 @@ __device__ __forceinline__ void k2_run(const DevDFA* __restrict__ dfas, const K2
 #ifdef K2_TRACE_CTR
         s_ectr = A.etrace + (size_t)e * kTraceW + 4;
 #endif
+#ifdef K2_TRACE_PHASE
+        s_tph = A.etrace + (size_t)e * kTraceW + 4;
+#endif
       }
     }
-#ifdef K2_TRACE_CTR
+#if defined(K2_TRACE_CTR) || defined(K2_TRACE_PHASE)
     __syncthreads();
 #endif
     prev = e;
@@ -2131,6 +2165,7 @@ __device__ __forceinline__ void k2_run(const DevDFA* __restrict__ dfas, const K2
       stage_dfa(d, smem);
       staged = g;
     }
+    K2_PHASE(0);
     const uint16_t* s_tab = (const uint16_t*)smem;
     if (DENSE)
       k2_dense_entry(d, A, g, s_tab, smem + d.o_cls, (const uint16_t*)(smem + d.o_accs), (const uint64_t*)(smem + d.o_masks), en);
@@ -2153,8 +2188,10 @@ __global__ void __launch_bounds__(kBlock) k2_dense_kernel(const DevDFA* __restri
 template <class T>
 static int upload_vec(const std::vector<T>& v, const T** dst, std::vector<void*>* allocs) {
   void* p = nullptr;
-  size_t bytes = std::max<size_t>(v.size() * sizeof(T), 16);
+  // whole 16-B units, zero padded: the kernels stage tables with 16-B loads (stage16)
+  const size_t bytes = (std::max<size_t>(v.size() * sizeof(T), 16) + 15) & ~(size_t)15;
   HIP_TRY(hipMalloc(&p, bytes));
+  HIP_TRY(hipMemset(p, 0, bytes));
   if (!v.empty()) HIP_TRY(hipMemcpy(p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
   allocs->push_back(p);
   *dst = (const T*)p;
