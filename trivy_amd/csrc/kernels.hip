@@ -1539,7 +1539,16 @@ __device__ T block_exclusive_scan(T v, T* out, T* s_wave) {
   return total;
 }
 
-constexpr uint32_t kEntryItems = 2 * kBlock;    // two chains per lane
+// K2's list kernel block (measurement builds vary it).  The stepping is bound by LDS bank
+// conflicts of the transition reads (random rows), so a CU's entries take the same time
+// however its waves are grouped: 1,024-thread blocks (one DFA staged for 16 waves, 292
+// entries of 2,048 items in about one round) ran 0.141 ms against 0.132 for 256 threads
+// (972 entries of 512), profiles/r05/c6.
+#ifndef K2_LIST_BLOCK
+#define K2_LIST_BLOCK 256
+#endif
+constexpr int kK2Block = K2_LIST_BLOCK;
+constexpr uint32_t kEntryItems = 2 * kK2Block;  // two chains per lane
 constexpr uint32_t kEntryChunks = kStreams * kBlock;
 
 // the layout into s_kind / s_gbase ([G] in LDS) and K2's work list (see above)
@@ -1980,11 +1989,11 @@ __device__ __forceinline__ void k2_list_pair(const DevDFA& d, const K2Args& A, c
 __device__ __forceinline__ void k2_list_entry(const DevDFA& d, const K2Args& A, const uint16_t* s_tab,
                                               const uint8_t* s_cls, const uint16_t* s_accs,
                                               const uint64_t* s_masks, uint4 en) {
-  for (uint32_t r0i = 0; r0i < en.z; r0i += 2 * kBlock)
-    k2_list_pair(d, A, s_tab, s_cls, s_accs, s_masks, en.x, en.y + r0i, min(en.z - r0i, (uint32_t)(2 * kBlock)));
+  for (uint32_t r0i = 0; r0i < en.z; r0i += 2 * kK2Block)
+    k2_list_pair(d, A, s_tab, s_cls, s_accs, s_masks, en.x, en.y + r0i, min(en.z - r0i, (uint32_t)(2 * kK2Block)));
 }
 
-// items [first, first + n) of an entry, n <= 2 * kBlock: two per lane
+// items [first, first + n) of an entry, n <= 2 * kK2Block: two per lane
 __device__ __forceinline__ void k2_list_pair(const DevDFA& d, const K2Args& A, const uint16_t* s_tab,
                                              const uint8_t* s_cls, const uint16_t* s_accs,
                                              const uint64_t* s_masks, uint32_t g, uint32_t first, uint32_t n) {
@@ -1993,7 +2002,7 @@ __device__ __forceinline__ void k2_list_pair(const DevDFA& d, const K2Args& A, c
   bool live[2];
 #pragma unroll
   for (int i = 0; i < 2; i++) {
-    const uint32_t k = threadIdx.x + (uint32_t)i * kBlock;
+    const uint32_t k = threadIdx.x + (uint32_t)i * kK2Block;
     live[i] = k < n;
     const uint2 item = A.items[first + (live[i] ? k : 0)];
     it[i].file = item.x;
@@ -2041,6 +2050,10 @@ __device__ __forceinline__ void k2_list_pair(const DevDFA& d, const K2Args& A, c
     c.s = s;
   };
   K2_PHASE(1);
+  // a wave without items steps nothing; a wave without second items steps one chain
+  // (an entry's last round leaves ghost lanes whose LDS reads would load the CU for nothing)
+  const bool any1 = __ballot(live[1]) != 0;
+  if (__ballot(live[0]) == 0) return;  // (live[1] implies live[0])
   // Each lane loads its own chains' 16-byte words, two words ahead of the one it steps
   // (six words in registers): the first word of a 128-B line comes from HBM, the next seven
   // from L2, and a load's latency hides behind two words of stepping.  (The quad-transposed
@@ -2049,19 +2062,29 @@ __device__ __forceinline__ void k2_list_pair(const DevDFA& d, const K2Args& A, c
   const uint8_t* p0 = A.data + (uint64_t)it[0].chunk * C;
   const uint8_t* p1 = A.data + (uint64_t)it[1].chunk * C;
   uint4 a0 = *(const uint4*)p0, a1 = *(const uint4*)(p0 + 16);
-  uint4 c0 = *(const uint4*)p1, c1 = *(const uint4*)(p1 + 16);
-  for (uint32_t o = 0; o < C; o += 16) {
-    uint4 a2 = make_uint4(0, 0, 0, 0), c2 = make_uint4(0, 0, 0, 0);
-    if (o + 32 < C) {
-      a2 = *(const uint4*)(p0 + o + 32);
-      c2 = *(const uint4*)(p1 + o + 32);
+  if (any1) {
+    uint4 c0 = *(const uint4*)p1, c1 = *(const uint4*)(p1 + 16);
+    for (uint32_t o = 0; o < C; o += 16) {
+      uint4 a2 = make_uint4(0, 0, 0, 0), c2 = make_uint4(0, 0, 0, 0);
+      if (o + 32 < C) {
+        a2 = *(const uint4*)(p0 + o + 32);
+        c2 = *(const uint4*)(p1 + o + 32);
+      }
+      word(it[0], o, a0);
+      word(it[1], o, c0);
+      a0 = a1;
+      a1 = a2;
+      c0 = c1;
+      c1 = c2;
     }
-    word(it[0], o, a0);
-    word(it[1], o, c0);
-    a0 = a1;
-    a1 = a2;
-    c0 = c1;
-    c1 = c2;
+  } else {
+    for (uint32_t o = 0; o < C; o += 16) {
+      uint4 a2 = make_uint4(0, 0, 0, 0);
+      if (o + 32 < C) a2 = *(const uint4*)(p0 + o + 32);
+      word(it[0], o, a0);
+      a0 = a1;
+      a1 = a2;
+    }
   }
   K2_PHASE(2);
   // matches that started in the chunk and run past it (inside the file): follow them
@@ -2174,7 +2197,7 @@ __device__ __forceinline__ void k2_run(const DevDFA* __restrict__ dfas, const K2
   }
 }
 
-__global__ void __launch_bounds__(kBlock) K2_WAVES k2_kernel(const DevDFA* __restrict__ dfas, K2Args A) {
+__global__ void __launch_bounds__(kK2Block) K2_WAVES k2_kernel(const DevDFA* __restrict__ dfas, K2Args A) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   k2_run<false>(dfas, A, A.entries, *A.nentries, A.claim, smem);
 }
@@ -2942,7 +2965,7 @@ int device_rules_create(int device, const Plan& p, uint32_t chunk, uint32_t ext_
   r->grid = prop.multiProcessorCount * 8;
   HIP_TRY(hipEventCreateWithFlags(&r->kernels_done, hipEventDisableTiming));
   int occ = 0;
-  HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void*)k2_kernel, kBlock, r->max_lds));
+  HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void*)k2_kernel, kK2Block, r->max_lds));
   r->k2_grid = r->cus * std::max(occ, 1);
   HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void*)k2_dense_kernel, kBlock, r->max_lds));
   r->k2_dense_grid = r->cus * std::max(occ, 1);
@@ -3237,7 +3260,7 @@ int enqueue_scan(DeviceRules* r, LaneState* l, const ScanInput& in, HostOut* out
     if (trace) HIP_TRY(hipMemsetAsync(l->etrace, 0, sizeof(unsigned long long) * entries_cap * kTraceW, st));
     A.etrace = trace ? l->etrace : nullptr;
     // one block per resident slot (the grids are persistent)
-    hipLaunchKernelGGL(k2_kernel, dim3(r->k2_grid), dim3(kBlock), r->max_lds, st, (const DevDFA*)r->d_groups, A);
+    hipLaunchKernelGGL(k2_kernel, dim3(r->k2_grid), dim3(kK2Block), r->max_lds, st, (const DevDFA*)r->d_groups, A);
     HIP_TRY(hipGetLastError());
     hipLaunchKernelGGL(k2_dense_kernel, dim3(r->k2_dense_grid), dim3(kBlock), r->max_lds, st,
                        (const DevDFA*)r->d_groups, A);
