@@ -511,6 +511,10 @@ def main():
     last = st[0]
     k2_read = last["k2_bytes"]  # last batch of the first device: chunk bytes K2 read
     pmc = _traffic_record(args.rules, int(launch_bytes))
+    k1_name = ("K1F keyword/anchor filter + exact verification and run counters (k1f_kernel)"
+               if last["k1_filter"] else "K1 keyword automaton (k1_kernel)")
+    if pmc and pmc.get("k1_kernel", "k1_kernel") != ("k1f_kernel" if last["k1_filter"] else "k1_kernel"):
+        pmc = None  # a pass of the other K1
     ngpus_s = "x%d" % ngpus
     line = {
         "metric": "secret-scan GB/s (builtin rules) at 1/2/4/8 MI355X; % of HBM peak",
@@ -539,7 +543,7 @@ def main():
                                    "collective" % (ngpus_s, len(devices))) + (
                                        ", EMULATED contexts (no GPU)" if args.emulate else ""),
                    "devices": devices if world == 1 else None},
-        "roofline": {"bound": "hbm", "kernel": "K1 keyword automaton (k1_kernel)",
+        "roofline": {"bound": "hbm", "kernel": k1_name,
                      "achieved": _r(k1_gbs), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": _frac(k1_gbs),
                      "traffic": pmc["k1_bytes_per_launch"] if pmc else None,
@@ -547,8 +551,13 @@ def main():
                      "traffic_source": pmc["csv"] if pmc else
                      "none: no FETCH_SIZE pass of this device code, rule set and batch size "
                      "in profiles/pmc/",
-                     "traffic_calibration": "FETCH_SIZE KiB x 1024 / 0.922 (K1's quad-transposed "
-                                            "64-B loads; profiles/r02/fetch_calib.json)",
+                     "traffic_calibration": (
+                         "FETCH_SIZE KiB x 1024 / %s (%s; profiles/r02/fetch_calib.json)" % (
+                             pmc.get("fetch_factor", 0.922),
+                             "16 contiguous bytes per lane" if pmc.get("k1_kernel") == "k1f_kernel"
+                             else "quad-transposed 64-B loads")) if pmc else None,
+                     "k1_listed_words_last_batch": last["k1f_listed"] if last["k1_filter"] else None,
+                     "k1_verified_arrivals_last_batch": last["k1f_arrivals"] if last["k1_filter"] else None,
                      "k1_gates_k2_frac": _frac(_gbs(d["sum_bytes"], kern_ms)),
                      "device_frac": _frac(_gbs(d["sum_bytes"], dev_ms)),
                      "aggregate": dict(agg, gpus=ngpus,

@@ -254,6 +254,8 @@ typedef struct tsg_stats {
   uint32_t k1f_listed, k1f_arrivals;
   /* chunks of the last batch whose K1 event word is not empty (the item passes' units) */
   uint32_t event_chunks;
+  /* 1: K1 ran as the filter-and-verify K1F (k1f_kernel), 0: as the automaton (k1_kernel) */
+  uint32_t k1_filter;
 } tsg_stats;
 int tsg_ctx_get_stats(const tsg_ctx* ctx, tsg_stats* out);
 

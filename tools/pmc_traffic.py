@@ -10,8 +10,8 @@ of the device code that ran (bench.py uses the traffic only while the sources st
 
 FETCH_SIZE is in KiB and counts memory-side read requests x 64 B (MI355X_MICROARCH.md, HBM
 section), so how many bytes one KiB stands for depends on the request width of the access
-pattern: exactly 1/2 for 16-B-per-lane streaming reads, 0.92 for K1/K2's quad-transposed
-64-B segment loads.  The factor per kernel comes from profiles/r02/fetch_calib.json (a
+pattern: exactly 1/2 for 16-B-per-lane streaming reads (k1f_kernel), 0.92 for the automaton
+K1's quad-transposed 64-B segment loads.  The factor per kernel comes from profiles/r02/fetch_calib.json (a
 calibration run on a known byte count, tools/fetch_calib.hip).  Launches with a grid below
 1/4 of the largest launch of the same kernel (the K1 sampling pass) are skipped.
 """
@@ -49,10 +49,12 @@ def record(rules, csv_path, bench_json, committed):
     for ln in open(bench_json):
         if ln.startswith("{"):
             line = json.loads(ln)
-    t1 = traffic(csv_path, "k1_kernel")
+    k1 = "k1f_kernel" if traffic(csv_path, "k1f_kernel") is not None else "k1_kernel"
+    t1 = traffic(csv_path, k1)
     t2 = traffic(csv_path, "k2_kernel")
     return {"rules": rules, "batch_bytes": line["roofline"]["algorithmic_bytes_per_launch"],
-            "kernels_sha256": kernel_source_sha(), "csv": committed,
+            "kernels_sha256": kernel_source_sha(), "csv": committed, "k1_kernel": k1,
+            "fetch_factor": fetch_factor(k1),
             "k1_bytes_per_launch": None if t1 is None else int(t1),
             "k2_bytes_per_launch": None if t2 is None else int(t2),
             "k2_item_bytes_last_batch": line["kernels"]["k2_item_bytes_last_batch"]}

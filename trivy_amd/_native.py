@@ -84,7 +84,7 @@ class Stats(C.Structure):
                 ("sum_prep_ms", C.c_double), ("sum_meta_ms", C.c_double),
                 ("k1x_records", C.c_uint32), ("k1x_inline", C.c_uint32),
                 ("k1f_listed", C.c_uint32), ("k1f_arrivals", C.c_uint32),
-                ("event_chunks", C.c_uint32)]
+                ("event_chunks", C.c_uint32), ("k1_filter", C.c_uint32)]
 
 
 # (name, restype, argtypes) -- every symbol include/trivy_secret.h declares

@@ -79,6 +79,8 @@ void device_rules_destroy(DeviceRules* d);
 // keyword bits K1 no longer reports after its adaptation (null before / without it)
 std::shared_ptr<const std::vector<uint8_t>> device_rules_kw_unknown(const DeviceRules* d);
 uint32_t device_rules_hot_states(const DeviceRules* d);
+// true: K1 runs as K1F (k1f_kernel, batches under 4 GiB); false: the automaton (k1_kernel)
+bool device_rules_k1_filter(const DeviceRules* d);
 
 int lane_create(DeviceRules* d, LaneState** out);
 void lane_destroy(LaneState* l);

@@ -660,10 +660,15 @@ __device__ __forceinline__ uint32_t f_load4u(const uint8_t* data, uint32_t a) { 
   return __builtin_amdgcn_alignbyte(p[1], p[0], a & 3u);
 }
 
-// a lane's 16 bytes of a tile (K1F_NT: non-temporal, the batch is read once)
+// a lane's 16 bytes of a tile, non-temporal (the batch streams through once): K1F 0.255 ->
+// 0.251 ms and K2 0.129 -> 0.122 ms per GiB against default-policy loads (profiles/r05/c3;
+// K1F_NT=0 builds the default policy for measurement)
+#ifndef K1F_NT
+#define K1F_NT 1
+#endif
 typedef uint32_t f_u32x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ uint4 f_tile_load(const uint8_t* p) {
-#if defined(K1F_NT)
+#if K1F_NT
   const f_u32x4 v = __builtin_nontemporal_load((const f_u32x4*)p);
   return make_uint4(v.x, v.y, v.z, v.w);
 #else
@@ -2977,6 +2982,7 @@ void device_rules_destroy(DeviceRules* d) { delete d; }
 
 std::shared_ptr<const std::vector<uint8_t>> device_rules_kw_unknown(const DeviceRules* d) { return d->kw_unknown; }
 uint32_t device_rules_hot_states(const DeviceRules* d) { return d->hot_states; }
+bool device_rules_k1_filter(const DeviceRules* d) { return d->use_k1f; }
 
 int lane_create(DeviceRules* d, LaneState** out) {
   HIP_TRY(hipSetDevice(d->device));

@@ -311,6 +311,7 @@ void update_stats(tsg_ctx* c, const Batch& b) {
   s.k1f_listed = b.counts[16];
   s.k1f_arrivals = b.counts[17];
   s.event_chunks = b.counts[1];
+  s.k1_filter = c->dr && device_rules_k1_filter(c->dr) && b.bytes + (1u << 16) < (1ull << 32) ? 1u : 0u;
   s.k1_hot_states = c->dr ? device_rules_hot_states(c->dr) : 0;
   s.batches++;
   s.sum_bytes += b.bytes;
