@@ -552,7 +552,7 @@ def main():
                      "none: no FETCH_SIZE pass of this device code, rule set and batch size "
                      "in profiles/pmc/",
                      "traffic_calibration": (
-                         "FETCH_SIZE KiB x 1024 / %s (%s; profiles/r02/fetch_calib.json)" % (
+                         "FETCH_SIZE KiB x 1024 / %s (%s; profiles/pmc/fetch_calib.json)" % (
                              pmc.get("fetch_factor", 0.922),
                              "16 contiguous bytes per lane" if pmc.get("k1_kernel") == "k1f_kernel"
                              else "quad-transposed 64-B loads")) if pmc else None,

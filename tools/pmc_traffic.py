@@ -11,7 +11,7 @@ of the device code that ran (bench.py uses the traffic only while the sources st
 FETCH_SIZE is in KiB and counts memory-side read requests x 64 B (MI355X_MICROARCH.md, HBM
 section), so how many bytes one KiB stands for depends on the request width of the access
 pattern: exactly 1/2 for 16-B-per-lane streaming reads (k1f_kernel), 0.92 for the automaton
-K1's quad-transposed 64-B segment loads.  The factor per kernel comes from profiles/r02/fetch_calib.json (a
+K1's quad-transposed 64-B segment loads.  The factor per kernel comes from profiles/pmc/fetch_calib.json (a
 calibration run on a known byte count, tools/fetch_calib.hip).  Launches with a grid below
 1/4 of the largest launch of the same kernel (the K1 sampling pass) are skipped.
 """
@@ -20,7 +20,7 @@ import json
 import os
 import sys
 
-CALIB = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "profiles", "r02", "fetch_calib.json")
+CALIB = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "profiles", "pmc", "fetch_calib.json")
 
 
 def fetch_factor(kernel):

@@ -2055,42 +2055,45 @@ __device__ __forceinline__ void k2_list_pair(const DevDFA& d, const K2Args& A, c
     c.s = s;
   };
   K2_PHASE(1);
-  // a wave without items steps nothing; a wave without second items steps one chain
-  // (an entry's last round leaves ghost lanes whose LDS reads would load the CU for nothing)
-  const bool any1 = __ballot(live[1]) != 0;
+  // a wave without items steps nothing (an entry's last round leaves ghost lanes whose LDS
+  // reads would load the CU for nothing)
   if (__ballot(live[0]) == 0) return;  // (live[1] implies live[0])
-  // Each lane loads its own chains' 16-byte words, two words ahead of the one it steps
-  // (six words in registers): the first word of a 128-B line comes from HBM, the next seven
-  // from L2, and a load's latency hides behind two words of stepping.  (The quad-transposed
-  // 64-B blocks loaded once per block and waited on at once exposed a memory round trip
-  // every 64 bytes: profiles/r05/sq1, 51 us per 512-item entry.)
-  const uint8_t* p0 = A.data + (uint64_t)it[0].chunk * C;
-  const uint8_t* p1 = A.data + (uint64_t)it[1].chunk * C;
-  uint4 a0 = *(const uint4*)p0, a1 = *(const uint4*)(p0 + 16);
-  if (any1) {
-    uint4 c0 = *(const uint4*)p1, c1 = *(const uint4*)(p1 + 16);
-    for (uint32_t o = 0; o < C; o += 16) {
-      uint4 a2 = make_uint4(0, 0, 0, 0), c2 = make_uint4(0, 0, 0, 0);
-      if (o + 32 < C) {
-        a2 = *(const uint4*)(p0 + o + 32);
-        c2 = *(const uint4*)(p1 + o + 32);
-      }
-      word(it[0], o, a0);
-      word(it[1], o, c0);
-      a0 = a1;
-      a1 = a2;
-      c0 = c1;
-      c1 = c2;
-    }
-  } else {
-    for (uint32_t o = 0; o < C; o += 16) {
-      uint4 a2 = make_uint4(0, 0, 0, 0);
-      if (o + 32 < C) a2 = *(const uint4*)(p0 + o + 32);
-      word(it[0], o, a0);
-      a0 = a1;
-      a1 = a2;
+  // Quad-transposed loads: the four lanes of a quad fetch 64 contiguous bytes of one lane's
+  // chunk per instruction (one 64-B memory request), two DPP stages give each lane its own
+  // chunk's four words.  (Each lane loading its own 16-B words, two words ahead, fetched
+  // every 64-B sector up to four times: 24 waves per CU keep ~6 MB of lines open per XCD
+  // against 4 MB of L2 -- 3.3x K2's item bytes in the FETCH pass and 0.139 against 0.126 ms
+  // in the bench, profiles/r05/bench.)
+  const uint32_t lane = threadIdx.x & 63, q = lane & 3;
+  const bool b0 = q & 1, b1 = (q >> 1) & 1;
+  uint4 x0[4], y0[4];
+  const uint8_t* dq = A.data + 16u * q;
+#define K2_LOAD_T(X, Y, J, T)                                                                 \
+  X[T] = *(const uint4*)(dq + (uint64_t)__shfl(it[0].chunk, (int)((lane & ~3u) + T)) * C + (J)); \
+  Y[T] = *(const uint4*)(dq + (uint64_t)__shfl(it[1].chunk, (int)((lane & ~3u) + T)) * C + (J));
+#define K2_LOAD(X, Y, J) \
+  K2_LOAD_T(X, Y, J, 0)  \
+  K2_LOAD_T(X, Y, J, 1)  \
+  K2_LOAD_T(X, Y, J, 2)  \
+  K2_LOAD_T(X, Y, J, 3)
+#define K2_BLOCK(X, Y, J)                                                       \
+  quad_transpose4(X, b0, b1);                                                   \
+  quad_transpose4(Y, b0, b1);                                                   \
+  _Pragma("unroll") for (int w = 0; w < 4; w++) {                              \
+    word(it[0], (uint32_t)(J) + 16u * w, X[w]);                                 \
+    word(it[1], (uint32_t)(J) + 16u * w, Y[w]);                                 \
+  }
+  K2_LOAD(x0, y0, 0)
+  // one 64-B block per chain, stepped in place, then reloaded
+  for (uint32_t j = 0; j < C; j += 64) {
+    K2_BLOCK(x0, y0, j)
+    if (j + 64 < C) {
+      K2_LOAD(x0, y0, j + 64)
     }
   }
+#undef K2_LOAD_T
+#undef K2_LOAD
+#undef K2_BLOCK
   K2_PHASE(2);
   // matches that started in the chunk and run past it (inside the file): follow them
 #pragma unroll
