@@ -315,6 +315,10 @@ const char* tsg_last_error(void);
  *                     after its adaptation (tsg_scan_batch_emulated)
  *   "k1_automaton"    "1": contexts created next run K1 as the LDS automaton instead of the
  *                     filter-and-verify K1F (k1f.hpp)
+ *   "group_states"    state cap of a K2 rule-group DFA in the next compiled rule sets
+ *                     (default 2,048 for rule sets of up to 256 rules, else 1,024)
+ *   "group_table_kib" table cap of a K2 rule-group DFA, 1..64 KiB (default 64 for rule
+ *                     sets of up to 256 rules, else 48)
  * Returns TSG_ERR_ARG for an unknown name. */
 int tsg_test_knob(const char* name, const char* value);
 

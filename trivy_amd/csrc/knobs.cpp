@@ -36,6 +36,11 @@ extern "C" int tsg_test_knob(const char* name, const char* value) {
   else if (!strcmp(name, "no_k1x")) k.no_k1x = x;
   else if (!strcmp(name, "emu_wordrec")) k.emu_wordrec = x;
   else if (!strcmp(name, "k1_automaton")) k.k1_automaton = x;
+  else if (!strcmp(name, "group_states")) k.group_states = x;
+  else if (!strcmp(name, "group_table_kib")) {
+    if (x < 0 || x > 64) return fail(TSG_ERR_ARG, "group_table_kib must be 0..64");
+    k.group_table_kib = x;
+  }
   else if (!strcmp(name, "x_step")) {
     if (x != 0 && x != 1 && x != 2 && x != 4) return fail(TSG_ERR_ARG, "x_step must be 0, 1, 2 or 4");
     k.x_step = x;
