@@ -129,3 +129,18 @@ def test_allow_exclude_binary_emulation_vs_oracle():
     args = [a for a in args if not A.IsBinary(a.Content, len(a.Content))]
     got = sc.ScanBatch(args, emulate_chunk=64)
     assert _vs_oracle(doc, args, got) > 5
+
+
+def test_group_caps(knob):
+    """K2 rule-group caps: the builtin rules (83, under 256) get groups of up to 2,048 states
+    / 64 KiB by default; the knobs set other caps, and a table cap past the u16 row offsets'
+    64 KiB is an argument error.  Every group fits its caps."""
+    from trivy_amd import _native as N
+    default = S.NewScanner(None).info()
+    knob("group_states", "1024")
+    knob("group_table_kib", "48")
+    small = S.NewScanner(None).info()
+    assert default["n_groups"] < small["n_groups"]
+    assert small["max_group_states"] <= 1024 < default["max_group_states"] <= 2048
+    with pytest.raises(Exception):
+        N.knob("group_table_kib", "65")
