@@ -695,45 +695,6 @@ struct K1FLane {
   // kEvRunD) and the OR of its windows by groups of four (g[i]: window ends 4i..4i+3).  In
   // three phases (bytes 13-15, 0-7, 8-12) so that at most 8 entries are live: the registers
   // left over hold more tiles in flight (kFDepth).
-#if defined(K1F_SEQ)
-  // The same results with the windows as running partials: after byte q, p1 = d0(b[q]),
-  // p2 = d0(b[q-1]) & d1(b[q]), p3 = d0(b[q-2]) & d1(b[q-1]) & d2(b[q]), so the window
-  // ending at q+1 is p3 & d3(b[q+1]).  Four entries are live at a time (plus bytes 13-15,
-  // read first for the look-behind partials of lane l+1): fewer registers, more tiles in flight.
-  __device__ __forceinline__ uint32_t tile(uint4 v, FCarry& cy, uint32_t (&g)[4]) const {
-    const uint4 e13 = entry(v.w, 1), e14 = entry(v.w, 2), e15 = entry(v.w, 3);
-    const uint32_t ao = k1f_and3(e13.x, e14.y, e15.z), bo = e14.x & e15.y, co = e15.x;
-    uint32_t p3 = f_prev(ao, cy.a), p2 = f_prev(bo, cy.b), p1 = f_prev(co, cy.c);
-    cy.a = ao;
-    cy.b = bo;
-    cy.c = co;
-    uint32_t rl[4];  // the window ending at the last byte of each dword
-#pragma unroll
-    for (int w = 0; w < 4; w++) {
-      const uint32_t word = w == 0 ? v.x : w == 1 ? v.y : w == 2 ? v.z : v.w;
-      uint4 e[4];
-#pragma unroll
-      for (int k = 0; k < 4; k++) e[k] = (w == 3 && k >= 1) ? (k == 1 ? e13 : k == 2 ? e14 : e15) : entry(word, k);
-      uint32_t acc = 0, r = 0;
-#pragma unroll
-      for (int k = 0; k < 4; k++) {
-        r = p3 & e[k].w;
-        p3 = p2 & e[k].z;
-        p2 = p1 & e[k].y;
-        p1 = e[k].x;
-        acc |= r;
-      }
-      g[w] = acc;
-      rl[w] = r;
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    const uint32_t m = k1f_flags(rl[0], rl[1], rl[2], rl[3]);
-    const uint32_t m1 = f_prev(m, cy.m), m2 = f_prev(m1, cy.m1);
-    cy.m = m;
-    cy.m1 = m1;
-    return k1f_runs(m, m1, m2);
-  }
-#else
   __device__ __forceinline__ uint32_t tile(uint4 v, FCarry& cy, uint32_t (&g)[4]) const {
     // bytes 13..15: the partial windows lane l+1 needs
     const uint4 e13 = entry(v.w, 1), e14 = entry(v.w, 2), e15 = entry(v.w, 3);
@@ -780,7 +741,6 @@ struct K1FLane {
     cy.m1 = m1;
     return k1f_runs(m, m1, m2);
   }
-#endif
 };
 
 // Verification of listed words (k1f_kernel drains its ring 64 words at a time):
