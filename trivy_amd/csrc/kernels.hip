@@ -1987,18 +1987,23 @@ struct K2Item {
   uint32_t chunk;   // base = chunk * C
 };
 
+template <bool RICH>
 __device__ __forceinline__ void k2_list_pair(const DevDFA& d, const K2Args& A, const uint16_t* s_tab,
                                              const uint8_t* s_cls, const uint16_t* s_accs,
                                              const uint64_t* s_masks, uint32_t g, uint32_t first, uint32_t n);
 
+template <bool RICH>
 __device__ __forceinline__ void k2_list_entry(const DevDFA& d, const K2Args& A, const uint16_t* s_tab,
                                               const uint8_t* s_cls, const uint16_t* s_accs,
                                               const uint64_t* s_masks, uint4 en) {
   for (uint32_t r0i = 0; r0i < en.z; r0i += 2 * kK2Block)
-    k2_list_pair(d, A, s_tab, s_cls, s_accs, s_masks, en.x, en.y + r0i, min(en.z - r0i, (uint32_t)(2 * kK2Block)));
+    k2_list_pair<RICH>(d, A, s_tab, s_cls, s_accs, s_masks, en.x, en.y + r0i, min(en.z - r0i, (uint32_t)(2 * kK2Block)));
 }
 
-// items [first, first + n) of an entry, n <= 2 * kK2Block: two per lane
+// items [first, first + n) of an entry, n <= 2 * kK2Block: two per lane.  RICH (the staged
+// table already limits the CU to two blocks, so a wave may hold 256 VGPRs): both chains
+// stepped in one loop and the next 64-B blocks loaded while the current ones are stepped.
+template <bool RICH>
 __device__ __forceinline__ void k2_list_pair(const DevDFA& d, const K2Args& A, const uint16_t* s_tab,
                                              const uint8_t* s_cls, const uint16_t* s_accs,
                                              const uint64_t* s_masks, uint32_t g, uint32_t first, uint32_t n) {
@@ -2054,6 +2059,44 @@ __device__ __forceinline__ void k2_list_pair(const DevDFA& d, const K2Args& A, c
     }
     c.s = s;
   };
+  // both chains in ONE loop: their transition reads issue back to back (RICH)
+  auto word2 = [&](uint32_t o, const uint4 v0, const uint4 v1) __attribute__((always_inline)) {
+    K2Item& c0 = it[0];
+    K2Item& c1 = it[1];
+    const int32_t lo0 = min(16, max(0, (int32_t)c0.lo - (int32_t)o)), hi0 = min(16, max(0, (int32_t)c0.hi - (int32_t)o));
+    const int32_t lo1 = min(16, max(0, (int32_t)c1.lo - (int32_t)o)), hi1 = min(16, max(0, (int32_t)c1.hi - (int32_t)o));
+    const uint32_t m0 = ((1u << hi0) - 1u) & ~((1u << lo0) - 1u), m1 = ((1u << hi1) - 1u) & ~((1u << lo1) - 1u);
+    uint32_t s0 = c0.s, s1 = c1.s, any0 = 0, any1 = 0;
+    const uint32_t r0 = s0, r1 = s1;
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+      const uint32_t e0 = s_tab[s0 + s_cls[byte_of(v0, k)]];
+      const uint32_t e1 = s_tab[s1 + s_cls[byte_of(v1, k)]];
+      const bool in0 = (m0 >> k) & 1u, in1 = (m1 >> k) & 1u;
+      any0 |= in0 ? e0 : 0u;
+      any1 |= in1 ? e1 : 0u;
+      s0 = in0 ? (e0 & 0x7FFFu) : s0;
+      s1 = in1 ? (e1 & 0x7FFFu) : s1;
+    }
+    if (__builtin_expect((any0 | any1) & 0x8000u, 0)) {  // an accept: one record per word
+      if (any0 & 0x8000u) {
+        if (A.diag) atomicAdd(&A.diag[3], 1u);
+        K2_CTR(0, atomicAdd, 1);
+        L.file = c0.file;
+        L.fs = A.off[c0.file];
+        L.accept_word(r0, v0, lo0, hi0, (uint64_t)c0.chunk * C + o);
+      }
+      if (any1 & 0x8000u) {
+        if (A.diag) atomicAdd(&A.diag[3], 1u);
+        K2_CTR(0, atomicAdd, 1);
+        L.file = c1.file;
+        L.fs = A.off[c1.file];
+        L.accept_word(r1, v1, lo1, hi1, (uint64_t)c1.chunk * C + o);
+      }
+    }
+    c0.s = s0;
+    c1.s = s1;
+  };
   K2_PHASE(1);
   // a wave without items steps nothing (an entry's last round leaves ghost lanes whose LDS
   // reads would load the CU for nothing)
@@ -2083,12 +2126,34 @@ __device__ __forceinline__ void k2_list_pair(const DevDFA& d, const K2Args& A, c
     word(it[0], (uint32_t)(J) + 16u * w, X[w]);                                 \
     word(it[1], (uint32_t)(J) + 16u * w, Y[w]);                                 \
   }
-  K2_LOAD(x0, y0, 0)
-  // one 64-B block per chain, stepped in place, then reloaded
-  for (uint32_t j = 0; j < C; j += 64) {
-    K2_BLOCK(x0, y0, j)
-    if (j + 64 < C) {
-      K2_LOAD(x0, y0, j + 64)
+  if constexpr (RICH) {
+#define K2_BLOCK2(X, Y, J)                                                      \
+  quad_transpose4(X, b0, b1);                                                   \
+  quad_transpose4(Y, b0, b1);                                                   \
+  _Pragma("unroll") for (int w = 0; w < 4; w++) word2((uint32_t)(J) + 16u * w, X[w], Y[w]);
+    uint4 x1[4], y1[4];
+    K2_LOAD(x0, y0, 0)
+    // two 64-B blocks per chain in registers: block j + 64 loads while block j steps
+    for (uint32_t j = 0; j < C; j += 128) {
+      if (j + 64 < C) {
+        K2_LOAD(x1, y1, j + 64)
+      }
+      K2_BLOCK2(x0, y0, j)
+      if (j + 64 >= C) break;
+      if (j + 128 < C) {
+        K2_LOAD(x0, y0, j + 128)
+      }
+      K2_BLOCK2(x1, y1, j + 64)
+    }
+#undef K2_BLOCK2
+  } else {
+    K2_LOAD(x0, y0, 0)
+    // one 64-B block per chain, stepped in place, then reloaded
+    for (uint32_t j = 0; j < C; j += 64) {
+      K2_BLOCK(x0, y0, j)
+      if (j + 64 < C) {
+        K2_LOAD(x0, y0, j + 64)
+      }
     }
   }
 #undef K2_LOAD_T
@@ -2150,7 +2215,7 @@ __device__ __forceinline__ void k2_dense_entry(const DevDFA& d, const K2Args& A,
 // K2: persistent grids over the work lists.  Blocks claim entries dynamically (one
 // atomic per entry), so blocks that drew light entries take more; a block restages the
 // DFA only when its next entry belongs to another group.
-template <bool DENSE>
+template <bool DENSE, bool RICH = false>
 __device__ __forceinline__ void k2_run(const DevDFA* __restrict__ dfas, const K2Args& A, const uint4* entries,
                                        uint32_t E, uint32_t* claim, uint8_t* smem) {
   __shared__ uint32_t s_e;
@@ -2201,13 +2266,20 @@ __device__ __forceinline__ void k2_run(const DevDFA* __restrict__ dfas, const K2
     if (DENSE)
       k2_dense_entry(d, A, g, s_tab, smem + d.o_cls, (const uint16_t*)(smem + d.o_accs), (const uint64_t*)(smem + d.o_masks), en);
     else
-      k2_list_entry(d, A, s_tab, smem + d.o_cls, (const uint16_t*)(smem + d.o_accs), (const uint64_t*)(smem + d.o_masks), en);
+      k2_list_entry<RICH>(d, A, s_tab, smem + d.o_cls, (const uint16_t*)(smem + d.o_accs), (const uint64_t*)(smem + d.o_masks), en);
   }
 }
 
 __global__ void __launch_bounds__(kK2Block) K2_WAVES k2_kernel(const DevDFA* __restrict__ dfas, K2Args A) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   k2_run<false>(dfas, A, A.entries, *A.nentries, A.claim, smem);
+}
+// the list pass when the staged table allows two blocks per CU at most (> 53 KiB): eight
+// waves per CU, so each may hold 256 VGPRs (k2_list_pair<true>)
+__global__ void __launch_bounds__(kK2Block) __attribute__((amdgpu_waves_per_eu(1, 2)))
+k2_kernel_rich(const DevDFA* __restrict__ dfas, K2Args A) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  k2_run<false, true>(dfas, A, A.entries, *A.nentries, A.claim, smem);
 }
 
 __global__ void __launch_bounds__(kBlock) k2_dense_kernel(const DevDFA* __restrict__ dfas, K2Args A) {
@@ -2542,6 +2614,7 @@ struct DeviceRules {
   int grid = 0;          // 8 blocks per CU
   int cus = 0;
   int k2_grid = 0, k2_dense_grid = 0;  // resident blocks of the persistent K2 kernels
+  bool k2_rich = false;                 // the list pass runs k2_kernel_rich (same residency)
   hipEvent_t kernels_done = nullptr;   // end of the kernels of the last enqueued batch
   bool kernels_done_valid = false;
   std::vector<void*> tables;
@@ -2932,6 +3005,7 @@ int device_rules_create(int device, const Plan& p, uint32_t chunk, uint32_t ext_
   }
   if (r->max_lds > 64 * 1024) {
     HIP_TRY(hipFuncSetAttribute((const void*)k2_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)r->max_lds));
+    HIP_TRY(hipFuncSetAttribute((const void*)k2_kernel_rich, hipFuncAttributeMaxDynamicSharedMemorySize, (int)r->max_lds));
     HIP_TRY(hipFuncSetAttribute((const void*)k2_dense_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)r->max_lds));
   }
@@ -2975,6 +3049,12 @@ int device_rules_create(int device, const Plan& p, uint32_t chunk, uint32_t ext_
   int occ = 0;
   HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void*)k2_kernel, kK2Block, r->max_lds));
   r->k2_grid = r->cus * std::max(occ, 1);
+  {  // when the staged table already holds the CU to as many blocks as the rich variant's
+     // registers do, that variant runs (builtin rules, 64 KiB groups: 2 blocks per CU)
+    int occ_rich = 0;
+    HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ_rich, (const void*)k2_kernel_rich, kK2Block, r->max_lds));
+    r->k2_rich = occ_rich >= 1 && occ_rich >= occ;
+  }
   HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void*)k2_dense_kernel, kBlock, r->max_lds));
   r->k2_dense_grid = r->cus * std::max(occ, 1);
   *out = r.release();
@@ -3269,7 +3349,10 @@ int enqueue_scan(DeviceRules* r, LaneState* l, const ScanInput& in, HostOut* out
     if (trace) HIP_TRY(hipMemsetAsync(l->etrace, 0, sizeof(unsigned long long) * entries_cap * kTraceW, st));
     A.etrace = trace ? l->etrace : nullptr;
     // one block per resident slot (the grids are persistent)
-    hipLaunchKernelGGL(k2_kernel, dim3(r->k2_grid), dim3(kK2Block), r->max_lds, st, (const DevDFA*)r->d_groups, A);
+    if (r->k2_rich)
+      hipLaunchKernelGGL(k2_kernel_rich, dim3(r->k2_grid), dim3(kK2Block), r->max_lds, st, (const DevDFA*)r->d_groups, A);
+    else
+      hipLaunchKernelGGL(k2_kernel, dim3(r->k2_grid), dim3(kK2Block), r->max_lds, st, (const DevDFA*)r->d_groups, A);
     HIP_TRY(hipGetLastError());
     hipLaunchKernelGGL(k2_dense_kernel, dim3(r->k2_dense_grid), dim3(kBlock), r->max_lds, st,
                        (const DevDFA*)r->d_groups, A);
