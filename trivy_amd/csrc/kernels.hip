@@ -1841,14 +1841,17 @@ struct Lane {
 
   // matches that started before b: follow them past b (noinject) until they all die
   __device__ K2_NOINLINE void tail(uint32_t s, uint64_t fe, uint64_t b) {
-    const uint8_t* data = A.data;
-    const uint8_t* dead = s_cls + (d.o_dead - d.o_cls);  // (staged: stage_dfa)
     if (b >= fe) {
       const uint32_t m = d.eot[state_of(s)];
       if (m) emit(m, fe);
       return;
     }
-    s = d.to_ni[state_of(s)];
+    tail_ni(d.to_ni[state_of(s)], fe, b);
+  }
+  // the same from the noinject row already looked up (s = to_ni of the chain's row, b < fe)
+  __device__ K2_NOINLINE void tail_ni(uint32_t s, uint64_t fe, uint64_t b) {
+    const uint8_t* data = A.data;
+    const uint8_t* dead = s_cls + (d.o_dead - d.o_cls);  // (staged: stage_dfa)
     // 16 bytes per load (the next word in flight), liveness checked once per word: a dead
     // noinject state is absorbing and accepts nothing, so stepping on inside the word
     // changes no output.  (The batch is padded, so whole-word loads past fe are safe.)
@@ -1985,6 +1988,7 @@ struct K2Item {
   uint32_t s, file;
   uint32_t lo, hi;  // the chunk's bytes inside its file: [base + lo, base + hi)
   uint32_t chunk;   // base = chunk * C
+  uint64_t fe;      // the file's end (the tail's bound)
 };
 
 template <bool RICH>
@@ -2017,12 +2021,16 @@ __device__ __forceinline__ void k2_list_pair(const DevDFA& d, const K2Args& A, c
     const uint2 item = A.items[first + (live[i] ? k : 0)];
     it[i].file = item.x;
     it[i].chunk = item.y;
-    const uint64_t fs = A.off[item.x], fe = A.off[item.x + 1];
     const uint64_t base = (uint64_t)item.y * C;
+    // the byte before the chunk, loaded beside the offsets (it is the context byte unless
+    // the file starts inside the chunk, and then the start state needs none)
+    const uint8_t before = base ? A.data[base - 1] : 0;
+    const uint64_t fs = A.off[item.x], fe = A.off[item.x + 1];
     const uint64_t a = max(fs, base);
+    it[i].fe = fe;
     it[i].lo = (uint32_t)(a - base);
     it[i].hi = live[i] ? (uint32_t)(min(fe, base + C) - base) : it[i].lo;  // a ghost steps nothing
-    it[i].s = a == fs ? d.start[0] : d.start[ctx_of(A.data[a - 1])];
+    it[i].s = a == fs ? d.start[0] : d.start[ctx_of(before)];
   }
   Lane L{d, A, s_tab, s_cls, s_accs, s_masks, 0, 0, g};
   if (C & 127) {  // chunk sizes that are not whole 128-byte lines (tests): lane by lane
@@ -2160,13 +2168,24 @@ __device__ __forceinline__ void k2_list_pair(const DevDFA& d, const K2Args& A, c
 #undef K2_LOAD
 #undef K2_BLOCK
   K2_PHASE(2);
-  // matches that started in the chunk and run past it (inside the file): follow them
+  // matches that started in the chunk and run past it (inside the file): follow them.  The
+  // noinject rows of both chains are looked up together, the file ends kept from the setup.
+  uint32_t ni[2];
+#pragma unroll
+  for (int i = 0; i < 2; i++) {
+    const uint64_t b = (uint64_t)it[i].chunk * C + it[i].hi;
+    ni[i] = live[i] && b < it[i].fe ? d.to_ni[L.state_of(it[i].s)] : 0u;
+  }
 #pragma unroll
   for (int i = 0; i < 2; i++)
     if (live[i]) {
+      const uint64_t b = (uint64_t)it[i].chunk * C + it[i].hi;
       L.file = it[i].file;
       L.fs = A.off[it[i].file];
-      L.tail(it[i].s, A.off[it[i].file + 1], (uint64_t)it[i].chunk * C + it[i].hi);
+      if (b < it[i].fe)
+        L.tail_ni(ni[i], it[i].fe, b);
+      else
+        L.tail(it[i].s, it[i].fe, b);
     }
   K2_PHASE(3);
 }
