@@ -1562,11 +1562,16 @@ __device__ void layout_block(const LayoutArgs& A, uint8_t* s_kind, uint32_t* s_g
   __shared__ unsigned long long s_carry[5];  // items, entries, dense groups, skipped groups, dense entries
   __shared__ uint2 s_dense[kBlock];  // dense groups of the tile: group, first dense entry
   __shared__ uint32_t s_ndense;
+  __shared__ uint4 s_lst[kBlock];    // this block's list groups of the tile: group, first entry, first item, items
+  __shared__ uint32_t s_nlst;
   const uint32_t ndent_all = (uint32_t)((A.nchunks + kEntryChunks - 1) / kEntryChunks);
   if (threadIdx.x < 5) s_carry[threadIdx.x] = 0;
   __syncthreads();
   for (uint32_t g0 = 0; g0 < A.G; g0 += blockDim.x) {
-    if (threadIdx.x == 0) s_ndense = 0;
+    if (threadIdx.x == 0) {
+      s_ndense = 0;
+      s_nlst = 0;
+    }
     const uint32_t g = g0 + threadIdx.x;
     const uint64_t cnt = g < A.G ? A.gcount[g] : 0;
     const bool dense_want = cnt * 2 > A.nchunks;
@@ -1598,13 +1603,19 @@ __device__ void layout_block(const LayoutArgs& A, uint8_t* s_kind, uint32_t* s_g
       if (blockIdx.x == 0) A.gskip[g] = k == kGroupSkip ? 1 : 0;
     }
     if (k == kGroupList && g % gridDim.x == blockIdx.x)
-      for (uint64_t i = 0; i < nent; i++) {
-        const uint32_t first = (uint32_t)(i * kEntryItems);
-        A.entries[e0 + i] = make_uint4(g, (uint32_t)(s_carry[0] + ipre) + first,
-                                       (uint32_t)min<uint64_t>(kEntryItems, cnt - first), kGroupList);
-      }
+      s_lst[atomicAdd(&s_nlst, 1u)] = make_uint4(g, (uint32_t)e0, (uint32_t)(s_carry[0] + ipre), (uint32_t)cnt);
     if (k == kGroupDense) s_dense[atomicAdd(&s_ndense, 1u)] = make_uint2(g, (uint32_t)d0);
     __syncthreads();
+    // a list group's entries (a hundred for a group of 65 k items) by the whole block (one
+    // thread writing them in a row held its block ~5 us, profiles/r05/ab/er2)
+    for (uint32_t t = 0; t < s_nlst; t++) {
+      const uint4 lg = s_lst[t];
+      const uint32_t nl = (lg.w + kEntryItems - 1) / kEntryItems;
+      for (uint32_t i = threadIdx.x; i < nl; i += blockDim.x) {
+        const uint32_t first = i * kEntryItems;
+        A.entries[(size_t)lg.y + i] = make_uint4(lg.x, lg.z + first, min(kEntryItems, lg.w - first), kGroupList);
+      }
+    }
     // a dense group's entries (nchunks / kEntryChunks of them: thousands) over the grid
     for (uint32_t t = 0; t < s_ndense; t++) {
       const uint2 dg = s_dense[t];
