@@ -1067,10 +1067,7 @@ static int64_t next_prefix(const Prog& p, const uint8_t* b, size_t n, int64_t po
   return q ? (int64_t)((const uint8_t*)q - b) : -1;
 }
 
-namespace {
-std::atomic<uint64_t> g_regexp_uid{1};
-}
-Regexp::Regexp() : uid_(g_regexp_uid.fetch_add(1, std::memory_order_relaxed)) {}
+Regexp::Regexp() = default;
 Regexp::~Regexp() = default;
 
 std::shared_ptr<Regexp> Regexp::Compile(const std::string& src, std::string* err) {
@@ -1657,72 +1654,10 @@ struct TwoPass {
   }
 };
 
-// A thread's matchers, reused across FindAll calls of the same compiled regexp: building
-// one (two Pike VMs' sparse queues and a backtracker, sized by the program) cost ~10 k
-// cycles per call, most of the resolver's time for rules with many tiny windows (TSG_PROF:
-// aws-secret-access-key, 2,600 calls over 4.9 KB of windows, 25 Mcyc).  Runs leave the
-// matchers clean (queues emptied, visited rows cleared), keys are unique per regexp (never
-// a reused address), and an entry in use is never handed out twice.
-namespace {
-struct CachedTwoPass {
-  uint64_t uid = 0;
-  bool submatch = false;
-  int engine = 0;
-  bool busy = false;
-  uint64_t last = 0;
-  std::unique_ptr<TwoPass> m;
-};
-constexpr size_t kTwoPassCache = 64;
-struct TwoPassLease {
-  CachedTwoPass* c = nullptr;
-  std::unique_ptr<TwoPass> own;  // (a regexp already in use on this thread, or no slot)
-  TwoPass* m = nullptr;
-  ~TwoPassLease() {
-    if (c) c->busy = false;
-  }
-};
-void lease_two_pass(const Prog& p, uint64_t uid, bool submatch, int engine, TwoPassLease* l) {
-  thread_local std::vector<CachedTwoPass> cache(kTwoPassCache);
-  thread_local uint64_t tick = 0;
-  ++tick;
-  CachedTwoPass* victim = nullptr;
-  for (auto& c : cache) {
-    if (c.m && c.uid == uid && c.submatch == submatch && c.engine == engine) {
-      if (c.busy) {  // nested use: a matcher of its own
-        l->own = std::make_unique<TwoPass>(p, submatch, engine);
-        l->m = l->own.get();
-        return;
-      }
-      c.busy = true;
-      c.last = tick;
-      l->c = &c;
-      l->m = c.m.get();
-      return;
-    }
-    if (!c.busy && (!victim || c.last < victim->last)) victim = &c;
-  }
-  if (victim && !(victim->m && victim->uid == uid)) {
-    victim->m = std::make_unique<TwoPass>(p, submatch, engine);
-    victim->uid = uid;
-    victim->submatch = submatch;
-    victim->engine = engine;
-    victim->busy = true;
-    victim->last = tick;
-    l->c = victim;
-    l->m = victim->m.get();
-    return;
-  }
-  l->own = std::make_unique<TwoPass>(p, submatch, engine);
-  l->m = l->own.get();
-}
-}  // namespace
-
 void Regexp::FindAll(const uint8_t* b, size_t n, bool submatch, std::vector<int64_t>* out,
                      size_t lo, size_t start_hi, int engine) const {
   // regexp.allMatches (regexp/regexp.go)
-  TwoPassLease lease;
-  lease_two_pass(prog_, uid_, submatch, engine, &lease);
-  TwoPass& m = *lease.m;
+  TwoPass m(prog_, submatch, engine);
   int64_t end = (int64_t)n;
   int64_t pos = (int64_t)lo, prev_end = -1;
   int64_t hi = start_hi == SIZE_MAX ? end : (int64_t)std::min<size_t>(start_hi, n);
@@ -1753,9 +1688,7 @@ void Regexp::FindAllWindows(const uint8_t* b, size_t n, bool submatch,
   // Go's allMatches iteration, skipping the stretches in which no match can start:
   // `pos` and the previous match end carry from one window to the next, so a match
   // that runs past its window is handled exactly as the global iteration would.
-  TwoPassLease lease;
-  lease_two_pass(prog_, uid_, submatch, 0, &lease);
-  TwoPass& m = *lease.m;
+  TwoPass m(prog_, submatch);
   const int64_t end = (int64_t)n;
   int64_t pos = 0, prev_end = -1;
   for (const auto& w : iv) {

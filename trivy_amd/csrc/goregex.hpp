@@ -91,8 +91,6 @@ class Regexp {
  public:
   Regexp();
   ~Regexp();
-  Regexp(const Regexp&) = delete;  // (uid_ keys per-thread matchers bound to prog_)
-  Regexp& operator=(const Regexp&) = delete;
   // regexp.Compile; returns nullptr and sets *err on a syntax error.
   static std::shared_ptr<Regexp> Compile(const std::string& src, std::string* err);
 
@@ -143,7 +141,6 @@ class Regexp {
   std::vector<std::string> names_;
   Prog prog_;
   std::shared_ptr<Ast> ast_;
-  uint64_t uid_;  // unique per compiled regexp (the per-thread matcher cache's key)
 };
 
 }  // namespace tsg
