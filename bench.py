@@ -320,7 +320,8 @@ class DeviceRun:
 
 
 STAT_SUMS = ("batches", "sum_bytes", "sum_k1_ms", "sum_gate_ms", "sum_k2_ms", "sum_h2d_ms", "sum_d2h_ms",
-             "sum_resolve_ms", "sum_prep_ms", "sum_meta_ms")
+             "sum_resolve_ms", "sum_prep_ms", "sum_meta_ms", "sum_k1_clock_ms", "sum_chain_clock_ms",
+             "sum_post_k1_clock_ms")
 
 
 def _gbs(nbytes, ms):
@@ -559,6 +560,15 @@ def main():
                      "k1_listed_words_last_batch": last["k1f_listed"] if last["k1_filter"] else None,
                      "k1_verified_arrivals_last_batch": last["k1f_arrivals"] if last["k1_filter"] else None,
                      "k1_gates_k2_frac": _frac(_gbs(d["sum_bytes"], kern_ms)),
+                     # the same spans by the device wall clock stamped inside the kernels (first
+                     # block start to last block end, tsg_stats.*_clock_ms): frac_clock is K1's,
+                     # chain_frac_clock K1's start to K2's end, every kernel and gap between
+                     "frac_events": _frac(k1_gbs),
+                     "frac_clock": _frac(_gbs(d["sum_bytes"], d["sum_k1_clock_ms"])),
+                     "chain_frac_clock": _frac(_gbs(d["sum_bytes"], d["sum_chain_clock_ms"])),
+                     "k1_clock_ms_per_batch": round(d["sum_k1_clock_ms"] / nbat, 4),
+                     "chain_clock_ms_per_batch": round(d["sum_chain_clock_ms"] / nbat, 4),
+                     "post_k1_clock_ms_per_batch": round(d["sum_post_k1_clock_ms"] / nbat, 4),
                      "device_frac": _frac(_gbs(d["sum_bytes"], dev_ms)),
                      "aggregate": dict(agg, gpus=ngpus,
                                        definition="job bytes / max over GPUs of that GPU's device "

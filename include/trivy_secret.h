@@ -256,6 +256,12 @@ typedef struct tsg_stats {
   uint32_t event_chunks;
   /* 1: K1 ran as the filter-and-verify K1F (k1f_kernel), 0: as the automaton (k1_kernel) */
   uint32_t k1_filter;
+  /* last batch, by the device wall clock stamped inside the kernels (0 when K1 was not
+   * K1F): K1F's first block start to its last block end; K1F's start to K2's last block
+   * end (every kernel and gap of the chain); the gates pass's start to K2's end */
+  double k1_clock_ms, chain_clock_ms, post_k1_clock_ms;
+  /* their sums over the batches collected so far */
+  double sum_k1_clock_ms, sum_chain_clock_ms, sum_post_k1_clock_ms;
 } tsg_stats;
 int tsg_ctx_get_stats(const tsg_ctx* ctx, tsg_stats* out);
 

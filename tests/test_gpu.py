@@ -134,6 +134,29 @@ def test_k1f_batch_sizes(builtin, size):
         assert np.array_equal(kw, rkw) and np.array_equal(ev, rev)
 
 
+@pytest.mark.parametrize("grid", [1, 3])
+def test_k1f_many_tiles_per_wave(builtin, knob, grid):
+    """K1F's steady state: with the grid capped to 1 or 3 blocks, each wave
+    streams hundreds of tiles -- the in-flight tile rotation across loop iterations, carries
+    across iterations, ring drains mid-range and the ring's wrap-around -- and the bits and
+    events still equal k1_reference (dense literals: many listed words per wave)."""
+    import numpy as np
+    knob("k1f_grid", grid)
+    big, _ = corpus.make_corpus(12 << 20, seed=40 + grid, plants_per_mib=3000)
+    listed = []
+    for batch in (big, corpus.k1_edge_batch(builtin.k1_literals(), 3 + grid)):
+        ctx = S.GpuContext(builtin, 0, chunk_bytes=256, adapt_mib=0xFFFFFFFF)
+        ctx.upload(batch)
+        ctx.kernels()
+        kw, ev = ctx.k1_output(256)
+        listed.append(ctx.stats()["k1f_listed"])
+        ctx.close()
+        rkw, rev = builtin.k1_reference(batch, 256)
+        assert np.array_equal(kw, rkw) and np.array_equal(ev, rev)
+    # far more listed words per wave than its ring holds, so it drained and wrapped
+    assert listed[0] > 16 * grid * 256, listed
+
+
 def test_k1_adaptation_exact(builtin):
     """Frequent literals dropped from K1 after sampling: same findings as the exact CPU path."""
     batch, _ = corpus.make_corpus(8 << 20, seed=31, plants_per_mib=40)

@@ -42,6 +42,8 @@ def main():
     out = {"variant": os.environ.get("TSG_LIB_VARIANT", "default"), "bytes": nb, "rules": rules, "knobs": knobs,
            "k1_ms": round(med("k1_ms"), 4), "gate_ms": round(med("gate_ms"), 4),
            "k2_ms": round(med("k2_ms"), 4),
+           "k1_clk_ms": round(med("k1_clock_ms"), 4), "chain_clk_ms": round(med("chain_clock_ms"), 4),
+           "post_k1_clk_ms": round(med("post_k1_clock_ms"), 4),
            "k1_GBps": round(nb / med("k1_ms") / 1e6, 1),
            "dev_GBps": round(nb / (med("k1_ms") + med("gate_ms") + med("k2_ms")) / 1e6, 1),
            "k2_items": rows[-1]["k2_items"], "k2_entries": rows[-1]["k2_launches"],

@@ -84,7 +84,10 @@ class Stats(C.Structure):
                 ("sum_prep_ms", C.c_double), ("sum_meta_ms", C.c_double),
                 ("k1x_records", C.c_uint32), ("k1x_inline", C.c_uint32),
                 ("k1f_listed", C.c_uint32), ("k1f_arrivals", C.c_uint32),
-                ("event_chunks", C.c_uint32), ("k1_filter", C.c_uint32)]
+                ("event_chunks", C.c_uint32), ("k1_filter", C.c_uint32),
+                ("k1_clock_ms", C.c_double), ("chain_clock_ms", C.c_double), ("post_k1_clock_ms", C.c_double),
+                ("sum_k1_clock_ms", C.c_double), ("sum_chain_clock_ms", C.c_double),
+                ("sum_post_k1_clock_ms", C.c_double)]
 
 
 # (name, restype, argtypes) -- every symbol include/trivy_secret.h declares

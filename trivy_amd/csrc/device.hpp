@@ -35,10 +35,12 @@ struct HostOut {
   uint8_t* gskip = nullptr;     // [groups] 1 = K2 skipped the group (item capacity)
   Candidate* cand = nullptr;    // [cand_cap] host-mapped: K2 candidates copied out
   Candidate* cand_dev = nullptr;  // device address of `cand`
-  uint32_t* counts = nullptr;   // [32] 0 candidates, 1 event chunks, 2 K2 list entries,
+  uint32_t* counts = nullptr;   // [48] 0 candidates, 1 event chunks, 2 K2 list entries,
                                 // 3 dense entries, 5 items, 6 entries, 7 skipped groups,
-                                // 8-11 K2 diagnostics (TSG_K2_DIAG), 14-15 K1X, 16-17 K1F
+                                // 8-11 K2 diagnostics (TSG_K2_DIAG), 14-15 K1X, 16-17 K1F,
+                                // 32-39 kernel clock stamps (u64)
   uint32_t files_cap = 0, cand_cap = 0, groups = 0, kw_words = 0;
+  uint32_t wall_khz = 0;        // the device wall clock's rate (hipDeviceAttributeWallClockRate)
   // stage boundaries of the batch on its lane's stream: data H2D | offsets H2D | prep |
   // wait for the previous batch's kernels | K1 | gates | K2 | outputs; ev[kEvDone]
   // completes the batch
@@ -69,6 +71,9 @@ inline uint64_t slot_room_bytes(uint32_t files_cap) { return (128u << 10) + 8ull
 
 struct ScanTimes {  // HIP-event milliseconds of one batch on its lane
   float h2d = 0, meta = 0, wait = 0, prep = 0, k1 = 0, gates = 0, k2 = 0, out = 0;
+  // device wall clock (stamped inside the kernels): K1F's first block start to last block
+  // end; K1F start to K2's last block end; the gates pass's start to K2's end
+  float k1_clk = 0, chain_clk = 0, post_k1_clk = 0;
 };
 
 struct LaneState;  // HBM buffers + stream + events of one lane

@@ -67,7 +67,8 @@ constexpr __host__ __device__ int k1_threads(int ldsk) { return ldsk == 156 ? 10
 // lane reads its own bank) when the automaton leaves room for it; else 256 words
 constexpr uint32_t kK1RepBytes = 256 * 32 * 4;
 constexpr int kBlock = 256;
-constexpr int kCounts = 32;  // per-batch device counters (lane_create)
+constexpr int kCounts = 48;  // per-batch device counters (lane_create); 32..39: kernel clocks
+constexpr int kClk = 32;     // u64 clock stamps at counts + kClk (device wall clock, see K1FArgs::clk)
 constexpr int kPad = 256;     // zero bytes before and after the batch in HBM (>= K1 warm-up)
 #ifndef ITEMS_BPC
 #define ITEMS_BPC 8  // item passes: blocks per CU
@@ -610,14 +611,22 @@ __global__ void __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(4, 8))
 // starts sets its bit without a global load, and a literal inside the captured bytes is
 // compared without one: the verification of the last words of the range (which nothing
 // overlaps) costs LDS latency, not HBM round trips under full streaming load.
-constexpr uint32_t kFQueue = 128;                          // ring entries (32 B) per wave
+#ifndef K1F_DMA
+#define K1F_DMA 0  // > 0: tiles in flight through an LDS ring filled by LDS-DMA (measurement)
+#endif
+#ifndef K1F_QUEUE
+#define K1F_QUEUE (K1F_DMA ? 64 : 128)
+#endif
+constexpr uint32_t kFQueue = K1F_QUEUE;                    // ring entries (32 B) per wave
+static_assert(kFQueue >= 64 && (kFQueue & (kFQueue - 1)) == 0, "a tile lists up to 64 words");
 constexpr uint32_t kFEntBytes = 256 * 256;                 // 256 entries x 16 replicas x 16 B
 constexpr uint32_t kFQueueOff = kFEntBytes;
 #ifndef K1F_THREADS
 #define K1F_THREADS 1024
 #endif
 constexpr int kFThreads = K1F_THREADS;                     // one block per CU
-constexpr uint32_t kFImgOff = kFQueueOff + (kFThreads / 64) * kFQueue * 32;
+constexpr uint32_t kFDmaOff = kFQueueOff + (kFThreads / 64) * kFQueue * 32;  // [wave][K1F_DMA][1 KiB]
+constexpr uint32_t kFImgOff = kFDmaOff + (kFThreads / 64) * K1F_DMA * 1024;
 constexpr uint32_t kFCfOff = kFImgOff + kFImgMax;
 constexpr uint32_t kFCfMax = 512;                          // coarse file map entries in LDS
 constexpr uint32_t kFStOff = kFCfOff + 4 * kFCfMax;        // block counters (listed, arrivals, waves done)
@@ -642,6 +651,11 @@ struct K1FArgs {
   uint32_t* ev;     // zeroed by prep; ORed into
   uint32_t* hits;   // [nlit] verified arrivals per record (sampling pass) or null
   uint32_t* stats;  // [2] listed words, verified arrivals (zeroed by prep)
+  // null, or the batch's clock stamps (u64, zeroed by prep; device wall clock): [0] ~first
+  // block start (atomicMax of the complement = min), [1] last block end; the gates pass
+  // writes [2] ~its first block start, K2 [3] its last block end.  The kernels' own
+  // durations, beside the HIP events around their launches (bench.py reports both).
+  unsigned long long* clk;
 };
 
 // lane i <- lane i - 1, lane 0 <- old (DPP wave_shr:1, out-of-range source keeps old)
@@ -733,6 +747,31 @@ struct K1FLane {
 #pragma unroll
       for (int k = 3; k < 8; k++) r[8 + k] = k1f_and3(e[k - 3].x, e[k - 2].y, e[k - 1].z) & e[k].w;
     }
+#pragma unroll
+    for (int i = 0; i < 4; i++) g[i] = k1f_or3(r[4 * i], r[4 * i + 1], r[4 * i + 2]) | r[4 * i + 3];
+    const uint32_t m = k1f_flags(r[3], r[7], r[11], r[15]);
+    const uint32_t m1 = f_prev(m, cy.m), m2 = f_prev(m1, cy.m1);
+    cy.m = m;
+    cy.m1 = m1;
+    return k1f_runs(m, m1, m2);
+  }
+  // the same with all 16 entries read at once (one LDS round trip per tile, 64 VGPRs of
+  // entries; measurement build K1F_ALL16)
+  __device__ __forceinline__ uint32_t tile16(uint4 v, FCarry& cy, uint32_t (&g)[4]) const {
+    uint4 e[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) e[k] = entry(k < 4 ? v.x : k < 8 ? v.y : k < 12 ? v.z : v.w, k & 3);
+    const uint32_t ao = k1f_and3(e[13].x, e[14].y, e[15].z), bo = e[14].x & e[15].y, co = e[15].x;
+    const uint32_t ai = f_prev(ao, cy.a), bi = f_prev(bo, cy.b), ci = f_prev(co, cy.c);
+    cy.a = ao;
+    cy.b = bo;
+    cy.c = co;
+    uint32_t r[16];
+    r[0] = ai & e[0].w;
+    r[1] = k1f_and3(bi, e[0].z, e[1].w);
+    r[2] = k1f_and3(ci, e[0].y, e[1].z) & e[2].w;
+#pragma unroll
+    for (int k = 3; k < 16; k++) r[k] = k1f_and3(e[k - 3].x, e[k - 2].y, e[k - 1].z) & e[k].w;
 #pragma unroll
     for (int i = 0; i < 4; i++) g[i] = k1f_or3(r[4 * i], r[4 * i + 1], r[4 * i + 2]) | r[4 * i + 3];
     const uint32_t m = k1f_flags(r[3], r[7], r[11], r[15]);
@@ -851,6 +890,7 @@ struct K1FVerify {
 
 __global__ void __launch_bounds__(kFThreads) k1f_kernel(DevK1F d, K1FArgs A) {
   __shared__ __attribute__((aligned(16))) uint8_t smem[kFLds];
+  if (A.clk && threadIdx.x == 0) atomicMax(&A.clk[0], ~(unsigned long long)wall_clock64());
   {  // the entries (replicated) and the image, every load issued before the stores
     constexpr uint32_t kRep = 256u * 16u / kFThreads, kImg = kFImgMax / 16 / kFThreads;
     uint4 e[kRep], m[kImg];
@@ -917,7 +957,11 @@ __global__ void __launch_bounds__(kFThreads) k1f_kernel(DevK1F d, K1FArgs A) {
   const uint8_t* base = A.data + 16u * lane;
   auto body = [&](uint4 v, uint32_t t) __attribute__((always_inline)) {
     const uint32_t pos = t * kFTile + 16u * lane;
+#if K1F_ALL16
+    const uint32_t rb = L.tile16(v, cy, g);
+#else
     const uint32_t rb = L.tile(v, cy, g);
+#endif
     // run events: one atomic per chunk (the leader lane of each chunk in the tile)
     const uint64_t bu = __ballot(rb & 1u), bd = __ballot(rb & 2u);
     if (__builtin_expect(bu | bd, 0)) {
@@ -937,6 +981,7 @@ __global__ void __launch_bounds__(kFThreads) k1f_kernel(DevK1F d, K1FArgs A) {
     const uint64_t hb = __ballot(bun != 0);
     if (__builtin_expect(hb != 0, 0)) {
       const uint32_t n = (uint32_t)__popcll(hb);
+      if (kFQueue < 128 && qn + n > kFQueue) drain(qn);  // (a small ring: room for the tile's words)
       const uint32_t wprev = f_prev(v.w, vw);  // bytes pos-4 .. pos-1 (all lanes: DPP)
       if (bun) {
         const uint32_t slot = __builtin_amdgcn_mbcnt_hi((uint32_t)(hb >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)hb, 0u));
@@ -952,6 +997,44 @@ __global__ void __launch_bounds__(kFThreads) k1f_kernel(DevK1F d, K1FArgs A) {
     }
     vw = v.w;
   };
+#if K1F_DMA
+  // tiles through an LDS ring of K1F_DMA slots per wave, filled by LDS-DMA (no VGPRs held
+  // by tiles in flight).  Slot k of the unrolled loop holds tile t + k.  The DMA is issued
+  // in asm so the compiler adds no vmcnt(0) of its own; the waits are counted here: tile t+k
+  // has landed once at most K1F_DMA - 1 younger vector-memory operations are outstanding
+  // (others -- verification loads, event atomics -- only make the wait stricter).
+  constexpr uint32_t kD = K1F_DMA;
+  uint8_t* dring = smem + kFDmaOff + wave * kD * 1024u;
+  const uint32_t dbase = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint8_t*)dring);
+  auto dma = [&](uint32_t t, uint32_t k) __attribute__((always_inline)) {
+    const uint8_t* g = base + (size_t)t * kFTile;
+    uint32_t keep;
+#if K1F_NT
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off nt\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(g), "s"(dbase + k * 1024u) : "memory");
+#else
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(g), "s"(dbase + k * 1024u) : "memory");
+#endif
+  };
+#pragma unroll
+  for (uint32_t k = 0; k < kD; k++) dma(t0 + k, k);
+  uint32_t t = t0;
+  for (; t < t1; t += kD) {
+    if (t + 2 * kD > t1 && qn) drain(qn);
+#pragma unroll
+    for (uint32_t k = 0; k < kD; k++) {
+      if (t + k < t1) {
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kD - 1) : "memory");
+        const uint4 v = *(const uint4*)(dring + k * 1024u + 16u * lane);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        dma(t + kD + k, k);  // (past the last tile: inside the batch's zero tail)
+        body(v, t + k);
+      }
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#else
   uint4 p[kFDepth];
 #pragma unroll
   for (uint32_t k = 0; k < kFDepth; k++) p[k] = f_tile_load(base + (t0 + k) * kFTile);
@@ -964,13 +1047,18 @@ __global__ void __launch_bounds__(kFThreads) k1f_kernel(DevK1F d, K1FArgs A) {
 #pragma unroll
     for (uint32_t k = 0; k < kFDepth; k++) {
       const uint4 v = p[k];
+#if K1F_NOLOAD  // (timing only: the wave's first tiles again and again, from L2)
+      p[k] = *(const uint4*)(base + (t0 + k) * kFTile);
+#else
       p[k] = f_tile_load(base + (t + kFDepth + k) * kFTile);
+#endif
       body(v, t + k);
     }
   }
 #pragma unroll
   for (uint32_t k = 0; k < kFDepth - 1; k++)
     if (t + k < t1) body(p[k], t + k);
+#endif
   if (qn) drain(qn);
   // the counters: per wave, per block in LDS, one global atomic per block (a same-address
   // atomic from every lane or wave at the end of the kernel serialised into its tail:
@@ -990,6 +1078,7 @@ __global__ void __launch_bounds__(kFThreads) k1f_kernel(DevK1F d, K1FArgs A) {
       const uint32_t bl = atomicAdd(&bst[0], 0u), ba = atomicAdd(&bst[1], 0u);
       if (bl) atomicAdd(&A.stats[0], bl);
       if (ba) atomicAdd(&A.stats[1], ba);
+      if (A.clk) atomicMax(&A.clk[1], (unsigned long long)wall_clock64());
     }
   }
 }
@@ -1373,8 +1462,10 @@ struct GateArgs {
   const unsigned long long* kwg;
   const unsigned long long* galw;
   unsigned long long* ggate;
+  unsigned long long* clk;  // K1FArgs::clk
 };
 __global__ void __launch_bounds__(kBlock) gates_kernel(GateArgs A) {
+  if (threadIdx.x == 0) atomicMax(&A.clk[2], ~(unsigned long long)wall_clock64());
   if (blockIdx.x < A.ev_blocks)
     ev_compact_block(A.ev, A.nchunks, A.evlist, A.nev, blockIdx.x, A.ev_blocks);
   else
@@ -1700,6 +1791,7 @@ struct K2Args {
   // XCC_ID << 32 | HW_ID, then (K2_TRACE_CTR builds only) replayed words, candidates,
   // tail bytes, longest tail} written by the block that ran it (TSG_K2_TRACE)
   unsigned long long* etrace;
+  unsigned long long* clk;  // K1FArgs::clk
 };
 constexpr int kTraceW = 8;
 #ifdef K2_TRACE_CTR  // measurement builds: per-entry counters of the running entry
@@ -2283,7 +2375,10 @@ __device__ __forceinline__ void k2_run(const DevDFA* __restrict__ dfas, const K2
     __syncthreads();
 #endif
     prev = e;
-    if (e >= E) break;
+    if (e >= E) {
+      if (threadIdx.x == 0) atomicMax(&A.clk[3], (unsigned long long)wall_clock64());
+      break;
+    }
     const uint4 en = entries[e];
     const uint32_t g = __builtin_amdgcn_readfirstlane(en.x);
     const DevDFA& d = dfas[g];  // (a reference: uniform fields load into SGPRs, no copy)
@@ -2891,7 +2986,9 @@ static int upload_k1f(DeviceRules* r) {
 // one K1F launch over the first ntiles tiles of the batch
 static int launch_k1f(DeviceRules* r, const K1FArgs& A, hipStream_t st) {
   const uint32_t wpb = kFThreads / 64;
-  const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>((A.ntiles + wpb - 1) / wpb, (uint64_t)r->cus));
+  uint64_t cap = (uint64_t)r->cus;
+  if (const int64_t g = knobs().k1f_grid.load()) cap = std::min<uint64_t>(cap, (uint64_t)g);  // (test knob)
+  const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>((A.ntiles + wpb - 1) / wpb, cap));
   k1f_kernel<<<grid, kFThreads, 0, st>>>(r->k1f, A);
   HIP_TRY(hipGetLastError());
   return TSG_OK;
@@ -2914,6 +3011,7 @@ static int adapt_k1f(DeviceRules* r, LaneState* l, const K1FArgs& A0, const uint
   A.ntiles = std::min<uint32_t>(A0.ntiles, (16u << 20) / kFTile);
   A.hits = r->d_fhits;
   A.stats = l->counts + 24;  // (the batch's own counters stay those of its real launch)
+  A.clk = nullptr;
   int rc;
   if ((rc = launch_k1f(r, A, l->st))) return rc;
   std::vector<uint32_t> hits(std::max<uint32_t>(1, nrec));
@@ -3150,6 +3248,11 @@ int host_out_alloc(const DeviceRules* d, uint32_t files_cap, HostOut* o) {
   if ((e = hipHostMalloc((void**)&h.blk, bytes, hipHostMallocMapped)) != hipSuccess) return fail_free(e, "hipHostMalloc");
   if ((e = hipHostGetDevicePointer((void**)&h.blk_dev, h.blk, 0)) != hipSuccess) return fail_free(e, "hipHostGetDevicePointer");
   h.counts = (uint32_t*)h.blk;
+  {
+    int khz = 0;
+    if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, d->device) == hipSuccess && khz > 0)
+      h.wall_khz = (uint32_t)khz;
+  }
   h.gskip = h.blk + o_gskip;
   h.ovf = h.blk + o_ovf;
   h.kw = (uint32_t*)(h.blk + o_kw);
@@ -3281,7 +3384,7 @@ int enqueue_scan(DeviceRules* r, LaneState* l, const ScanInput& in, HostOut* out
   const uint64_t adapt_bytes = r->adapt_mib == 0xFFFFFFFFu ? ~0ull : (uint64_t)(r->adapt_mib ? r->adapt_mib : 16) << 20;
   if (k1f) {
     K1FArgs A{data, l->off, l->cf, (uint32_t)total, C, F, (uint32_t)((total + kFTile - 1) / kFTile), F ? (uint32_t)ncf : 0u,
-              l->kw, l->ev_bits, nullptr, l->counts + 16};
+              l->kw, l->ev_bits, nullptr, l->counts + 16, (unsigned long long*)(l->counts + kClk)};
     if (!r->adapted && total >= adapt_bytes && (rc = adapt_k1f(r, l, A, in.data))) return rc;
     if (total && (rc = launch_k1f(r, A, st))) return rc;
   } else if (!r->adapted && k1_items >= 64 && total >= adapt_bytes) {
@@ -3330,7 +3433,8 @@ int enqueue_scan(DeviceRules* r, LaneState* l, const ScanInput& in, HostOut* out
   const bool work = F && G && nchunks;
   if (work) {
     const uint32_t cgrid = (uint32_t)std::min<uint64_t>((nchunks + kEvPer * kBlock - 1) / (kEvPer * kBlock), (uint64_t)r->grid);
-    GateArgs GA{l->ev_bits, nchunks, l->evlist, l->counts + 1, cgrid, l->kw, F, W, r->GW, r->d_kwg, r->d_galw, l->ggate};
+    GateArgs GA{l->ev_bits, nchunks, l->evlist, l->counts + 1, cgrid, l->kw, F, W, r->GW, r->d_kwg, r->d_galw, l->ggate,
+                (unsigned long long*)(l->counts + kClk)};
     gates_kernel<<<cgrid + (F + kBlock - 1) / kBlock, kBlock, 0, st>>>(GA);
     HIP_TRY(hipGetLastError());
     // both items passes (bcount holds grid x G); ITEMS_BPC blocks per CU
@@ -3378,6 +3482,7 @@ int enqueue_scan(DeviceRules* r, LaneState* l, const ScanInput& in, HostOut* out
     if (trace && (rc = ensure(&l->etrace, &l->etrace_cap, (size_t)entries_cap * kTraceW))) return rc;
     if (trace) HIP_TRY(hipMemsetAsync(l->etrace, 0, sizeof(unsigned long long) * entries_cap * kTraceW, st));
     A.etrace = trace ? l->etrace : nullptr;
+    A.clk = (unsigned long long*)(l->counts + kClk);
     // one block per resident slot (the grids are persistent)
     if (r->k2_rich)
       hipLaunchKernelGGL(k2_kernel_rich, dim3(r->k2_grid), dim3(kK2Block), r->max_lds, st, (const DevDFA*)r->d_groups, A);
@@ -3438,6 +3543,14 @@ int batch_times(const HostOut* o, ScanTimes* t) {
   t->gates = x[5];
   t->k2 = x[6];
   t->out = x[7];
+  // the kernels' own spans by the device wall clock (stamps in counts + kClk; 0 if a
+  // kernel did not run)
+  const unsigned long long* c = (const unsigned long long*)(o->counts + kClk);
+  const double per_ms = o->wall_khz ? (double)o->wall_khz : 100000.0;
+  const unsigned long long k1s = ~c[0], k1e = c[1], k2e = c[3];
+  t->k1_clk = c[0] && k1e > k1s ? (float)((k1e - k1s) / per_ms) : 0.f;
+  t->chain_clk = c[0] && k2e > k1s ? (float)((k2e - k1s) / per_ms) : 0.f;
+  t->post_k1_clk = c[2] && k2e > ~c[2] ? (float)((k2e - ~c[2]) / per_ms) : 0.f;
   return TSG_OK;
 }
 

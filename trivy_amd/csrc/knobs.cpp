@@ -37,6 +37,10 @@ extern "C" int tsg_test_knob(const char* name, const char* value) {
   else if (!strcmp(name, "emu_wordrec")) k.emu_wordrec = x;
   else if (!strcmp(name, "k1_automaton")) k.k1_automaton = x;
   else if (!strcmp(name, "group_states")) k.group_states = x;
+  else if (!strcmp(name, "k1f_grid")) {  // cap on K1F's blocks: many tiles per wave in small tests
+    if (x < 0) return fail(TSG_ERR_ARG, "k1f_grid must be >= 0");
+    k.k1f_grid = x;
+  }
   else if (!strcmp(name, "group_table_kib")) {
     if (x < 0 || x > 64) return fail(TSG_ERR_ARG, "group_table_kib must be 0..64");
     k.group_table_kib = x;

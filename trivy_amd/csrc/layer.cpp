@@ -47,16 +47,16 @@ int open_at_retry(int dfd, const char* path, int flags) {
 }
 
 // A failed open of a file the walk listed (analyzer.go:411-416): a permission error skips the
-// file, and so does a file gone or replaced since the listing (ENOENT, ELOOP under
-// O_NOFOLLOW, ENOTDIR), which the walk would not have listed; any other error -- a descriptor
-// table still full after open_at_retry's wait included -- fails the scan ("unable to open").
+// file; any other error -- a file gone since the listing, or a descriptor table still full
+// after open_at_retry's wait -- fails the scan ("unable to open"), as os.Open's error does
+// there.  Files are opened following symlinks, as os.Open does (fs.go:66-70).
 // Thread-safe: the parallel readers record the first such error.
 struct OpenErr {
   std::mutex m;
   std::atomic<bool> set{false};
   std::string msg;
   void add(int e, const std::string& path) {
-    if (e == EACCES || e == EPERM || e == ENOENT || e == ELOOP || e == ENOTDIR) return;
+    if (e == EACCES || e == EPERM) return;  // fs.ErrPermission
     std::lock_guard<std::mutex> g(m);
     if (!set) msg = "unable to open " + path + ": " + strerror(e);
     set = true;
@@ -1249,7 +1249,7 @@ int fs_collect(const tsg_ruleset* rs, const char* root, const char* const* skip_
         }
         return true;
       }
-      const int fd = open_at_retry(dfd, dfd >= 0 ? name : path.c_str(), O_RDONLY | O_NOFOLLOW | O_CLOEXEC);
+      const int fd = open_at_retry(dfd, dfd >= 0 ? name : path.c_str(), O_RDONLY | O_CLOEXEC);
       if (fd < 0) {  // analyzer.go:411-416 (OpenErr)
         oe.add(errno, path);
         return true;
@@ -1480,7 +1480,7 @@ extern "C" int tsg_fs_pack_shard(const tsg_ruleset* rs, const char* root, const 
     tsg::OpenErr oe;
     tsg::pool_for(mine.size(), 16, [&](size_t k) {
       const tsg::FsFile& f = *files[mine[k]];
-      const int fd = tsg::open_at_retry(-1, f.full.c_str(), O_RDONLY | O_NOFOLLOW | O_CLOEXEC);
+      const int fd = tsg::open_at_retry(-1, f.full.c_str(), O_RDONLY | O_CLOEXEC);
       if (fd < 0) {  // analyzer.go:411-416 (OpenErr)
         oe.add(errno, f.full);
         return;
@@ -1558,7 +1558,7 @@ extern "C" int tsg_fs_scan(tsg_ctx* ctx, const char* root, const char* const* sk
     tsg::OpenErr oe;
     rc = tsg::scan_in_pieces(ctx, L.get(), [&](size_t k, uint8_t* dst) -> uint64_t {
       const tsg::FsFile& f = *files[kept[k]];
-      const int fd = tsg::open_at_retry(-1, f.full.c_str(), O_RDONLY | O_NOFOLLOW | O_CLOEXEC);
+      const int fd = tsg::open_at_retry(-1, f.full.c_str(), O_RDONLY | O_CLOEXEC);
       if (fd < 0) {  // analyzer.go:411-416 (OpenErr)
         oe.add(errno, f.full);
         drop[k] = 1;

@@ -93,7 +93,7 @@ struct Batch {
   std::unique_ptr<tsg_result> res;
   BatchResult br;
   ScanTimes t;
-  uint32_t counts[32] = {};
+  uint32_t counts[48] = {};
   double resolve_ms = 0;
   uint64_t files_found = 0;
 };
@@ -310,6 +310,12 @@ void update_stats(tsg_ctx* c, const Batch& b) {
   s.k1x_inline = b.counts[15];
   s.k1f_listed = b.counts[16];
   s.k1f_arrivals = b.counts[17];
+  s.k1_clock_ms = b.t.k1_clk;
+  s.chain_clock_ms = b.t.chain_clk;
+  s.post_k1_clock_ms = b.t.post_k1_clk;
+  s.sum_k1_clock_ms += b.t.k1_clk;
+  s.sum_chain_clock_ms += b.t.chain_clk;
+  s.sum_post_k1_clock_ms += b.t.post_k1_clk;
   s.event_chunks = b.counts[1];
   s.k1_filter = c->dr && device_rules_k1_filter(c->dr) && b.bytes + (1u << 16) < (1ull << 32) ? 1u : 0u;
   s.k1_hot_states = c->dr ? device_rules_hot_states(c->dr) : 0;

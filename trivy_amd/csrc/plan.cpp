@@ -1051,6 +1051,14 @@ void resolve_batch(const Ruleset& rs, const Plan& plan, const BatchView& b,
   }, 1);
   out->res.clear();
   out->res.resize(nslots);
+  // a sparse keyword array holds only the rows the device wrote (flag bit 2): every file
+  // that needs resolution must have one (reading any other row would read stale bits).
+  // Checked here on the caller, not inside the parallel pass: a throw from a pool worker
+  // would terminate the process.
+  if (ko.sparse_kw)
+    for (uint32_t f : need_files)
+      if (b.offsets[f + 1] != b.offsets[f] && !(ko.overflow[f] & 4))
+        throw std::runtime_error("keyword row of a resolved file not written");
 
   static const bool prof = getenv("TSG_PROF") != nullptr;
   if (prof)
@@ -1095,9 +1103,7 @@ void resolve_batch(const Ruleset& rs, const Plan& plan, const BatchView& b,
       scan_file(rs, std::string(pp, pn), content, 0, nullptr, &res);
       return;
     }
-    // a sparse keyword array holds only the rows the device wrote (flag bit 2): every file
-    // that needs resolution has one; reading any other row would read stale bits
-    if (ko.sparse_kw && !(ko.overflow[f] & 4)) throw std::runtime_error("keyword row of a resolved file not written");
+    // (a sparse keyword array has this file's row: checked before the parallel pass)
     const uint32_t* kw = ko.kw + (size_t)f * plan.kw_words;
     // folding runes present: bit 0 U+0130, bit 1 U+212A, bit 2 U+017F
     uint32_t fbbits = 0;
