@@ -1,11 +1,14 @@
 """GPU parity tests (MI355X): the HIP path through the C ABI against the reference's
-fixtures, the oracle, the exact CPU path and the emulated kernel algorithm."""
+fixtures, the oracle (through its committed results: tests/golden/oracle_small/, made by
+tools/gen_oracle_fixtures.py --samples; no oracle code runs on the GPU box), the exact CPU
+path and the emulated kernel algorithm."""
 import os
 
 import pytest
 
 from tests.conftest import GOLDEN
 from tests.helpers import canon_secret, reference_cases
+from tools.gen_oracle_fixtures import sample_expect
 from trivy_amd import corpus
 from trivy_amd import secret as S
 
@@ -176,18 +179,28 @@ def test_small_files_vs_cpu_exact(builtin):
     assert builtin.ScanBatch(batch, device=0) == builtin.ScanBatch(batch, nthreads=16)
 
 
+def _vs_sample(name, args, got):
+    """got == the oracle's results for sample `name` (tools/gen_oracle_fixtures.py ran
+    oracle/secret.py over the same seeded inputs; tests/golden/oracle_small/), file by file;
+    returns the number of findings."""
+    want = sample_expect(name, args)
+    n = 0
+    for a, g, w in zip(args, got, want):
+        assert canon_secret(g) == w, a.FilePath
+        n += len(w["Findings"] or [])
+    assert len(got) == len(want)
+    return n
+
+
+def _args_of(b, every=1):
+    return [S.ScanArgs(b.path(i), bytes(b.data[int(b.offsets[i]):int(b.offsets[i + 1])]))
+            for i in range(0, b.nfiles, every)]
+
+
 def test_corpus_vs_oracle(builtin):
-    from oracle import secret as O
     batch, _ = corpus.make_corpus(256 << 10, seed=7, plants_per_mib=300)
     got = builtin.ScanBatch(batch, device=0)
-    osc = O.NewScanner(None)
-    n = 0
-    for i in range(batch.nfiles):
-        c = bytes(batch.data[int(batch.offsets[i]):int(batch.offsets[i + 1])])
-        want = canon_secret(osc.Scan(batch.path(i), c))
-        assert canon_secret(got[i]) == want, i
-        n += len(want["Findings"] or [])
-    assert n > 20
+    assert _vs_sample("corpus", _args_of(batch), got) > 20
 
 
 def test_corpus_vs_cpu_exact(builtin):
@@ -253,20 +266,12 @@ def test_fold_runes_gpu_vs_oracle(builtin):
     on the device, file by file against the oracle.  Derived behaviour (Go 1.19's
     unicode.SimpleFold / unicode.ToLower), not pinned by a
     reference fixture."""
-    from oracle import secret as O
     batch = corpus.fold_runes_batch(3, nbytes=128 << 10, plants=400, frac=0.6)
     data = bytes(batch.data[:int(batch.offsets[-1])])
     for rune in ("\u0130", "\u212a", "\u017f"):
         assert data.count(rune.encode()) > 5, rune
     got = builtin.ScanBatch(batch, device=0)
-    osc = O.NewScanner(None)
-    nf = 0
-    for i in range(batch.nfiles):
-        c = bytes(batch.data[int(batch.offsets[i]):int(batch.offsets[i + 1])])
-        want = canon_secret(osc.Scan(batch.path(i), c))
-        assert canon_secret(got[i]) == want, batch.path(i)
-        nf += len(want["Findings"] or [])
-    assert nf > 10
+    assert _vs_sample("fold_runes", _args_of(batch), got) > 10
 
 
 @pytest.mark.parametrize("chunk", [64, 256])
@@ -426,7 +431,6 @@ def test_source_tree_config0_gpu(tmp_path):
     """configs[0] (8 MiB tree): `trivy fs` secret analysis on the device through the native
     fs ingest == the exact CPU path on every file and the oracle on every 32nd file (the
     Python oracle runs at 15-60 KB/s), and the sorted AnalysisResult == the CPU path's."""
-    from oracle import secret as O
     from trivy_amd import analyzer as A
     from trivy_amd import configs
     from trivy_amd import walker as W
@@ -437,14 +441,7 @@ def test_source_tree_config0_gpu(tmp_path):
     fs = W.NativeFS(an.scanner, root)
     got = an.scanner.ScanBatch(fs.batch, device=0)
     assert got == an.scanner.ScanBatch(fs.batch, nthreads=16)
-    osc = O.NewScanner(None)
-    n = 0
-    for i in range(0, fs.batch.nfiles, 32):
-        c = bytes(fs.batch.data[int(fs.batch.offsets[i]):int(fs.batch.offsets[i + 1])])
-        want = canon_secret(osc.Scan(fs.batch.path(i), c))
-        assert canon_secret(got[i]) == want, fs.batch.path(i)
-        n += len(want["Findings"] or [])
-    assert n > 5
+    assert _vs_sample("config0_tree", _args_of(fs.batch, 32), got[::32]) > 5
     assert W.analyze_fs(an, root, device=0) == W.analyze_fs(an, root)
 
 
@@ -495,7 +492,6 @@ def test_multi_two_contexts_one_device_gpu(builtin):
     """tsg_multi with two contexts on device 0 in one process (the one-GPU rehearsal of
     the node-wide dispatcher): LPT shards, results in input order == exact CPU path, and
     the oracle on a sample."""
-    from oracle import secret as O
     b, _ = corpus.make_corpus(24 << 20, seed=77, plants_per_mib=40)
     m = S.MultiGpu(builtin, [0, 0], slot_mib=4)
     got = m.scan_batch(b)
@@ -503,10 +499,7 @@ def test_multi_two_contexts_one_device_gpu(builtin):
     m.close()
     assert got == builtin.ScanBatch(b, nthreads=16)
     assert min(per) > 0 and sum(per) == int(b.offsets[-1])
-    osc = O.NewScanner(None)
-    for i in range(0, b.nfiles, 97):
-        c = bytes(b.data[int(b.offsets[i]):int(b.offsets[i + 1])])
-        assert canon_secret(got[i]) == canon_secret(osc.Scan(b.path(i), c)), b.path(i)
+    _vs_sample("multi", _args_of(b, 97), got[::97])
 
 
 def test_slot_ingest_gpu(tmp_path):
@@ -514,7 +507,6 @@ def test_slot_ingest_gpu(tmp_path):
     tsg_layer_pack_slot): the slot holds exactly the pageable pack's batch,
     its device scan equals the exact CPU path on every file and the oracle on a sample."""
     import numpy as np
-    from oracle import secret as O
     from trivy_amd import analyzer as A
     from trivy_amd import configs
     from trivy_amd import walker as W
@@ -525,17 +517,14 @@ def test_slot_ingest_gpu(tmp_path):
     root = str(tmp_path / "tree")
     configs.source_tree(root, 6 << 20, seed=3)
     tar = configs.layer_tar(6 << 20, seed=5, binary_frac=0.1)
-    osc = O.NewScanner(None)
-    for got, ref in [(W.SlotIngest.fs(ctx, root), W.NativeFS(sc, root)),
-                     (W.SlotIngest.layer(ctx, tar), W.NativeLayer(sc, tar))]:
+    for name, got, ref in [("slot_fs", W.SlotIngest.fs(ctx, root), W.NativeFS(sc, root)),
+                           ("slot_layer", W.SlotIngest.layer(ctx, tar), W.NativeLayer(sc, tar))]:
         assert np.array_equal(got.batch.offsets, ref.batch.offsets)
         n = int(ref.batch.offsets[-1])
         assert bytes(got.batch.data[:n]) == bytes(ref.batch.data[:n])
         res = got.scan()
         assert res == sc.ScanBatch(ref.batch, nthreads=16)
-        for i in range(0, ref.batch.nfiles, 41):
-            c = bytes(ref.batch.data[int(ref.batch.offsets[i]):int(ref.batch.offsets[i + 1])])
-            assert canon_secret(res[i]) == canon_secret(osc.Scan(ref.batch.path(i), c)), ref.batch.path(i)
+        _vs_sample(name, _args_of(ref.batch, 41), res[::41])
         got.release()
     ctx.close()
 
@@ -628,7 +617,6 @@ def test_file_larger_than_slot_gpu():
     """A file larger than the context's pinned slot (slot_mib=1: a 3 MiB file, and a 1 MiB
     one just over it) gets a piece of its own; the slot and the lane's HBM buffers grow on
     the device (layer.cpp scan_in_pieces, tsg_slot_acquire).  Every file == the oracle."""
-    from oracle import secret as O
     from trivy_amd import analyzer as A
     from trivy_amd import configs
     from trivy_amd import walker as W
@@ -642,11 +630,5 @@ def test_file_larger_than_slot_gpu():
     ref = W.NativeLayer(sc, tar)
     b = ref.batch
     assert paths == [b.path(i) for i in range(b.nfiles)]
-    osc = O.NewScanner(None)
-    nfind = 0
-    for i in range(b.nfiles):
-        c = bytes(b.data[int(b.offsets[i]):int(b.offsets[i + 1])])
-        want = canon_secret(osc.Scan(paths[i], c))
-        assert canon_secret(res[i]) == want, paths[i]
-        nfind += len(want["Findings"] or [])
+    nfind = _vs_sample("big_layer", _args_of(b), res)
     assert "/opt/big/text0.log" in paths and nfind > 20

@@ -1,10 +1,12 @@
 """configs[3] / configs[4] parity on the device: HIP kernels + host resolution through the
-C ABI, file by file against the oracle (oracle/secret.py, a restatement of scanner.go) and
+C ABI, file by file against the oracle (oracle/secret.py, a restatement of scanner.go, through
+its committed results in tests/golden/oracle_small/) and
 against the exact CPU path on larger batches.  No reference fixture covers these rule
 sets; the oracle is pinned by the reference fixtures (test_oracle_reference.py)."""
 import pytest
 
 from tests.helpers import canon_secret
+from tools.gen_oracle_fixtures import sample_expect
 from trivy_amd import analyzer as A
 from trivy_amd import configs
 from trivy_amd import secret as S
@@ -18,14 +20,15 @@ def user1000():
     return doc, S.NewScanner(S.config_from_dict(doc))
 
 
-def _vs_oracle(doc, args, got):
-    from oracle import secret as O
-    osc = O.NewScanner(O.config_from_dict(doc))
+def _vs_oracle(name, args, got):
+    """got == the oracle's results for sample `name` (oracle/secret.py over the same seeded
+    inputs, committed under tests/golden/oracle_small/ by tools/gen_oracle_fixtures.py)."""
     n = 0
-    for a, g in zip(args, got):
-        want = canon_secret(osc.Scan(a.FilePath, a.Content))
-        assert canon_secret(g) == want, a.FilePath
-        n += len(want["Findings"] or [])
+    want = sample_expect(name, args)
+    assert len(want) == len(got)
+    for a, g, w in zip(args, got, want):
+        assert canon_secret(g) == w, a.FilePath
+        n += len(w["Findings"] or [])
     return n
 
 
@@ -93,7 +96,7 @@ def test_user_rules_1000_gpu_vs_oracle(user1000):
     doc, sc = user1000
     args = configs.mixed_batch(doc, 256 << 10, seed=61, plants_per_file=0.6)
     got = sc.ScanBatch(args, device=0)
-    assert _vs_oracle(doc, args, got) > 10
+    assert _vs_oracle("user1000", args, got) > 10
 
 
 def test_user_rules_1000_gpu_vs_exact(user1000):
@@ -110,7 +113,7 @@ def test_allow_exclude_binary_gpu_vs_oracle():
     args = configs.mixed_batch(doc, 256 << 10, seed=62, plants_per_file=0.5, binary_frac=0.3)
     args = [a for a in args if not A.IsBinary(a.Content, len(a.Content))]
     got = sc.ScanBatch(args, device=0)
-    assert _vs_oracle(doc, args, got) > 5
+    assert _vs_oracle("allow_exclude", args, got) > 5
 
 
 def test_allow_exclude_binary_gpu_vs_exact():

@@ -95,15 +95,15 @@ LAYER_WORKER = textwrap.dedent("""
         want, opq2, wh2 = W.analyze_layer(an, io.BytesIO(tar))
         assert [canon_secret(s) for s in got] == [canon_secret(s) for s in want]
         assert (opq, wh) == (opq2, wh2) and len(got) > 10
-        if device is not None:  # the device union against the oracle on a sample
-            from oracle import secret as O
-            osc = O.NewScanner(None)
+        if device is not None:  # the device union against the oracle's committed results
+            from tools.gen_oracle_fixtures import sample_expect
             lay = W.NativeLayer(an.scanner, tar)
             b = lay.batch
-            content = {b.path(i): bytes(b.data[int(b.offsets[i]):int(b.offsets[i + 1])])
-                       for i in range(b.nfiles)}
+            args = [S.ScanArgs(b.path(i), bytes(b.data[int(b.offsets[i]):int(b.offsets[i + 1])]))
+                    for i in range(b.nfiles)]
+            want = dict(zip([a.FilePath for a in args], sample_expect("two_rank_layer", args)))
             for s in got[::4]:
-                assert canon_secret(s) == canon_secret(osc.Scan(s["FilePath"], content[s["FilePath"]]))
+                assert canon_secret(s) == want[s["FilePath"]]
         print("OK", len(got))
     else:
         assert out is None

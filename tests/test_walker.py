@@ -213,8 +213,9 @@ def test_native_layer_gpu_vs_oracle(analyzer):
     native layer ingest of a seeded layer with whiteouts, an opaque dir, system / .git /
     node_modules trees and a --skip-dirs entry (walker/tar.go:33-86), the "/" prefix of image
     files (analyzer/secret/secret.go:94-96), then the device scan; every 16th scanned file
-    and every file with findings == oracle Scan of the same path and content."""
-    from oracle import secret as O
+    == oracle Scan of the same path and content, for every file (the oracle's results are
+    committed: tests/golden/oracle_small/layer36.json.gz)."""
+    from tools.gen_oracle_fixtures import sample_expect
     from trivy_amd import configs
     tar = configs.layer_tar(12 << 20, seed=36)
     lay = W.NativeLayer(analyzer.scanner, tar, skip_dirs=["/deep"])
@@ -225,17 +226,13 @@ def test_native_layer_gpu_vs_oracle(analyzer):
                    for p in paths)
     assert lay.wh and lay.opq
     got = analyzer.scanner.ScanBatch(b, device=0)
-    osc = O.NewScanner(None)
-    checked = nfind = 0
+    args = [S.ScanArgs(paths[i], bytes(b.data[int(b.offsets[i]):int(b.offsets[i + 1])])) for i in range(b.nfiles)]
+    want = sample_expect("layer36", args)  # oracle/secret.py over every file (tests/golden/oracle_small/)
+    nfind = 0
     for i in range(b.nfiles):
-        if i % 16 and not got[i]["Findings"]:
-            continue
-        c = bytes(b.data[int(b.offsets[i]):int(b.offsets[i + 1])])
-        want = canon_secret(osc.Scan(paths[i], c))
-        assert canon_secret(got[i]) == want, paths[i]
-        checked += 1
-        nfind += len(want["Findings"] or [])
-    assert checked > 200 and nfind > 100
+        assert canon_secret(got[i]) == want[i], paths[i]
+        nfind += len(want[i]["Findings"] or [])
+    assert b.nfiles > 200 and nfind > 100
     # the walker's view of the same layer (whiteouts, opaque dirs, kept files) is the oracle's
     want_files = []
     opq, wh = W.LayerTar(skip_dirs=["/deep"]).Walk(io.BytesIO(tar), lambda p, n, rd: (
