@@ -137,6 +137,38 @@ def test_k1f_batch_sizes(builtin, size):
         assert np.array_equal(kw, rkw) and np.array_equal(ev, rev)
 
 
+@pytest.mark.parametrize("chunk", [16, 64, 256, 1024])
+@pytest.mark.parametrize("grid", [0, 3])
+def test_k1f_event_list(builtin, knob, chunk, grid):
+    """K1F lists the event chunks itself (K1FArgs::evlist: each block's LDS bitmap of its
+    range, first-touch appends in the zone a previous block's literals reach): the list
+    holds every chunk with events exactly once (its length == the non-empty words of
+    k1_reference's events), and the findings through the item passes, which then gate files
+    from their keyword bits, equal the exact CPU path and the gates-pass path
+    (no_k1f_list).  grid 3: ranges of megabytes; the default grid: ranges of a few tiles
+    that the zone covers whole."""
+    import numpy as np
+    if grid:
+        knob("k1f_grid", grid)
+    batch, _ = corpus.make_corpus(6 << 20, seed=70 + chunk, plants_per_mib=800)
+    edge = corpus.k1_edge_batch(builtin.k1_literals(), 5)
+    for b in (batch, edge):
+        want = builtin.ScanBatch(b, nthreads=16)
+        _, rev = builtin.k1_reference(b, chunk)
+        for legacy in ("", "1"):
+            knob("no_k1f_list", legacy)
+            ctx = S.GpuContext(builtin, 0, chunk_bytes=chunk, adapt_mib=0xFFFFFFFF)
+            ctx.upload(b)
+            ctx.kernels()
+            nev = ctx.stats()["event_chunks"]
+            _, ev = ctx.k1_output(chunk)
+            got = ctx.scan()
+            ctx.close()
+            assert np.array_equal(ev, rev)
+            assert nev == int(np.count_nonzero(rev)), (legacy, nev, int(np.count_nonzero(rev)))
+            assert got == want, legacy
+
+
 @pytest.mark.parametrize("grid", [1, 3])
 def test_k1f_many_tiles_per_wave(builtin, knob, grid):
     """K1F's steady state: with the grid capped to 1 or 3 blocks, each wave

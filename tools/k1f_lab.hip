@@ -10,7 +10,10 @@
 //   V1  + the 16 entry reads per tile (ds_read_b128, replicated layout), ANDed together
 //   V2  + the window ANDs and the bucket union per word, ballot of listed words
 //   V3  + the run flags and run events (k1f_flags / k1f_runs, DPP look-behind), ballots
-// and times each; V3 also stamps the shader clock against the 100 MHz wall clock.
+//   V4  V3 with the 16 entries of a tile read at once
+//   V5  V3 without the cross-lane look-behind (the DPP moves)
+// and times each (V3 also at 512 threads per block, one and two blocks per CU); V3 stamps
+// the shader clock against the 100 MHz wall clock.
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -I trivy_amd/csrc -I include \
 //          -o tools/k1f_lab tools/k1f_lab.hip
 #include <hip/hip_runtime.h>
@@ -48,6 +51,7 @@ __device__ __forceinline__ uint32_t ror1(uint32_t v) {
   return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x13C, 0xF, 0xF, false);
 }
 __device__ __forceinline__ uint32_t prev(uint32_t cur, uint32_t p) { return shr1(cur, ror1(p)); }
+__device__ __forceinline__ uint32_t prev_none(uint32_t cur, uint32_t p) { return cur ^ p; }
 
 struct Carry {
   uint32_t a, b, c, m, m1;
@@ -55,10 +59,40 @@ struct Carry {
 
 template <int V>
 struct Lane {
+  __device__ __forceinline__ uint32_t prev(uint32_t cur, uint32_t p) const {
+    if constexpr (V == 5) return prev_none(cur, p);
+    return ::prev(cur, p);
+  }
   const uint8_t* smem;
   uint32_t lane16;
   __device__ __forceinline__ uint4 entry(uint32_t w, int k) const {
     return *(const uint4*)(smem + __builtin_amdgcn_perm(w, lane16, 0x0C0C0000u | ((4u + (uint32_t)k) << 8)));
+  }
+  // V4: V3's logic with all 16 entries read at once (one LDS round trip per tile)
+  __device__ __forceinline__ uint32_t tile16(uint4 v, Carry& cy, uint32_t& un) const {
+    uint4 e[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) e[k] = entry(k < 4 ? v.x : k < 8 ? v.y : k < 12 ? v.z : v.w, k & 3);
+    const uint32_t ao = k1f_and3(e[13].x, e[14].y, e[15].z), bo = e[14].x & e[15].y, co = e[15].x;
+    const uint32_t ai = prev(ao, cy.a), bi = prev(bo, cy.b), ci = prev(co, cy.c);
+    cy.a = ao;
+    cy.b = bo;
+    cy.c = co;
+    uint32_t r[16];
+    r[0] = ai & e[0].w;
+    r[1] = k1f_and3(bi, e[0].z, e[1].w);
+    r[2] = k1f_and3(ci, e[0].y, e[1].z) & e[2].w;
+#pragma unroll
+    for (int k = 3; k < 16; k++) r[k] = k1f_and3(e[k - 3].x, e[k - 2].y, e[k - 1].z) & e[k].w;
+    uint32_t g[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) g[i] = k1f_or3(r[4 * i], r[4 * i + 1], r[4 * i + 2]) | r[4 * i + 3];
+    un = k1f_or3(g[0], g[1], g[2]) | g[3];
+    const uint32_t m = k1f_flags(r[3], r[7], r[11], r[15]);
+    const uint32_t m1 = prev(m, cy.m), m2 = prev(m1, cy.m1);
+    cy.m = m;
+    cy.m1 = m1;
+    return k1f_runs(m, m1, m2);
   }
   // returns run bits (V3) and the bucket union (V>=2) / AND of everything (V1)
   __device__ __forceinline__ uint32_t tile(uint4 v, Carry& cy, uint32_t& un) const {
@@ -146,13 +180,13 @@ __global__ void __launch_bounds__(1024) lab_k(const uint8_t* data, const uint4* 
       acc ^= v.x ^ v.y ^ v.z ^ v.w;
     } else {
       uint32_t un;
-      const uint32_t rb = L.tile(v, cy, un);
+      const uint32_t rb = V == 4 ? L.tile16(v, cy, un) : L.tile(v, cy, un);
       if constexpr (V == 1) {
         acc ^= un;
       } else {
         const uint64_t hb = __ballot((un & 0xFFFFu) != 0);
         if (__builtin_expect(hb != 0, 0)) nl += (uint32_t)__popcll(hb);
-        if constexpr (V == 3) {
+        if constexpr (V >= 3) {
           const uint64_t bu = __ballot(rb & 1u), bd = __ballot(rb & 2u);
           if (__builtin_expect((bu | bd) != 0, 0)) nr += (uint32_t)__popcll(bu | bd);
         }
@@ -176,7 +210,7 @@ __global__ void __launch_bounds__(1024) lab_k(const uint8_t* data, const uint4* 
   for (int k = 0; k < D - 1; k++)
     if (t + k < t1) body(p[k]);
   out[blockIdx.x * blockDim.x + threadIdx.x] = acc + nl + nr;
-  if (V == 3 && blockIdx.x == 0 && threadIdx.x == 0) {
+  if (V == 3 && blockIdx.x == 0 && threadIdx.x == 0 && blockDim.x == 1024) {
     clk[0] = clock64() - c0;
     clk[1] = wall_clock64() - w0;
   }
@@ -265,6 +299,11 @@ int main(int argc, char** argv) {
   R("V1_entries", 1);
   R("V2_filter", 2);
   const float ms = R("V3_runs", 3);
+  R("V4_all16", 4);
+  R("V5_noDPP", 5);
+  run("V3_512thr", [&] { lab_k<3><<<cus, 512>>>(buf, dent, nt, out, clk); }, reps);
+  run("V3_2x512", [&] { lab_k<3><<<2 * cus, 512>>>(buf, dent, nt, out, clk); }, reps);
+  run("V0_512thr", [&] { lab_k<0><<<cus, 512>>>(buf, dent, nt, out, clk); }, reps);
   unsigned long long c[2];
   CHECK(hipMemcpy(c, clk, 16, hipMemcpyDeviceToHost));
   printf("{\"block0_cycles\": %llu, \"block0_wall_ticks\": %llu, \"shader_MHz\": %.0f, \"kernel_ms\": %.4f}\n", c[0], c[1],

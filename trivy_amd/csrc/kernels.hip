@@ -630,7 +630,10 @@ constexpr uint32_t kFImgOff = kFDmaOff + (kFThreads / 64) * K1F_DMA * 1024;
 constexpr uint32_t kFCfOff = kFImgOff + kFImgMax;
 constexpr uint32_t kFCfMax = 512;                          // coarse file map entries in LDS
 constexpr uint32_t kFStOff = kFCfOff + 4 * kFCfMax;        // block counters (listed, arrivals, waves done)
-constexpr uint32_t kFLds = kFStOff + 16;                   // 146 KiB at 1024 threads
+constexpr uint32_t kFBitsOff = kFStOff + 16;               // the block's event-chunk bitmap (event list)
+constexpr uint32_t kFBitsWords = 3 * kFThreads;             // 12 KiB: 98,304 chunks of the block's range
+constexpr uint32_t kFLds = kFBitsOff + 4 * kFBitsWords;    // 158 KiB at 1024 threads
+static_assert(kFLds <= 160 * 1024, "K1F's LDS");
 #ifndef K1F_DEPTH
 #define K1F_DEPTH 4
 #endif
@@ -656,6 +659,17 @@ struct K1FArgs {
   // writes [2] ~its first block start, K2 [3] its last block end.  The kernels' own
   // durations, beside the HIP events around their launches (bench.py reports both).
   unsigned long long* clk;
+  // the event list (null: none; the gates pass compacts the events instead): every chunk
+  // whose event word K1F makes non-zero, once, in no particular order (ItemArgs::evlist).
+  // A chunk of a block's range at least `zone` bytes past its start gets events from that
+  // block alone (a literal ends at most zone - 1 bytes past its window end): the block marks
+  // it in an LDS bitmap and lists its marked chunks at its end.  Any other chunk (the first
+  // zone bytes of a range, which the previous block's literals reach too) is listed by the
+  // atomic that turns its event word non-zero.
+  uint32_t* evlist;
+  uint32_t* nev;
+  uint32_t zone;
+  uint32_t evcap;  // entries of evlist (a bound; the list holds each chunk once)
 };
 
 // lane i <- lane i - 1, lane 0 <- old (DPP wave_shr:1, out-of-range source keeps old)
@@ -793,6 +807,24 @@ __device__ __forceinline__ uint32_t f_wat(const uint32_t (&w)[6], uint32_t o) {
   return __builtin_amdgcn_alignbyte(hi, lo, o & 3u);
 }
 
+// event bits `bits` for chunk c (K1FArgs::evlist): c in [c_lo, c_hi) -> the block's bitmap
+struct K1FMark {
+  const K1FArgs& A;
+  uint32_t* lbm;  // LDS bitmap of chunks [c_lo, c_hi)
+  uint32_t c_lo, c_hi;
+  __device__ __forceinline__ void operator()(uint32_t c, uint32_t bits) const {
+    if (!A.evlist) {
+      atomicOr(&A.ev[c], bits);
+    } else if (c >= c_lo && c < c_hi) {
+      atomicOr(&A.ev[c], bits);
+      atomicOr(&lbm[(c - c_lo) >> 5], 1u << ((c - c_lo) & 31));
+    } else if (atomicOr(&A.ev[c], bits) == 0u) {  // (rare: the zone, and chunks past the range)
+      const uint32_t i = atomicAdd(A.nev, 1u);
+      if (i < A.evcap) A.evlist[i] = c;
+    }
+  }
+};
+
 struct K1FVerify {
   const DevK1F& d;
   const K1FArgs& A;
@@ -801,12 +833,13 @@ struct K1FVerify {
   uint32_t eshift, lane16;
   const uint32_t* lcf;  // cf[kc0 .. kc0 + ncl) in LDS
   uint32_t kc0, ncl;
+  const K1FMark& mark;
 
   // a verified occurrence of record i starting at s, ending at e (< total)
   __device__ __forceinline__ void report(const K1FLit& L, uint32_t i, uint32_t s, uint32_t e, uint32_t& narr) const {
     narr++;
     if (A.hits) atomicAdd(&A.hits[i], 1u);
-    if (L.ev) atomicOr(&A.ev[e / A.chunk], L.ev);
+    if (L.ev) mark(e / A.chunk, L.ev);
     if (L.kw >= 0) {
       // the same file holds the first bytes of the coarse blocks of s and past e's: no file
       // starts in (s, e], the literal lies inside the file holding e
@@ -921,9 +954,16 @@ __global__ void __launch_bounds__(kFThreads) k1f_kernel(DevK1F d, K1FArgs A) {
   for (uint32_t i = threadIdx.x; i < ncl; i += blockDim.x) lcf[i] = A.cf[kc0 + i];
   uint32_t* bst = (uint32_t*)(smem + kFStOff);
   if (threadIdx.x < 3) bst[threadIdx.x] = 0;
+  // the event list: the block's non-zone chunks [c_lo, c_hi) in the LDS bitmap
+  uint32_t* lbm = (uint32_t*)(smem + kFBitsOff);
+  const uint32_t c_hi = (uint32_t)(min<uint64_t>(bb1, A.total + (uint64_t)A.chunk - 1) / A.chunk);
+  const uint32_t c_lo = min(c_hi, (uint32_t)((bb0 + A.zone + A.chunk - 1) / A.chunk));
+  const uint32_t nbw = A.evlist ? (c_hi - c_lo + 31) / 32 : 0u;  // (<= kFBitsWords: launch_k1f)
+  for (uint32_t i = threadIdx.x; i < nbw; i += blockDim.x) lbm[i] = 0;
+  const K1FMark mark{A, lbm, c_lo, c_hi};
   __syncthreads();
   const uint32_t t0 = (uint32_t)((uint64_t)gw * A.ntiles / nw), t1 = (uint32_t)((uint64_t)(gw + 1) * A.ntiles / nw);
-  if (t0 >= t1) return;  // (no block barrier below)
+  if (t0 < t1) {  // (waves without tiles wait at the block barrier below)
   const K1FLane L{d, A, smem, lane, (lane & 15u) << 4};
   uint4* ring = (uint4*)(smem + kFQueueOff) + 2 * wave * kFQueue;  // 2 x uint4 per entry
   uint32_t qh = 0, qn = 0, nlisted = 0, narr = 0;
@@ -934,7 +974,7 @@ __global__ void __launch_bounds__(kFThreads) k1f_kernel(DevK1F d, K1FArgs A) {
       const uint32_t i = (qh + lane) & (kFQueue - 1);
       const uint4 x = ring[2 * i], y = ring[2 * i + 1];
       const uint32_t w[6] = {x.z, x.w, y.x, y.y, y.z, 0u};
-      const K1FVerify V{d, A, smem + kFImgOff, smem, 8, (lane & 15u) << 4, lcf, kc0, ncl};
+      const K1FVerify V{d, A, smem + kFImgOff, smem, 8, (lane & 15u) << 4, lcf, kc0, ncl, mark};
       V.verify(x.x, x.y & 0xFu, x.y >> 16, w, narr);
     }
     __builtin_amdgcn_wave_barrier();
@@ -972,7 +1012,7 @@ __global__ void __launch_bounds__(kFThreads) k1f_kernel(DevK1F d, K1FArgs A) {
         const uint64_t above = ld & (~0ull << lane << 1);
         const uint64_t gm = (above ? (above & (~above + 1)) - 1 : ~0ull) & (~0ull << lane);
         const uint32_t bits = ((bu & gm) ? kEvRunU : 0u) | ((bd & gm) ? kEvRunD : 0u);
-        if (bits) atomicOr(&A.ev[c], bits);
+        if (bits) mark(c, bits);
       }
     }
     // listed words
@@ -1066,20 +1106,45 @@ __global__ void __launch_bounds__(kFThreads) k1f_kernel(DevK1F d, K1FArgs A) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) narr += __shfl_xor(narr, o);
   if (lane == 0) {
-    uint32_t nact = 0;  // the block's waves with tiles
-    for (uint32_t w = 0; w < wpb; w++) {
-      const uint32_t g0 = blockIdx.x * wpb + w;
-      nact += (uint64_t)g0 * A.ntiles / nw < (uint64_t)(g0 + 1) * A.ntiles / nw ? 1u : 0u;
-    }
     atomicAdd(&bst[0], nlisted);
     atomicAdd(&bst[1], narr);
-    __threadfence_block();
-    if (atomicAdd(&bst[2], 1u) == nact - 1) {
-      const uint32_t bl = atomicAdd(&bst[0], 0u), ba = atomicAdd(&bst[1], 0u);
-      if (bl) atomicAdd(&A.stats[0], bl);
-      if (ba) atomicAdd(&A.stats[1], ba);
-      if (A.clk) atomicMax(&A.clk[1], (unsigned long long)wall_clock64());
+  }
+  }  // (t0 < t1)
+  __syncthreads();
+  if (nbw) {  // the block's marked chunks into the event list: one claim per block
+    uint32_t wv[kFBitsWords / kFThreads], n = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < kFBitsWords / kFThreads; k++) {
+      const uint32_t i = threadIdx.x + k * kFThreads;
+      wv[k] = i < nbw ? lbm[i] : 0u;
+      n += __popc(wv[k]);
     }
+    uint32_t inc = n;  // inclusive scan over the wave, then over the block's waves in LDS
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t t = __shfl_up(inc, o);
+      if (lane >= (uint32_t)o) inc += t;
+    }
+    uint32_t* s_w = (uint32_t*)(smem + kFQueueOff);  // (the verification rings are drained)
+    if (lane == 63) s_w[wave] = inc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      uint32_t tot = 0;
+      for (uint32_t w = 0; w < wpb; w++) tot += s_w[w];
+      s_w[kFThreads / 64] = tot ? atomicAdd(A.nev, tot) : 0u;
+    }
+    __syncthreads();
+    uint32_t at = s_w[kFThreads / 64] + inc - n;
+    for (uint32_t w = 0; w < wave; w++) at += s_w[w];
+#pragma unroll
+    for (uint32_t k = 0; k < kFBitsWords / kFThreads; k++)
+      for (uint32_t b = wv[k]; b; b &= b - 1, at++)
+        if (at < A.evcap) A.evlist[at] = c_lo + 32 * (threadIdx.x + k * kFThreads) + __builtin_ctz(b);
+  }
+  if (threadIdx.x == 0) {
+    if (bst[0]) atomicAdd(&A.stats[0], bst[0]);
+    if (bst[1]) atomicAdd(&A.stats[1], bst[1]);
+    if (A.clk) atomicMax(&A.clk[1], (unsigned long long)wall_clock64());
   }
 }
 
@@ -1387,8 +1452,9 @@ struct ItemArgs {
   const uint64_t* off;
   const uint32_t* cf;  // coarse file map (file_of)
   const uint32_t* ev;
-  const uint32_t* evlist;           // chunks with event bits (ev_compact_block)
+  const uint32_t* evlist;           // chunks with event bits (ev_compact_block, or K1F)
   const uint32_t* nev;              // [1] length of evlist
+  uint32_t evcap;                   // entries of evlist (a bound on *nev)
   const unsigned long long* ggate;  // [F * GW]
   const unsigned long long* gofbit;  // [32 * GW] groups listening to event bit b; bit 31 = every chunk
   const uint32_t* gevents;          // [G]
@@ -1399,7 +1465,24 @@ struct ItemArgs {
   uint32_t* bcount;           // [gridDim.x * G] each count block's counts, for the emit pass
   uint32_t* cursor;           // [G]
   uint2* items;
+  // ggate == null (K1F listed the events, no gates pass ran): a file's group gates from its
+  // keyword bits, as ggate_file computes them
+  const uint32_t* kw;
+  uint32_t W;
+  const unsigned long long* kwg;
+  const unsigned long long* galw;
+  unsigned long long* clk;  // K1FArgs::clk ([2]: the item passes' first block start)
 };
+
+// word w of file f's group gates (ggate_file's value)
+__device__ __forceinline__ unsigned long long file_gate(const ItemArgs& A, uint32_t f, uint32_t w) {
+  if (A.ggate) return A.ggate[(size_t)f * A.GW + w];
+  const uint32_t* kwf = A.kw + (size_t)f * A.W;
+  unsigned long long acc = A.galw[w];
+  for (uint32_t i = 0; i < A.W; i++)
+    for (uint32_t bits = kwf[i]; bits; bits &= bits - 1) acc |= A.kwg[(size_t)(i * 32 + __builtin_ctz(bits)) * A.GW + w];
+  return acc;
+}
 
 // Chunks whose K1 event word is not empty, compacted into `list`.  One pass: each thread tests 32 consecutive chunks (eight 16-B loads in flight), the block
 // scans the counts and claims its output range with one atomic per 32 * kBlock chunks.
@@ -1502,7 +1585,7 @@ __device__ __forceinline__ ItemLds item_lds_load(const ItemArgs& A, uint8_t* sme
 
 template <class V>
 __device__ __forceinline__ void gen_items(const ItemArgs& A, const ItemLds& T, uint64_t t, V visit) {
-  const uint32_t nev = *A.nev;
+  const uint32_t nev = min(*A.nev, A.evcap);
   const uint32_t C = A.chunk;
   if (t < nev) {
     const uint64_t e = A.evlist[t];
@@ -1540,7 +1623,7 @@ __device__ __forceinline__ void gen_items(const ItemArgs& A, const ItemLds& T, u
       for (uint32_t w = 0; w < A.GW; w++) {
         unsigned long long cand = 0;
         for (uint32_t bits = evb; bits; bits &= bits - 1) cand |= T.gofbit[__builtin_ctz(bits) * A.GW + w];
-        cand &= A.ggate[(size_t)f * A.GW + w] & ~T.gofbit[31 * A.GW + w];
+        cand &= file_gate(A, f, w) & ~T.gofbit[31 * A.GW + w];
         while (cand) {
           const uint32_t g = w * 64 + __builtin_ctzll(cand);
           cand &= cand - 1;
@@ -1559,7 +1642,7 @@ __device__ __forceinline__ void gen_items(const ItemArgs& A, const ItemLds& T, u
     const uint64_t fs = A.off[f], fe = A.off[f + 1];
     if (fe == fs) return;
     for (uint32_t w = 0; w < A.GW; w++) {
-      unsigned long long cand = A.ggate[(size_t)f * A.GW + w] & T.gofbit[31 * A.GW + w];
+      unsigned long long cand = file_gate(A, f, w) & T.gofbit[31 * A.GW + w];
       while (cand) {
         const uint32_t g = w * 64 + __builtin_ctzll(cand);
         cand &= cand - 1;
@@ -1574,11 +1657,12 @@ __device__ __forceinline__ void gen_items(const ItemArgs& A, const ItemLds& T, u
 // count pass: items per group (block totals in LDS, one global atomic per group and block)
 __global__ void __launch_bounds__(kBlock) items_count_kernel(ItemArgs A) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  if (!A.ggate && threadIdx.x == 0) atomicMax(&A.clk[2], ~(unsigned long long)wall_clock64());  // (no gates pass)
   const ItemLds T = item_lds_load(A, smem);
   uint32_t* s_count = (uint32_t*)(smem + item_lds_bytes(A.G, A.GW));
   for (uint32_t g = threadIdx.x; g < A.G; g += blockDim.x) s_count[g] = 0;
   __syncthreads();
-  const uint64_t nt = (uint64_t)*A.nev + A.F, stride = (uint64_t)gridDim.x * blockDim.x;
+  const uint64_t nt = (uint64_t)min(*A.nev, A.evcap) + A.F, stride = (uint64_t)gridDim.x * blockDim.x;
   for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < nt; t += stride)
     gen_items(A, T, t, [&](uint32_t, uint32_t g, uint64_t lo, uint64_t hi) { atomicAdd(&s_count[g], (uint32_t)(hi - lo + 1)); });
   __syncthreads();
@@ -1746,7 +1830,7 @@ __global__ void __launch_bounds__(kBlock) items_emit_kernel(ItemArgs A, LayoutAr
   uint32_t* s_gbase = s_base + A.G;
   uint8_t* s_kind = (uint8_t*)(s_gbase + A.G);
   layout_block(LA, s_kind, s_gbase);
-  const uint64_t nt = (uint64_t)*A.nev + A.F, stride = (uint64_t)gridDim.x * blockDim.x;
+  const uint64_t nt = (uint64_t)min(*A.nev, A.evcap) + A.F, stride = (uint64_t)gridDim.x * blockDim.x;
   const uint64_t t0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   for (uint32_t g = threadIdx.x; g < A.G; g += blockDim.x) {
     const uint32_t n = s_kind[g] == kGroupList ? A.bcount[(size_t)blockIdx.x * A.G + g] : 0;
@@ -2748,6 +2832,7 @@ struct DeviceRules {
   DevK1X k1x{};
   bool has_k1x = false;
   bool use_k1f = false;  // K1 is the filter-and-verify K1F (k1f.hpp), else the automaton
+  uint32_t k1f_maxlen = 4;  // longest K1F literal (its event list's zone)
   DevK1F k1f{};
   K1FTables k1ft;        // host copy (the adaptation rebuilds it)
   uint32_t* d_fhits = nullptr;  // [n_lit] K1F sampling counters
@@ -2980,16 +3065,35 @@ static int upload_k1f(DeviceRules* r) {
   HIP_TRY(hipMemcpy((void*)r->k1f.img, t.img.data(), t.img.size(), hipMemcpyHostToDevice));
   r->k1f.img_bytes = (uint32_t)t.img.size();
   r->k1f.nlit = t.nlit;
+  // the event list's zone (K1FArgs::zone): a literal ends at most len - 2 bytes past the
+  // start of a range its window end precedes
+  const K1FLit* recs = (const K1FLit*)(t.img.data() + kFImgLits);
+  r->k1f_maxlen = 4;
+  for (uint32_t i = 0; i < t.nlit; i++) r->k1f_maxlen = std::max<uint32_t>(r->k1f_maxlen, recs[i].len);
   return TSG_OK;
+}
+
+// K1F's grid for ntiles tiles: one block per CU
+static int k1f_grid(const DeviceRules* r, uint32_t ntiles) {
+  const uint32_t wpb = kFThreads / 64;
+  uint64_t cap = (uint64_t)r->cus;
+  if (const int64_t g = knobs().k1f_grid.load()) cap = std::min<uint64_t>(cap, (uint64_t)g);  // (test knob)
+  return (int)std::max<uint64_t>(1, std::min<uint64_t>((ntiles + wpb - 1) / wpb, cap));
+}
+
+// K1F builds the event list itself (K1FArgs::evlist) when chunks tile its 1 KiB tiles and a
+// block's range of chunks fits the LDS bitmap
+static bool k1f_lists(const DeviceRules* r, uint32_t ntiles, uint32_t chunk) {
+  if (chunk == 0 || chunk > kFTile || kFTile % chunk) return false;
+  const uint64_t grid = (uint64_t)k1f_grid(r, ntiles), wpb = kFThreads / 64, nw = grid * wpb;
+  const uint64_t block_tiles = (wpb * ntiles + nw - 1) / nw + 1;  // (ranges differ by at most one tile per wave)
+  return block_tiles * (kFTile / chunk) <= 32ull * kFBitsWords;
 }
 
 // one K1F launch over the first ntiles tiles of the batch
 static int launch_k1f(DeviceRules* r, const K1FArgs& A, hipStream_t st) {
-  const uint32_t wpb = kFThreads / 64;
-  uint64_t cap = (uint64_t)r->cus;
-  if (const int64_t g = knobs().k1f_grid.load()) cap = std::min<uint64_t>(cap, (uint64_t)g);  // (test knob)
-  const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>((A.ntiles + wpb - 1) / wpb, cap));
-  k1f_kernel<<<grid, kFThreads, 0, st>>>(r->k1f, A);
+  if (A.evlist && !k1f_lists(r, A.ntiles, A.chunk)) return fail(TSG_ERR_INTERNAL, "K1F event list without room");
+  k1f_kernel<<<k1f_grid(r, A.ntiles), kFThreads, 0, st>>>(r->k1f, A);
   HIP_TRY(hipGetLastError());
   return TSG_OK;
 }
@@ -3012,6 +3116,8 @@ static int adapt_k1f(DeviceRules* r, LaneState* l, const K1FArgs& A0, const uint
   A.hits = r->d_fhits;
   A.stats = l->counts + 24;  // (the batch's own counters stay those of its real launch)
   A.clk = nullptr;
+  A.evlist = nullptr;
+  A.nev = nullptr;
   int rc;
   if ((rc = launch_k1f(r, A, l->st))) return rc;
   std::vector<uint32_t> hits(std::max<uint32_t>(1, nrec));
@@ -3173,7 +3279,9 @@ int device_rules_create(int device, const Plan& p, uint32_t chunk, uint32_t ext_
   HIP_TRY(hipGetDeviceProperties(&prop, device));
   r->cus = prop.multiProcessorCount;
   r->grid = prop.multiProcessorCount * 8;
-  HIP_TRY(hipEventCreateWithFlags(&r->kernels_done, hipEventDisableTiming));
+  // (orders the next batch's kernels after this one's on the same device: a device-scope
+  // release is enough)
+  HIP_TRY(hipEventCreateWithFlags(&r->kernels_done, hipEventDisableTiming | hipEventReleaseToDevice));
   int occ = 0;
   HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void*)k2_kernel, kK2Block, r->max_lds));
   r->k2_grid = r->cus * std::max(occ, 1);
@@ -3259,8 +3367,14 @@ int host_out_alloc(const DeviceRules* d, uint32_t files_cap, HostOut* o) {
   if ((e = hipHostMalloc((void**)&h.cand, sizeof(Candidate) * (size_t)h.cand_cap, hipHostMallocMapped)) != hipSuccess)
     return fail_free(e, "hipHostMalloc");
   if ((e = hipHostGetDevicePointer((void**)&h.cand_dev, h.cand, 0)) != hipSuccess) return fail_free(e, "hipHostGetDevicePointer");
-  for (auto& ev : h.ev)
-    if ((e = hipEventCreate(&ev)) != hipSuccess) return fail_free(e, "hipEventCreate");
+  // ev[0 .. kEvDone) only time the stages: no system-scope fence when they are recorded (the
+  // default event writes back and invalidates the caches, a gap of 6-13 us after each kernel
+  // they follow: profiles/r05/final3/bench/timeline.txt); ev[kEvDone] completes the batch for
+  // the host and keeps it
+  for (int k = 0; k <= kEvDone; k++)
+    if ((e = k < kEvDone ? hipEventCreateWithFlags(&h.ev[k], hipEventDisableSystemFence) : hipEventCreate(&h.ev[k])) !=
+        hipSuccess)
+      return fail_free(e, "hipEventCreate");
   *o = h;
   return TSG_OK;
 }
@@ -3382,10 +3496,22 @@ int enqueue_scan(DeviceRules* r, LaneState* l, const ScanInput& in, HostOut* out
   // ---- K1
   const uint64_t k1_items = (nchunks + k1_item_chunks - 1) / k1_item_chunks;
   const uint64_t adapt_bytes = r->adapt_mib == 0xFFFFFFFFu ? ~0ull : (uint64_t)(r->adapt_mib ? r->adapt_mib : 16) << 20;
+  const uint32_t k1f_tiles = (uint32_t)((total + kFTile - 1) / kFTile);
+  // K1F lists the event chunks itself: no compaction pass, and the item passes gate files
+  // from their keyword bits (no gates pass at all)
+  // (K1X, when a plan has it, adds events after K1: the gates pass lists them all)
+  const bool k1f_list = k1f && total && !r->has_k1x && !knobs().no_k1f_list.load() && k1f_lists(r, k1f_tiles, C);
   if (k1f) {
-    K1FArgs A{data, l->off, l->cf, (uint32_t)total, C, F, (uint32_t)((total + kFTile - 1) / kFTile), F ? (uint32_t)ncf : 0u,
-              l->kw, l->ev_bits, nullptr, l->counts + 16, (unsigned long long*)(l->counts + kClk)};
+    K1FArgs A{data, l->off, l->cf, (uint32_t)total, C, F, k1f_tiles, F ? (uint32_t)ncf : 0u,
+              l->kw, l->ev_bits, nullptr, l->counts + 16, (unsigned long long*)(l->counts + kClk),
+              nullptr, nullptr, r->k1f_maxlen, 0};
     if (!r->adapted && total >= adapt_bytes && (rc = adapt_k1f(r, l, A, in.data))) return rc;
+    if (k1f_list) {
+      A.evlist = l->evlist;
+      A.nev = l->counts + 1;
+      A.evcap = (uint32_t)std::min<size_t>(l->evlist_cap, 0xFFFFFFFFu);
+      A.zone = r->k1f_maxlen;  // (after the adaptation's rebuild)
+    }
     if (total && (rc = launch_k1f(r, A, st))) return rc;
   } else if (!r->adapted && k1_items >= 64 && total >= adapt_bytes) {
     if ((rc = adapt_k1(r, l, total, F, nchunks, k1_items))) return rc;
@@ -3429,14 +3555,24 @@ int enqueue_scan(DeviceRules* r, LaneState* l, const ScanInput& in, HostOut* out
   IA.cursor = l->cursor;
   IA.evlist = l->evlist;
   IA.nev = l->counts + 1;
+  IA.evcap = (uint32_t)std::min<size_t>(l->evlist_cap, 0xFFFFFFFFu);
   IA.items = l->items;
+  IA.kw = l->kw;
+  IA.W = W;
+  IA.kwg = r->d_kwg;
+  IA.galw = r->d_galw;
+  IA.clk = (unsigned long long*)(l->counts + kClk);
   const bool work = F && G && nchunks;
-  if (work) {
+  if (work && k1f_list) {
+    IA.ggate = nullptr;  // (files gated from their keyword bits in the item passes)
+  } else if (work) {
     const uint32_t cgrid = (uint32_t)std::min<uint64_t>((nchunks + kEvPer * kBlock - 1) / (kEvPer * kBlock), (uint64_t)r->grid);
     GateArgs GA{l->ev_bits, nchunks, l->evlist, l->counts + 1, cgrid, l->kw, F, W, r->GW, r->d_kwg, r->d_galw, l->ggate,
                 (unsigned long long*)(l->counts + kClk)};
     gates_kernel<<<cgrid + (F + kBlock - 1) / kBlock, kBlock, 0, st>>>(GA);
     HIP_TRY(hipGetLastError());
+  }
+  if (work) {
     // both items passes (bcount holds grid x G); ITEMS_BPC blocks per CU
     const int igrid = std::min(r->grid, r->cus * ITEMS_BPC);
     const size_t ilds = item_lds_host(G, r->GW);
