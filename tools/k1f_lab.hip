@@ -13,7 +13,9 @@
 //   V4  V3 with the 16 entries of a tile read at once
 //   V5  V3 without the cross-lane look-behind (the DPP moves)
 // and times each (V3 also at 512 threads per block, one and two blocks per CU); V3 stamps
-// the shader clock against the 100 MHz wall clock.
+// the shader clock against the 100 MHz wall clock.  L64_*: the same work with each lane
+// holding 64 contiguous bytes (lab64_k), the per-word overheads (look-behind, run flags of
+// the neighbours) paid once per 64 B instead of per 16 B.
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -I trivy_amd/csrc -I include \
 //          -o tools/k1f_lab tools/k1f_lab.hip
 #include <hip/hip_runtime.h>
@@ -93,6 +95,45 @@ struct Lane {
     cy.m = m;
     cy.m1 = m1;
     return k1f_runs(m, m1, m2);
+  }
+  // one 16-B sub-word of a lane's 64 contiguous bytes (lab64_k): look-behind partials in
+  // (ai, bi, ci), its own bytes 13..15's partials out (for the next sub-word), the bucket
+  // union and the run flags m (k1f_flags)
+  __device__ __forceinline__ void sub(uint4 v, uint32_t& ai, uint32_t& bi, uint32_t& ci, uint32_t& un,
+                                      uint32_t& m) const {
+    uint32_t r[16];
+    {
+      uint4 e[8];
+#pragma unroll
+      for (int k = 0; k < 8; k++) e[k] = entry(k < 4 ? v.x : v.y, k & 3);
+      r[0] = ai & e[0].w;
+      r[1] = k1f_and3(bi, e[0].z, e[1].w);
+      r[2] = k1f_and3(ci, e[0].y, e[1].z) & e[2].w;
+#pragma unroll
+      for (int k = 3; k < 8; k++) r[k] = k1f_and3(e[k - 3].x, e[k - 2].y, e[k - 1].z) & e[k].w;
+      r[8] = k1f_and3(e[5].x, e[6].y, e[7].z);
+      r[9] = e[6].x & e[7].y;
+      r[10] = e[7].x;
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    {
+      uint4 e[8];
+#pragma unroll
+      for (int k = 0; k < 8; k++) e[k] = entry(k < 4 ? v.z : v.w, k & 3);
+      r[8] &= e[0].w;
+      r[9] = k1f_and3(r[9], e[0].z, e[1].w);
+      r[10] = k1f_and3(r[10], e[0].y, e[1].z) & e[2].w;
+#pragma unroll
+      for (int k = 3; k < 8; k++) r[8 + k] = k1f_and3(e[k - 3].x, e[k - 2].y, e[k - 1].z) & e[k].w;
+      ai = k1f_and3(e[5].x, e[6].y, e[7].z);
+      bi = e[6].x & e[7].y;
+      ci = e[7].x;
+    }
+    uint32_t g[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) g[i] = k1f_or3(r[4 * i], r[4 * i + 1], r[4 * i + 2]) | r[4 * i + 3];
+    un = k1f_or3(g[0], g[1], g[2]) | g[3];
+    m = k1f_flags(r[3], r[7], r[11], r[15]);
   }
   // returns run bits (V3) and the bucket union (V>=2) / AND of everything (V1)
   __device__ __forceinline__ uint32_t tile(uint4 v, Carry& cy, uint32_t& un) const {
@@ -216,6 +257,72 @@ __global__ void __launch_bounds__(1024) lab_k(const uint8_t* data, const uint4* 
   }
 }
 
+// lane-contiguous 64 B: 4 KiB tiles, lane l's bytes [64 l, 64 l + 64) by four 16-B loads
+// (each load instruction of the wave covers its 4 KiB at a 64-B stride); one tile in flight.
+// V0: loads only; V1: the filter and run flags of the four sub-words, the look-behind from
+// the previous lane once per 64 B (DPP), the run events of the four sub-words from their
+// flags in registers
+template <int V>
+__global__ void __launch_bounds__(1024) lab64_k(const uint8_t* data, const uint4* ent, uint32_t ntiles,
+                                                 uint32_t* out, unsigned long long* clk) {
+  __shared__ __attribute__((aligned(16))) uint8_t smem[65536];
+  if (V >= 1) {
+    for (uint32_t i = threadIdx.x; i < 4096; i += blockDim.x) ((uint4*)smem)[i] = ent[i >> 4];
+    __syncthreads();
+  }
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6, wpb = blockDim.x >> 6;
+  const uint32_t gw = blockIdx.x * wpb + wave, nw = gridDim.x * wpb;
+  const uint32_t nt4 = ntiles / 4;
+  const uint32_t t0 = (uint32_t)((uint64_t)gw * nt4 / nw), t1 = (uint32_t)((uint64_t)(gw + 1) * nt4 / nw);
+  const Lane<3> L{smem, (lane & 15u) << 4};
+  uint32_t ca = 0, cb = 0, cc = 0, cm3 = 0, cm2 = 0;
+  uint32_t acc = 0, nl = 0, nr = 0;
+  const uint8_t* base = data + 64u * lane;
+  auto body = [&](const uint4 (&v)[4]) __attribute__((always_inline)) {
+    if constexpr (V == 0) {
+#pragma unroll
+      for (int k = 0; k < 4; k++) acc ^= v[k].x ^ v[k].y ^ v[k].z ^ v[k].w;
+    } else {
+      // the last sub-word's bytes 13..15: the next lane's look-behind
+      const uint4 e13 = L.entry(v[3].w, 1), e14 = L.entry(v[3].w, 2), e15 = L.entry(v[3].w, 3);
+      const uint32_t ao = k1f_and3(e13.x, e14.y, e15.z), bo = e14.x & e15.y, co = e15.x;
+      uint32_t ai = prev(ao, ca), bi = prev(bo, cb), ci = prev(co, cc);
+      ca = ao;
+      cb = bo;
+      cc = co;
+      uint32_t un[4], m[4];
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        __builtin_amdgcn_sched_barrier(0);
+        L.sub(v[k], ai, bi, ci, un[k], m[k]);
+      }
+      const uint32_t pm3 = prev(m[3], cm3), pm2 = prev(m[2], cm2);
+      cm3 = m[3];
+      cm2 = m[2];
+      const uint32_t rb = k1f_runs(m[0], pm3, pm2) | k1f_runs(m[1], m[0], pm3) | k1f_runs(m[2], m[1], m[0]) |
+                          k1f_runs(m[3], m[2], m[1]);
+      const uint32_t u = k1f_or3(un[0], un[1], un[2]) | un[3];
+      const uint64_t hb = __ballot((u & 0xFFFFu) != 0);
+      if (__builtin_expect(hb != 0, 0)) nl += (uint32_t)__popcll(hb);
+      const uint64_t bu = __ballot(rb & 1u), bd = __ballot(rb & 2u);
+      if (__builtin_expect((bu | bd) != 0, 0)) nr += (uint32_t)__popcll(bu | bd);
+    }
+  };
+  uint4 p[4];
+#pragma unroll
+  for (int k = 0; k < 4; k++) p[k] = ld16(base + (size_t)t0 * 4 * kTile + 16 * k);
+  for (uint32_t t = t0; t < t1; t++) {
+    uint4 v[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      v[k] = p[k];
+      p[k] = ld16(base + (size_t)(t + 1) * 4 * kTile + 16 * k);
+    }
+    body(v);
+  }
+  out[blockIdx.x * blockDim.x + threadIdx.x] = acc + nl + nr;
+}
+
 template <typename F>
 static float run(const char* name, F launch, int reps) {
   hipEvent_t a, b;
@@ -304,6 +411,8 @@ int main(int argc, char** argv) {
   run("V3_512thr", [&] { lab_k<3><<<cus, 512>>>(buf, dent, nt, out, clk); }, reps);
   run("V3_2x512", [&] { lab_k<3><<<2 * cus, 512>>>(buf, dent, nt, out, clk); }, reps);
   run("V0_512thr", [&] { lab_k<0><<<cus, 512>>>(buf, dent, nt, out, clk); }, reps);
+  run("L64_V0_loads", [&] { lab64_k<0><<<cus, 1024>>>(buf, dent, nt, out, clk); }, reps);
+  run("L64_V1_full", [&] { lab64_k<1><<<cus, 1024>>>(buf, dent, nt, out, clk); }, reps);
   unsigned long long c[2];
   CHECK(hipMemcpy(c, clk, 16, hipMemcpyDeviceToHost));
   printf("{\"block0_cycles\": %llu, \"block0_wall_ticks\": %llu, \"shader_MHz\": %.0f, \"kernel_ms\": %.4f}\n", c[0], c[1],

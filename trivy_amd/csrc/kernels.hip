@@ -676,9 +676,10 @@ struct K1FArgs {
 __device__ __forceinline__ uint32_t f_shr1(uint32_t v, uint32_t old) {
   return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)v, 0x138, 0xF, 0xF, false);
 }
-// lane i <- lane i - 1, lane 0 <- lane 63 (DPP wave_ror:1)
+// lane i <- lane i - 1, lane 0 <- lane 63 (DPP wave_ror:1; every lane has a source, so no
+// "old" operand: one instruction instead of a zeroing move and the DPP move)
 __device__ __forceinline__ uint32_t f_ror1(uint32_t v) {
-  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x13C, 0xF, 0xF, false);
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x13C, 0xF, 0xF, true);
 }
 // lane l <- lane l - 1 of this tile, lane 0 <- lane 63 of the previous tile
 __device__ __forceinline__ uint32_t f_prev(uint32_t cur, uint32_t prev) { return f_shr1(cur, f_ror1(prev)); }
@@ -1472,17 +1473,8 @@ struct ItemArgs {
   const unsigned long long* kwg;
   const unsigned long long* galw;
   unsigned long long* clk;  // K1FArgs::clk ([2]: the item passes' first block start)
+  uint32_t kwg_lds;         // kwg staged in the passes' LDS (its bytes; 0: read from global)
 };
-
-// word w of file f's group gates (ggate_file's value)
-__device__ __forceinline__ unsigned long long file_gate(const ItemArgs& A, uint32_t f, uint32_t w) {
-  if (A.ggate) return A.ggate[(size_t)f * A.GW + w];
-  const uint32_t* kwf = A.kw + (size_t)f * A.W;
-  unsigned long long acc = A.galw[w];
-  for (uint32_t i = 0; i < A.W; i++)
-    for (uint32_t bits = kwf[i]; bits; bits &= bits - 1) acc |= A.kwg[(size_t)(i * 32 + __builtin_ctz(bits)) * A.GW + w];
-  return acc;
-}
 
 // Chunks whose K1 event word is not empty, compacted into `list`.  One pass: each thread tests 32 consecutive chunks (eight 16-B loads in flight), the block
 // scans the counts and claims its output range with one atomic per 32 * kBlock chunks.
@@ -1546,13 +1538,26 @@ struct GateArgs {
   const unsigned long long* galw;
   unsigned long long* ggate;
   unsigned long long* clk;  // K1FArgs::clk
+  uint32_t kwg_lds;         // kwg staged in LDS (its bytes; 0: read from global)
 };
+// (a file's gate is an OR over its keyword bits of kwg rows: from global memory, one L2
+// round trip per bit -- a file of a 1,000-rule set holds a hundred of them -- so the table
+// is staged in LDS when it fits)
+constexpr uint32_t kKwgLdsMax = 48 * 1024;
 __global__ void __launch_bounds__(kBlock) gates_kernel(GateArgs A) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   if (threadIdx.x == 0) atomicMax(&A.clk[2], ~(unsigned long long)wall_clock64());
-  if (blockIdx.x < A.ev_blocks)
+  if (blockIdx.x < A.ev_blocks) {
     ev_compact_block(A.ev, A.nchunks, A.evlist, A.nev, blockIdx.x, A.ev_blocks);
-  else
-    ggate_file((blockIdx.x - A.ev_blocks) * blockDim.x + threadIdx.x, A.kw, A.F, A.W, A.kwg, A.galw, A.GW, A.ggate);
+  } else {
+    const unsigned long long* kwg = A.kwg;
+    if (A.kwg_lds) {
+      stage16(smem, A.kwg, A.kwg_lds);
+      __syncthreads();
+      kwg = (const unsigned long long*)smem;
+    }
+    ggate_file((blockIdx.x - A.ev_blocks) * blockDim.x + threadIdx.x, A.kw, A.F, A.W, kwg, A.galw, A.GW, A.ggate);
+  }
 }
 
 // Items of the K2 list: (file f, chunk c) for group g iff g is gated for f and a chunk in
@@ -1564,12 +1569,14 @@ __global__ void __launch_bounds__(kBlock) gates_kernel(GateArgs A) {
 // visit(f, g, c_lo, c_hi): items c_lo..c_hi.
 // the group tables gen_items reads per candidate, staged in the item passes' LDS
 static inline size_t item_lds_host(uint32_t G, uint32_t GW) { return 256 * (size_t)GW + 8 * (size_t)G; }
+constexpr uint32_t kItemKwgLdsMax = 16 * 1024;  // kwg staged in the item passes' LDS up to this
 struct ItemLds {
   const unsigned long long* gofbit;  // [32 * GW]
   const uint32_t* gback;             // [G]
   const uint32_t* gevents;           // [G]
+  const unsigned long long* kwg;     // [32 * W * GW] (LDS when ItemArgs::kwg_lds, else global)
 };
-__device__ __forceinline__ uint32_t item_lds_bytes(uint32_t G, uint32_t GW) { return 256 * GW + 8 * G; }
+__device__ __forceinline__ uint32_t item_lds_bytes(const ItemArgs& A) { return 256 * A.GW + 8 * A.G + A.kwg_lds; }
 // copies the tables to smem (8-aligned); the caller's __syncthreads() publishes them
 __device__ __forceinline__ ItemLds item_lds_load(const ItemArgs& A, uint8_t* smem) {
   unsigned long long* gofbit = (unsigned long long*)smem;
@@ -1580,7 +1587,23 @@ __device__ __forceinline__ ItemLds item_lds_load(const ItemArgs& A, uint8_t* sme
     gback[i] = A.gback[i];
     gevents[i] = A.gevents[i];
   }
-  return ItemLds{gofbit, gback, gevents};
+  const unsigned long long* kwg = A.kwg;
+  if (A.kwg_lds) {
+    unsigned long long* k = (unsigned long long*)(gevents + A.G);
+    for (uint32_t i = threadIdx.x; i < A.kwg_lds / 8; i += blockDim.x) k[i] = A.kwg[i];
+    kwg = k;
+  }
+  return ItemLds{gofbit, gback, gevents, kwg};
+}
+
+// word w of file f's group gates (ggate_file's value)
+__device__ __forceinline__ unsigned long long file_gate(const ItemArgs& A, const ItemLds& T, uint32_t f, uint32_t w) {
+  if (A.ggate) return A.ggate[(size_t)f * A.GW + w];
+  const uint32_t* kwf = A.kw + (size_t)f * A.W;
+  unsigned long long acc = A.galw[w];
+  for (uint32_t i = 0; i < A.W; i++)
+    for (uint32_t bits = kwf[i]; bits; bits &= bits - 1) acc |= T.kwg[(size_t)(i * 32 + __builtin_ctz(bits)) * A.GW + w];
+  return acc;
 }
 
 template <class V>
@@ -1623,7 +1646,7 @@ __device__ __forceinline__ void gen_items(const ItemArgs& A, const ItemLds& T, u
       for (uint32_t w = 0; w < A.GW; w++) {
         unsigned long long cand = 0;
         for (uint32_t bits = evb; bits; bits &= bits - 1) cand |= T.gofbit[__builtin_ctz(bits) * A.GW + w];
-        cand &= file_gate(A, f, w) & ~T.gofbit[31 * A.GW + w];
+        cand &= file_gate(A, T, f, w) & ~T.gofbit[31 * A.GW + w];
         while (cand) {
           const uint32_t g = w * 64 + __builtin_ctzll(cand);
           cand &= cand - 1;
@@ -1642,7 +1665,7 @@ __device__ __forceinline__ void gen_items(const ItemArgs& A, const ItemLds& T, u
     const uint64_t fs = A.off[f], fe = A.off[f + 1];
     if (fe == fs) return;
     for (uint32_t w = 0; w < A.GW; w++) {
-      unsigned long long cand = file_gate(A, f, w) & T.gofbit[31 * A.GW + w];
+      unsigned long long cand = file_gate(A, T, f, w) & T.gofbit[31 * A.GW + w];
       while (cand) {
         const uint32_t g = w * 64 + __builtin_ctzll(cand);
         cand &= cand - 1;
@@ -1659,7 +1682,7 @@ __global__ void __launch_bounds__(kBlock) items_count_kernel(ItemArgs A) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   if (!A.ggate && threadIdx.x == 0) atomicMax(&A.clk[2], ~(unsigned long long)wall_clock64());  // (no gates pass)
   const ItemLds T = item_lds_load(A, smem);
-  uint32_t* s_count = (uint32_t*)(smem + item_lds_bytes(A.G, A.GW));
+  uint32_t* s_count = (uint32_t*)(smem + item_lds_bytes(A));
   for (uint32_t g = threadIdx.x; g < A.G; g += blockDim.x) s_count[g] = 0;
   __syncthreads();
   const uint64_t nt = (uint64_t)min(*A.nev, A.evcap) + A.F, stride = (uint64_t)gridDim.x * blockDim.x;
@@ -1825,7 +1848,7 @@ __device__ void layout_block(const LayoutArgs& A, uint8_t* s_kind, uint32_t* s_g
 __global__ void __launch_bounds__(kBlock) items_emit_kernel(ItemArgs A, LayoutArgs LA) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const ItemLds T = item_lds_load(A, smem);  // (published by layout_block's barriers)
-  uint32_t* s_count = (uint32_t*)(smem + item_lds_bytes(A.G, A.GW));
+  uint32_t* s_count = (uint32_t*)(smem + item_lds_bytes(A));
   uint32_t* s_base = s_count + A.G;
   uint32_t* s_gbase = s_base + A.G;
   uint8_t* s_kind = (uint8_t*)(s_gbase + A.G);
@@ -3230,7 +3253,7 @@ int device_rules_create(int device, const Plan& p, uint32_t chunk, uint32_t ext_
   }
   r->max_lds = std::max<uint32_t>(r->max_lds, 16);
   {  // the item passes' LDS: group tables (item_lds_bytes), counts, ranges, bases, kinds
-    const size_t emit_lds = item_lds_host(G, r->GW) + 13 * (size_t)G + 16;
+    const size_t emit_lds = item_lds_host(G, r->GW) + kItemKwgLdsMax + 13 * (size_t)G + 16;
     if (emit_lds > 160 * 1024) return fail(TSG_ERR_INTERNAL, "too many rule groups for the item passes");
     if (emit_lds > 64 * 1024) {
       HIP_TRY(hipFuncSetAttribute((const void*)items_emit_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)emit_lds));
@@ -3567,15 +3590,18 @@ int enqueue_scan(DeviceRules* r, LaneState* l, const ScanInput& in, HostOut* out
     IA.ggate = nullptr;  // (files gated from their keyword bits in the item passes)
   } else if (work) {
     const uint32_t cgrid = (uint32_t)std::min<uint64_t>((nchunks + kEvPer * kBlock - 1) / (kEvPer * kBlock), (uint64_t)r->grid);
+    const uint32_t kwg_bytes = (uint32_t)(32ull * W * r->GW * 8);
     GateArgs GA{l->ev_bits, nchunks, l->evlist, l->counts + 1, cgrid, l->kw, F, W, r->GW, r->d_kwg, r->d_galw, l->ggate,
-                (unsigned long long*)(l->counts + kClk)};
-    gates_kernel<<<cgrid + (F + kBlock - 1) / kBlock, kBlock, 0, st>>>(GA);
+                (unsigned long long*)(l->counts + kClk), kwg_bytes <= kKwgLdsMax ? kwg_bytes : 0u};
+    gates_kernel<<<cgrid + (F + kBlock - 1) / kBlock, kBlock, GA.kwg_lds, st>>>(GA);
     HIP_TRY(hipGetLastError());
   }
   if (work) {
     // both items passes (bcount holds grid x G); ITEMS_BPC blocks per CU
     const int igrid = std::min(r->grid, r->cus * ITEMS_BPC);
-    const size_t ilds = item_lds_host(G, r->GW);
+    const uint32_t kwg_bytes = (uint32_t)(32ull * W * r->GW * 8);
+    IA.kwg_lds = !IA.ggate && kwg_bytes <= kItemKwgLdsMax ? kwg_bytes : 0u;
+    const size_t ilds = item_lds_host(G, r->GW) + IA.kwg_lds;
     hipLaunchKernelGGL(items_count_kernel, dim3(igrid), dim3(kBlock), ilds + G * sizeof(uint32_t) + 16, st, IA);
     HIP_TRY(hipGetLastError());
     LayoutArgs LA{l->gcount, G, nchunks, items_cap, max_dense, l->entries, l->counts + 2,
