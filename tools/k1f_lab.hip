@@ -12,6 +12,8 @@
 //   V3  + the run flags and run events (k1f_flags / k1f_runs, DPP look-behind), ballots
 //   V4  V3 with the 16 entries of a tile read at once
 //   V5  V3 without the cross-lane look-behind (the DPP moves)
+//   V6  V3 with each tile consumed before its queue register is reloaded (no register
+//       copies at the loop's back edge, so no vmcnt(0) there)
 // and times each (V3 also at 512 threads per block, one and two blocks per CU); V3 stamps
 // the shader clock against the 100 MHz wall clock.  L64_*: the same work with each lane
 // holding 64 contiguous bytes (lab64_k), the per-word overheads (look-behind, run flags of
@@ -62,7 +64,7 @@ struct Carry {
 template <int V>
 struct Lane {
   __device__ __forceinline__ uint32_t prev(uint32_t cur, uint32_t p) const {
-    if constexpr (V == 5) return prev_none(cur, p);
+    if constexpr (V == 5) return prev_none(cur, p);  // (V6 keeps the DPP)
     return ::prev(cur, p);
   }
   const uint8_t* smem;
@@ -221,7 +223,7 @@ __global__ void __launch_bounds__(1024) lab_k(const uint8_t* data, const uint4* 
       acc ^= v.x ^ v.y ^ v.z ^ v.w;
     } else {
       uint32_t un;
-      const uint32_t rb = V == 4 ? L.tile16(v, cy, un) : L.tile(v, cy, un);
+      const uint32_t rb = V == 4 ? L.tile16(v, cy, un) : L.tile(v, cy, un);  // (V6: V3's tile)
       if constexpr (V == 1) {
         acc ^= un;
       } else {
@@ -242,9 +244,14 @@ __global__ void __launch_bounds__(1024) lab_k(const uint8_t* data, const uint4* 
   for (; t + D <= t1; t += D) {
 #pragma unroll
     for (int k = 0; k < D; k++) {
-      const uint4 v = p[k];
-      p[k] = ld16(base + (size_t)(t + D + k) * kTile);
-      body(v);
+      if constexpr (V >= 6) {  // the tile consumed before its register is reloaded: no copies
+        body(p[k]);
+        p[k] = ld16(base + (size_t)(t + D + k) * kTile);
+      } else {
+        const uint4 v = p[k];
+        p[k] = ld16(base + (size_t)(t + D + k) * kTile);
+        body(v);
+      }
     }
   }
 #pragma unroll
@@ -408,6 +415,7 @@ int main(int argc, char** argv) {
   const float ms = R("V3_runs", 3);
   R("V4_all16", 4);
   R("V5_noDPP", 5);
+  R("V6_noCopyQ", 6);
   run("V3_512thr", [&] { lab_k<3><<<cus, 512>>>(buf, dent, nt, out, clk); }, reps);
   run("V3_2x512", [&] { lab_k<3><<<2 * cus, 512>>>(buf, dent, nt, out, clk); }, reps);
   run("V0_512thr", [&] { lab_k<0><<<cus, 512>>>(buf, dent, nt, out, clk); }, reps);

@@ -632,7 +632,9 @@ constexpr uint32_t kFCfMax = 512;                          // coarse file map en
 constexpr uint32_t kFStOff = kFCfOff + 4 * kFCfMax;        // block counters (listed, arrivals, waves done)
 constexpr uint32_t kFBitsOff = kFStOff + 16;               // the block's event-chunk bitmap (event list)
 constexpr uint32_t kFBitsWords = 3 * kFThreads;             // 12 KiB: 98,304 chunks of the block's range
-constexpr uint32_t kFLds = kFBitsOff + 4 * kFBitsWords;    // 158 KiB at 1024 threads
+constexpr uint32_t kFZoneOff = kFBitsOff + 4 * kFBitsWords;  // zone chunks marked: own [0, 32), next [32, 64) words
+constexpr uint32_t kFZoneChunks = 1024;                     // zone chunks per side (launch_k1f checks)
+constexpr uint32_t kFLds = kFZoneOff + 2 * kFZoneChunks / 8;  // 158 KiB at 1024 threads
 static_assert(kFLds <= 160 * 1024, "K1F's LDS");
 #ifndef K1F_DEPTH
 #define K1F_DEPTH 4
@@ -663,13 +665,17 @@ struct K1FArgs {
   // whose event word K1F makes non-zero, once, in no particular order (ItemArgs::evlist).
   // A chunk of a block's range at least `zone` bytes past its start gets events from that
   // block alone (a literal ends at most zone - 1 bytes past its window end): the block marks
-  // it in an LDS bitmap and lists its marked chunks at its end.  Any other chunk (the first
-  // zone bytes of a range, which the previous block's literals reach too) is listed by the
-  // atomic that turns its event word non-zero.
+  // it in an LDS bitmap and lists its marked chunks at its end.  The chunks of the first
+  // zone bytes of a range get events from that block and the blocks before it: each block
+  // marks the zone chunks it touches (its own zone and the next range's) in LDS, and at its
+  // end claims them in `claim` (a bit per chunk, zeroed by prep); the block whose claim
+  // sets a chunk's bit lists it.  (No atomic in the tile loop returns a value: a returning
+  // one there made the compiler wait for every tile load in flight.)
   uint32_t* evlist;
   uint32_t* nev;
   uint32_t zone;
   uint32_t evcap;  // entries of evlist (a bound; the list holds each chunk once)
+  uint32_t* claim;
 };
 
 // lane i <- lane i - 1, lane 0 <- old (DPP wave_shr:1, out-of-range source keeps old)
@@ -808,20 +814,22 @@ __device__ __forceinline__ uint32_t f_wat(const uint32_t (&w)[6], uint32_t o) {
   return __builtin_amdgcn_alignbyte(hi, lo, o & 3u);
 }
 
-// event bits `bits` for chunk c (K1FArgs::evlist): c in [c_lo, c_hi) -> the block's bitmap
+// event bits `bits` for chunk c (K1FArgs::evlist): c in [c_lo, c_hi) -> the block's bitmap,
+// c in [z_lo, c_lo) (its zone) or [c_hi, c_hi + kFZoneChunks) (the next range's) -> the zone
+// bitmaps
 struct K1FMark {
   const K1FArgs& A;
   uint32_t* lbm;  // LDS bitmap of chunks [c_lo, c_hi)
-  uint32_t c_lo, c_hi;
+  uint32_t* lzm;  // LDS bitmaps of chunks [z_lo, z_lo + kFZoneChunks), [c_hi, c_hi + kFZoneChunks)
+  uint32_t z_lo, c_lo, c_hi;
   __device__ __forceinline__ void operator()(uint32_t c, uint32_t bits) const {
-    if (!A.evlist) {
-      atomicOr(&A.ev[c], bits);
-    } else if (c >= c_lo && c < c_hi) {
-      atomicOr(&A.ev[c], bits);
+    atomicOr(&A.ev[c], bits);
+    if (!A.evlist) return;
+    if (c >= c_lo && c < c_hi) {
       atomicOr(&lbm[(c - c_lo) >> 5], 1u << ((c - c_lo) & 31));
-    } else if (atomicOr(&A.ev[c], bits) == 0u) {  // (rare: the zone, and chunks past the range)
-      const uint32_t i = atomicAdd(A.nev, 1u);
-      if (i < A.evcap) A.evlist[i] = c;
+    } else {
+      const uint32_t z = c < c_lo ? c - z_lo : kFZoneChunks + (c - c_hi);
+      if (z < 2 * kFZoneChunks) atomicOr(&lzm[z >> 5], 1u << (z & 31));
     }
   }
 };
@@ -955,13 +963,17 @@ __global__ void __launch_bounds__(kFThreads) k1f_kernel(DevK1F d, K1FArgs A) {
   for (uint32_t i = threadIdx.x; i < ncl; i += blockDim.x) lcf[i] = A.cf[kc0 + i];
   uint32_t* bst = (uint32_t*)(smem + kFStOff);
   if (threadIdx.x < 3) bst[threadIdx.x] = 0;
-  // the event list: the block's non-zone chunks [c_lo, c_hi) in the LDS bitmap
+  // the event list: the block's non-zone chunks [c_lo, c_hi) in the LDS bitmap, the zone
+  // chunks in the zone bitmaps
   uint32_t* lbm = (uint32_t*)(smem + kFBitsOff);
-  const uint32_t c_hi = (uint32_t)(min<uint64_t>(bb1, A.total + (uint64_t)A.chunk - 1) / A.chunk);
+  uint32_t* lzm = (uint32_t*)(smem + kFZoneOff);
+  const uint32_t z_lo = (uint32_t)(bb0 / A.chunk);
+  const uint32_t c_hi = max(z_lo, (uint32_t)(min<uint64_t>(bb1, A.total + (uint64_t)A.chunk - 1) / A.chunk));
   const uint32_t c_lo = min(c_hi, (uint32_t)((bb0 + A.zone + A.chunk - 1) / A.chunk));
   const uint32_t nbw = A.evlist ? (c_hi - c_lo + 31) / 32 : 0u;  // (<= kFBitsWords: launch_k1f)
   for (uint32_t i = threadIdx.x; i < nbw; i += blockDim.x) lbm[i] = 0;
-  const K1FMark mark{A, lbm, c_lo, c_hi};
+  if (threadIdx.x < 2 * kFZoneChunks / 32) lzm[threadIdx.x] = 0;
+  const K1FMark mark{A, lbm, lzm, z_lo, c_lo, c_hi};
   __syncthreads();
   const uint32_t t0 = (uint32_t)((uint64_t)gw * A.ntiles / nw), t1 = (uint32_t)((uint64_t)(gw + 1) * A.ntiles / nw);
   if (t0 < t1) {  // (waves without tiles wait at the block barrier below)
@@ -983,12 +995,15 @@ __global__ void __launch_bounds__(kFThreads) k1f_kernel(DevK1F d, K1FArgs A) {
     qn -= n;
   };
   FCarry cy{0, 0, 0, 0, 0};  // (the warm-up tile's own inputs do not reach its outputs)
-  uint32_t g[4], vw = 0;     // vw: the previous tile's last dword per lane (captured bytes)
+  // vw: lane 63's last dword of the previous tile (the captured bytes before lane 0's word),
+  // kept in a scalar register: a per-lane copy of the tile's .w held its queue register past
+  // the reload and made the loop wait for the loads in flight at its back edge
+  uint32_t g[4], vw = 0;
   {  // warm-up: the tile before t0 (zero bytes before the batch) gives the carries
     uint4 v = make_uint4(0, 0, 0, 0);
     if (t0 > 0) v = *(const uint4*)(A.data + (size_t)(t0 - 1) * kFTile + 16u * lane);
     (void)L.tile(v, cy, g);
-    vw = v.w;
+    vw = __builtin_amdgcn_readlane(v.w, 63);
   }
   // the tiles of the range, kFDepth loads in flight (memory latency bounds a wave with fewer:
   // profiles/r05/kv2).  A listed word enters the ring with its 20 bytes (the 4 before it
@@ -1023,7 +1038,7 @@ __global__ void __launch_bounds__(kFThreads) k1f_kernel(DevK1F d, K1FArgs A) {
     if (__builtin_expect(hb != 0, 0)) {
       const uint32_t n = (uint32_t)__popcll(hb);
       if (kFQueue < 128 && qn + n > kFQueue) drain(qn);  // (a small ring: room for the tile's words)
-      const uint32_t wprev = f_prev(v.w, vw);  // bytes pos-4 .. pos-1 (all lanes: DPP)
+      const uint32_t wprev = f_shr1(v.w, vw);  // bytes pos-4 .. pos-1 (all lanes: DPP)
       if (bun) {
         const uint32_t slot = __builtin_amdgcn_mbcnt_hi((uint32_t)(hb >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)hb, 0u));
         const uint32_t gm = ((g[0] & 0xFFFFu) ? 1u : 0u) | ((g[1] & 0xFFFFu) ? 2u : 0u) | ((g[2] & 0xFFFFu) ? 4u : 0u) |
@@ -1036,7 +1051,7 @@ __global__ void __launch_bounds__(kFThreads) k1f_kernel(DevK1F d, K1FArgs A) {
       nlisted += n;
       if (qn >= 64) drain(64);
     }
-    vw = v.w;
+    vw = __builtin_amdgcn_readlane(v.w, 63);
   };
 #if K1F_DMA
   // tiles through an LDS ring of K1F_DMA slots per wave, filled by LDS-DMA (no VGPRs held
@@ -1085,15 +1100,17 @@ __global__ void __launch_bounds__(kFThreads) k1f_kernel(DevK1F d, K1FArgs A) {
     // are in flight: a verification at the very end (a literal read back, a file lookup)
     // would extend the kernel by its latency (profiles/r05/ab3)
     if (t + 2 * kFDepth > t1 && qn) drain(qn);
+    // each tile is consumed before its queue register is reloaded: no register copies at
+    // the loop's back edge, whose vmcnt(0) waited for the youngest load every kFDepth tiles
+    // (the loop waits vmcnt(kFDepth - 1) before each tile instead)
 #pragma unroll
     for (uint32_t k = 0; k < kFDepth; k++) {
-      const uint4 v = p[k];
+      body(p[k], t + k);
 #if K1F_NOLOAD  // (timing only: the wave's first tiles again and again, from L2)
       p[k] = *(const uint4*)(base + (t0 + k) * kFTile);
 #else
       p[k] = f_tile_load(base + (t + kFDepth + k) * kFTile);
 #endif
-      body(v, t + k);
     }
   }
 #pragma unroll
@@ -1112,6 +1129,17 @@ __global__ void __launch_bounds__(kFThreads) k1f_kernel(DevK1F d, K1FArgs A) {
   }
   }  // (t0 < t1)
   __syncthreads();
+  if (A.evlist && threadIdx.x < 2 * kFZoneChunks / 32) {  // the zone chunks this block touched
+    for (uint32_t b = lzm[threadIdx.x]; b; b &= b - 1) {
+      const uint32_t z = 32 * threadIdx.x + __builtin_ctz(b);
+      const uint32_t c = z < kFZoneChunks ? z_lo + z : c_hi + (z - kFZoneChunks);
+      const uint32_t bit = 1u << (c & 31);
+      if (!(atomicOr(&A.claim[c >> 5], bit) & bit)) {
+        const uint32_t i = atomicAdd(A.nev, 1u);
+        if (i < A.evcap) A.evlist[i] = c;
+      }
+    }
+  }
   if (nbw) {  // the block's marked chunks into the event list: one claim per block
     uint32_t wv[kFBitsWords / kFThreads], n = 0;
 #pragma unroll
@@ -2904,6 +2932,8 @@ struct LaneState {
   size_t xcount_cap = 0;
   uint32_t* evlist = nullptr;
   size_t evlist_cap = 0;
+  uint32_t* zclaim = nullptr;  // K1F's zone claims (K1FArgs::claim): a bit per chunk
+  size_t zclaim_cap = 0;
   uint32_t* kw = nullptr;
   size_t kw_cap = 0;
   unsigned long long* ggate = nullptr;
@@ -2932,7 +2962,7 @@ struct LaneState {
     if (!d) return;
     (void)hipSetDevice(d->device);
     if (st) (void)hipStreamSynchronize(st);
-    void* bufs[] = {data_alloc, meta, cf, ev_bits, xlist, xcount, evlist, kw, ggate, ovf, hascand,
+    void* bufs[] = {data_alloc, meta, cf, ev_bits, xlist, xcount, evlist, zclaim, kw, ggate, ovf, hascand,
                     items, entries, dentries, cand, counts, gcount, bcount, cursor, gskip, etrace};
     for (void* b : bufs) (void)hipFree(b);
     if (st) (void)hipStreamDestroy(st);
@@ -3108,6 +3138,7 @@ static int k1f_grid(const DeviceRules* r, uint32_t ntiles) {
 // block's range of chunks fits the LDS bitmap
 static bool k1f_lists(const DeviceRules* r, uint32_t ntiles, uint32_t chunk) {
   if (chunk == 0 || chunk > kFTile || kFTile % chunk) return false;
+  if ((r->k1f_maxlen + chunk - 1) / chunk + 1 > kFZoneChunks) return false;
   const uint64_t grid = (uint64_t)k1f_grid(r, ntiles), wpb = kFThreads / 64, nw = grid * wpb;
   const uint64_t block_tiles = (wpb * ntiles + nw - 1) / nw + 1;  // (ranges differ by at most one tile per wave)
   return block_tiles * (kFTile / chunk) <= 32ull * kFBitsWords;
@@ -3442,6 +3473,8 @@ int enqueue_scan(DeviceRules* r, LaneState* l, const ScanInput& in, HostOut* out
   if (r->has_k1x && (rc = ensure(&l->xlist, &l->xlist_cap, (size_t)(total / 256 + 65536)))) return rc;
   if (r->has_k1x && (rc = ensure(&l->xcount, &l->xcount_cap, (size_t)std::max(r->cus, 1)))) return rc;
   if ((rc = ensure(&l->evlist, &l->evlist_cap, (size_t)nchunks_pad))) return rc;
+  const uint64_t zclaim_words = nchunks_pad / 32 + 2;
+  if (k1f && (rc = ensure(&l->zclaim, &l->zclaim_cap, (size_t)zclaim_words))) return rc;
   if ((rc = ensure(&l->kw, &l->kw_cap, (size_t)F * W + 1))) return rc;
   if ((rc = ensure(&l->ggate, &l->ggate_cap, (size_t)F * r->GW + 1))) return rc;
   if ((rc = ensure(&l->ovf, &l->ovf_cap, (size_t)F + 1))) return rc;
@@ -3499,6 +3532,7 @@ int enqueue_scan(DeviceRules* r, LaneState* l, const ScanInput& in, HostOut* out
     zero(l->hascand, F);
     zero(l->counts, sizeof(uint32_t) * kCounts);
     if (k1f) zero(l->ev_bits, sizeof(uint32_t) * nchunks_pad);  // K1F ORs events in
+    if (k1f) zero(l->zclaim, sizeof(uint32_t) * zclaim_words);    // K1F's zone claims
     zero(l->gcount, sizeof(uint32_t) * G);
     zero(l->cursor, sizeof(uint32_t) * G);
     zero(l->gskip, G);
@@ -3527,13 +3561,14 @@ int enqueue_scan(DeviceRules* r, LaneState* l, const ScanInput& in, HostOut* out
   if (k1f) {
     K1FArgs A{data, l->off, l->cf, (uint32_t)total, C, F, k1f_tiles, F ? (uint32_t)ncf : 0u,
               l->kw, l->ev_bits, nullptr, l->counts + 16, (unsigned long long*)(l->counts + kClk),
-              nullptr, nullptr, r->k1f_maxlen, 0};
+              nullptr, nullptr, r->k1f_maxlen, 0, nullptr};
     if (!r->adapted && total >= adapt_bytes && (rc = adapt_k1f(r, l, A, in.data))) return rc;
     if (k1f_list) {
       A.evlist = l->evlist;
       A.nev = l->counts + 1;
       A.evcap = (uint32_t)std::min<size_t>(l->evlist_cap, 0xFFFFFFFFu);
       A.zone = r->k1f_maxlen;  // (after the adaptation's rebuild)
+      A.claim = l->zclaim;
     }
     if (total && (rc = launch_k1f(r, A, st))) return rc;
   } else if (!r->adapted && k1_items >= 64 && total >= adapt_bytes) {
