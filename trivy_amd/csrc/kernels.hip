@@ -2530,13 +2530,9 @@ __device__ __forceinline__ void k2_run(const DevDFA* __restrict__ dfas, const K2
   }
 }
 
-// The list pass, then (the same blocks, as they run out of list entries) the dense entries:
-// a dense pass of its own was a launch of ~9 us per batch, mostly with no dense entry at all
-static_assert(kK2Block == kBlock, "dense entries are sized for kBlock threads");
 __global__ void __launch_bounds__(kK2Block) K2_WAVES k2_kernel(const DevDFA* __restrict__ dfas, K2Args A) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   k2_run<false>(dfas, A, A.entries, *A.nentries, A.claim, smem);
-  k2_run<true>(dfas, A, A.dentries, *A.ndentries, A.claim + 1, smem);
 }
 // the list pass when the staged table allows two blocks per CU at most (> 53 KiB): eight
 // waves per CU, so each may hold 256 VGPRs (k2_list_pair<true>)
@@ -2544,9 +2540,12 @@ __global__ void __launch_bounds__(kK2Block) __attribute__((amdgpu_waves_per_eu(1
 k2_kernel_rich(const DevDFA* __restrict__ dfas, K2Args A) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   k2_run<false, true>(dfas, A, A.entries, *A.nentries, A.claim, smem);
-  k2_run<true>(dfas, A, A.dentries, *A.ndentries, A.claim + 1, smem);
 }
 
+__global__ void __launch_bounds__(kBlock) k2_dense_kernel(const DevDFA* __restrict__ dfas, K2Args A) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  k2_run<true>(dfas, A, A.dentries, *A.ndentries, A.claim + 1, smem);
+}
 
 // ---------------------------------------------------------------- host side
 template <class T>
@@ -2874,7 +2873,7 @@ struct DeviceRules {
   uint32_t chunk = 256, ext_cap = 1u << 16, adapt_mib = 0;
   int grid = 0;          // 8 blocks per CU
   int cus = 0;
-  int k2_grid = 0;  // resident blocks of the persistent K2 kernel (list, then dense entries)
+  int k2_grid = 0, k2_dense_grid = 0;  // resident blocks of the persistent K2 kernels
   bool k2_rich = false;                 // the list pass runs k2_kernel_rich (same residency)
   hipEvent_t kernels_done = nullptr;   // end of the kernels of the last enqueued batch
   bool kernels_done_valid = false;
@@ -3295,6 +3294,8 @@ int device_rules_create(int device, const Plan& p, uint32_t chunk, uint32_t ext_
   if (r->max_lds > 64 * 1024) {
     HIP_TRY(hipFuncSetAttribute((const void*)k2_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)r->max_lds));
     HIP_TRY(hipFuncSetAttribute((const void*)k2_kernel_rich, hipFuncAttributeMaxDynamicSharedMemorySize, (int)r->max_lds));
+    HIP_TRY(hipFuncSetAttribute((const void*)k2_dense_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)r->max_lds));
   }
   const uint32_t* cg = nullptr;
   if ((rc = upload_vec(gmask, &cg, &r->tables))) return rc;
@@ -3344,6 +3345,8 @@ int device_rules_create(int device, const Plan& p, uint32_t chunk, uint32_t ext_
     HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ_rich, (const void*)k2_kernel_rich, kK2Block, r->max_lds));
     r->k2_rich = occ_rich >= 1 && occ_rich >= occ;
   }
+  HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void*)k2_dense_kernel, kBlock, r->max_lds));
+  r->k2_dense_grid = r->cus * std::max(occ, 1);
   *out = r.release();
   return TSG_OK;
 }
@@ -3682,7 +3685,10 @@ int enqueue_scan(DeviceRules* r, LaneState* l, const ScanInput& in, HostOut* out
       hipLaunchKernelGGL(k2_kernel_rich, dim3(r->k2_grid), dim3(kK2Block), r->max_lds, st, (const DevDFA*)r->d_groups, A);
     else
       hipLaunchKernelGGL(k2_kernel, dim3(r->k2_grid), dim3(kK2Block), r->max_lds, st, (const DevDFA*)r->d_groups, A);
-    HIP_TRY(hipGetLastError());  // (the dense entries run in the same launch, after the list)
+    HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL(k2_dense_kernel, dim3(r->k2_dense_grid), dim3(kBlock), r->max_lds, st,
+                       (const DevDFA*)r->d_groups, A);
+    HIP_TRY(hipGetLastError());
     // (the dense pass on a second stream beside the list pass: K2 0.125 -> 0.152 ms per
     // batch, the two grids slowed each other; profiles/r04/e)
   }
