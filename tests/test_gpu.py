@@ -144,8 +144,8 @@ def test_k1f_event_list(builtin, knob, chunk, grid):
     range, first-touch appends in the zone a previous block's literals reach): the list
     holds every chunk with events exactly once (its length == the non-empty words of
     k1_reference's events), and the findings through the item passes, which then gate files
-    from their keyword bits, equal the exact CPU path and the gates-pass path
-    (no_k1f_list).  grid 3: ranges of megabytes; the default grid: ranges of a few tiles
+    from their keyword bits, equal the exact CPU path and the gates-pass path (the default:
+    the list is opt-in, knob k1f_list).  grid 3: ranges of megabytes; the default grid: ranges of a few tiles
     that the zone covers whole."""
     import numpy as np
     if grid:
@@ -155,8 +155,8 @@ def test_k1f_event_list(builtin, knob, chunk, grid):
     for b in (batch, edge):
         want = builtin.ScanBatch(b, nthreads=16)
         _, rev = builtin.k1_reference(b, chunk)
-        for legacy in ("", "1"):
-            knob("no_k1f_list", legacy)
+        for listing in ("1", ""):
+            knob("k1f_list", listing)
             ctx = S.GpuContext(builtin, 0, chunk_bytes=chunk, adapt_mib=0xFFFFFFFF)
             ctx.upload(b)
             ctx.kernels()
@@ -165,8 +165,8 @@ def test_k1f_event_list(builtin, knob, chunk, grid):
             got = ctx.scan()
             ctx.close()
             assert np.array_equal(ev, rev)
-            assert nev == int(np.count_nonzero(rev)), (legacy, nev, int(np.count_nonzero(rev)))
-            assert got == want, legacy
+            assert nev == int(np.count_nonzero(rev)), (listing, nev, int(np.count_nonzero(rev)))
+            assert got == want, listing
 
 
 @pytest.mark.parametrize("grid", [1, 3])

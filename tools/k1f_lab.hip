@@ -14,6 +14,9 @@
 //   V5  V3 without the cross-lane look-behind (the DPP moves)
 //   V6  V3 with each tile consumed before its queue register is reloaded (no register
 //       copies at the loop's back edge, so no vmcnt(0) there)
+//   V7  V6 with two copies of the table in LDS, the waves of SIMDs {0,1} reading one and
+//       those of {2,3} the other
+//   V8  V6 with three of four waves starting ~8 us late (staggered phases)
 // and times each (V3 also at 512 threads per block, one and two blocks per CU); V3 stamps
 // the shader clock against the 100 MHz wall clock.  L64_*: the same work with each lane
 // holding 64 contiguous bytes (lab64_k), the per-word overheads (look-behind, run flags of
@@ -201,20 +204,23 @@ struct Lane {
 template <int V>
 __global__ void __launch_bounds__(1024) lab_k(const uint8_t* data, const uint4* ent, uint32_t ntiles,
                                                uint32_t* out, unsigned long long* clk) {
-  __shared__ __attribute__((aligned(16))) uint8_t smem[65536];
+  __shared__ __attribute__((aligned(16))) uint8_t smem[V == 7 ? 131072 : 65536];
   long long c0 = 0, w0 = 0;
   if (V == 3 && blockIdx.x == 0 && threadIdx.x == 0) {
     c0 = clock64();
     w0 = wall_clock64();
   }
   if (V >= 1) {
-    for (uint32_t i = threadIdx.x; i < 4096; i += blockDim.x) ((uint4*)smem)[i] = ent[i >> 4];
+    for (uint32_t i = threadIdx.x; i < (V == 7 ? 8192u : 4096u); i += blockDim.x) ((uint4*)smem)[i] = ent[(i & 4095) >> 4];
     __syncthreads();
   }
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6, wpb = blockDim.x >> 6;
   const uint32_t gw = blockIdx.x * wpb + wave, nw = gridDim.x * wpb;
   const uint32_t t0 = (uint32_t)((uint64_t)gw * ntiles / nw), t1 = (uint32_t)((uint64_t)(gw + 1) * ntiles / nw);
-  const Lane<V> L{smem, (lane & 15u) << 4};
+  // V7: the table copy of the wave's SIMD half (HW_ID bits 5:4 = SIMD)
+  const uint32_t simd = ((uint32_t)__builtin_amdgcn_s_getreg(4 | (31 << 11)) >> 4) & 3u;
+  const Lane<V> L{smem + (V == 7 ? (simd >> 1) * 65536u : 0u), (lane & 15u) << 4};
+  if (V == 8 && (wave & 3)) __builtin_amdgcn_s_sleep(127);  // staggered starts (127 x 64 cycles)
   Carry cy{0, 0, 0, 0, 0};
   uint32_t acc = 0, nl = 0, nr = 0;
   const uint8_t* base = data + 16u * lane;
@@ -416,11 +422,14 @@ int main(int argc, char** argv) {
   R("V4_all16", 4);
   R("V5_noDPP", 5);
   R("V6_noCopyQ", 6);
+  R("V7_tablePerSimdHalf", 7);
+  R("V8_stagger", 8);
   run("V3_512thr", [&] { lab_k<3><<<cus, 512>>>(buf, dent, nt, out, clk); }, reps);
   run("V3_2x512", [&] { lab_k<3><<<2 * cus, 512>>>(buf, dent, nt, out, clk); }, reps);
+  run("V6_2x512", [&] { lab_k<6><<<2 * cus, 512>>>(buf, dent, nt, out, clk); }, reps);
+  run("V6_4x256", [&] { lab_k<6><<<4 * cus, 256>>>(buf, dent, nt, out, clk); }, reps);
   run("V0_512thr", [&] { lab_k<0><<<cus, 512>>>(buf, dent, nt, out, clk); }, reps);
-  run("L64_V0_loads", [&] { lab64_k<0><<<cus, 1024>>>(buf, dent, nt, out, clk); }, reps);
-  run("L64_V1_full", [&] { lab64_k<1><<<cus, 1024>>>(buf, dent, nt, out, clk); }, reps);
+  // (L64: lane-contiguous 64 B streams at 3.8 TB/s -- profiles/r06/c/lab.json -- not pursued)
   unsigned long long c[2];
   CHECK(hipMemcpy(c, clk, 16, hipMemcpyDeviceToHost));
   printf("{\"block0_cycles\": %llu, \"block0_wall_ticks\": %llu, \"shader_MHz\": %.0f, \"kernel_ms\": %.4f}\n", c[0], c[1],

@@ -31,7 +31,7 @@ uint64_t ctx_slot_bytes(const tsg_ctx* c);
 struct Knobs {
   std::atomic<int64_t> tar_range_kib{0}, piece_mib{0}, pike_only{0}, no_k1x{0}, emu_wordrec{0},
       x_step{0}, k1_automaton{0}, group_states{0}, group_table_kib{0}, k1f_grid{0},
-      no_k1f_list{0};
+      k1f_list{0};
   std::mutex m;
   std::string emu_kw_unknown;
 };

@@ -3557,7 +3557,9 @@ int enqueue_scan(DeviceRules* r, LaneState* l, const ScanInput& in, HostOut* out
   // K1F lists the event chunks itself: no compaction pass, and the item passes gate files
   // from their keyword bits (no gates pass at all)
   // (K1X, when a plan has it, adds events after K1: the gates pass lists them all)
-  const bool k1f_list = k1f && total && !r->has_k1x && !knobs().no_k1f_list.load() && k1f_lists(r, k1f_tiles, C);
+  // (opt-in, knob k1f_list: kernel-only on the configs[1] batch it cost K1F ~3 us and the
+  // item passes ~5 us more than the gates pass it replaces, profiles/r06/d)
+  const bool k1f_list = k1f && total && !r->has_k1x && knobs().k1f_list.load() && k1f_lists(r, k1f_tiles, C);
   if (k1f) {
     K1FArgs A{data, l->off, l->cf, (uint32_t)total, C, F, k1f_tiles, F ? (uint32_t)ncf : 0u,
               l->kw, l->ev_bits, nullptr, l->counts + 16, (unsigned long long*)(l->counts + kClk),

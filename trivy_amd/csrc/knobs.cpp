@@ -37,7 +37,7 @@ extern "C" int tsg_test_knob(const char* name, const char* value) {
   else if (!strcmp(name, "emu_wordrec")) k.emu_wordrec = x;
   else if (!strcmp(name, "k1_automaton")) k.k1_automaton = x;
   else if (!strcmp(name, "group_states")) k.group_states = x;
-  else if (!strcmp(name, "no_k1f_list")) k.no_k1f_list = x;  // K1F without its event list (the gates pass compacts)
+  else if (!strcmp(name, "k1f_list")) k.k1f_list = x;  // K1F lists the event chunks (no gates pass)
   else if (!strcmp(name, "k1f_grid")) {  // cap on K1F's blocks: many tiles per wave in small tests
     if (x < 0) return fail(TSG_ERR_ARG, "k1f_grid must be >= 0");
     k.k1f_grid = x;
