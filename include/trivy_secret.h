@@ -307,7 +307,7 @@ const char* tsg_last_error(void);
  * Process-wide switches that change how (never what) the library computes, for tests and
  * measurements only.  They are set through this call alone: the library reads no
  * environment variable that changes a plan, a kernel or a result (the profiling switches
- * TSG_PROF, TSG_PROF2, TSG_LAYER_PROF, TSG_K2_DIAG, TSG_K2_TRACE and TSG_DEBUG_RESOLVE only
+ * TSG_PROF, TSG_PROF2, TSG_LAYER_PROF, TSG_K2_DIAG, TSG_K2_TRACE, TSG_K1F_TRACE and TSG_DEBUG_RESOLVE only
  * add timings, counters or traces).  value NULL or "" resets the knob.
  *   "tar_range_kib"   sub-range floor of the parallel tar index walk (default 64 MiB)
  *   "piece_mib"       piece floor of tsg_layer_scan / tsg_fs_scan (default 16)
@@ -325,6 +325,10 @@ const char* tsg_last_error(void);
  *                     (default 2,048 for rule sets of up to 256 rules, else 1,024)
  *   "group_table_kib" table cap of a K2 rule-group DFA, 1..64 KiB (default 64 for rule
  *                     sets of up to 256 rules, else 48)
+ *   "k1f_grid"        cap on K1F's blocks (default: one per CU): many tiles per wave in
+ *                     small test batches
+ *   "k1f_list"        "1": K1F lists the chunks with events itself (no gates pass; the item
+ *                     passes gate files from their keyword bits)
  * Returns TSG_ERR_ARG for an unknown name. */
 int tsg_test_knob(const char* name, const char* value);
 

@@ -28,10 +28,7 @@ for v in "$@"; do
     x8) build $v -DK1X_WORDS=8 ;;
     xdiag) build $v -DK1X_DIAG ;;
     f16) build $v -DK1F_ALL16=1 ;;       # K1F: all 16 entries of a tile read at once
-    fdma2) build $v -DK1F_DMA=2 ;;       # K1F: tiles through an LDS-DMA ring, 2 slots per wave
-    fdma2q) build $v -DK1F_DMA=2 -DK1F_ALL16=1 ;;
     fq64) build $v -DK1F_QUEUE=64 ;;     # K1F: the register queue with the small verification ring
-    fnold) build $v -DK1F_NOLOAD=1 ;;    # K1F: timing only, no tile loads in the loop (wrong results)
     fd2) build $v -DK1F_DEPTH=2 ;;       # K1F: register queue depths
     fd3) build $v -DK1F_DEPTH=3 ;;        # K1X: verify counters in k2_long_tails (slot probes),
                                          # k2_tail_bytes (entries examined), k2_tail_max (matches)

@@ -105,5 +105,6 @@ int lane_events(LaneState* l, uint32_t* ev, size_t n);
 // K2 per-entry trace of the lane's last batch (TSG_K2_TRACE; empty otherwise): per entry
 // {start, end, group << 32 | items, XCC_ID << 32 | HW_ID}
 int lane_k2_trace(LaneState* l, std::vector<unsigned long long>* out);
+int lane_k1f_trace(LaneState* l, std::vector<unsigned long long>* out);  // TSG_K1F_TRACE
 
 }  // namespace tsg

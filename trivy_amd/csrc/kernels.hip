@@ -611,11 +611,8 @@ __global__ void __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(4, 8))
 // starts sets its bit without a global load, and a literal inside the captured bytes is
 // compared without one: the verification of the last words of the range (which nothing
 // overlaps) costs LDS latency, not HBM round trips under full streaming load.
-#ifndef K1F_DMA
-#define K1F_DMA 0  // > 0: tiles in flight through an LDS ring filled by LDS-DMA (measurement)
-#endif
 #ifndef K1F_QUEUE
-#define K1F_QUEUE (K1F_DMA ? 64 : 128)
+#define K1F_QUEUE 128
 #endif
 constexpr uint32_t kFQueue = K1F_QUEUE;                    // ring entries (32 B) per wave
 static_assert(kFQueue >= 64 && (kFQueue & (kFQueue - 1)) == 0, "a tile lists up to 64 words");
@@ -625,8 +622,7 @@ constexpr uint32_t kFQueueOff = kFEntBytes;
 #define K1F_THREADS 1024
 #endif
 constexpr int kFThreads = K1F_THREADS;                     // one block per CU
-constexpr uint32_t kFDmaOff = kFQueueOff + (kFThreads / 64) * kFQueue * 32;  // [wave][K1F_DMA][1 KiB]
-constexpr uint32_t kFImgOff = kFDmaOff + (kFThreads / 64) * K1F_DMA * 1024;
+constexpr uint32_t kFImgOff = kFQueueOff + (kFThreads / 64) * kFQueue * 32;
 constexpr uint32_t kFCfOff = kFImgOff + kFImgMax;
 constexpr uint32_t kFCfMax = 512;                          // coarse file map entries in LDS
 constexpr uint32_t kFStOff = kFCfOff + 4 * kFCfMax;        // block counters (listed, arrivals, waves done)
@@ -639,6 +635,7 @@ static_assert(kFLds <= 160 * 1024, "K1F's LDS");
 #ifndef K1F_DEPTH
 #define K1F_DEPTH 4
 #endif
+
 constexpr uint32_t kFDepth = K1F_DEPTH;                    // tiles in flight per wave
 
 struct DevK1F {
@@ -676,6 +673,9 @@ struct K1FArgs {
   uint32_t zone;
   uint32_t evcap;  // entries of evlist (a bound; the list holds each chunk once)
   uint32_t* claim;
+  // null, or per wave (measurements, TSG_K1F_TRACE): {start after the staging, end of its
+  // tiles, tiles << 32 | listed words, XCC_ID << 32 | HW_ID} (wall clock, 100 MHz)
+  unsigned long long* wtrace;
 };
 
 // lane i <- lane i - 1, lane 0 <- old (DPP wave_shr:1, out-of-range source keeps old)
@@ -961,7 +961,7 @@ __global__ void __launch_bounds__(kFThreads) k1f_kernel(DevK1F d, K1FArgs A) {
   const uint32_t ncl = kc1 > kc0 ? (uint32_t)min<uint64_t>(kc1 - kc0, kFCfMax) : 0u;
   uint32_t* lcf = (uint32_t*)(smem + kFCfOff);
   for (uint32_t i = threadIdx.x; i < ncl; i += blockDim.x) lcf[i] = A.cf[kc0 + i];
-  uint32_t* bst = (uint32_t*)(smem + kFStOff);
+  uint32_t* bst = (uint32_t*)(smem + kFStOff);  // listed words, arrivals, next chunk
   if (threadIdx.x < 3) bst[threadIdx.x] = 0;
   // the event list: the block's non-zone chunks [c_lo, c_hi) in the LDS bitmap, the zone
   // chunks in the zone bitmaps
@@ -975,8 +975,44 @@ __global__ void __launch_bounds__(kFThreads) k1f_kernel(DevK1F d, K1FArgs A) {
   if (threadIdx.x < 2 * kFZoneChunks / 32) lzm[threadIdx.x] = 0;
   const K1FMark mark{A, lbm, lzm, z_lo, c_lo, c_hi};
   __syncthreads();
-  const uint32_t t0 = (uint32_t)((uint64_t)gw * A.ntiles / nw), t1 = (uint32_t)((uint64_t)(gw + 1) * A.ntiles / nw);
-  if (t0 < t1) {  // (waves without tiles wait at the block barrier below)
+  // The block's tiles [bt0, bt1), handed to its waves in chunks as they ask (an LDS counter)
+  // rather than in equal shares: waves of one CU run at very different speeds -- issue goes
+  // to the older wave first -- and with equal shares the block waited for its slowest wave
+  // (one launch: wave times 129-241 us, median 184; tools/k1ftrace.py, profiles/r06/g).
+  // Chunk sizes shrink (guided): the first chunk of each wave is a 32nd of the block's tiles,
+  // then 128ths, then 512ths.  A chunk starts with the carries of the tile before it: lanes
+  // 62 and 63 load that tile's last 32 bytes (the other lanes repeat their addresses) and the
+  // tile logic runs once on them.
+  const uint32_t bt0 = (uint32_t)((uint64_t)blockIdx.x * wpb * A.ntiles / nw);
+  const uint32_t bt1 = (uint32_t)((uint64_t)(blockIdx.x + 1) * wpb * A.ntiles / nw);
+  const uint32_t T = bt1 - bt0;
+  const uint32_t s1 = T / (2 * wpb), s2 = max(1u, s1 / 4), s3 = max(1u, s1 / 16);
+  const uint32_t p1 = s1 * wpb, p3 = s1 ? min(T - p1, T / 8) : 0u, p2 = T - p1 - p3;
+  const uint32_t n1 = s1 ? wpb : 0u, n2 = s1 ? (p2 + s2 - 1) / s2 : T, n3 = (p3 + s3 - 1) / s3;
+  // chunk c -> block tiles [a, b); false past the last chunk
+  auto chunk_of = [&](uint32_t c, uint32_t& a, uint32_t& b) __attribute__((always_inline)) {
+    if (c < n1) {
+      a = c * s1;
+      b = a + s1;
+    } else if (c < n1 + n2) {
+      const uint32_t w = s1 ? s2 : 1u;
+      a = p1 + (c - n1) * w;
+      b = min(a + w, p1 + p2);
+    } else if (c < n1 + n2 + n3) {
+      a = p1 + p2 + (c - n1 - n2) * s3;
+      b = min(a + s3, T);
+    } else {
+      return false;
+    }
+    return true;
+  };
+  if (A.wtrace && lane == 0) {
+    A.wtrace[4 * gw] = wall_clock64();
+    A.wtrace[4 * gw + 3] = ((unsigned long long)__builtin_amdgcn_s_getreg(20 | (15 << 11)) << 32) |
+                           (uint32_t)__builtin_amdgcn_s_getreg(4 | (31 << 11));
+  }
+  uint32_t ntile = 0;  // (trace: tiles this wave scanned)
+  {
   const K1FLane L{d, A, smem, lane, (lane & 15u) << 4};
   uint4* ring = (uint4*)(smem + kFQueueOff) + 2 * wave * kFQueue;  // 2 x uint4 per entry
   uint32_t qh = 0, qn = 0, nlisted = 0, narr = 0;
@@ -994,22 +1030,14 @@ __global__ void __launch_bounds__(kFThreads) k1f_kernel(DevK1F d, K1FArgs A) {
     qh = (qh + n) & (kFQueue - 1);
     qn -= n;
   };
-  FCarry cy{0, 0, 0, 0, 0};  // (the warm-up tile's own inputs do not reach its outputs)
+  FCarry cy{0, 0, 0, 0, 0};  // (a chunk's carry tile's own inputs do not reach its outputs)
   // vw: lane 63's last dword of the previous tile (the captured bytes before lane 0's word),
   // kept in a scalar register: a per-lane copy of the tile's .w held its queue register past
   // the reload and made the loop wait for the loads in flight at its back edge
   uint32_t g[4], vw = 0;
-  {  // warm-up: the tile before t0 (zero bytes before the batch) gives the carries
-    uint4 v = make_uint4(0, 0, 0, 0);
-    if (t0 > 0) v = *(const uint4*)(A.data + (size_t)(t0 - 1) * kFTile + 16u * lane);
-    (void)L.tile(v, cy, g);
-    vw = __builtin_amdgcn_readlane(v.w, 63);
-  }
-  // the tiles of the range, kFDepth loads in flight (memory latency bounds a wave with fewer:
-  // profiles/r05/kv2).  A listed word enters the ring with its 20 bytes (the 4 before it
-  // from the previous lane), so its verification reads LDS, not the batch; 64 listed words
-  // are verified together.  The batch has a zero tail of 8 KiB: loads past the last tile
-  // stay inside it.
+  // A listed word enters the ring with its 20 bytes (the 4 before it from the previous
+  // lane), so its verification reads LDS, not the batch; 64 listed words are verified
+  // together.  The batch has a zero tail of 8 KiB: no load leaves the batch and its tail.
   const uint8_t* base = A.data + 16u * lane;
   auto body = [&](uint4 v, uint32_t t) __attribute__((always_inline)) {
     const uint32_t pos = t * kFTile + 16u * lane;
@@ -1053,70 +1081,77 @@ __global__ void __launch_bounds__(kFThreads) k1f_kernel(DevK1F d, K1FArgs A) {
     }
     vw = __builtin_amdgcn_readlane(v.w, 63);
   };
-#if K1F_DMA
-  // tiles through an LDS ring of K1F_DMA slots per wave, filled by LDS-DMA (no VGPRs held
-  // by tiles in flight).  Slot k of the unrolled loop holds tile t + k.  The DMA is issued
-  // in asm so the compiler adds no vmcnt(0) of its own; the waits are counted here: tile t+k
-  // has landed once at most K1F_DMA - 1 younger vector-memory operations are outstanding
-  // (others -- verification loads, event atomics -- only make the wait stricter).
-  constexpr uint32_t kD = K1F_DMA;
-  uint8_t* dring = smem + kFDmaOff + wave * kD * 1024u;
-  const uint32_t dbase = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint8_t*)dring);
-  auto dma = [&](uint32_t t, uint32_t k) __attribute__((always_inline)) {
-    const uint8_t* g = base + (size_t)t * kFTile;
-    uint32_t keep;
-#if K1F_NT
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off nt\n\ts_mov_b32 m0, %0"
-                 : "=&s"(keep) : "v"(g), "s"(dbase + k * 1024u) : "memory");
-#else
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-                 : "=&s"(keep) : "v"(g), "s"(dbase + k * 1024u) : "memory");
-#endif
+  // The wave's tile stream: per claimed chunk its carry tile, then its tiles; kFDepth loads
+  // in flight (memory latency bounds a wave with fewer: profiles/r05/kv2).  Slot k of the
+  // queue holds stream element j (j = k mod kFDepth): the tile's data in p[k], its batch tile
+  // and kind in scalars.  Every slot always loads (a past-the-end slot reloads the block's
+  // first tile, never consumed): a conditional load made the compiler wait for all loads.
+  enum : uint32_t { kReal = 0, kCarry = 1, kCarry0 = 2, kEnd = 3 };
+  uint32_t gc = 0, ga = 0, gb = 0, gj = 0;  // generator: chunk, its tiles [ga, gb), next tile
+  bool gdone = false;
+  auto claim = [&]() __attribute__((always_inline)) {
+    uint32_t c = 0;
+    if (lane == 0) c = atomicAdd(&bst[2], 1u);
+    return (uint32_t)__builtin_amdgcn_readfirstlane(c);
   };
-#pragma unroll
-  for (uint32_t k = 0; k < kD; k++) dma(t0 + k, k);
-  uint32_t t = t0;
-  for (; t < t1; t += kD) {
-    if (t + 2 * kD > t1 && qn) drain(qn);
-#pragma unroll
-    for (uint32_t k = 0; k < kD; k++) {
-      if (t + k < t1) {
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kD - 1) : "memory");
-        const uint4 v = *(const uint4*)(dring + k * 1024u + 16u * lane);
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        dma(t + kD + k, k);  // (past the last tile: inside the batch's zero tail)
-        body(v, t + k);
+  // the next stream element: (batch tile, kind)
+  auto next = [&](uint32_t& tile, uint32_t& kind) __attribute__((always_inline)) {
+    if (!gdone && gj == gb) {
+      gc = claim();
+      if (chunk_of(gc, ga, gb)) {
+        tile = bt0 + ga;
+        kind = tile ? kCarry : kCarry0;
+        tile = tile ? tile - 1 : 0u;
+        gj = ga;
+        return;
       }
+      gdone = true;
     }
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#else
+    if (gdone) {
+      tile = bt0;
+      kind = kEnd;
+      return;
+    }
+    tile = bt0 + gj++;
+    kind = kReal;
+  };
+  auto load = [&](uint32_t tile, uint32_t kind) __attribute__((always_inline)) {
+    // a carry tile: lanes 62 and 63 load its last 32 bytes, the others repeat lane 62's
+    return f_tile_load(A.data + (size_t)tile * kFTile + 16u * (kind == kReal ? lane : max(lane, 62u)));
+  };
   uint4 p[kFDepth];
+  uint32_t tq[kFDepth], kq[kFDepth];
 #pragma unroll
-  for (uint32_t k = 0; k < kFDepth; k++) p[k] = f_tile_load(base + (t0 + k) * kFTile);
-  uint32_t t = t0;
-  for (; t + kFDepth <= t1; t += kFDepth) {
-    // the words listed so far are verified before the range's last tiles, while their loads
+  for (uint32_t k = 0; k < kFDepth; k++) {
+    next(tq[k], kq[k]);
+    p[k] = load(tq[k], kq[k]);
+  }
+  for (;;) {
+    // the words listed so far are verified once the stream has ended, while the last loads
     // are in flight: a verification at the very end (a literal read back, a file lookup)
     // would extend the kernel by its latency (profiles/r05/ab3)
-    if (t + 2 * kFDepth > t1 && qn) drain(qn);
+    if (gdone && qn) drain(qn);
+    bool end = false;
     // each tile is consumed before its queue register is reloaded: no register copies at
-    // the loop's back edge, whose vmcnt(0) waited for the youngest load every kFDepth tiles
-    // (the loop waits vmcnt(kFDepth - 1) before each tile instead)
+    // the loop's back edge, whose vmcnt(0) waited for the youngest load every kFDepth tiles.
+    // Every slot reloads, even past the end (the same number of loads on every path, or the
+    // compiler's wait counts fall back to waiting for nearly all of them).
 #pragma unroll
     for (uint32_t k = 0; k < kFDepth; k++) {
-      body(p[k], t + k);
-#if K1F_NOLOAD  // (timing only: the wave's first tiles again and again, from L2)
-      p[k] = *(const uint4*)(base + (t0 + k) * kFTile);
-#else
-      p[k] = f_tile_load(base + (t + kFDepth + k) * kFTile);
-#endif
+      end = end || kq[k] == kEnd;
+      if (!end && kq[k] == kReal) {
+        body(p[k], tq[k]);
+        ntile++;
+      } else if (!end) {  // a chunk's carry tile
+        const uint4 v = kq[k] == kCarry0 ? make_uint4(0, 0, 0, 0) : p[k];
+        (void)L.tile(v, cy, g);
+        vw = __builtin_amdgcn_readlane(v.w, 63);
+      }
+      next(tq[k], kq[k]);
+      p[k] = load(tq[k], kq[k]);
     }
+    if (end) break;
   }
-#pragma unroll
-  for (uint32_t k = 0; k < kFDepth - 1; k++)
-    if (t + k < t1) body(p[k], t + k);
-#endif
   if (qn) drain(qn);
   // the counters: per wave, per block in LDS, one global atomic per block (a same-address
   // atomic from every lane or wave at the end of the kernel serialised into its tail:
@@ -1127,7 +1162,11 @@ __global__ void __launch_bounds__(kFThreads) k1f_kernel(DevK1F d, K1FArgs A) {
     atomicAdd(&bst[0], nlisted);
     atomicAdd(&bst[1], narr);
   }
-  }  // (t0 < t1)
+  if (A.wtrace && lane == 0) {
+    A.wtrace[4 * gw + 1] = wall_clock64();
+    A.wtrace[4 * gw + 2] = ((unsigned long long)ntile << 32) | nlisted;
+  }
+  }
   __syncthreads();
   if (A.evlist && threadIdx.x < 2 * kFZoneChunks / 32) {  // the zone chunks this block touched
     for (uint32_t b = lzm[threadIdx.x]; b; b &= b - 1) {
@@ -2934,6 +2973,8 @@ struct LaneState {
   size_t evlist_cap = 0;
   uint32_t* zclaim = nullptr;  // K1F's zone claims (K1FArgs::claim): a bit per chunk
   size_t zclaim_cap = 0;
+  unsigned long long* wtrace = nullptr;  // K1F's per-wave trace (TSG_K1F_TRACE)
+  size_t wtrace_cap = 0, wtrace_n = 0;
   uint32_t* kw = nullptr;
   size_t kw_cap = 0;
   unsigned long long* ggate = nullptr;
@@ -2962,7 +3003,7 @@ struct LaneState {
     if (!d) return;
     (void)hipSetDevice(d->device);
     if (st) (void)hipStreamSynchronize(st);
-    void* bufs[] = {data_alloc, meta, cf, ev_bits, xlist, xcount, evlist, zclaim, kw, ggate, ovf, hascand,
+    void* bufs[] = {data_alloc, meta, cf, ev_bits, xlist, xcount, evlist, zclaim, wtrace, kw, ggate, ovf, hascand,
                     items, entries, dentries, cand, counts, gcount, bcount, cursor, gskip, etrace};
     for (void* b : bufs) (void)hipFree(b);
     if (st) (void)hipStreamDestroy(st);
@@ -3563,7 +3604,7 @@ int enqueue_scan(DeviceRules* r, LaneState* l, const ScanInput& in, HostOut* out
   if (k1f) {
     K1FArgs A{data, l->off, l->cf, (uint32_t)total, C, F, k1f_tiles, F ? (uint32_t)ncf : 0u,
               l->kw, l->ev_bits, nullptr, l->counts + 16, (unsigned long long*)(l->counts + kClk),
-              nullptr, nullptr, r->k1f_maxlen, 0, nullptr};
+              nullptr, nullptr, r->k1f_maxlen, 0, nullptr, nullptr};
     if (!r->adapted && total >= adapt_bytes && (rc = adapt_k1f(r, l, A, in.data))) return rc;
     if (k1f_list) {
       A.evlist = l->evlist;
@@ -3571,6 +3612,14 @@ int enqueue_scan(DeviceRules* r, LaneState* l, const ScanInput& in, HostOut* out
       A.evcap = (uint32_t)std::min<size_t>(l->evlist_cap, 0xFFFFFFFFu);
       A.zone = r->k1f_maxlen;  // (after the adaptation's rebuild)
       A.claim = l->zclaim;
+    }
+    static const bool wtrace = getenv("TSG_K1F_TRACE") != nullptr;
+    if (wtrace && total) {
+      const size_t nw = (size_t)k1f_grid(r, k1f_tiles) * (kFThreads / 64);
+      if ((rc = ensure(&l->wtrace, &l->wtrace_cap, 4 * nw))) return rc;
+      HIP_TRY(hipMemsetAsync(l->wtrace, 0, sizeof(unsigned long long) * 4 * nw, st));
+      A.wtrace = l->wtrace;
+      l->wtrace_n = 4 * nw;
     }
     if (total && (rc = launch_k1f(r, A, st))) return rc;
   } else if (!r->adapted && k1_items >= 64 && total >= adapt_bytes) {
@@ -3763,6 +3812,14 @@ int lane_k2_trace(LaneState* l, std::vector<unsigned long long>* out) {
   const size_t n = std::min<size_t>((size_t)counts[2] * kTraceW, l->etrace_cap);
   out->resize(n);
   if (n) HIP_TRY(hipMemcpy(out->data(), l->etrace, n * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+  return TSG_OK;
+}
+
+int lane_k1f_trace(LaneState* l, std::vector<unsigned long long>* out) {
+  HIP_TRY(hipSetDevice(l->d->device));
+  HIP_TRY(hipStreamSynchronize(l->st));
+  out->assign(l->wtrace ? l->wtrace_n : 0, 0);
+  if (!out->empty()) HIP_TRY(hipMemcpy(out->data(), l->wtrace, out->size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
   return TSG_OK;
 }
 

@@ -791,6 +791,14 @@ int tsg_batch_kernels(tsg_ctx* c, uint32_t slot_id, uint32_t nfiles, uint32_t* k
       update_stats(c, b);
       if (kw) rc = lane_kw(l, kw, std::min(kw_len, W * nfiles));
       if (ev && !rc) rc = lane_events(l, ev, ev_len);
+      if (const char* tp = getenv("TSG_K1F_TRACE")) {  // append K1F's per-wave trace (measurements)
+        std::vector<unsigned long long> tr;
+        if (!rc) rc = lane_k1f_trace(l, &tr);
+        if (FILE* f = tr.empty() ? nullptr : fopen(tp, "ab")) {
+          fwrite(tr.data(), sizeof(unsigned long long), tr.size(), f);
+          fclose(f);
+        }
+      }
       if (const char* tp = getenv("TSG_K2_TRACE")) {  // append the K2 entry trace (measurements)
         std::vector<unsigned long long> tr;
         if (!rc) rc = lane_k2_trace(l, &tr);
