@@ -29,6 +29,7 @@ for v in "$@"; do
     xdiag) build $v -DK1X_DIAG ;;
     f16) build $v -DK1F_ALL16=1 ;;       # K1F: all 16 entries of a tile read at once
     fq64) build $v -DK1F_QUEUE=64 ;;     # K1F: the register queue with the small verification ring
+    ftr) build $v -DK1F_WTRACE=1 ;;      # K1F: per-wave trace (TSG_K1F_TRACE, tools/k1ftrace.py)
     fd2) build $v -DK1F_DEPTH=2 ;;       # K1F: register queue depths
     fd3) build $v -DK1F_DEPTH=3 ;;        # K1X: verify counters in k2_long_tails (slot probes),
                                          # k2_tail_bytes (entries examined), k2_tail_max (matches)

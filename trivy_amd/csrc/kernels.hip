@@ -614,6 +614,9 @@ __global__ void __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(4, 8))
 #ifndef K1F_QUEUE
 #define K1F_QUEUE 128
 #endif
+#ifndef K1F_WTRACE
+#define K1F_WTRACE 0  // per-wave trace (TSG_K1F_TRACE; measurement builds, variant "ftr")
+#endif
 constexpr uint32_t kFQueue = K1F_QUEUE;                    // ring entries (32 B) per wave
 static_assert(kFQueue >= 64 && (kFQueue & (kFQueue - 1)) == 0, "a tile lists up to 64 words");
 constexpr uint32_t kFEntBytes = 256 * 256;                 // 256 entries x 16 replicas x 16 B
@@ -1006,11 +1009,13 @@ __global__ void __launch_bounds__(kFThreads) k1f_kernel(DevK1F d, K1FArgs A) {
     }
     return true;
   };
+#if K1F_WTRACE
   if (A.wtrace && lane == 0) {
     A.wtrace[4 * gw] = wall_clock64();
     A.wtrace[4 * gw + 3] = ((unsigned long long)__builtin_amdgcn_s_getreg(20 | (15 << 11)) << 32) |
                            (uint32_t)__builtin_amdgcn_s_getreg(4 | (31 << 11));
   }
+#endif
   uint32_t ntile = 0;  // (trace: tiles this wave scanned)
   {
   const K1FLane L{d, A, smem, lane, (lane & 15u) << 4};
@@ -1040,13 +1045,14 @@ __global__ void __launch_bounds__(kFThreads) k1f_kernel(DevK1F d, K1FArgs A) {
   // together.  The batch has a zero tail of 8 KiB: no load leaves the batch and its tail.
   const uint8_t* base = A.data + 16u * lane;
   auto body = [&](uint4 v, uint32_t t) __attribute__((always_inline)) {
+    t = min((uint32_t)__builtin_amdgcn_readfirstlane(t), A.ntiles - 1);  // (see load)
     const uint32_t pos = t * kFTile + 16u * lane;
 #if K1F_ALL16
     const uint32_t rb = L.tile16(v, cy, g);
 #else
     const uint32_t rb = L.tile(v, cy, g);
 #endif
-    // run events: one atomic per chunk (the leader lane of each chunk in the tile)
+      // run events: one atomic per chunk (the leader lane of each chunk in the tile)
     const uint64_t bu = __ballot(rb & 1u), bd = __ballot(rb & 2u);
     if (__builtin_expect(bu | bd, 0)) {
       const uint32_t c = pos / A.chunk;
@@ -1117,6 +1123,8 @@ __global__ void __launch_bounds__(kFThreads) k1f_kernel(DevK1F d, K1FArgs A) {
   };
   auto load = [&](uint32_t tile, uint32_t kind) __attribute__((always_inline)) {
     // a carry tile: lanes 62 and 63 load its last 32 bytes, the others repeat lane 62's
+    // (the tile is wave-uniform and below ntiles; both are enforced, not assumed)
+    tile = min((uint32_t)__builtin_amdgcn_readfirstlane(tile), A.ntiles - 1);
     return f_tile_load(A.data + (size_t)tile * kFTile + 16u * (kind == kReal ? lane : max(lane, 62u)));
   };
   uint4 p[kFDepth];
@@ -1162,10 +1170,12 @@ __global__ void __launch_bounds__(kFThreads) k1f_kernel(DevK1F d, K1FArgs A) {
     atomicAdd(&bst[0], nlisted);
     atomicAdd(&bst[1], narr);
   }
+#if K1F_WTRACE
   if (A.wtrace && lane == 0) {
     A.wtrace[4 * gw + 1] = wall_clock64();
     A.wtrace[4 * gw + 2] = ((unsigned long long)ntile << 32) | nlisted;
   }
+#endif
   }
   __syncthreads();
   if (A.evlist && threadIdx.x < 2 * kFZoneChunks / 32) {  // the zone chunks this block touched
