@@ -614,6 +614,9 @@ __global__ void __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(4, 8))
 #ifndef K1F_QUEUE
 #define K1F_QUEUE 128
 #endif
+#ifndef K1F_PACE
+#define K1F_PACE 1  // issue priority by progress (0: none; measurement builds)
+#endif
 #ifndef K1F_WTRACE
 #define K1F_WTRACE 0  // per-wave trace (TSG_K1F_TRACE; measurement builds, variant "ftr")
 #endif
@@ -964,7 +967,7 @@ __global__ void __launch_bounds__(kFThreads) k1f_kernel(DevK1F d, K1FArgs A) {
   const uint32_t ncl = kc1 > kc0 ? (uint32_t)min<uint64_t>(kc1 - kc0, kFCfMax) : 0u;
   uint32_t* lcf = (uint32_t*)(smem + kFCfOff);
   for (uint32_t i = threadIdx.x; i < ncl; i += blockDim.x) lcf[i] = A.cf[kc0 + i];
-  uint32_t* bst = (uint32_t*)(smem + kFStOff);  // listed words, arrivals, next chunk
+  uint32_t* bst = (uint32_t*)(smem + kFStOff);  // listed words, arrivals, tiles done (pace)
   if (threadIdx.x < 3) bst[threadIdx.x] = 0;
   // the event list: the block's non-zone chunks [c_lo, c_hi) in the LDS bitmap, the zone
   // chunks in the zone bitmaps
@@ -978,37 +981,7 @@ __global__ void __launch_bounds__(kFThreads) k1f_kernel(DevK1F d, K1FArgs A) {
   if (threadIdx.x < 2 * kFZoneChunks / 32) lzm[threadIdx.x] = 0;
   const K1FMark mark{A, lbm, lzm, z_lo, c_lo, c_hi};
   __syncthreads();
-  // The block's tiles [bt0, bt1), handed to its waves in chunks as they ask (an LDS counter)
-  // rather than in equal shares: waves of one CU run at very different speeds -- issue goes
-  // to the older wave first -- and with equal shares the block waited for its slowest wave
-  // (one launch: wave times 129-241 us, median 184; tools/k1ftrace.py, profiles/r06/g).
-  // Chunk sizes shrink (guided): the first chunk of each wave is a 32nd of the block's tiles,
-  // then 128ths, then 512ths.  A chunk starts with the carries of the tile before it: lanes
-  // 62 and 63 load that tile's last 32 bytes (the other lanes repeat their addresses) and the
-  // tile logic runs once on them.
-  const uint32_t bt0 = (uint32_t)((uint64_t)blockIdx.x * wpb * A.ntiles / nw);
-  const uint32_t bt1 = (uint32_t)((uint64_t)(blockIdx.x + 1) * wpb * A.ntiles / nw);
-  const uint32_t T = bt1 - bt0;
-  const uint32_t s1 = T / (2 * wpb), s2 = max(1u, s1 / 4), s3 = max(1u, s1 / 16);
-  const uint32_t p1 = s1 * wpb, p3 = s1 ? min(T - p1, T / 8) : 0u, p2 = T - p1 - p3;
-  const uint32_t n1 = s1 ? wpb : 0u, n2 = s1 ? (p2 + s2 - 1) / s2 : T, n3 = (p3 + s3 - 1) / s3;
-  // chunk c -> block tiles [a, b); false past the last chunk
-  auto chunk_of = [&](uint32_t c, uint32_t& a, uint32_t& b) __attribute__((always_inline)) {
-    if (c < n1) {
-      a = c * s1;
-      b = a + s1;
-    } else if (c < n1 + n2) {
-      const uint32_t w = s1 ? s2 : 1u;
-      a = p1 + (c - n1) * w;
-      b = min(a + w, p1 + p2);
-    } else if (c < n1 + n2 + n3) {
-      a = p1 + p2 + (c - n1 - n2) * s3;
-      b = min(a + s3, T);
-    } else {
-      return false;
-    }
-    return true;
-  };
+  const uint32_t t0 = (uint32_t)((uint64_t)gw * A.ntiles / nw), t1 = (uint32_t)((uint64_t)(gw + 1) * A.ntiles / nw);
 #if K1F_WTRACE
   if (A.wtrace && lane == 0) {
     A.wtrace[4 * gw] = wall_clock64();
@@ -1017,7 +990,7 @@ __global__ void __launch_bounds__(kFThreads) k1f_kernel(DevK1F d, K1FArgs A) {
   }
 #endif
   uint32_t ntile = 0;  // (trace: tiles this wave scanned)
-  {
+  if (t0 < t1) {  // (waves without tiles wait at the block barrier below)
   const K1FLane L{d, A, smem, lane, (lane & 15u) << 4};
   uint4* ring = (uint4*)(smem + kFQueueOff) + 2 * wave * kFQueue;  // 2 x uint4 per entry
   uint32_t qh = 0, qn = 0, nlisted = 0, narr = 0;
@@ -1035,7 +1008,7 @@ __global__ void __launch_bounds__(kFThreads) k1f_kernel(DevK1F d, K1FArgs A) {
     qh = (qh + n) & (kFQueue - 1);
     qn -= n;
   };
-  FCarry cy{0, 0, 0, 0, 0};  // (a chunk's carry tile's own inputs do not reach its outputs)
+  FCarry cy{0, 0, 0, 0, 0};  // (the warm-up tile's own inputs do not reach its outputs)
   // vw: lane 63's last dword of the previous tile (the captured bytes before lane 0's word),
   // kept in a scalar register: a per-lane copy of the tile's .w held its queue register past
   // the reload and made the loop wait for the loads in flight at its back edge
@@ -1045,7 +1018,6 @@ __global__ void __launch_bounds__(kFThreads) k1f_kernel(DevK1F d, K1FArgs A) {
   // together.  The batch has a zero tail of 8 KiB: no load leaves the batch and its tail.
   const uint8_t* base = A.data + 16u * lane;
   auto body = [&](uint4 v, uint32_t t) __attribute__((always_inline)) {
-    t = min((uint32_t)__builtin_amdgcn_readfirstlane(t), A.ntiles - 1);  // (see load)
     const uint32_t pos = t * kFTile + 16u * lane;
 #if K1F_ALL16
     const uint32_t rb = L.tile16(v, cy, g);
@@ -1087,79 +1059,58 @@ __global__ void __launch_bounds__(kFThreads) k1f_kernel(DevK1F d, K1FArgs A) {
     }
     vw = __builtin_amdgcn_readlane(v.w, 63);
   };
-  // The wave's tile stream: per claimed chunk its carry tile, then its tiles; kFDepth loads
-  // in flight (memory latency bounds a wave with fewer: profiles/r05/kv2).  Slot k of the
-  // queue holds stream element j (j = k mod kFDepth): the tile's data in p[k], its batch tile
-  // and kind in scalars.  Every slot always loads (a past-the-end slot reloads the block's
-  // first tile, never consumed): a conditional load made the compiler wait for all loads.
-  enum : uint32_t { kReal = 0, kCarry = 1, kCarry0 = 2, kEnd = 3 };
-  uint32_t gc = 0, ga = 0, gb = 0, gj = 0;  // generator: chunk, its tiles [ga, gb), next tile
-  bool gdone = false;
-  auto claim = [&]() __attribute__((always_inline)) {
-    uint32_t c = 0;
-    if (lane == 0) c = atomicAdd(&bst[2], 1u);
-    return (uint32_t)__builtin_amdgcn_readfirstlane(c);
-  };
-  // the next stream element: (batch tile, kind)
-  auto next = [&](uint32_t& tile, uint32_t& kind) __attribute__((always_inline)) {
-    if (!gdone && gj == gb) {
-      gc = claim();
-      if (chunk_of(gc, ga, gb)) {
-        tile = bt0 + ga;
-        kind = tile ? kCarry : kCarry0;
-        tile = tile ? tile - 1 : 0u;
-        gj = ga;
-        return;
-      }
-      gdone = true;
-    }
-    if (gdone) {
-      tile = bt0;
-      kind = kEnd;
-      return;
-    }
-    tile = bt0 + gj++;
-    kind = kReal;
-  };
-  auto load = [&](uint32_t tile, uint32_t kind) __attribute__((always_inline)) {
-    // a carry tile: lanes 62 and 63 load its last 32 bytes, the others repeat lane 62's
-    // (the tile is wave-uniform and below ntiles; both are enforced, not assumed)
-    tile = min((uint32_t)__builtin_amdgcn_readfirstlane(tile), A.ntiles - 1);
-    return f_tile_load(A.data + (size_t)tile * kFTile + 16u * (kind == kReal ? lane : max(lane, 62u)));
-  };
-  uint4 p[kFDepth];
-  uint32_t tq[kFDepth], kq[kFDepth];
-#pragma unroll
-  for (uint32_t k = 0; k < kFDepth; k++) {
-    next(tq[k], kq[k]);
-    p[k] = load(tq[k], kq[k]);
+  {  // warm-up: the tile before t0 (zero bytes before the batch) gives the carries
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (t0 > 0) v = *(const uint4*)(A.data + (size_t)(t0 - 1) * kFTile + 16u * lane);
+    (void)L.tile(v, cy, g);
+    vw = __builtin_amdgcn_readlane(v.w, 63);
   }
-  for (;;) {
-    // the words listed so far are verified once the stream has ended, while the last loads
+  // Issue priority by progress: the waves of a CU share it unevenly -- issue goes to the
+  // older wave first -- so with equal tile ranges the block waited for its slowest wave (one
+  // launch: 129-241 us for the same 256 tiles, median 184; TSG_K1F_TRACE, tools/k1ftrace.py,
+  // profiles/r06/g).  Every kFDepth tiles a wave adds its progress to a block counter and
+  // runs at high priority while it is behind the block's mean.
+  uint32_t nact = 0;  // the block's waves with tiles
+  for (uint32_t w = 0; w < wpb; w++) {
+    const uint64_t g0 = (uint64_t)blockIdx.x * wpb + w;
+    nact += g0 * A.ntiles / nw < (g0 + 1) * A.ntiles / nw ? 1u : 0u;
+  }
+  auto pace = [&](uint32_t done) __attribute__((always_inline)) {
+    uint32_t all = 0;
+    if (lane == 0) all = atomicAdd(&bst[2], kFDepth) + kFDepth;
+    all = __builtin_amdgcn_readfirstlane(all);
+    if (done * nact < all) __builtin_amdgcn_s_setprio(3);
+    else __builtin_amdgcn_s_setprio(0);
+  };
+  // the tiles of the range, kFDepth loads in flight (memory latency bounds a wave with fewer:
+  // profiles/r05/kv2).  The batch has a zero tail of 8 KiB: loads past the last tile stay
+  // inside it.
+  uint4 p[kFDepth];
+#pragma unroll
+  for (uint32_t k = 0; k < kFDepth; k++) p[k] = f_tile_load(base + (size_t)(t0 + k) * kFTile);
+  uint32_t t = t0;
+  for (; t + kFDepth <= t1; t += kFDepth) {
+    // the words listed so far are verified before the range's last tiles, while their loads
     // are in flight: a verification at the very end (a literal read back, a file lookup)
     // would extend the kernel by its latency (profiles/r05/ab3)
-    if (gdone && qn) drain(qn);
-    bool end = false;
+    if (t + 2 * kFDepth > t1 && qn) drain(qn);
+#if K1F_PACE
+    pace(t - t0 + kFDepth);
+#endif
     // each tile is consumed before its queue register is reloaded: no register copies at
-    // the loop's back edge, whose vmcnt(0) waited for the youngest load every kFDepth tiles.
-    // Every slot reloads, even past the end (the same number of loads on every path, or the
-    // compiler's wait counts fall back to waiting for nearly all of them).
+    // the loop's back edge, whose vmcnt(0) waited for the youngest load every kFDepth tiles
+    // (the loop waits vmcnt(kFDepth - 1) before each tile instead)
 #pragma unroll
     for (uint32_t k = 0; k < kFDepth; k++) {
-      end = end || kq[k] == kEnd;
-      if (!end && kq[k] == kReal) {
-        body(p[k], tq[k]);
-        ntile++;
-      } else if (!end) {  // a chunk's carry tile
-        const uint4 v = kq[k] == kCarry0 ? make_uint4(0, 0, 0, 0) : p[k];
-        (void)L.tile(v, cy, g);
-        vw = __builtin_amdgcn_readlane(v.w, 63);
-      }
-      next(tq[k], kq[k]);
-      p[k] = load(tq[k], kq[k]);
+      body(p[k], t + k);
+      p[k] = f_tile_load(base + (size_t)(t + kFDepth + k) * kFTile);
     }
-    if (end) break;
   }
+#pragma unroll
+  for (uint32_t k = 0; k < kFDepth - 1; k++)
+    if (t + k < t1) body(p[k], t + k);
+  ntile = t1 - t0;
+  __builtin_amdgcn_s_setprio(0);
   if (qn) drain(qn);
   // the counters: per wave, per block in LDS, one global atomic per block (a same-address
   // atomic from every lane or wave at the end of the kernel serialised into its tail:
