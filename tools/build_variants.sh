@@ -30,8 +30,8 @@ for v in "$@"; do
     f16) build $v -DK1F_ALL16=1 ;;       # K1F: all 16 entries of a tile read at once
     fq64) build $v -DK1F_QUEUE=64 ;;     # K1F: the register queue with the small verification ring
     ftr) build $v -DK1F_WTRACE=1 ;;      # K1F: per-wave trace (TSG_K1F_TRACE, tools/k1ftrace.py)
-    ftr0) build $v -DK1F_WTRACE=1 -DK1F_PACE=0 ;;  # the same without the priority pacing
-    fp0) build $v -DK1F_PACE=0 ;;        # K1F: no priority pacing
+    ftr0) build $v -DK1F_WTRACE=1 -DK1F_SHARES=0 ;;  # the same with equal wave ranges
+    fe) build $v -DK1F_SHARES=0 ;;       # K1F: equal wave ranges
     fd2) build $v -DK1F_DEPTH=2 ;;       # K1F: register queue depths
     fd3) build $v -DK1F_DEPTH=3 ;;        # K1X: verify counters in k2_long_tails (slot probes),
                                          # k2_tail_bytes (entries examined), k2_tail_max (matches)

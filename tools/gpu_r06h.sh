@@ -1,6 +1,6 @@
 #!/bin/bash
-# Round 6: K1F issue-priority pacing -- K1F device tests, kernel-only timing of the default
-# (pacing) and fp0 (none), per-wave traces of both (ftr / ftr0 builds).
+# Round 6: K1F wave ranges by SIMD slot -- K1F device tests, kernel-only timing of the default
+# (slot shares) and fe (equal ranges), per-wave traces of both (ftr / ftr0 builds).
 set -o pipefail
 out=gpurun_out/r06/${1:-j}
 mkdir -p $out
@@ -8,7 +8,7 @@ echo "== k1f tests" && timeout -k 10 500 python -u -m pytest tests/test_gpu.py -
   -k "k1_matches or k1f_ or adaptation or corpus_vs or event_list" > $out/k1f_tests.log 2>&1 || { tail -30 $out/k1f_tests.log; exit 1; }
 tail -1 $out/k1f_tests.log
 for rep in 1 2; do
-for v in default fp0; do
+for v in default fe; do
   if [ $v = default ]; then unset TSG_LIB_VARIANT; else export TSG_LIB_VARIANT=$v; fi
   timeout -k 10 240 python -u tools/kab.py 1024 7 > $out/kab_${v}_$rep.json 2> $out/kab_$v.err || { echo "fail $v"; tail $out/kab_$v.err; exit 2; }
   echo $rep $v $(python -c "import json; d=json.load(open('$out/kab_${v}_$rep.json')); print('k1', d['k1_ms'], d['k1_clk_ms'], 'gates', d['gate_ms'], 'k2', d['k2_ms'], 'chain', d['chain_clk_ms'])")

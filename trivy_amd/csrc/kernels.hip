@@ -614,8 +614,8 @@ __global__ void __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(4, 8))
 #ifndef K1F_QUEUE
 #define K1F_QUEUE 128
 #endif
-#ifndef K1F_PACE
-#define K1F_PACE 1  // issue priority by progress (0: none; measurement builds)
+#ifndef K1F_SHARES
+#define K1F_SHARES 1  // tile ranges by the waves' SIMD slots (0: equal; measurement builds)
 #endif
 #ifndef K1F_WTRACE
 #define K1F_WTRACE 0  // per-wave trace (TSG_K1F_TRACE; measurement builds, variant "ftr")
@@ -967,7 +967,7 @@ __global__ void __launch_bounds__(kFThreads) k1f_kernel(DevK1F d, K1FArgs A) {
   const uint32_t ncl = kc1 > kc0 ? (uint32_t)min<uint64_t>(kc1 - kc0, kFCfMax) : 0u;
   uint32_t* lcf = (uint32_t*)(smem + kFCfOff);
   for (uint32_t i = threadIdx.x; i < ncl; i += blockDim.x) lcf[i] = A.cf[kc0 + i];
-  uint32_t* bst = (uint32_t*)(smem + kFStOff);  // listed words, arrivals, tiles done (pace)
+  uint32_t* bst = (uint32_t*)(smem + kFStOff);  // listed words, arrivals
   if (threadIdx.x < 3) bst[threadIdx.x] = 0;
   // the event list: the block's non-zone chunks [c_lo, c_hi) in the LDS bitmap, the zone
   // chunks in the zone bitmaps
@@ -981,7 +981,29 @@ __global__ void __launch_bounds__(kFThreads) k1f_kernel(DevK1F d, K1FArgs A) {
   if (threadIdx.x < 2 * kFZoneChunks / 32) lzm[threadIdx.x] = 0;
   const K1FMark mark{A, lbm, lzm, z_lo, c_lo, c_hi};
   __syncthreads();
-  const uint32_t t0 = (uint32_t)((uint64_t)gw * A.ntiles / nw), t1 = (uint32_t)((uint64_t)(gw + 1) * A.ntiles / nw);
+  // The block's tiles [bt0, bt1) split over its waves unequally: the four waves a SIMD holds
+  // do not share it evenly -- per wave of one launch, 140 / 166 / 196 / 228 us for the same
+  // 256 tiles by the wave's slot on its SIMD, which follows the wave's index in the block
+  // (slot = wave / 4: waves are created in order and dealt round-robin to the SIMDs;
+  // TSG_K1F_TRACE, tools/k1ftrace.py, profiles/r06/j).  With equal ranges the block waited
+  // for its slot-3 waves; ranges in proportion to the slots' measured speeds end together.
+  // (Any split is correct: each wave scans its own contiguous range after the tile before.)
+  uint32_t t0, t1;
+  {
+    const uint64_t bt0 = (uint64_t)blockIdx.x * wpb * A.ntiles / nw, bt1 = (uint64_t)(blockIdx.x + 1) * wpb * A.ntiles / nw;
+#if K1F_SHARES
+    constexpr uint32_t kShare[4] = {306, 258, 219, 188};  // per slot (1 / its wave time)
+    const uint32_t tot = (wpb / 4) * (kShare[0] + kShare[1] + kShare[2] + kShare[3]);
+    uint32_t before = 0;
+    for (uint32_t w = 0; w < wave; w++) before += kShare[(w * 4 / wpb) & 3];
+    const uint32_t mine = kShare[(wave * 4 / wpb) & 3];
+    t0 = (uint32_t)(bt0 + (bt1 - bt0) * before / tot);
+    t1 = (uint32_t)(bt0 + (bt1 - bt0) * (before + mine) / tot);
+#else
+    t0 = (uint32_t)((uint64_t)gw * A.ntiles / nw);
+    t1 = (uint32_t)((uint64_t)(gw + 1) * A.ntiles / nw);
+#endif
+  }
 #if K1F_WTRACE
   if (A.wtrace && lane == 0) {
     A.wtrace[4 * gw] = wall_clock64();
@@ -1065,23 +1087,6 @@ __global__ void __launch_bounds__(kFThreads) k1f_kernel(DevK1F d, K1FArgs A) {
     (void)L.tile(v, cy, g);
     vw = __builtin_amdgcn_readlane(v.w, 63);
   }
-  // Issue priority by progress: the waves of a CU share it unevenly -- issue goes to the
-  // older wave first -- so with equal tile ranges the block waited for its slowest wave (one
-  // launch: 129-241 us for the same 256 tiles, median 184; TSG_K1F_TRACE, tools/k1ftrace.py,
-  // profiles/r06/g).  Every kFDepth tiles a wave adds its progress to a block counter and
-  // runs at high priority while it is behind the block's mean.
-  uint32_t nact = 0;  // the block's waves with tiles
-  for (uint32_t w = 0; w < wpb; w++) {
-    const uint64_t g0 = (uint64_t)blockIdx.x * wpb + w;
-    nact += g0 * A.ntiles / nw < (g0 + 1) * A.ntiles / nw ? 1u : 0u;
-  }
-  auto pace = [&](uint32_t done) __attribute__((always_inline)) {
-    uint32_t all = 0;
-    if (lane == 0) all = atomicAdd(&bst[2], kFDepth) + kFDepth;
-    all = __builtin_amdgcn_readfirstlane(all);
-    if (done * nact < all) __builtin_amdgcn_s_setprio(3);
-    else __builtin_amdgcn_s_setprio(0);
-  };
   // the tiles of the range, kFDepth loads in flight (memory latency bounds a wave with fewer:
   // profiles/r05/kv2).  The batch has a zero tail of 8 KiB: loads past the last tile stay
   // inside it.
@@ -1094,9 +1099,6 @@ __global__ void __launch_bounds__(kFThreads) k1f_kernel(DevK1F d, K1FArgs A) {
     // are in flight: a verification at the very end (a literal read back, a file lookup)
     // would extend the kernel by its latency (profiles/r05/ab3)
     if (t + 2 * kFDepth > t1 && qn) drain(qn);
-#if K1F_PACE
-    pace(t - t0 + kFDepth);
-#endif
     // each tile is consumed before its queue register is reloaded: no register copies at
     // the loop's back edge, whose vmcnt(0) waited for the youngest load every kFDepth tiles
     // (the loop waits vmcnt(kFDepth - 1) before each tile instead)
@@ -1110,7 +1112,6 @@ __global__ void __launch_bounds__(kFThreads) k1f_kernel(DevK1F d, K1FArgs A) {
   for (uint32_t k = 0; k < kFDepth - 1; k++)
     if (t + k < t1) body(p[k], t + k);
   ntile = t1 - t0;
-  __builtin_amdgcn_s_setprio(0);
   if (qn) drain(qn);
   // the counters: per wave, per block in LDS, one global atomic per block (a same-address
   // atomic from every lane or wave at the end of the kernel serialised into its tail:
