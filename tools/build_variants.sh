@@ -32,6 +32,11 @@ for v in "$@"; do
     ftr) build $v -DK1F_WTRACE=1 ;;      # K1F: per-wave trace (TSG_K1F_TRACE, tools/k1ftrace.py)
     ftr0) build $v -DK1F_WTRACE=1 -DK1F_SHARES=0 ;;  # the same with equal wave ranges
     fe) build $v -DK1F_SHARES=0 ;;       # K1F: equal wave ranges
+    fs8) build $v -DK1F_STEAL=8 ;;       # K1F: reserve 1/8 of a block's tiles, claimed in chunks
+    fs16) build $v -DK1F_STEAL=16 ;;     # K1F: reserve 1/16 of a block's tiles
+    fs4) build $v -DK1F_STEAL=4 ;;       # K1F: reserve 1/4
+    fc16) build $v -DK1F_STEAL=8 -DK1F_STEAL_CHUNK=16 ;;  # K1F: 16-tile reserve chunks
+    fc4) build $v -DK1F_STEAL=8 -DK1F_STEAL_CHUNK=4 ;;
     fd2) build $v -DK1F_DEPTH=2 ;;       # K1F: register queue depths
     fd3) build $v -DK1F_DEPTH=3 ;;        # K1X: verify counters in k2_long_tails (slot probes),
                                          # k2_tail_bytes (entries examined), k2_tail_max (matches)

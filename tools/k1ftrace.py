@@ -42,7 +42,9 @@ def run(out, mib=1024):
 
 def report(out):
     t = np.fromfile(os.path.join(out, "k1ftrace.bin"), dtype=np.uint64).reshape(-1, 4)
-    t = t[t[:, 1] > 0]
+    slot = (np.arange(len(t)) % 16) // 4  # record = block * 16 + wave; SIMD slot = wave / 4
+    keep = t[:, 1] > 0
+    t, slot = t[keep], slot[keep]
     s, e = t[:, 0].astype(np.int64), t[:, 1].astype(np.int64)
     t0 = s.min()
     dur, end, start = (e - s) / 100.0, (e - t0) / 100.0, (s - t0) / 100.0  # us
@@ -56,6 +58,11 @@ def report(out):
     rep["late5pct"] = {"listed_mean": round(float(listed[late].mean()), 1), "listed_mean_all": round(float(listed.mean()), 1),
                        "start_mean_us": round(float(start[late].mean()), 1), "xcc": np.bincount(xcc[late], minlength=8).tolist()}
     rep["end_by_xcc_us"] = [round(float(end[xcc == x].max()), 1) if (xcc == x).any() else None for x in range(8)]
+    upt = [float((dur[slot == k] / np.maximum(tiles[slot == k], 1)).mean()) for k in range(4)]
+    rep["by_slot"] = {"dur_us": [round(float(dur[slot == k].mean()), 1) for k in range(4)],
+                      "end_us_max": [round(float(end[slot == k].max()), 1) for k in range(4)],
+                      "us_per_tile": [round(u, 3) for u in upt],
+                      "shares_next": [round(1000 * (1 / u) / sum(1 / v for v in upt)) for u in upt]}
     print(json.dumps(rep, indent=1))
 
 

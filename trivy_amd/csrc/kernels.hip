@@ -617,6 +617,12 @@ __global__ void __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(4, 8))
 #ifndef K1F_SHARES
 #define K1F_SHARES 1  // tile ranges by the waves' SIMD slots (0: equal; measurement builds)
 #endif
+#ifndef K1F_STEAL
+#define K1F_STEAL 0  // 1/K1F_STEAL of a block's tiles claimed in chunks by the first waves done
+#endif               // (0: none; measured without gain, profiles/r06/o: variants fs*, fc*)
+#ifndef K1F_STEAL_CHUNK
+#define K1F_STEAL_CHUNK 8  // tiles per claim
+#endif
 #ifndef K1F_WTRACE
 #define K1F_WTRACE 0  // per-wave trace (TSG_K1F_TRACE; measurement builds, variant "ftr")
 #endif
@@ -631,7 +637,7 @@ constexpr int kFThreads = K1F_THREADS;                     // one block per CU
 constexpr uint32_t kFImgOff = kFQueueOff + (kFThreads / 64) * kFQueue * 32;
 constexpr uint32_t kFCfOff = kFImgOff + kFImgMax;
 constexpr uint32_t kFCfMax = 512;                          // coarse file map entries in LDS
-constexpr uint32_t kFStOff = kFCfOff + 4 * kFCfMax;        // block counters (listed, arrivals, waves done)
+constexpr uint32_t kFStOff = kFCfOff + 4 * kFCfMax;        // block counters (listed, arrivals, reserve claims)
 constexpr uint32_t kFBitsOff = kFStOff + 16;               // the block's event-chunk bitmap (event list)
 constexpr uint32_t kFBitsWords = 3 * kFThreads;             // 12 KiB: 98,304 chunks of the block's range
 constexpr uint32_t kFZoneOff = kFBitsOff + 4 * kFBitsWords;  // zone chunks marked: own [0, 32), next [32, 64) words
@@ -986,22 +992,35 @@ __global__ void __launch_bounds__(kFThreads) k1f_kernel(DevK1F d, K1FArgs A) {
   // 256 tiles by the wave's slot on its SIMD, which follows the wave's index in the block
   // (slot = wave / 4: waves are created in order and dealt round-robin to the SIMDs;
   // TSG_K1F_TRACE, tools/k1ftrace.py, profiles/r06/j).  With equal ranges the block waited
-  // for its slot-3 waves; ranges in proportion to the slots' measured speeds end together.
+  // for its slot-3 waves; ranges in proportion to the slots' measured speeds end closer
+  // together.  A slot's speed depends on the shares (the more tiles slot 0 takes, the slower
+  // the others' tiles run), so the shares are a fixed point: 1 / (us per tile) of each slot
+  // measured with the previous shares, three rounds from equal ranges (k1ftrace.py
+  // "shares_next"; 0.248 -> 0.2298 -> 0.2227 -> 0.2196 ms per GiB, profiles/r06/l, m, o).
   // (Any split is correct: each wave scans its own contiguous range after the tile before.)
-  uint32_t t0, t1;
+  // With K1F_STEAL the last 1/K1F_STEAL of the block's tiles is a reserve [bs, bt1) the
+  // waves claim in chunks of K1F_STEAL_CHUNK tiles (an LDS counter) once their own range is
+  // done.  The shares leave a block's waves 16-32 us apart at the end; the reserve evens
+  // them out (every slot's waves 201-203 us) but the launch is no shorter: the blocks' own
+  // means differ by as much (189-200 us), and every chunk restarts the load queue
+  // (profiles/r06/o: 0.2191-0.2205 ms per GiB for 1/8 and 1/16, 0.227 for 1/4, shares
+  // alone 0.2193-0.2199).
+  uint32_t t0, t1, bs, bt1;
   {
-    const uint64_t bt0 = (uint64_t)blockIdx.x * wpb * A.ntiles / nw, bt1 = (uint64_t)(blockIdx.x + 1) * wpb * A.ntiles / nw;
+    const uint64_t bt0 = (uint64_t)blockIdx.x * wpb * A.ntiles / nw;
+    bt1 = (uint32_t)((uint64_t)(blockIdx.x + 1) * wpb * A.ntiles / nw);
+    bs = K1F_STEAL ? bt1 - (uint32_t)((bt1 - bt0) / K1F_STEAL) : bt1;
 #if K1F_SHARES
-    constexpr uint32_t kShare[4] = {306, 258, 219, 188};  // per slot (1 / its wave time)
+    constexpr uint32_t kShare[4] = {361, 282, 207, 150};  // per slot: its speed, all four slots busy
     const uint32_t tot = (wpb / 4) * (kShare[0] + kShare[1] + kShare[2] + kShare[3]);
     uint32_t before = 0;
     for (uint32_t w = 0; w < wave; w++) before += kShare[(w * 4 / wpb) & 3];
     const uint32_t mine = kShare[(wave * 4 / wpb) & 3];
-    t0 = (uint32_t)(bt0 + (bt1 - bt0) * before / tot);
-    t1 = (uint32_t)(bt0 + (bt1 - bt0) * (before + mine) / tot);
+    t0 = (uint32_t)(bt0 + (bs - bt0) * before / tot);
+    t1 = (uint32_t)(bt0 + (bs - bt0) * (before + mine) / tot);
 #else
-    t0 = (uint32_t)((uint64_t)gw * A.ntiles / nw);
-    t1 = (uint32_t)((uint64_t)(gw + 1) * A.ntiles / nw);
+    t0 = (uint32_t)(bt0 + (bs - bt0) * wave / wpb);
+    t1 = (uint32_t)(bt0 + (bs - bt0) * (wave + 1) / wpb);
 #endif
   }
 #if K1F_WTRACE
@@ -1012,7 +1031,7 @@ __global__ void __launch_bounds__(kFThreads) k1f_kernel(DevK1F d, K1FArgs A) {
   }
 #endif
   uint32_t ntile = 0;  // (trace: tiles this wave scanned)
-  if (t0 < t1) {  // (waves without tiles wait at the block barrier below)
+  if (t0 < t1 || bs < bt1) {  // (waves without tiles wait at the block barrier below)
   const K1FLane L{d, A, smem, lane, (lane & 15u) << 4};
   uint4* ring = (uint4*)(smem + kFQueueOff) + 2 * wave * kFQueue;  // 2 x uint4 per entry
   uint32_t qh = 0, qn = 0, nlisted = 0, narr = 0;
@@ -1081,18 +1100,22 @@ __global__ void __launch_bounds__(kFThreads) k1f_kernel(DevK1F d, K1FArgs A) {
     }
     vw = __builtin_amdgcn_readlane(v.w, 63);
   };
-  {  // warm-up: the tile before t0 (zero bytes before the batch) gives the carries
-    uint4 v = make_uint4(0, 0, 0, 0);
-    if (t0 > 0) v = *(const uint4*)(A.data + (size_t)(t0 - 1) * kFTile + 16u * lane);
+  for (;;) {  // the wave's own range, then reserve chunks
+  if (t0 < t1) {
+  // the range's loads: the tile before t0 (its carries; zero bytes before the batch) first,
+  // then the first kFDepth tiles, so the warm-up waits only for its own load.  The batch has
+  // a zero tail of 8 KiB: loads past the last tile stay inside it.
+  const uint4 vwu = f_tile_load(A.data + (size_t)(t0 > 0 ? t0 - 1 : 0) * kFTile + 16u * lane);
+  uint4 p[kFDepth];
+#pragma unroll
+  for (uint32_t k = 0; k < kFDepth; k++) p[k] = f_tile_load(base + (size_t)(t0 + k) * kFTile);
+  {
+    const uint4 v = t0 > 0 ? vwu : make_uint4(0, 0, 0, 0);
     (void)L.tile(v, cy, g);
     vw = __builtin_amdgcn_readlane(v.w, 63);
   }
   // the tiles of the range, kFDepth loads in flight (memory latency bounds a wave with fewer:
-  // profiles/r05/kv2).  The batch has a zero tail of 8 KiB: loads past the last tile stay
-  // inside it.
-  uint4 p[kFDepth];
-#pragma unroll
-  for (uint32_t k = 0; k < kFDepth; k++) p[k] = f_tile_load(base + (size_t)(t0 + k) * kFTile);
+  // profiles/r05/kv2)
   uint32_t t = t0;
   for (; t + kFDepth <= t1; t += kFDepth) {
     // the words listed so far are verified before the range's last tiles, while their loads
@@ -1111,7 +1134,16 @@ __global__ void __launch_bounds__(kFThreads) k1f_kernel(DevK1F d, K1FArgs A) {
 #pragma unroll
   for (uint32_t k = 0; k < kFDepth - 1; k++)
     if (t + k < t1) body(p[k], t + k);
-  ntile = t1 - t0;
+  ntile += t1 - t0;
+  }
+  if (bs >= bt1) break;
+  uint32_t c = 0;
+  if (lane == 0) c = atomicAdd(&bst[2], (uint32_t)K1F_STEAL_CHUNK);
+  c = __builtin_amdgcn_readfirstlane(c);
+  if (c >= bt1 - bs) break;
+  t0 = bs + c;
+  t1 = min(t0 + (uint32_t)K1F_STEAL_CHUNK, bt1);
+  }
   if (qn) drain(qn);
   // the counters: per wave, per block in LDS, one global atomic per block (a same-address
   // atomic from every lane or wave at the end of the kernel serialised into its tail:
