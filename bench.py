@@ -514,6 +514,8 @@ def main():
     pmc = _traffic_record(args.rules, int(launch_bytes))
     k1_name = ("K1F keyword/anchor filter + exact verification and run counters (k1f_kernel)"
                if last["k1_filter"] else "K1 keyword automaton (k1_kernel)")
+    if last["k1x_records"]:  # a large rule set: K1X ran after K1, inside the same K1 events
+        k1_name += " + K1X hashed prefilter and verify (k1x_kernel, k1x_verify_kernel)"
     if pmc and pmc.get("k1_kernel", "k1_kernel") != ("k1f_kernel" if last["k1_filter"] else "k1_kernel"):
         pmc = None  # a pass of the other K1
     ngpus_s = "x%d" % ngpus

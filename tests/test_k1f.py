@@ -85,21 +85,20 @@ def test_quiet_literals_remove_only_their_bits(builtin):
     assert st["groups"] < int(batch.offsets[-1]) / 1024 * 8
 
 
-def test_k1f_applies_or_declines_per_config():
-    """configs[4] (allow rules, exclude blocks) runs K1F; the 1,000-rule set of configs[3]
-    either runs it with the same semantics or declines with a reason (the automaton and
-    K1X run then)."""
+def test_k1f_applies_per_config():
+    """configs[4] (allow rules, exclude blocks) and the 1,000-rule set of configs[3] run K1F
+    with k1_reference's semantics.  configs[3]'s K1 keeps a slot per keyword id: the 783
+    keywords K1X takes are never-matching slots (dfa.hpp never_literal), so K1F holds its
+    121 real literals (it declined the 904 slots before round 6)."""
     for name, doc in (("allow-exclude", configs.allow_exclude_doc()),
                       ("user1000", configs.user_rules_doc(1000, seed=4))):
         sc = S.NewScanner(S.config_from_dict(doc))
         batch = corpus.k1_edge_batch(sc.k1_literals(), 4, nfiles=200)
-        try:
-            kw, ev, fk, fe, _ = _eq(sc, batch, 256)
-        except RuntimeError as e:
-            assert name == "user1000" and "K1F does not apply" in str(e)
-            continue
+        kw, ev, fk, fe, st = _eq(sc, batch, 256)
         assert np.array_equal(kw, fk)
         assert np.array_equal(ev, fe)
+        if name == "user1000":
+            assert st["records"] == 121
 
 
 def test_sample_priced_filter(builtin):

@@ -559,6 +559,7 @@ std::unique_ptr<DFA> build_keyword_dfa(const std::vector<std::string>& kws, cons
       nfa.n[nfa.start].match = (int)i;  // "" is contained in everything
       continue;
     }
+    if (k == never_literal()) continue;
     uint32_t cur = nfa.start;
     for (size_t j = 0; j < k.size(); j++) {
       uint8_t c = (uint8_t)k[j];

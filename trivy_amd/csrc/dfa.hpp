@@ -95,7 +95,13 @@ int64_t max_match_len(const Prog& prog);
 // anchor literals of K2's events too (an event may only fire more often than the match it
 // anchors, never less), so 'A' and 'a' share one byte class: 42 classes instead of 68 for
 // the builtin rules, and the automaton fits 16-bit byte offsets (kernels.hip K1).
+// A literal equal to never_literal() is a slot that matches nothing: it keeps its id (a
+// keyword left out of K1, which K1X or the host checks) without adding to the automaton.
 std::unique_ptr<DFA> build_keyword_dfa(const std::vector<std::string>& lower_keywords,
                                        const DFAOptions& opt, std::string* err);
+inline const std::string& never_literal() {
+  static const std::string s("\0\xff\0never", 8);
+  return s;
+}
 
 }  // namespace tsg

@@ -174,7 +174,7 @@ bool k1f_build(const Plan& p, const std::vector<uint8_t>& quiet, K1FTables* t, s
   for (int i = 0; i < n; i++) {
     if (p.k1_lits[i].empty()) return no("an empty literal");
     if (p.k1_lits[i].size() > 0xFFFF) return no("a literal longer than 65535 bytes");
-    if (quiet.empty() || !quiet[i]) act.push_back(i);
+    if ((quiet.empty() || !quiet[i]) && p.k1_lits[i] != never_literal()) act.push_back(i);
   }
   if (act.size() > 400) return no("more than 400 literals");
   // The price of a bucket: its expected windows per byte under the text model, or with a

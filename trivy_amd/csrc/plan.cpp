@@ -446,7 +446,7 @@ std::unique_ptr<Plan> build_plan(const Ruleset& rs, const PlanOptions& opt, std:
   auto build_k1 = [&](bool with_anchors) -> bool {
     std::vector<std::string> lits = kws;
     for (size_t k = 0; k < lits.size(); k++)
-      if (kw_dropped[k] || kw_hashed[k]) lits[k] = "\xff\xff";
+      if (kw_dropped[k] || kw_hashed[k]) lits[k] = never_literal();
     std::map<std::string, std::pair<int32_t, uint32_t>> xl;  // K1X literal -> keyword id, events
     for (size_t k = 0; k < kws.size(); k++)
       if (kw_hashed[k]) xl[ascii_lower(kws[k])] = {(int32_t)k, 0u};

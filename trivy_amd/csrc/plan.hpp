@@ -52,7 +52,8 @@ struct Plan {
   std::vector<uint32_t> kw_mask_events;
   std::vector<uint32_t> lit_event;     // [n_lit] event bits of each literal
   std::vector<std::string> k1_lits;    // [n_lit] the automaton's literals (ASCII case folded
-                                       // when matched); a keyword left out is "\xff\xff"
+                                       // when matched); a keyword left out is
+                                       // never_literal() (dfa.hpp: matches nothing)
   std::vector<uint16_t> kw_len;        // [n_kw] byte length of each keyword literal
   // K1X: literals of >= 4 bytes that K1's LDS-resident automaton has no room for (large
   // user rule sets) -- keywords, and anchor literals with their event bits -- found by a
