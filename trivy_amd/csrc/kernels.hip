@@ -1524,7 +1524,7 @@ struct ItemArgs {
   uint64_t nchunks;
   uint32_t F, G, GW, chunk, maxback;
   uint32_t* count;            // [G]
-  uint32_t* bcount;           // [gridDim.x * G] each count block's counts, for the emit pass
+  uint32_t* bcount;           // [gridDim.x * G] each count block's place in each group's items
   uint32_t* cursor;           // [G]
   uint2* items;
   // ggate == null (K1F listed the events, no gates pass ran): a file's group gates from its
@@ -1605,9 +1605,14 @@ struct GateArgs {
 // round trip per bit -- a file of a 1,000-rule set holds a hundred of them -- so the table
 // is staged in LDS when it fits)
 constexpr uint32_t kKwgLdsMax = 48 * 1024;
+#ifndef GATES_STAMPS
+#define GATES_STAMPS 8  // blocks that stamp the chain's start (measurement builds: more)
+#endif
 __global__ void __launch_bounds__(kBlock) gates_kernel(GateArgs A) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  if (threadIdx.x == 0) atomicMax(&A.clk[2], ~(unsigned long long)wall_clock64());
+  // (the chain's start: the first blocks only -- blocks are dispatched in order, and ~850
+  // same-address atomics at the start of every block of the launch queue on one line)
+  if (threadIdx.x == 0 && blockIdx.x < GATES_STAMPS) atomicMax(&A.clk[2], ~(unsigned long long)wall_clock64());
   if (blockIdx.x < A.ev_blocks) {
     ev_compact_block(A.ev, A.nchunks, A.evlist, A.nev, blockIdx.x, A.ev_blocks);
   } else {
@@ -1739,9 +1744,13 @@ __device__ __forceinline__ void gen_items(const ItemArgs& A, const ItemLds& T, u
 // Both item passes run a fixed grid over the work units t in [0, nev + F) (nev is read on
 // the device, so the host never waits for it), each block visiting the same units twice.
 // count pass: items per group (block totals in LDS, one global atomic per group and block)
+#ifndef ITEMS_BASE_IN_COUNT
+#define ITEMS_BASE_IN_COUNT 1  // (0: the emit pass reserves the block's ranges; measurement builds)
+#endif
 __global__ void __launch_bounds__(kBlock) items_count_kernel(ItemArgs A) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  if (!A.ggate && threadIdx.x == 0) atomicMax(&A.clk[2], ~(unsigned long long)wall_clock64());  // (no gates pass)
+  if (!A.ggate && threadIdx.x == 0 && blockIdx.x < GATES_STAMPS)  // (no gates pass)
+    atomicMax(&A.clk[2], ~(unsigned long long)wall_clock64());
   const ItemLds T = item_lds_load(A, smem);
   uint32_t* s_count = (uint32_t*)(smem + item_lds_bytes(A));
   for (uint32_t g = threadIdx.x; g < A.G; g += blockDim.x) s_count[g] = 0;
@@ -1750,9 +1759,15 @@ __global__ void __launch_bounds__(kBlock) items_count_kernel(ItemArgs A) {
   for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < nt; t += stride)
     gen_items(A, T, t, [&](uint32_t, uint32_t g, uint64_t lo, uint64_t hi) { atomicAdd(&s_count[g], (uint32_t)(hi - lo + 1)); });
   __syncthreads();
+  // the block's place in each group's region, reserved here: the emit pass's blocks then
+  // start without a returning atomic per group (those queued on the groups' cursors)
   for (uint32_t g = threadIdx.x; g < A.G; g += blockDim.x) {
+#if ITEMS_BASE_IN_COUNT
+    A.bcount[(size_t)blockIdx.x * A.G + g] = s_count[g] ? atomicAdd(&A.count[g], s_count[g]) : 0u;
+#else
     A.bcount[(size_t)blockIdx.x * A.G + g] = s_count[g];
     if (s_count[g]) atomicAdd(&A.count[g], s_count[g]);
+#endif
   }
 }
 
@@ -1904,8 +1919,8 @@ __device__ void layout_block(const LayoutArgs& A, uint8_t* s_kind, uint32_t* s_g
 }
 
 // emit pass (same grid as the count pass, so block b generates the items block b counted):
-// the layout (above), then the block reserves one range per listed group with a single
-// global atomic and writes its items into it
+// the layout (above), then the block writes its items into the range of each listed group
+// the count pass reserved for it
 __global__ void __launch_bounds__(kBlock) items_emit_kernel(ItemArgs A, LayoutArgs LA) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const ItemLds T = item_lds_load(A, smem);  // (published by layout_block's barriers)
@@ -1917,8 +1932,12 @@ __global__ void __launch_bounds__(kBlock) items_emit_kernel(ItemArgs A, LayoutAr
   const uint64_t nt = (uint64_t)min(*A.nev, A.evcap) + A.F, stride = (uint64_t)gridDim.x * blockDim.x;
   const uint64_t t0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   for (uint32_t g = threadIdx.x; g < A.G; g += blockDim.x) {
+#if ITEMS_BASE_IN_COUNT
+    s_base[g] = s_kind[g] == kGroupList ? s_gbase[g] + A.bcount[(size_t)blockIdx.x * A.G + g] : 0u;
+#else
     const uint32_t n = s_kind[g] == kGroupList ? A.bcount[(size_t)blockIdx.x * A.G + g] : 0;
     s_base[g] = n ? s_gbase[g] + atomicAdd(&A.cursor[g], n) : 0;
+#endif
     s_count[g] = 0;
   }
   __syncthreads();
@@ -2517,6 +2536,13 @@ __device__ __forceinline__ void k2_run(const DevDFA* __restrict__ dfas, const K2
 #ifdef K2_TRACE_PHASE
   if (threadIdx.x == 0) s_tph = nullptr;
 #endif
+  // An empty list (the dense pass, usually) ends the block without a claim: 512 blocks'
+  // returning atomics on one address took ~10 us of an empty launch.  (A plain load of the
+  // claim counter before each atomic, to skip the claims past the list's end, made the
+  // list pass 0.110 -> 0.145 ms per GiB: loads and atomics on the counters' line, which
+  // also holds the candidate counter, profiles/r06/k2p.)
+  if (E == 0) return;
+  bool ran = false;  // (the end stamp: only a block that ran an entry)
   for (;;) {
     if (threadIdx.x == 0) s_e = atomicAdd(claim, 1u);
     __syncthreads();
@@ -2544,9 +2570,10 @@ __device__ __forceinline__ void k2_run(const DevDFA* __restrict__ dfas, const K2
 #endif
     prev = e;
     if (e >= E) {
-      if (threadIdx.x == 0) atomicMax(&A.clk[3], (unsigned long long)wall_clock64());
+      if (ran && threadIdx.x == 0) atomicMax(&A.clk[3], (unsigned long long)wall_clock64());
       break;
     }
+    ran = true;
     const uint4 en = entries[e];
     const uint32_t g = __builtin_amdgcn_readfirstlane(en.x);
     const DevDFA& d = dfas[g];  // (a reference: uniform fields load into SGPRs, no copy)
