@@ -944,7 +944,8 @@ struct K1FVerify {
 
 __global__ void __launch_bounds__(kFThreads) k1f_kernel(DevK1F d, K1FArgs A) {
   __shared__ __attribute__((aligned(16))) uint8_t smem[kFLds];
-  if (A.clk && threadIdx.x == 0) atomicMax(&A.clk[0], ~(unsigned long long)wall_clock64());
+  if (A.clk && threadIdx.x == 0 && blockIdx.x < 8)  // (the first blocks dispatched: GATES_STAMPS)
+    atomicMax(&A.clk[0], ~(unsigned long long)wall_clock64());
   {  // the entries (replicated) and the image, every load issued before the stores
     constexpr uint32_t kRep = 256u * 16u / kFThreads, kImg = kFImgMax / 16 / kFThreads;
     uint4 e[kRep], m[kImg];
@@ -1674,10 +1675,13 @@ __device__ __forceinline__ unsigned long long file_gate(const ItemArgs& A, const
 
 template <class V>
 __device__ __forceinline__ void gen_items(const ItemArgs& A, const ItemLds& T, uint64_t t, V visit) {
+  // (the unit's list entry is loaded beside the list's length, not after it: one memory
+  // round trip less on the chain every item pass waits for)
+  const uint32_t ev_t = t < A.evcap ? A.evlist[t] : 0u;
   const uint32_t nev = min(*A.nev, A.evcap);
   const uint32_t C = A.chunk;
   if (t < nev) {
-    const uint64_t e = A.evlist[t];
+    const uint64_t e = ev_t;
     const uint32_t evb = A.ev[e] & ~kEvAlways;
     const uint64_t ce = (e + 1) * C;
     // the event words of the kMaxBack chunks before e, loaded together (a dependent load per
