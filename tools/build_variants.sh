@@ -38,6 +38,7 @@ for v in "$@"; do
     fc16) build $v -DK1F_STEAL=8 -DK1F_STEAL_CHUNK=16 ;;  # K1F: 16-tile reserve chunks
     fc4) build $v -DK1F_STEAL=8 -DK1F_STEAL_CHUNK=4 ;;
     gs1) build $v -DGATES_STAMPS=0xFFFFFFFFu ;;  # gates: every block stamps the chain's start
+    fnoend) build $v -DK1F_NO_END_ATOMICS=1 ;;  # K1F: no block-end counters / stamp (timing probe; stats read 0)
     ib0) build $v -DITEMS_BASE_IN_COUNT=0 ;;  # items: the emit pass reserves the blocks' ranges
     fd2) build $v -DK1F_DEPTH=2 ;;       # K1F: register queue depths
     fd3) build $v -DK1F_DEPTH=3 ;;        # K1X: verify counters in k2_long_tails (slot probes),

@@ -623,6 +623,9 @@ __global__ void __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(4, 8))
 #ifndef K1F_STEAL_CHUNK
 #define K1F_STEAL_CHUNK 8  // tiles per claim
 #endif
+#ifndef K1F_NO_END_ATOMICS
+#define K1F_NO_END_ATOMICS 0  // (1: no block-end counters or stamp; a timing probe only)
+#endif
 #ifndef K1F_WTRACE
 #define K1F_WTRACE 0  // per-wave trace (TSG_K1F_TRACE; measurement builds, variant "ftr")
 #endif
@@ -1204,7 +1207,7 @@ __global__ void __launch_bounds__(kFThreads) k1f_kernel(DevK1F d, K1FArgs A) {
       for (uint32_t b = wv[k]; b; b &= b - 1, at++)
         if (at < A.evcap) A.evlist[at] = c_lo + 32 * (threadIdx.x + k * kFThreads) + __builtin_ctz(b);
   }
-  if (threadIdx.x == 0) {
+  if (threadIdx.x == 0 && !K1F_NO_END_ATOMICS) {
     if (bst[0]) atomicAdd(&A.stats[0], bst[0]);
     if (bst[1]) atomicAdd(&A.stats[1], bst[1]);
     if (A.clk) atomicMax(&A.clk[1], (unsigned long long)wall_clock64());
