@@ -23,6 +23,6 @@ echo "== FETCH_SIZE" && timeout -k 10 -s KILL 300 rocprofv3 --pmc FETCH_SIZE --o
 echo "== SQ" && timeout -k 10 -s KILL 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS SQ_WAIT_ANY --output-format csv -d $out/pmc_sq -o run -- \
   python bench.py --steps 1 --warmup 0 --no-cpu-baseline > $out/pmc_sq.out 2>&1 || { tail $out/pmc_sq.out; exit 6; }
 python tools/pmc_traffic.py --record builtin $out/pmc_fetch/run_counter_collection.csv $out/bench.json \
-  profiles/r06/final/bench_pmc_fetch.csv > $out/pmc_builtin.json || exit 7
+  profiles/r06/${1:-final}/bench_pmc_fetch.csv > $out/pmc_builtin.json || exit 7
 cat $out/pmc_builtin.json
 echo done
