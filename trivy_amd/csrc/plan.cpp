@@ -939,22 +939,21 @@ void resolve_batch(const Ruleset& rs, const Plan& plan, const BatchView& b,
     size_t ntrans = 0;
     for (size_t i = 0; i < nkc; i++) ntrans += (kc[i].rule & kCandTrans) && kc[i].end != kCandWhole;
     if (ntrans) {
-      expanded.reserve(nkc + ntrans);
-      for (size_t i = 0; i < nkc; i++) {
-        const Candidate& c = kc[i];
+      // one record's candidates into `out` (a word record replays its word from the batch)
+      auto expand = [&](const Candidate& c, std::vector<Candidate>& out) {
         if (!(c.rule & kCandTrans) || c.end == kCandWhole) {
-          expanded.push_back(c);
-          continue;
+          out.push_back(c);
+          return;
         }
         const bool word = words && (c.rule & kCandWord);
         const uint32_t g = (c.rule >> 16) & (words ? 0x3FFFu : 0x7FFFu), ix = c.rule & 0xFFFFu;
-        if (g >= plan.groups.size()) continue;
+        if (g >= plan.groups.size()) return;
         const GroupPlan& gp = plan.groups[g];
         const DFA& d = *gp.dfa;
         const uint32_t ncd = (uint32_t)std::max(2, d.nclasses);  // the device's row width
         if (word) {  // kCandWord: replay the word from row ix at byte `end` to the word's end
           size_t st = ix / ncd;
-          if (st >= (size_t)d.nstates || c.file >= F) continue;
+          if (st >= (size_t)d.nstates || c.file >= F) return;
           const uint64_t f0 = b.offsets[c.file], flen = b.offsets[c.file + 1] - f0;
           const uint64_t pend = std::min<uint64_t>(flen, (((f0 + c.end) | 15) + 1) - f0);
           for (uint64_t p = c.end; p < pend; p++) {
@@ -962,18 +961,34 @@ void resolve_batch(const Ruleset& rs, const Plan& plan, const BatchView& b,
             if (d.acc[e]) {
               const auto& m = d.masks[d.acc[e]];
               for (size_t k = 0; k < gp.rules.size(); k++)
-                if ((m[k / 64] >> (k % 64)) & 1) expanded.push_back({c.file, gp.rules[k], (uint32_t)p});
+                if ((m[k / 64] >> (k % 64)) & 1) out.push_back({c.file, gp.rules[k], (uint32_t)p});
             }
             st = d.next[e];
           }
-          continue;
+          return;
         }
         const size_t st = ix / ncd, cl = std::min<size_t>(ix % ncd, (size_t)d.nclasses - 1);
-        if (st >= (size_t)d.nstates) continue;
+        if (st >= (size_t)d.nstates) return;
         const auto& m = d.masks[d.acc[st * d.nclasses + cl]];
         for (size_t k = 0; k < gp.rules.size(); k++)
-          if ((m[k / 64] >> (k % 64)) & 1) expanded.push_back({c.file, gp.rules[k], c.end});
-      }
+          if ((m[k / 64] >> (k % 64)) & 1) out.push_back({c.file, gp.rules[k], c.end});
+      };
+      // In parallel, in record order: each word record's replay reads the batch at its own
+      // place (a cache and TLB miss in a pinned multi-GiB slot), and serially that was half
+      // of a layer piece's resolution (12-15 of ~28 Mcyc per 256 MiB piece, TSG_PROF).
+      constexpr size_t kRecBlk = 2048;
+      const size_t nrb = (nkc + kRecBlk - 1) / kRecBlk;
+      std::vector<std::vector<Candidate>> parts(nrb);
+      parallel_for(nrb, nthreads, [&](size_t bi) {
+        auto& out = parts[bi];
+        const size_t i1 = std::min(nkc, (bi + 1) * kRecBlk);
+        out.reserve(i1 - bi * kRecBlk + 16);
+        for (size_t i = bi * kRecBlk; i < i1; i++) expand(kc[i], out);
+      }, 1);
+      size_t total = 0;
+      for (const auto& pt : parts) total += pt.size();
+      expanded.reserve(total);
+      for (const auto& pt : parts) expanded.insert(expanded.end(), pt.begin(), pt.end());
       kc = expanded.data();
       nkc = expanded.size();
     }
