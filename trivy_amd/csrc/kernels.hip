@@ -1804,26 +1804,6 @@ struct LayoutArgs {
   uint32_t* stats;    // [1] items listed, [2] entries, [3] skipped groups
 };
 
-// exclusive prefix sum of v over the block; returns the total
-template <class T>
-__device__ T block_exclusive_scan(T v, T* out, T* s_wave) {
-  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
-  T x = v;
-  for (int o = 1; o < 64; o <<= 1) {
-    const T y = __shfl_up(x, o);
-    if (lane >= (uint32_t)o) x += y;
-  }
-  if (lane == 63) s_wave[wave] = x;
-  __syncthreads();
-  T before = 0, total = 0;
-  for (uint32_t w = 0; w < nw; w++) {
-    before += w < wave ? s_wave[w] : 0;
-    total += s_wave[w];
-  }
-  *out = before + x - v;
-  __syncthreads();
-  return total;
-}
 
 // K2's list kernel block (measurement builds vary it).  The stepping is bound by LDS bank
 // conflicts of the transition reads (random rows), so a CU's entries take the same time
@@ -1837,9 +1817,43 @@ constexpr int kK2Block = K2_LIST_BLOCK;
 constexpr uint32_t kEntryItems = 2 * kK2Block;  // two chains per lane
 constexpr uint32_t kEntryChunks = kStreams * kBlock;
 
+// exclusive prefix sums of N values at once over the block (one LDS exchange, two barriers
+// for all of them); returns the totals in tot.  s_wave: [N * waves]
+template <int N>
+__device__ void block_exclusive_scan_n(const unsigned long long (&v)[N], unsigned long long (&out)[N],
+                                       unsigned long long (&tot)[N], unsigned long long* s_wave) {
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  unsigned long long x[N];
+#pragma unroll
+  for (int k = 0; k < N; k++) x[k] = v[k];
+  for (int o = 1; o < 64; o <<= 1) {
+#pragma unroll
+    for (int k = 0; k < N; k++) {
+      const unsigned long long y = __shfl_up(x[k], o);
+      if (lane >= (uint32_t)o) x[k] += y;
+    }
+  }
+  if (lane == 63)
+#pragma unroll
+    for (int k = 0; k < N; k++) s_wave[k * nw + wave] = x[k];
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < N; k++) {
+    unsigned long long before = 0, total = 0;
+    for (uint32_t w = 0; w < nw; w++) {
+      const unsigned long long t = s_wave[k * nw + w];
+      before += w < wave ? t : 0;
+      total += t;
+    }
+    out[k] = before + x[k] - v[k];
+    tot[k] = total;
+  }
+  __syncthreads();
+}
+
 // the layout into s_kind / s_gbase ([G] in LDS) and K2's work list (see above)
 __device__ void layout_block(const LayoutArgs& A, uint8_t* s_kind, uint32_t* s_gbase) {
-  __shared__ unsigned long long s_wave64[kBlock / 64];
+  __shared__ unsigned long long s_wave64[3 * (kBlock / 64)];
   __shared__ unsigned long long s_carry[5];  // items, entries, dense groups, skipped groups, dense entries
   __shared__ uint2 s_dense[kBlock];  // dense groups of the tile: group, first dense entry
   __shared__ uint32_t s_ndense;
@@ -1856,24 +1870,23 @@ __device__ void layout_block(const LayoutArgs& A, uint8_t* s_kind, uint32_t* s_g
     const uint32_t g = g0 + threadIdx.x;
     const uint64_t cnt = g < A.G ? A.gcount[g] : 0;
     const bool dense_want = cnt * 2 > A.nchunks;
-    // dense budget first (in group order), then the item capacity for list groups
-    unsigned long long dpre;
-    const unsigned long long dtot = block_exclusive_scan<unsigned long long>(dense_want ? 1 : 0, &dpre, s_wave64);
-    const bool dense = dense_want && s_carry[2] + dpre < A.max_dense;
+    // dense budget first (in group order), then the item capacity for list groups (the
+    // scans of one tile of groups in two rounds of one block exchange each: five separate
+    // scans cost ten barriers per tile, a 1,000-rule set has four tiles)
     const bool want_list = cnt && !dense_want;
-    unsigned long long ipre;
-    const unsigned long long itot = block_exclusive_scan<unsigned long long>(want_list ? cnt : 0, &ipre, s_wave64);
+    unsigned long long p1[2], t1[2];
+    block_exclusive_scan_n<2>({dense_want ? 1ull : 0ull, want_list ? cnt : 0ull}, p1, t1, s_wave64);
+    const unsigned long long dpre = p1[0], dtot = t1[0], ipre = p1[1], itot = t1[1];
+    const bool dense = dense_want && s_carry[2] + dpre < A.max_dense;
     const bool list = want_list && s_carry[0] + ipre + cnt <= A.items_cap;
     // items of groups that fit are placed at their prefix position (a skipped group's
     // range stays unused: the regions keep group order)
     const uint64_t nent = list ? (cnt + kEntryItems - 1) / kEntryItems : 0;
     const uint64_t ndent = dense ? ndent_all : 0;
-    unsigned long long epre, dpre2;
-    const unsigned long long etot = block_exclusive_scan<unsigned long long>(nent, &epre, s_wave64);
-    const unsigned long long dtot2 = block_exclusive_scan<unsigned long long>(ndent, &dpre2, s_wave64);
     const bool skip = cnt && !list && !dense;
-    unsigned long long spre;
-    const unsigned long long stot = block_exclusive_scan<unsigned long long>(skip ? 1 : 0, &spre, s_wave64);
+    unsigned long long p2[3], t2[3];
+    block_exclusive_scan_n<3>({(unsigned long long)nent, (unsigned long long)ndent, skip ? 1ull : 0ull}, p2, t2, s_wave64);
+    const unsigned long long epre = p2[0], etot = t2[0], dpre2 = p2[1], dtot2 = t2[1], stot = t2[2];
     // (entries_cap covers every list entry the item capacity allows plus max_dense dense
     // groups, so the work list always fits)
     const uint64_t e0 = s_carry[1] + epre, d0 = s_carry[4] + dpre2;
